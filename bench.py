@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json's metric: Mrays/s (+ ms/frame) at 1920x1080, 4 spp, depth 4.
+
+Workload (config C4, the 1M-triangle scene the north-star target is quoted on; it fits one MI355X):
+1000x500-quad heightfield = 1,000,000 triangles, procedural textures, 4 point + directional + spot
+light, equirect sky, camera (0.3,3,-7) -> origin, all reference features on (AA, accumulate, gamma,
+normal map, skybox, lighted, stochastic NEE).  A step = one prt_render of the full 4-spp frame
+(2 reference frames x 2 AA paths per pixel), inputs resident in HBM.
+
+Mrays/s = (closest-hit segments + any-hit shadow rays) / time, counted on the device.
+N > 1: one process per GPU (torchrun), pixel tiles 32x32 round-robin over ranks, RCCL gather of the
+per-rank tile buffers to rank 0, untile there; value = all ranks' rays / max-over-ranks time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "physically-based-ray-tracer_amd"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VISITS_JSON = os.path.join(ROOT, "profiles", "reference_visits_c4.json")
+
+
+def algorithmic_bytes_per_ray():
+    """B_ray = 256*N_int + 192*N_leaf + 64*N_tlas + 192*N_inst + 48 + 16, with N measured on the
+    reference's own BVH8_CPU (tinybvh v1.4.2, oracle/_ref) for this workload (profiles/reference_visits_c4.json)."""
+    with open(VISITS_JSON) as f:
+        v = json.load(f)
+    out = {}
+    for kind in ("closest", "anyhit"):
+        n = v[kind]
+        out[kind] = 256.0 * n["n_int"] + 192.0 * n["n_leaf"] + 64.0 * n["n_tlas"] + 192.0 * n["n_inst"] + 48 + 16
+    out["per_shaded_hit"] = 12.0   # 3 texels
+    out["per_pixel_frame"] = 36.0  # accumulator read+write + rgb8
+    return out, v
+
+
+def cpu_baseline(sd, threads):
+    """The oracle (C restatement, OpenMP over rows) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    W, H = 480, 270  # 1/16 of the 1080p pixels, same scene, 4 spp, depth 4
+    osc = oracle.OracleScene(sd, W, H)
+    t0 = time.perf_counter()
+    _, _, _, st = osc.render(W, H, spp=4, bounces=4, nthreads=threads)
+    dt = time.perf_counter() - t0
+    rays = st.segments + st.shadow_rays
+    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"C4 scene at {W}x{H}, 4 spp, depth 4 ({rays} rays, {dt:.2f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=4)
+    ap.add_argument("--bounces", type=int, default=4)
+    ap.add_argument("--scene", default="c4", choices=["c3", "c4"])
+    ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import prt
+    from prt import scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    sd = scenes.config_c4() if args.scene == "c4" else scenes.config_c3()
+    W, H = args.width, args.height
+    ctx = prt.Context(local)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    scene = prt.Scene.from_data(sd)
+    ctx.set_scene(scene)
+    ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
+    info = ctx.scene_info()
+
+    dev = torch.device("cuda", local)
+    avg = torch.zeros((H * W, 4), dtype=torch.float32, device=dev)
+    rgb = torch.zeros(H * W, dtype=torch.int32, device=dev)
+    if world > 1:
+        per = ctx.tile_buffer_pixels(W, H, args.tile, world)
+        tiles = torch.zeros((per, 4), dtype=torch.float32, device=dev)
+        gathered = torch.zeros((world, per, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+
+    def step(i):
+        if world == 1:
+            _, _, st = ctx.render(W, H, args.spp, args.bounces, frame_index=2 * i, avg=avg.data_ptr(),
+                                  rgb8=rgb.data_ptr(), device_out=True, stats=True)
+        else:
+            st = ctx.render_tiles(W, H, args.spp, args.bounces, args.tile, rank, world, tiles.data_ptr(),
+                                  frame_index=2 * i, stats=True)
+            dist.gather(tiles, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                ctx.untile(gathered.data_ptr(), W, H, args.tile, world, avg.data_ptr(), rgb.data_ptr())
+        return st
+
+    for i in range(args.warmup):
+        step(i)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    seg = shadow = 0
+    ms_trace = []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        st = step(args.warmup + i)
+        seg += st.segments
+        shadow += st.shadow_rays
+        ms_trace.append(st.ms_trace)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    rays = seg + shadow
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([seg, shadow], dtype=torch.float64, device=dev)
+        dist.all_reduce(r)
+        seg, shadow = int(r[0].item()), int(r[1].item())
+        rays = seg + shadow
+
+    if rank == 0:
+        ms_step = elapsed * 1000.0 / args.steps
+        value = rays / elapsed / 1e6
+        bpr, visits = algorithmic_bytes_per_ray()
+        # dominant kernel: k_trace_frames; algorithmic bytes per launch / its HIP-event duration
+        steps_rays_seg = seg / args.steps
+        steps_rays_sh = shadow / args.steps
+        alg_bytes = steps_rays_seg * bpr["closest"] + steps_rays_sh * bpr["anyhit"]
+        kern_ms = float(np.mean(ms_trace))
+        achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+        out = {
+            "metric": "Mrays/s (closest-hit segments + shadow any-hit rays) at 1920x1080, 4 spp, depth 4",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak" if world == 1 else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded procedural heightfield, textures, sky; scenes.py)",
+            "config": {"workload": f"{sd.name}: {info.triangles} tris, {W}x{H}, {args.spp} spp, depth {args.bounces}",
+                       "global_batch": W * H, "seq_len": args.bounces,
+                       "parallelism": f"pixel-tile{args.tile} x{world}" if world > 1 else "single-gpu",
+                       "rays_per_step": int(rays / args.steps), "segments_per_step": int(seg / args.steps),
+                       "shadow_per_step": int(shadow / args.steps),
+                       "mpix_per_s": round(W * H / (ms_step / 1e3) / 1e6, 2)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "k_trace_frames", "kernel_ms": round(kern_ms, 3),
+                         "bytes_per_ray": {k: round(v, 1) for k, v in bpr.items()}},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(sd, threads)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

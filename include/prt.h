@@ -1,0 +1,195 @@
+/*
+ * prt.h -- C ABI of the MI355X-native path-tracing hot path.
+ *
+ * Drop-in boundary for the reference's per-pixel hot path (Iancic/Physically-Based-Ray-Tracer):
+ * a Renderer::Tick shim replaces Core/Renderer.cpp:43-141 with prt_render(),
+ * after handing over the data the hot path reads without copying:
+ *
+ *   prt_set_textures   <- Model::{albedo,normal,metalness,emission}Texture (template/surface.h:49-94)
+ *   prt_set_meshes     <- Model fat-triangle arrays (Core/Model.h:36-44, Core/Model.cpp:25-119)
+ *   prt_set_instances  <- Scene::blases[i].transform + gameobjects[i]->modelIndex (Core/Scene.cpp:220-223,
+ *                         Core/tiny_bvh.h:1243-1256)
+ *   prt_set_lights     <- Renderer point-light SoA (Core/Renderer.h:80-88), directionalLights[0], spotlights[0]
+ *   prt_set_sky        <- Camera::skyPixels (Core/Camera.cpp:9)
+ *   prt_set_camera     <- Camera::camPos/topLeft/topRight/bottomLeft (Core/Camera.cpp:29-36)
+ *   prt_render         <- the OpenMP pixel loop + Renderer::Trace (Core/Renderer.cpp:43-141,150-406)
+ *
+ * Conventions: plain pointers and sizes, no C++ types; every call returns PRT_OK (0) or a negative
+ * prt_status; prt_last_error() gives the message for the calling thread.  No exceptions cross the ABI.
+ * One host thread per context.  All scene arrays are copied to device memory (HBM) during the call;
+ * the caller may free them afterwards.  A HIP device must be present: there is no CPU fallback.
+ */
+#ifndef PRT_H
+#define PRT_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PRT_ABI_VERSION 1
+
+typedef enum {
+    PRT_OK = 0,
+    PRT_ERR_INVALID_ARGUMENT = -1,
+    PRT_ERR_NO_DEVICE = -2,
+    PRT_ERR_HIP = -3,
+    PRT_ERR_OUT_OF_MEMORY = -4,
+    PRT_ERR_NOT_READY = -5,     /* scene/camera incomplete */
+    PRT_ERR_UNSUPPORTED = -6
+} prt_status;
+
+/* Render flags: the public Renderer bools, Core/Renderer.h:33,48 */
+#define PRT_FLAG_AA          (1u << 0)
+#define PRT_FLAG_ACCUMULATE  (1u << 1)
+#define PRT_FLAG_GAMMA       (1u << 2)
+#define PRT_FLAG_NORMALMAP   (1u << 3)
+#define PRT_FLAG_SKYBOX      (1u << 4)
+#define PRT_FLAG_LIGHTED     (1u << 5)
+#define PRT_FLAG_STOCHASTIC  (1u << 6)
+/* the reference's defaults (Core/Renderer.h:33,48) */
+#define PRT_FLAGS_DEFAULT    (0x7Fu)
+
+/* Renderer::RENDER_STATES, Core/Renderer.h:37-46 */
+typedef enum {
+    PRT_MODE_BRDF = 0, PRT_MODE_BASECOLOR = 1, PRT_MODE_GEOMETRYNORMAL = 2, PRT_MODE_SHADINGNORMAL = 3,
+    PRT_MODE_METAL = 4, PRT_MODE_ROUGHNESS = 5, PRT_MODE_EMISSIVE = 6
+} prt_render_mode;
+
+typedef struct prt_ctx prt_ctx;
+
+typedef struct {
+    int32_t device;      /* HIP device ordinal (one process per GPU) */
+    uint32_t flags;      /* reserved, 0 */
+} prt_device_desc;
+
+/* one packed 0x00RRGGBB texture, exactly Surface::pixels (template/surface.cpp:47-66) */
+typedef struct {
+    int32_t width, height;
+    const uint32_t* pixels;
+} prt_texture;
+
+/* one Model (Core/Model.h:36-44).  T = tri_count, V = vertex_count. */
+typedef struct {
+    int32_t tri_count;
+    int32_t vertex_count;
+    const float* triangles;      /* float4 x 3T : Model::triangles (fat, w ignored)            */
+    const float* fixed_normals;  /* float4 x 3T : Model::fixedNormals                          */
+    const float* fixed_uvs;      /* float2 x 3T : Model::fixedTextureCoords                    */
+    const int32_t* indices;      /* int x 3T    : Model::indices                               */
+    const float* vertices;       /* float3 x V  : Model::vertices                              */
+    const float* face_normals;   /* float3 x T  : Model::faceNormals                           */
+    int32_t albedo_tex;          /* required (Core/Scene.cpp:160 dereferences it)              */
+    int32_t normal_tex;          /* -1 = none */
+    int32_t metalness_tex;       /* -1 = none (G = roughness, B = metalness, Scene.cpp:175-181) */
+    int32_t emission_tex;        /* -1 = none */
+} prt_mesh;
+
+/* lights as the hot path reads them (Core/Renderer.cpp:216-310) */
+typedef struct {
+    float point_pos[4][3];   /* posX/posY/posZ SoA of the 4 SIMD point lights */
+    float point_color[4][3];
+    float dir_pos[3], dir_color[3];                  /* directionalLights[0]->transform */
+    float spot_pos[3], spot_color[3], spot_rot[3];   /* spotlights[0]->transform        */
+} prt_lights;
+
+/* Camera screen plane (Core/Camera.cpp:29-36, 113-139) */
+typedef struct {
+    float pos[3];
+    float top_left[3], top_right[3], bottom_left[3];
+} prt_camera;
+
+typedef struct {
+    int32_t width, height;
+    int32_t spp;            /* camera paths per pixel in this call; with AA one reference frame = 2 paths */
+    int32_t bounces;        /* Renderer::bounces (closest-hit segments per path), 0..16 */
+    uint32_t flags;         /* PRT_FLAG_* */
+    int32_t render_mode;    /* prt_render_mode */
+    uint32_t frame_index;   /* first reference frame of this call (RNG stream) */
+    uint32_t seed;          /* added to the per-pixel seed base */
+} prt_render_params;
+
+typedef struct {
+    uint64_t segments;      /* closest-hit queries (TLAS intersections) */
+    uint64_t shadow_rays;   /* any-hit queries (IsOccluded) */
+    uint64_t paths;         /* camera paths traced */
+    double   ms;            /* device time of the render (HIP events) */
+    double   ms_trace;      /* device time of the path-tracing kernel(s) only */
+} prt_stats;
+
+/* closest-hit record, tinybvh::Intersection (Core/tiny_bvh.h:545-567) minus user data */
+typedef struct {
+    float t, u, v;
+    uint32_t prim, inst;
+} prt_hit;
+
+/* ---- context ---- */
+int prt_abi_version(void);
+const char* prt_last_error(void);
+int prt_device_count(int32_t* count);
+int prt_create(const prt_device_desc* desc, prt_ctx** out);
+int prt_destroy(prt_ctx* ctx);
+/* run subsequent work on an external hipStream_t (e.g. torch's current stream); NULL = ctx-owned stream */
+int prt_set_stream(prt_ctx* ctx, void* hip_stream);
+
+/* ---- scene (Scene / Model / Camera state) ---- */
+int prt_set_textures(prt_ctx* ctx, const prt_texture* textures, int32_t count);
+int prt_set_meshes(prt_ctx* ctx, const prt_mesh* meshes, int32_t count);
+/* transforms: 16*count floats, row-major BLASInstance::transform; mesh_index: count */
+int prt_set_instances(prt_ctx* ctx, const float* transforms, const uint32_t* mesh_index, int32_t count);
+int prt_set_lights(prt_ctx* ctx, const prt_lights* lights);
+/* float RGB equirect, w*h*3; NULL/0 = no sky (misses shade 0 even with PRT_FLAG_SKYBOX) */
+int prt_set_sky(prt_ctx* ctx, const float* rgb, int32_t width, int32_t height);
+int prt_set_camera(prt_ctx* ctx, const prt_camera* cam);
+/* Camera::Camera basis from position/target and aspect (Core/Camera.cpp:29-36) */
+int prt_camera_look_at(const float pos[3], const float target[3], float aspect, prt_camera* out);
+
+/* ---- rendering (Renderer::Tick) ----
+ * Traces params.spp camera paths per pixel as spp/2 (AA) or spp reference frames and folds each
+ * frame into the persistent accumulation state exactly as Core/Renderer.cpp:81-104 does.
+ * Outputs (either may be NULL): avg_rgba = float4 W*H average, rgb8 = 0x00RRGGBB W*H.
+ * They are host pointers unless PRT_OUT_DEVICE is set in out_flags (then device pointers). */
+#define PRT_OUT_DEVICE (1u << 0)
+int prt_render(prt_ctx* ctx, const prt_render_params* params, float* avg_rgba, uint32_t* rgb8,
+               uint32_t out_flags, prt_stats* stats);
+/* Reset the accumulation state: memset of the accumulator (Core/Renderer.cpp:147) and, with
+ * full != 0, also samplesPerPixel/distances (fresh Renderer). */
+int prt_reset_accumulation(prt_ctx* ctx, int32_t full);
+
+/* ---- multi-GPU pixel-tile sharding (one process per GPU, RCCL gather done by the caller) ----
+ * The image is cut into tile_size x tile_size tiles numbered in row-major order; rank r renders
+ * tiles r, r+world, r+2*world, ...  into a compact float4 buffer laid out
+ * [local_tile][tile_size*tile_size] (pixels outside the image are written as 0).
+ * prt_tile_buffer_pixels() gives the element count (per rank, equal on all ranks: the max). */
+int prt_tile_buffer_pixels(int32_t width, int32_t height, int32_t tile_size, int32_t world, int64_t* pixels);
+int prt_render_tiles(prt_ctx* ctx, const prt_render_params* params, int32_t tile_size, int32_t rank,
+                     int32_t world, float* tiles_rgba_device, prt_stats* stats);
+/* rank-0 side: gathered [world][tile_buffer_pixels] float4 device buffer -> W*H avg_rgba + rgb8 (device) */
+int prt_untile(prt_ctx* ctx, const float* gathered_device, int32_t width, int32_t height, int32_t tile_size,
+               int32_t world, float* avg_rgba_device, uint32_t* rgb8_device);
+
+/* ---- geometry-only queries (the traversal kernels on their own) ---- */
+/* primary-ray closest hits for every pixel (config C2): out = W*H prt_hit (host or device per out_flags) */
+int prt_trace_primary(prt_ctx* ctx, int32_t width, int32_t height, prt_hit* hits, uint32_t out_flags,
+                      prt_stats* stats);
+/* arbitrary rays: origins/dirs float3 x n (dirs normalised like the tinybvh::Ray ctor), tmax n (NULL = 1e30) */
+int prt_intersect(prt_ctx* ctx, int32_t n, const float* origins, const float* dirs, const float* tmax,
+                  prt_hit* hits);
+int prt_occluded(prt_ctx* ctx, int32_t n, const float* origins, const float* dirs, const float* tmax,
+                 int32_t* occluded);
+
+/* ---- introspection ---- */
+typedef struct {
+    int64_t blas_nodes;     /* device BVH nodes over all meshes */
+    int64_t blas_leaves;
+    int64_t device_bytes;   /* BVH + triangle + shading arrays resident in HBM */
+    int32_t max_depth;
+    int32_t triangles;
+} prt_scene_info;
+int prt_get_scene_info(prt_ctx* ctx, prt_scene_info* info);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PRT_H */

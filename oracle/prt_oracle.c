@@ -1,0 +1,1085 @@
+/*
+ * oracle/prt_oracle.c -- TEST INFRASTRUCTURE ONLY.  See prt_oracle.h for scope and pinning.
+ *
+ * Floating point: compiled with -O2 -ffp-contract=off (no FMA contraction, IEEE
+ * +,-,*,/,sqrt).  Every expression keeps the reference's C++ evaluation order.
+ * Transcendentals (pow, sin, cos, atan2, acos) are evaluated in double and rounded
+ * once to float ("correctly rounded float libm" restatement of the reference's
+ * std::pow/cos/sin/atan2f/acosf); the MSVC libm the reference links is not
+ * reproducible off Windows.  _mm_rcp_ps (Core/Renderer.cpp:237) is restated as an
+ * exact reciprocal (documented divergence, <=3.7e-4 relative on that term).
+ *
+ * Canonical RNG stream: one xorshift32 stream per
+ * (pixel p, reference frame f), seed = InitSeed(seed + p + W*H*f)
+ * (template/tmpl8math.cpp:19-30; 0 -> 0x12345678).  Draw order: AA jitter x, y,
+ * then Trace(r1) draws, then Trace(r2) draws; inside Trace: light-class pick,
+ * [point: whichLight], [lobe], u.x, u.y.
+ *
+ * Closest-hit rule: Moeller-Trumbore exactly as BVH8_CPU's leaf
+ * (Core/tiny_bvh.h:6412-6440, det eps 1e-6, u in [0,1], v >= 0, u+v <= 1, t > 0);
+ * among equal t the lexicographically smallest (instance, prim) wins, so the hit is
+ * a pure function of the ray and the triangle set (independent of BVH shape).
+ * Box tests are conservative (inflated), so no triangle the MT test accepts is culled.
+ */
+#include "prt_oracle.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define EPSILON 0.01f            /* template/common.h:26 */
+#define BVH_FAR 1e30f            /* Core/tiny_bvh.h:131 */
+#define PI_F 3.141592653589f     /* Core/BRDF.h:27 (the macro seen by Renderer/Camera/BRDF) */
+#define MIN_DIELECTRICS_F0 0.4f  /* Core/BRDF.h:65 */
+#define MAXDEPTH 64
+
+/* ------------------------------------------------------------------ vector math */
+typedef struct { float x, y, z; } f3;
+typedef struct { float x, y; } f2;
+typedef struct { float x, y, z, w; } f4;
+
+static inline f3 v3(float x, float y, float z) { f3 r = {x, y, z}; return r; }
+static inline f3 add3(f3 a, f3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline f3 sub3(f3 a, f3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline f3 mul3(f3 a, f3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline f3 muls(f3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }      /* float3 * float */
+static inline f3 smul(float s, f3 a) { return v3(s * a.x, s * a.y, s * a.z); }      /* float * float3 */
+static inline f3 divs(f3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
+static inline f3 neg3(f3 a) { return v3(-a.x, -a.y, -a.z); }
+static inline float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; } /* tmpl8math.h:495 */
+static inline f3 cross3(f3 a, f3 b) {                                                /* tmpl8math.h:553 */
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static inline float length3(f3 a) { return sqrtf(dot3(a, a)); }                     /* tmpl8math.h:509 */
+/* tmpl8 normalize: v * (1 / sqrtf(dot(v,v))), tmpl8math.h:139,517 (also glm's, func_geometric.inl:104) */
+static inline f3 norm_t8(f3 v) { float inv = 1.0f / sqrtf(dot3(v, v)); return muls(v, inv); }
+/* tinybvh_normalize, Core/tiny_bvh.h:404-408 */
+static inline f3 norm_bvh(f3 a) {
+    float l = sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
+    float rl = l == 0 ? 0 : (1.0f / l);
+    return muls(a, rl);
+}
+/* tinybvh_safercp, Core/tiny_bvh.h:341 */
+static inline float safercp(float x) { return x > 1e-12f ? (1.0f / x) : (x < -1e-12f ? (1.0f / x) : BVH_FAR); }
+/* std::min / std::max (precomp.h:35 'using namespace std') */
+static inline float smin(float a, float b) { return (b < a) ? b : a; }
+static inline float smax(float a, float b) { return (a < b) ? b : a; }
+/* tmpl8 fminf/fmaxf/clamp/saturate, tmpl8math.h:137-138,446; BRDF.h:163 */
+static inline float t8min(float a, float b) { return a < b ? a : b; }
+static inline float t8max(float a, float b) { return a > b ? a : b; }
+static inline float clampf_(float f, float a, float b) { return t8max(a, t8min(f, b)); }
+static inline float saturate_(float x) { return clampf_(x, 0.0f, 1.0f); }
+static inline f3 lerp3(f3 a, f3 b, float t) { return add3(a, smul(t, sub3(b, a))); } /* tmpl8math.h:470 */
+static inline float lerpf(float a, float b, float t) { return a + t * (b - a); }     /* tmpl8math.h:468 */
+static inline f3 reflect3(f3 i, f3 n) { return sub3(i, muls(smul(2.0f, n), dot3(n, i))); } /* tmpl8math.h:547 */
+
+/* correctly-rounded float transcendentals (see header comment) */
+static inline float cr_pow(float x, float y) { return (float)pow((double)x, (double)y); }
+static inline float cr_sin(float x) { return (float)sin((double)x); }
+static inline float cr_cos(float x) { return (float)cos((double)x); }
+static inline float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+static inline float cr_acos(float x) { return (float)acos((double)x); }
+
+/* tinybvh_transform_point / _vector, Core/tiny_bvh.h:409-422 */
+static inline f3 xform_point(f3 v, const float* T) {
+    f3 res = v3(T[0] * v.x + T[1] * v.y + T[2] * v.z + T[3],
+                T[4] * v.x + T[5] * v.y + T[6] * v.z + T[7],
+                T[8] * v.x + T[9] * v.y + T[10] * v.z + T[11]);
+    const float w = T[12] * v.x + T[13] * v.y + T[14] * v.z + T[15];
+    if (w == 1) return res; else return muls(res, 1.f / w);
+}
+static inline f3 xform_vector(f3 v, const float* T) {
+    return v3(T[0] * v.x + T[1] * v.y + T[2] * v.z, T[4] * v.x + T[5] * v.y + T[6] * v.z,
+              T[8] * v.x + T[9] * v.y + T[10] * v.z);
+}
+
+/* MESA 4x4 inverse, template/tmpl8math.h:701-746 (== BLASInstance::InvertTransform, tiny_bvh.h:7883-7905) */
+static void mesa_inverse(const float* c, float* out) {
+    float inv[16];
+    inv[0] = c[5] * c[10] * c[15] - c[5] * c[11] * c[14] - c[9] * c[6] * c[15] + c[9] * c[7] * c[14] + c[13] * c[6] * c[11] - c[13] * c[7] * c[10];
+    inv[1] = -c[1] * c[10] * c[15] + c[1] * c[11] * c[14] + c[9] * c[2] * c[15] - c[9] * c[3] * c[14] - c[13] * c[2] * c[11] + c[13] * c[3] * c[10];
+    inv[2] = c[1] * c[6] * c[15] - c[1] * c[7] * c[14] - c[5] * c[2] * c[15] + c[5] * c[3] * c[14] + c[13] * c[2] * c[7] - c[13] * c[3] * c[6];
+    inv[3] = -c[1] * c[6] * c[11] + c[1] * c[7] * c[10] + c[5] * c[2] * c[11] - c[5] * c[3] * c[10] - c[9] * c[2] * c[7] + c[9] * c[3] * c[6];
+    inv[4] = -c[4] * c[10] * c[15] + c[4] * c[11] * c[14] + c[8] * c[6] * c[15] - c[8] * c[7] * c[14] - c[12] * c[6] * c[11] + c[12] * c[7] * c[10];
+    inv[5] = c[0] * c[10] * c[15] - c[0] * c[11] * c[14] - c[8] * c[2] * c[15] + c[8] * c[3] * c[14] + c[12] * c[2] * c[11] - c[12] * c[3] * c[10];
+    inv[6] = -c[0] * c[6] * c[15] + c[0] * c[7] * c[14] + c[4] * c[2] * c[15] - c[4] * c[3] * c[14] - c[12] * c[2] * c[7] + c[12] * c[3] * c[6];
+    inv[7] = c[0] * c[6] * c[11] - c[0] * c[7] * c[10] - c[4] * c[2] * c[11] + c[4] * c[3] * c[10] + c[8] * c[2] * c[7] - c[8] * c[3] * c[6];
+    inv[8] = c[4] * c[9] * c[15] - c[4] * c[11] * c[13] - c[8] * c[5] * c[15] + c[8] * c[7] * c[13] + c[12] * c[5] * c[11] - c[12] * c[7] * c[9];
+    inv[9] = -c[0] * c[9] * c[15] + c[0] * c[11] * c[13] + c[8] * c[1] * c[15] - c[8] * c[3] * c[13] - c[12] * c[1] * c[11] + c[12] * c[3] * c[9];
+    inv[10] = c[0] * c[5] * c[15] - c[0] * c[7] * c[13] - c[4] * c[1] * c[15] + c[4] * c[3] * c[13] + c[12] * c[1] * c[7] - c[12] * c[3] * c[5];
+    inv[11] = -c[0] * c[5] * c[11] + c[0] * c[7] * c[9] + c[4] * c[1] * c[11] - c[4] * c[3] * c[9] - c[8] * c[1] * c[7] + c[8] * c[3] * c[5];
+    inv[12] = -c[4] * c[9] * c[14] + c[4] * c[10] * c[13] + c[8] * c[5] * c[14] - c[8] * c[6] * c[13] - c[12] * c[5] * c[10] + c[12] * c[6] * c[9];
+    inv[13] = c[0] * c[9] * c[14] - c[0] * c[10] * c[13] - c[8] * c[1] * c[14] + c[8] * c[2] * c[13] + c[12] * c[1] * c[10] - c[12] * c[2] * c[9];
+    inv[14] = -c[0] * c[5] * c[14] + c[0] * c[6] * c[13] + c[4] * c[1] * c[14] - c[4] * c[2] * c[13] - c[12] * c[1] * c[6] + c[12] * c[2] * c[5];
+    inv[15] = c[0] * c[5] * c[10] - c[0] * c[6] * c[9] - c[4] * c[1] * c[10] + c[4] * c[2] * c[9] + c[8] * c[1] * c[6] - c[8] * c[2] * c[5];
+    const float det = c[0] * inv[0] + c[1] * inv[4] + c[2] * inv[8] + c[3] * inv[12];
+    if (det != 0) {
+        const float invdet = 1.0f / det;
+        for (int i = 0; i < 16; i++) out[i] = inv[i] * invdet;
+    } else {
+        for (int i = 0; i < 16; i++) out[i] = (i % 5 == 0) ? 1.0f : 0.0f; /* mat4 default = identity */
+    }
+}
+
+/* ------------------------------------------------------------------ RNG (tmpl8math.cpp:19-48) */
+static inline uint32_t wang_hash(uint32_t s) {
+    s = (s ^ 61) ^ (s >> 16);
+    s *= 9, s = s ^ (s >> 4);
+    s *= 0x27d4eb2d;
+    s = s ^ (s >> 15);
+    return s;
+}
+uint32_t orc_init_seed(uint32_t base) {
+    uint32_t s = wang_hash((base + 1) * 17);
+    return s ? s : 0x12345678u;
+}
+static inline float rnd(uint32_t* seed) {
+    uint32_t s = *seed;
+    s ^= s << 13; s ^= s >> 17; s ^= s << 5;
+    *seed = s;
+    return (float)s * 2.3283064365387e-10f;
+}
+void orc_rng_floats(uint32_t seed, int32_t n, float* out) { for (int i = 0; i < n; i++) out[i] = rnd(&seed); }
+
+/* ------------------------------------------------------------------ scene */
+typedef struct { int32_t w, h; uint32_t* px; } tex_t;
+typedef struct { float bmin[3], bmax[3]; int32_t left_first, count; } bnode_t;
+typedef struct {
+    int32_t ntri, nvert;
+    float *tri, *fn, *fuv, *vert, *facen;
+    int32_t* idx;
+    int32_t tex[4]; /* albedo, normal, metalness, emission */
+    /* built-in BVH */
+    bnode_t* nodes; int32_t nnodes;
+    uint32_t* prim;  /* leaf order -> triangle index */
+    float* mt;       /* 9 floats per tri: v0, e1, e2 (same as BVHTri4Leaf, tiny_bvh.h:4614-4619) */
+    float bmin[3], bmax[3];
+} mesh_t;
+typedef struct { float T[16], inv[16], nrm[16]; float bmin[3], bmax[3]; int32_t mesh; } inst_t;
+
+struct orc_scene {
+    tex_t* tex; int32_t ntex;
+    mesh_t* mesh; int32_t nmesh;
+    inst_t* inst; int32_t ninst;
+    float ppos[12], pcol[12], dpos[3], dcol[3], spos[3], scol[3], srot[3];
+    float* sky; int32_t skyw, skyh;
+    float cam[12];
+    orc_backend backend; int has_backend;
+    int built;
+};
+
+orc_scene* orc_scene_create(void) { return (orc_scene*)calloc(1, sizeof(orc_scene)); }
+void orc_scene_destroy(orc_scene* s) {
+    if (!s) return;
+    for (int i = 0; i < s->ntex; i++) free(s->tex[i].px);
+    for (int i = 0; i < s->nmesh; i++) {
+        mesh_t* m = &s->mesh[i];
+        free(m->tri); free(m->fn); free(m->fuv); free(m->vert); free(m->facen); free(m->idx);
+        free(m->nodes); free(m->prim); free(m->mt);
+    }
+    free(s->tex); free(s->mesh); free(s->inst); free(s->sky); free(s);
+}
+static void* dupmem(const void* p, size_t n) { void* q = malloc(n ? n : 1); if (p && n) memcpy(q, p, n); return q; }
+
+int orc_add_texture(orc_scene* s, int32_t w, int32_t h, const uint32_t* px) {
+    if (w <= 0 || h <= 0 || !px) return -1;
+    s->tex = (tex_t*)realloc(s->tex, sizeof(tex_t) * (s->ntex + 1));
+    s->tex[s->ntex].w = w; s->tex[s->ntex].h = h;
+    s->tex[s->ntex].px = (uint32_t*)dupmem(px, sizeof(uint32_t) * (size_t)w * h);
+    return s->ntex++;
+}
+int orc_add_mesh(orc_scene* s, int32_t T, const float* tri, const float* fn, const float* fuv, const int32_t* idx,
+                 const float* vert, int32_t nv, const float* facen, int32_t a, int32_t n, int32_t m, int32_t e) {
+    if (T <= 0 || !tri || !fn || !fuv || !idx || !vert || !facen) return -1;
+    if (a < 0 || a >= s->ntex) return -2; /* Scene.cpp:160 dereferences albedoTexture unconditionally */
+    s->mesh = (mesh_t*)realloc(s->mesh, sizeof(mesh_t) * (s->nmesh + 1));
+    mesh_t* M = &s->mesh[s->nmesh];
+    memset(M, 0, sizeof(*M));
+    M->ntri = T; M->nvert = nv;
+    M->tri = (float*)dupmem(tri, sizeof(float) * 12 * (size_t)T);
+    M->fn = (float*)dupmem(fn, sizeof(float) * 12 * (size_t)T);
+    M->fuv = (float*)dupmem(fuv, sizeof(float) * 6 * (size_t)T);
+    M->idx = (int32_t*)dupmem(idx, sizeof(int32_t) * 3 * (size_t)T);
+    M->vert = (float*)dupmem(vert, sizeof(float) * 3 * (size_t)nv);
+    M->facen = (float*)dupmem(facen, sizeof(float) * 3 * (size_t)T);
+    M->tex[0] = a; M->tex[1] = n; M->tex[2] = m; M->tex[3] = e;
+    return s->nmesh++;
+}
+int orc_add_instance(orc_scene* s, int32_t mesh, const float* T16) {
+    if (mesh < 0 || mesh >= s->nmesh) return -1;
+    s->inst = (inst_t*)realloc(s->inst, sizeof(inst_t) * (s->ninst + 1));
+    inst_t* I = &s->inst[s->ninst];
+    memset(I, 0, sizeof(*I));
+    memcpy(I->T, T16, sizeof(float) * 16);
+    I->mesh = mesh;
+    return s->ninst++;
+}
+void orc_set_lights(orc_scene* s, const float* pp, const float* pc, const float* dp, const float* dc,
+                    const float* sp, const float* sc, const float* sr) {
+    memcpy(s->ppos, pp, 48); memcpy(s->pcol, pc, 48);
+    memcpy(s->dpos, dp, 12); memcpy(s->dcol, dc, 12);
+    memcpy(s->spos, sp, 12); memcpy(s->scol, sc, 12); memcpy(s->srot, sr, 12);
+}
+void orc_set_sky(orc_scene* s, int32_t w, int32_t h, const float* rgb) {
+    free(s->sky); s->sky = NULL; s->skyw = s->skyh = 0;
+    if (w > 0 && h > 0 && rgb) { s->sky = (float*)dupmem(rgb, sizeof(float) * 3 * (size_t)w * h); s->skyw = w; s->skyh = h; }
+}
+void orc_set_camera(orc_scene* s, const float* p, const float* tl, const float* tr, const float* bl) {
+    memcpy(s->cam, p, 12); memcpy(s->cam + 3, tl, 12); memcpy(s->cam + 6, tr, 12); memcpy(s->cam + 9, bl, 12);
+}
+void orc_set_backend(orc_scene* s, const orc_backend* b) {
+    if (b) { s->backend = *b; s->has_backend = 1; } else s->has_backend = 0;
+}
+
+/* Camera::Camera basis, Core/Camera.cpp:29-36 (tmpUp = (0,1,0), Camera.h:211) */
+void orc_camera_lookat(const float* p3, const float* t3, float aspect, float* tl, float* tr, float* bl) {
+    f3 camPos = v3(p3[0], p3[1], p3[2]), camTarget = v3(t3[0], t3[1], t3[2]);
+    f3 ahead = norm_t8(sub3(camTarget, camPos));
+    f3 right = norm_t8(cross3(ahead, v3(0, 1, 0)));
+    f3 up = norm_t8(cross3(right, ahead));
+    f3 a2 = muls(ahead, 2.0f), ar = smul(aspect, right);
+    f3 TL = add3(sub3(add3(camPos, a2), ar), up);
+    f3 TR = add3(add3(add3(camPos, a2), ar), up);
+    f3 BL = sub3(sub3(add3(camPos, a2), ar), up);
+    tl[0] = TL.x; tl[1] = TL.y; tl[2] = TL.z;
+    tr[0] = TR.x; tr[1] = TR.y; tr[2] = TR.z;
+    bl[0] = BL.x; bl[1] = BL.y; bl[2] = BL.z;
+}
+
+/* ------------------------------------------------------------------ built-in BVH (binary, binned SAH)
+ * A restatement of tinybvh's BVH::Build (binned SAH over centroid bins, Core/tiny_bvh.h:1840-1960)
+ * used only to accelerate the oracle; the hit rule above makes the result BVH-independent. */
+typedef struct { float bmin[3], bmax[3]; int cnt; } bin_t;
+static inline float area_of(const float* mn, const float* mx) {
+    float ex = mx[0] - mn[0], ey = mx[1] - mn[1], ez = mx[2] - mn[2];
+    if (ex < 0 || ey < 0 || ez < 0) return 0;
+    return ex * ey + ey * ez + ez * ex;
+}
+static inline void grow(float* mn, float* mx, const float* p) {
+    for (int k = 0; k < 3; k++) { if (p[k] < mn[k]) mn[k] = p[k]; if (p[k] > mx[k]) mx[k] = p[k]; }
+}
+static void build_mesh_bvh(mesh_t* M) {
+    const int T = M->ntri;
+    float* cen = (float*)malloc(sizeof(float) * 3 * (size_t)T);
+    float* tb = (float*)malloc(sizeof(float) * 6 * (size_t)T);
+    M->prim = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)T);
+    M->mt = (float*)malloc(sizeof(float) * 9 * (size_t)T);
+    for (int i = 0; i < T; i++) {
+        const float* a = M->tri + 12 * (size_t)i;
+        float* mn = tb + 6 * (size_t)i; float* mx = mn + 3;
+        for (int k = 0; k < 3; k++) { mn[k] = a[k]; mx[k] = a[k]; }
+        grow(mn, mx, a + 4); grow(mn, mx, a + 8);
+        for (int k = 0; k < 3; k++) cen[3 * (size_t)i + k] = (mn[k] + mx[k]) * 0.5f;
+        M->prim[i] = (uint32_t)i;
+        /* e1 = v1 - v0, e2 = v2 - v0 as in BVH8_CPU::ConvertFrom, tiny_bvh.h:4614-4616 */
+        float* q = M->mt + 9 * (size_t)i;
+        q[0] = a[0]; q[1] = a[1]; q[2] = a[2];
+        q[3] = a[4] - a[0]; q[4] = a[5] - a[1]; q[5] = a[6] - a[2];
+        q[6] = a[8] - a[0]; q[7] = a[9] - a[1]; q[8] = a[10] - a[2];
+    }
+    int cap = 2 * T + 1;
+    M->nodes = (bnode_t*)malloc(sizeof(bnode_t) * (size_t)cap);
+    int nn = 1;
+    int stack[128], sp = 0;
+    bnode_t* root = &M->nodes[0];
+    root->left_first = 0; root->count = T;
+    stack[sp++] = 0;
+    enum { NB = 16 };
+    while (sp) {
+        int ni = stack[--sp];
+        bnode_t* N = &M->nodes[ni];
+        float mn[3] = {1e30f, 1e30f, 1e30f}, mx[3] = {-1e30f, -1e30f, -1e30f};
+        float cmn[3] = {1e30f, 1e30f, 1e30f}, cmx[3] = {-1e30f, -1e30f, -1e30f};
+        for (int i = 0; i < N->count; i++) {
+            uint32_t p = M->prim[N->left_first + i];
+            grow(mn, mx, tb + 6 * (size_t)p); grow(mn, mx, tb + 6 * (size_t)p + 3);
+            grow(cmn, cmx, cen + 3 * (size_t)p);
+        }
+        /* conservative inflation (see file header) */
+        for (int k = 0; k < 3; k++) {
+            float ext = fabsf(mn[k]) > fabsf(mx[k]) ? fabsf(mn[k]) : fabsf(mx[k]);
+            float pad = ext * 1e-6f + 1e-7f;
+            N->bmin[k] = mn[k] - pad; N->bmax[k] = mx[k] + pad;
+        }
+        if (N->count <= 4) continue;
+        float best = 1e30f; int bax = -1, bsplit = 0;
+        for (int ax = 0; ax < 3; ax++) {
+            float lo = cmn[ax], hi = cmx[ax];
+            if (!(hi > lo)) continue;
+            bin_t bins[NB];
+            for (int b = 0; b < NB; b++) { bins[b].cnt = 0; for (int k = 0; k < 3; k++) { bins[b].bmin[k] = 1e30f; bins[b].bmax[k] = -1e30f; } }
+            float sc = NB / (hi - lo);
+            for (int i = 0; i < N->count; i++) {
+                uint32_t p = M->prim[N->left_first + i];
+                int b = (int)((cen[3 * (size_t)p + ax] - lo) * sc); if (b >= NB) b = NB - 1; if (b < 0) b = 0;
+                bins[b].cnt++; grow(bins[b].bmin, bins[b].bmax, tb + 6 * (size_t)p); grow(bins[b].bmin, bins[b].bmax, tb + 6 * (size_t)p + 3);
+            }
+            float la[NB], ra[NB]; int lc[NB], rc[NB];
+            float amn[3] = {1e30f, 1e30f, 1e30f}, amx[3] = {-1e30f, -1e30f, -1e30f}; int c = 0;
+            for (int b = 0; b < NB - 1; b++) {
+                c += bins[b].cnt; if (bins[b].cnt) { grow(amn, amx, bins[b].bmin); grow(amn, amx, bins[b].bmax); }
+                la[b] = area_of(amn, amx); lc[b] = c;
+            }
+            float bmn[3] = {1e30f, 1e30f, 1e30f}, bmx[3] = {-1e30f, -1e30f, -1e30f}; c = 0;
+            for (int b = NB - 1; b > 0; b--) {
+                c += bins[b].cnt; if (bins[b].cnt) { grow(bmn, bmx, bins[b].bmin); grow(bmn, bmx, bins[b].bmax); }
+                ra[b - 1] = area_of(bmn, bmx); rc[b - 1] = c;
+            }
+            for (int b = 0; b < NB - 1; b++) {
+                if (!lc[b] || !rc[b]) continue;
+                float cost = la[b] * lc[b] + ra[b] * rc[b];
+                if (cost < best) { best = cost; bax = ax; bsplit = b; }
+            }
+        }
+        float leafcost = area_of(mn, mx) * N->count;
+        if (bax < 0 || (best >= leafcost && N->count <= 16)) {
+            if (bax < 0 && N->count > 16) { bax = -2; } else continue;
+        }
+        int lcount;
+        if (bax == -2) { lcount = N->count / 2; } /* all centroids equal: median split */
+        else {
+            float lo = cmn[bax], sc = NB / (cmx[bax] - lo);
+            int i = N->left_first, j = N->left_first + N->count - 1;
+            while (i <= j) {
+                uint32_t p = M->prim[i];
+                int b = (int)((cen[3 * (size_t)p + bax] - lo) * sc); if (b >= NB) b = NB - 1; if (b < 0) b = 0;
+                if (b <= bsplit) i++; else { uint32_t t = M->prim[i]; M->prim[i] = M->prim[j]; M->prim[j] = t; j--; }
+            }
+            lcount = i - N->left_first;
+            if (lcount == 0 || lcount == N->count) lcount = N->count / 2;
+        }
+        int l = nn, r = nn + 1; nn += 2;
+        M->nodes[l].left_first = N->left_first; M->nodes[l].count = lcount;
+        M->nodes[r].left_first = N->left_first + lcount; M->nodes[r].count = N->count - lcount;
+        N->left_first = l; N->count = 0;
+        if (sp + 2 > 128) { fprintf(stderr, "oracle bvh: stack overflow\n"); exit(1); }
+        stack[sp++] = r; stack[sp++] = l;
+    }
+    M->nnodes = nn;
+    for (int k = 0; k < 3; k++) { M->bmin[k] = M->nodes[0].bmin[k]; M->bmax[k] = M->nodes[0].bmax[k]; }
+    free(cen); free(tb);
+}
+
+int orc_build(orc_scene* s) {
+    for (int i = 0; i < s->nmesh; i++) if (!s->mesh[i].nodes) build_mesh_bvh(&s->mesh[i]);
+    for (int i = 0; i < s->ninst; i++) {
+        inst_t* I = &s->inst[i];
+        mesa_inverse(I->T, I->inv);
+        /* Scene::GetGeometryNormal/GetShadingNormal: matrix.Inverted().Transposed(), Scene.cpp:51-55 */
+        for (int r = 0; r < 4; r++) for (int c = 0; c < 4; c++) I->nrm[4 * r + c] = I->inv[4 * c + r];
+        /* world AABB of the 8 corners (BLASInstance::Update, tiny_bvh.h:7868-7880), inflated */
+        const mesh_t* M = &s->mesh[I->mesh];
+        float mn[3] = {1e30f, 1e30f, 1e30f}, mx[3] = {-1e30f, -1e30f, -1e30f};
+        for (int j = 0; j < 8; j++) {
+            f3 p = v3(j & 1 ? M->bmax[0] : M->bmin[0], j & 2 ? M->bmax[1] : M->bmin[1], j & 4 ? M->bmax[2] : M->bmin[2]);
+            f3 t = xform_point(p, I->T);
+            float tt[3] = {t.x, t.y, t.z};
+            grow(mn, mx, tt);
+        }
+        for (int k = 0; k < 3; k++) {
+            float ext = fabsf(mn[k]) > fabsf(mx[k]) ? fabsf(mn[k]) : fabsf(mx[k]);
+            float pad = ext * 1e-5f + 1e-6f;
+            I->bmin[k] = mn[k] - pad; I->bmax[k] = mx[k] + pad;
+        }
+    }
+    s->built = 1;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ traversal */
+typedef struct { float t, u, v; uint32_t prim, inst; } hit_t;
+
+/* conservative slab test; returns entry distance or BVH_FAR */
+static inline float slab(const float* bmin, const float* bmax, f3 O, f3 rD, float tcur) {
+    float tx1 = (bmin[0] - O.x) * rD.x, tx2 = (bmax[0] - O.x) * rD.x;
+    float ty1 = (bmin[1] - O.y) * rD.y, ty2 = (bmax[1] - O.y) * rD.y;
+    float tz1 = (bmin[2] - O.z) * rD.z, tz2 = (bmax[2] - O.z) * rD.z;
+    float tmin = t8max(t8max(t8max(0.0f, t8min(tx1, tx2)), t8min(ty1, ty2)), t8min(tz1, tz2));
+    float tmax = t8min(t8min(t8max(tx1, tx2), t8max(ty1, ty2)), t8max(tz1, tz2));
+    tmin = tmin * 0.999999f; tmax = tmax * 1.000001f;
+    if (tmin <= tmax && tmin <= tcur) return tmin;
+    return BVH_FAR;
+}
+
+/* BVH8_CPU leaf Moeller-Trumbore, Core/tiny_bvh.h:6412-6430 (lane arithmetic, same op order) */
+static inline int mt_test(const float* q, f3 O, f3 D, float* t_out, float* u_out, float* v_out) {
+    const float v0x = q[0], v0y = q[1], v0z = q[2], e1x = q[3], e1y = q[4], e1z = q[5], e2x = q[6], e2y = q[7], e2z = q[8];
+    const float hx = D.y * e2z - D.z * e2y;
+    const float hy = D.z * e2x - D.x * e2z;
+    const float hz = D.x * e2y - D.y * e2x;
+    const float sx = O.x - v0x, sy = O.y - v0y, sz = O.z - v0z;
+    const float det = e1x * hx + e1y * hy + e1z * hz;
+    const int m1 = (det <= -0.000001f) || (det >= 0.000001f);
+    const float inv_det = 1.0f / det;
+    const float u = (sx * hx + sy * hy + sz * hz) * inv_det;
+    const float qx = sy * e1z - sz * e1y;
+    const float qy = sz * e1x - sx * e1z;
+    const float qz = sx * e1y - sy * e1x;
+    const float v = (D.x * qx + D.y * qy + D.z * qz) * inv_det;
+    const int m2 = (u >= 0.0f) && (u <= 1.0f);
+    const int m3 = (v >= 0.0f) && (u + v <= 1.0f);
+    const float t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
+    if (m1 && m2 && m3 && t > 0.0f) { *t_out = t; *u_out = u; *v_out = v; return 1; }
+    return 0;
+}
+
+static inline int better(float t, uint32_t inst, uint32_t prim, const hit_t* h) {
+    if (t < h->t) return 1;
+    if (t == h->t && (inst < h->inst || (inst == h->inst && prim < h->prim))) return 1;
+    return 0;
+}
+
+static void blas_closest(const mesh_t* M, uint32_t inst, f3 O, f3 D, f3 rD, hit_t* h) {
+    int stack[128], sp = 0; int ni = 0;
+    if (slab(M->nodes[0].bmin, M->nodes[0].bmax, O, rD, h->t) == BVH_FAR) return;
+    while (1) {
+        const bnode_t* N = &M->nodes[ni];
+        if (N->count) {
+            for (int i = 0; i < N->count; i++) {
+                uint32_t p = M->prim[N->left_first + i];
+                float t, u, v;
+                if (mt_test(M->mt + 9 * (size_t)p, O, D, &t, &u, &v) && better(t, inst, p, h)) {
+                    h->t = t; h->u = u; h->v = v; h->prim = p; h->inst = inst;
+                }
+            }
+            if (!sp) break;
+            ni = stack[--sp];
+            continue;
+        }
+        int c1 = N->left_first, c2 = c1 + 1;
+        float d1 = slab(M->nodes[c1].bmin, M->nodes[c1].bmax, O, rD, h->t);
+        float d2 = slab(M->nodes[c2].bmin, M->nodes[c2].bmax, O, rD, h->t);
+        if (d1 > d2) { float tf = d1; d1 = d2; d2 = tf; int ti = c1; c1 = c2; c2 = ti; }
+        if (d1 == BVH_FAR) { if (!sp) break; ni = stack[--sp]; }
+        else { ni = c1; if (d2 != BVH_FAR) stack[sp++] = c2; }
+    }
+}
+static int blas_anyhit(const mesh_t* M, f3 O, f3 D, f3 rD, float tmax) {
+    int stack[128], sp = 0; int ni = 0;
+    if (slab(M->nodes[0].bmin, M->nodes[0].bmax, O, rD, tmax) == BVH_FAR) return 0;
+    while (1) {
+        const bnode_t* N = &M->nodes[ni];
+        if (N->count) {
+            for (int i = 0; i < N->count; i++) {
+                uint32_t p = M->prim[N->left_first + i];
+                float t, u, v;
+                if (mt_test(M->mt + 9 * (size_t)p, O, D, &t, &u, &v) && t < tmax) return 1; /* tiny_bvh.h:6594 */
+            }
+            if (!sp) break;
+            ni = stack[--sp];
+            continue;
+        }
+        int c1 = N->left_first, c2 = c1 + 1;
+        float d1 = slab(M->nodes[c1].bmin, M->nodes[c1].bmax, O, rD, tmax);
+        float d2 = slab(M->nodes[c2].bmin, M->nodes[c2].bmax, O, rD, tmax);
+        if (d1 > d2) { float tf = d1; d1 = d2; d2 = tf; int ti = c1; c1 = c2; c2 = ti; }
+        if (d1 == BVH_FAR) { if (!sp) break; ni = stack[--sp]; }
+        else { ni = c1; if (d2 != BVH_FAR) stack[sp++] = c2; }
+    }
+    return 0;
+}
+
+/* optional ray log (single-threaded collection for the roofline visit counts) */
+typedef struct { float* buf; int64_t cap, n; } raylog_t;
+static raylog_t g_log_closest, g_log_any;
+static int g_logging = 0;
+static inline void log_ray(raylog_t* L, f3 O, f3 D, float tmax) {
+    if (L->n < L->cap) {
+        float* q = L->buf + 7 * L->n;
+        q[0] = O.x; q[1] = O.y; q[2] = O.z; q[3] = D.x; q[4] = D.y; q[5] = D.z; q[6] = tmax;
+    }
+    L->n++;
+}
+
+/* BVH::IntersectTLAS, Core/tiny_bvh.h:2500-2565: per instance, O/D by invTransform (D not renormalised) */
+static void scene_closest(const orc_scene* s, f3 O, f3 D, f3 rD, hit_t* h) {
+    if (g_logging) log_ray(&g_log_closest, O, D, h->t);
+    if (s->has_backend) {
+        float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z}, r[3] = {rD.x, rD.y, rD.z};
+        s->backend.closest(s->backend.user, o, d, r, &h->t, &h->u, &h->v, &h->prim, &h->inst);
+        return;
+    }
+    for (int i = 0; i < s->ninst; i++) {
+        const inst_t* I = &s->inst[i];
+        if (slab(I->bmin, I->bmax, O, rD, h->t) == BVH_FAR) continue;
+        f3 Oi = xform_point(O, I->inv), Di = xform_vector(D, I->inv);
+        f3 rDi = v3(safercp(Di.x), safercp(Di.y), safercp(Di.z));
+        blas_closest(&s->mesh[I->mesh], (uint32_t)i, Oi, Di, rDi, h);
+    }
+}
+/* BVH::IsOccludedTLAS, Core/tiny_bvh.h:2611-2673 */
+static int scene_anyhit(const orc_scene* s, f3 O, f3 D, f3 rD, float tmax) {
+    if (g_logging) log_ray(&g_log_any, O, D, tmax);
+    if (s->has_backend) {
+        float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z}, r[3] = {rD.x, rD.y, rD.z};
+        return s->backend.anyhit(s->backend.user, o, d, r, tmax);
+    }
+    for (int i = 0; i < s->ninst; i++) {
+        const inst_t* I = &s->inst[i];
+        if (slab(I->bmin, I->bmax, O, rD, tmax) == BVH_FAR) continue;
+        f3 Oi = xform_point(O, I->inv), Di = xform_vector(D, I->inv);
+        f3 rDi = v3(safercp(Di.x), safercp(Di.y), safercp(Di.z));
+        if (blas_anyhit(&s->mesh[I->mesh], Oi, Di, rDi, tmax)) return 1;
+    }
+    return 0;
+}
+
+/* tinybvh::Ray ctor, Core/tiny_bvh.h:578-584 */
+typedef struct { f3 O, D, rD; } ray_t;
+static inline ray_t make_ray(f3 origin, f3 direction) {
+    ray_t r; r.O = origin; r.D = norm_bvh(direction);
+    r.rD = v3(safercp(r.D.x), safercp(r.D.y), safercp(r.D.z));
+    return r;
+}
+
+/* ------------------------------------------------------------------ BRDF (Core/BRDF.cpp) */
+typedef struct { f3 base; float metal; f3 emis; float rough; } mat_t;   /* MaterialProperties, BRDF.h:165-176 */
+typedef struct {
+    f3 specF0, diffR; float rough, alpha, alpha2; f3 F;
+    float NdotL, NdotV, LdotH, NdotH, VdotH; int Vback, Lback;
+} brdf_t;                                                                  /* BrdfData, BRDF.h:178-208 */
+
+static inline float luminance(f3 c) { return dot3(c, v3(0.2126f, 0.7152f, 0.0722f)); }          /* :16-19 */
+static inline f3 specular_f0(f3 base, float metal) {                                                  /* :21-30 */
+    return lerp3(v3(MIN_DIELECTRICS_F0, MIN_DIELECTRICS_F0, MIN_DIELECTRICS_F0), base, metal);
+}
+static inline f3 diffuse_refl(f3 base, float metal) { return muls(base, 1.0f - metal); }              /* :32-35 */
+static inline float shadowed_f90(f3 F0) { const float t = (1.0f / MIN_DIELECTRICS_F0); return smin(1.0f, t * luminance(F0)); } /* :100-104 */
+static inline f3 fresnel(f3 f0, float f90, float NdotS) {                                            /* :84-87 */
+    float p = cr_pow(1.0f - NdotS, 5.0f);
+    return add3(f0, muls(v3(f90 - f0.x, f90 - f0.y, f90 - f0.z), p));
+}
+static inline float ggx_d(float a2, float NdotH) {                                                    /* :218-222 */
+    float b = ((a2 - 1.0f) * NdotH * NdotH + 1.0f);
+    return a2 / (PI_F * b * b);
+}
+static inline float g2_lagarde(float a2, float NdotL, float NdotV) {                                 /* :170-175 */
+    float a = NdotV * sqrtf(a2 + NdotL * (NdotL - a2 * NdotL));
+    float b = NdotL * sqrtf(a2 + NdotV * (NdotV - a2 * NdotV));
+    return 0.5f / (a + b);
+}
+static brdf_t prepare_brdf(f3 N, f3 L, f3 V, const mat_t* m) {                                       /* :398-437 */
+    brdf_t d;
+    f3 H = norm_t8(add3(L, V));
+    float NdotL = dot3(N, L), NdotV = dot3(N, V);
+    d.Vback = (NdotV <= 0.0f); d.Lback = (NdotL <= 0.0f);
+    d.NdotL = smin(smax(0.00001f, NdotL), 1.0f);
+    d.NdotV = smin(smax(0.00001f, NdotV), 1.0f);
+    d.LdotH = saturate_(dot3(L, H));
+    d.NdotH = saturate_(dot3(N, H));
+    d.VdotH = saturate_(dot3(V, H));
+    /* :422 srgbToLinear(material.baseColor) is computed and unused: no side effect, omitted */
+    d.specF0 = specular_f0(m->base, m->metal);
+    d.diffR = diffuse_refl(m->base, m->metal);
+    d.rough = m->rough; d.alpha = m->rough * m->rough; d.alpha2 = d.alpha * d.alpha;
+    d.F = fresnel(d.specF0, shadowed_f90(d.specF0), d.LdotH);
+    return d;
+}
+/* evalCombinedBRDF, BRDF.cpp:439-452 (evalMicrofacet :385-396 with G2_DIVIDED_BY_DENOMINATOR, evalLambertian :112-115) */
+static f3 eval_combined(f3 N, f3 L, f3 V, const mat_t* m) {
+    const brdf_t d = prepare_brdf(N, L, V, m);
+    if (d.Vback || d.Lback) return v3(0.0f, 0.0f, 0.0f);
+    float D = ggx_d(smax(0.00001f, d.alpha2), d.NdotH);
+    float G2 = g2_lagarde(d.alpha2, d.NdotL, d.NdotV);
+    f3 spec = muls(d.F, G2 * D * d.NdotL);
+    f3 diff = muls(d.diffR, ((1.0f / PI_F) * d.NdotL));
+    return add3(mul3(v3(1.0f - d.F.x, 1.0f - d.F.y, 1.0f - d.F.z), diff), spec);
+}
+/* getRotationToZAxis :43-49, rotatePoint :56-60 */
+static inline f4 rot_to_z(f3 in) {
+    if (in.z < -0.99999f) { f4 r = {1.0f, 0.0f, 0.0f, 0.0f}; return r; }
+    f4 q = {in.y, -in.x, 0.0f, 1.0f + in.z};
+    float inv = 1.0f / sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    f4 r = {q.x * inv, q.y * inv, q.z * inv, q.w * inv};
+    return r;
+}
+static inline f3 rotate_point(f4 q, f3 v) {
+    f3 qa = v3(q.x, q.y, q.z);
+    f3 t1 = smul(2.0f * dot3(qa, v), qa);
+    f3 t2 = smul(q.w * q.w - dot3(qa, qa), v);
+    f3 t3 = smul(2.0f * q.w, cross3(qa, v));
+    return add3(add3(t1, t2), t3);
+}
+/* sampleGGXVNDF (Heitz), BRDF.cpp:224-269 */
+static f3 sample_vndf(f3 Ve, float ax, float ay, f2 u) {
+    f3 Vh = norm_t8(v3(ax * Ve.x, ay * Ve.y, Ve.z));
+    float lensq = Vh.x * Vh.x + Vh.y * Vh.y;
+    f3 T1 = lensq > 0.0f ? muls(v3(-Vh.y, Vh.x, 0.0f), 1.0f / sqrtf(lensq)) : v3(1.0f, 0.0f, 0.0f);
+    f3 T2 = cross3(Vh, T1);
+    float r = sqrtf(u.x);
+    float phi = (2.0f * PI_F) * u.y;
+    float t1 = r * cr_cos(phi);
+    float t2 = r * cr_sin(phi);
+    float s = 0.5f * (1.0f + Vh.z);
+    t2 = lerpf(sqrtf(1.0f - t1 * t1), t2, s);
+    f3 Nh = add3(add3(smul(t1, T1), smul(t2, T2)), smul(sqrtf(smax(0.0f, 1.0f - t1 * t1 - t2 * t2)), Vh));
+    return norm_t8(v3(ax * Nh.x, ay * Nh.y, smax(0.0f, Nh.z)));
+}
+/* evalIndirectCombinedBRDF, BRDF.cpp:454-502 */
+static int eval_indirect(f2 u, f3 N, f3 V, const mat_t* m, int type, f3* dir, f3* weight) {
+    f4 q = rot_to_z(N);
+    f3 Vl = rotate_point(q, V);
+    const f3 Nl = v3(0.0f, 0.0f, 1.0f);
+    f3 rl = v3(0.0f, 0.0f, 0.0f);
+    if (type == 1) { /* DIFFUSE_TYPE */
+        float a = sqrtf(u.x), b = (2.0f * PI_F) * u.y;                      /* sampleHemisphere :62-76 */
+        rl = v3(a * cr_cos(b), a * cr_sin(b), sqrtf(1.0f - u.x));
+        const brdf_t d = prepare_brdf(Nl, rl, Vl, m);
+        *weight = muls(d.diffR, 1.0f);                                      /* lambertian() == 1 */
+        f3 Hs = sample_vndf(Vl, d.alpha, d.alpha, u);
+        float VdotH = smax(0.00001f, smin(1.0f, dot3(Vl, Hs)));
+        f3 F = fresnel(d.specF0, shadowed_f90(d.specF0), VdotH);
+        *weight = mul3(*weight, v3(1.0f - F.x, 1.0f - F.y, 1.0f - F.z));
+    } else if (type == 2) { /* SPECULAR_TYPE: sampleSpecularMicrofacet :351-383, weight taken by value */
+        const brdf_t d = prepare_brdf(Nl, v3(0.0f, 0.0f, 1.0f), Vl, m);
+        f3 H = (d.alpha == 0.0f) ? v3(0.0f, 0.0f, 1.0f) : sample_vndf(Vl, d.alpha, d.alpha, u);
+        rl = reflect3(neg3(Vl), H);
+    }
+    if (luminance(*weight) == 0.0f) return 0;
+    f4 qi = {-q.x, -q.y, -q.z, q.w};
+    *dir = norm_t8(rotate_point(qi, rl));
+    return 1;
+}
+/* getBrdfProbability, BRDF.cpp:504-526 */
+static float brdf_probability(const mat_t* m, f3 V, f3 N) {
+    float sF0 = luminance(specular_f0(m->base, m->metal));
+    float dR = luminance(diffuse_refl(m->base, m->metal));
+    float ff = smax(0.0f, dot3(V, N));
+    f3 F0v = v3(sF0, sF0, sF0);
+    float fr = saturate_(luminance(fresnel(F0v, shadowed_f90(F0v), ff)));
+    float adj = fr * 0.5f;
+    float spec = adj;
+    float diff = dR * (1.0f - adj) * 1.5f;
+    float p = spec / smax(0.0001f, (spec + diff));
+    return clampf_(p, 0.05f, 0.7f);
+}
+
+/* ------------------------------------------------------------------ scene queries (Core/Scene.cpp) */
+static inline f3 texel_color(uint32_t c) {                                 /* :225-229 */
+    const float s = 1.0f / 255.0f;
+    return v3((float)((c >> 16) & 0xFF) * s, (float)((c >> 8) & 0xFF) * s, (float)(c & 0xFF) * s);
+}
+static inline f3 texel_normal(uint32_t c) {                                /* :231-235 */
+    const float s = 2.0f / 255.0f;
+    return v3((float)((c >> 16) & 0xFF) * s - 1.0f, (float)((c >> 8) & 0xFF) * s - 1.0f, (float)(c & 0xFF) * s - 1.0f);
+}
+static inline float srgb1(float c) { return (c <= 0.04045f) ? (c / 12.92f) : cr_pow((c + 0.055f) / 1.055f, 2.4f); }
+static inline f3 srgb_to_linear(f3 c) { return v3(srgb1(c.x), srgb1(c.y), srgb1(c.z)); } /* :256-263 */
+
+static inline f2 hit_uv(const mesh_t* M, uint32_t prim, float u, float v, float w) {
+    const float* t = M->fuv + 6 * (size_t)prim;
+    /* v * uv2 + u * uv1 + w * uv0, Scene.cpp:75-77,156-158 */
+    f2 r;
+    r.x = v * t[4] + u * t[2] + w * t[0];
+    r.y = v * t[5] + u * t[3] + w * t[1];
+    return r;
+}
+static inline int texel_index(const tex_t* A, f2 uv) {                     /* :160-165 */
+    int iu = (int)(uv.x * (float)A->w) % A->w;
+    int iv = (int)(uv.y * (float)A->h) % A->h;
+    return iu + iv * A->w;
+}
+static inline f3 geometry_normal(const orc_scene* s, uint32_t inst, uint32_t prim) {   /* :47-58 */
+    const inst_t* I = &s->inst[inst]; const mesh_t* M = &s->mesh[I->mesh];
+    const float* f = M->facen + 3 * (size_t)prim;
+    return xform_vector(v3(f[0], f[1], f[2]), I->nrm);
+}
+static f3 shading_normal(const orc_scene* s, uint32_t inst, uint32_t prim, float u, float v, int normalmapped) { /* :60-138 */
+    const inst_t* I = &s->inst[inst]; const mesh_t* M = &s->mesh[I->mesh];
+    float w = 1.0f - u - v;
+    const float* n0 = M->fn + 12 * (size_t)prim; const float* n1 = n0 + 4; const float* n2 = n0 + 8;
+    if (M->tex[1] >= 0 && normalmapped) {
+        f2 uv = hit_uv(M, prim, u, v, w);
+        const tex_t* A = &s->tex[M->tex[0]];
+        f3 nc = texel_normal(s->tex[M->tex[1]].px[texel_index(A, uv)]);
+        int i0 = M->idx[3 * (size_t)prim], i1 = M->idx[3 * (size_t)prim + 1], i2 = M->idx[3 * (size_t)prim + 2];
+        f3 p0 = v3(M->vert[3 * (size_t)i0], M->vert[3 * (size_t)i0 + 1], M->vert[3 * (size_t)i0 + 2]);
+        f3 p1 = v3(M->vert[3 * (size_t)i1], M->vert[3 * (size_t)i1 + 1], M->vert[3 * (size_t)i1 + 2]);
+        f3 p2 = v3(M->vert[3 * (size_t)i2], M->vert[3 * (size_t)i2 + 1], M->vert[3 * (size_t)i2 + 2]);
+        f3 edge1 = sub3(p1, p0), edge2 = sub3(p2, p0);
+        const float* t = M->fuv + 6 * (size_t)prim;
+        f2 d1 = {t[2] - t[0], t[3] - t[1]}, d2 = {t[4] - t[0], t[5] - t[1]};
+        float det = d1.x * d2.y - d1.y * d2.x;
+        float invDet = 1.0f / det;
+        f3 T = norm_t8(smul(invDet, sub3(smul(d2.y, edge1), smul(d1.y, edge2))));
+        f3 B = norm_t8(smul(invDet, add3(smul(-d2.x, edge1), smul(d1.x, edge2))));
+        f3 fn = v3(n0[0] * w + n1[0] * u + n2[0] * v, n0[1] * w + n1[1] * u + n2[1] * v, n0[2] * w + n1[2] * u + n2[2] * v);
+        fn = xform_vector(fn, I->nrm);
+        f3 N = norm_t8(fn);
+        /* glm: colorNorm * transpose(TBN) = (dot(row_x), ...), type_mat3x3.inl:477-483 */
+        f3 r = v3(T.x * nc.x + B.x * nc.y + N.x * nc.z, T.y * nc.x + B.y * nc.y + N.y * nc.z, T.z * nc.x + B.z * nc.y + N.z * nc.z);
+        return norm_t8(r);
+    }
+    f3 it = v3(n0[0] * w + n1[0] * u + n2[0] * v, n0[1] * w + n1[1] * u + n2[1] * v, n0[2] * w + n1[2] * u + n2[2] * v);
+    return xform_vector(it, I->nrm); /* NOT normalised (Scene.cpp:134-136) */
+}
+static mat_t material(const orc_scene* s, uint32_t inst, uint32_t prim, float u, float v) { /* :140-218 */
+    const inst_t* I = &s->inst[inst]; const mesh_t* M = &s->mesh[I->mesh];
+    float w = 1.0f - u - v;
+    f2 uv = hit_uv(M, prim, u, v, w);
+    const tex_t* A = &s->tex[M->tex[0]];
+    int px = texel_index(A, uv);
+    mat_t m;
+    m.base = srgb_to_linear(texel_color(A->px[px]));
+    m.metal = 0.0f; m.rough = 0.0f; m.emis = v3(0.0f, 0.0f, 0.0f);
+    if (M->tex[2] >= 0) {
+        uint32_t c = s->tex[M->tex[2]].px[px];
+        const float sc = 1.0f / 255.0f;
+        m.rough = (float)((c >> 8) & 255) * sc;
+        m.metal = (float)(c & 255) * sc;
+    }
+    if (M->tex[3] >= 0) m.emis = texel_color(s->tex[M->tex[3]].px[px]);
+    return m;
+}
+
+/* Camera::SampleSkybox, Core/Camera.cpp:43-74 */
+static f3 sample_sky(const orc_scene* s, f3 D) {
+    if (!s->sky) return v3(0.0f, 0.0f, 0.0f);
+    float u = 0.5f + (cr_atan2(D.z, D.x) / (2.0f * PI_F));
+    float v = cr_acos(D.y) / PI_F;
+    float uTex = u * (float)s->skyw, vTex = v * (float)s->skyh;
+    uint32_t u0 = (uint32_t)floorf(uTex) % (uint32_t)s->skyw;
+    uint32_t v0 = (uint32_t)floorf(vTex) % (uint32_t)s->skyh;
+    uint32_t u1 = (u0 + 1) % (uint32_t)s->skyw, v1 = (v0 + 1) % (uint32_t)s->skyh;
+    float du = uTex - (float)u0, dv = vTex - (float)v0;
+    uint32_t W = (uint32_t)s->skyw;
+    uint32_t i00 = (u0 + v0 * W) * 3, i01 = (u1 + v0 * W) * 3, i10 = (u0 + v1 * W) * 3, i11 = (u1 + v1 * W) * 3;
+    const float* P = s->sky;
+    f3 c00 = v3(P[i00], P[i00 + 1], P[i00 + 2]), c01 = v3(P[i01], P[i01 + 1], P[i01 + 2]);
+    f3 c10 = v3(P[i10], P[i10 + 1], P[i10 + 2]), c11 = v3(P[i11], P[i11 + 1], P[i11 + 2]);
+    f3 a = add3(c00, smul(du, sub3(c01, c00)));
+    f3 b = add3(c10, smul(du, sub3(c11, c10)));
+    return add3(a, smul(dv, sub3(b, a)));
+}
+
+/* ------------------------------------------------------------------ Trace (Core/Renderer.cpp:150-406) */
+typedef struct { uint64_t seg, shadow; } cnt_t;
+
+static f3 trace(const orc_scene* s, const orc_params* P, ray_t r, uint32_t* seed, float* t_primary, cnt_t* cnt) {
+    f3 R[MAXDEPTH], TP[MAXDEPTH];
+    int nd = 0;
+    f3 Lend = v3(0.0f, 0.0f, 0.0f);
+    const uint32_t fl = P->flags;
+    for (int depth = 0;; depth++) {
+        if (depth >= P->bounces) { Lend = v3(0.0f, 0.0f, 0.0f); break; }                 /* :152 */
+        hit_t h; h.t = BVH_FAR; h.u = h.v = 0.0f; h.prim = 0; h.inst = 0;
+        scene_closest(s, r.O, r.D, r.rD, &h); cnt->seg++;                                /* :157 */
+        if (depth == 0 && t_primary) *t_primary = h.t;
+        if (h.t >= BVH_FAR) { Lend = (fl & ORC_SKYBOX) ? sample_sky(s, r.D) : v3(0.0f, 0.0f, 0.0f); break; } /* :159 */
+        f3 I = add3(r.O, smul(h.t, r.D));                                                /* tiny_bvh.h:586 */
+        f3 V = neg3(r.D);
+        f3 N = shading_normal(s, h.inst, h.prim, h.u, h.v, (fl & ORC_NORMALMAP) != 0);
+        mat_t m = material(s, h.inst, h.prim, h.u, h.v);
+        if (P->render_mode != ORC_MODE_BRDF) {                                            /* :170-194 */
+            switch (P->render_mode) {
+            case ORC_MODE_BASECOLOR: Lend = m.base; break;
+            case ORC_MODE_METAL: Lend = v3(m.metal, m.metal, m.metal); break;
+            case ORC_MODE_ROUGHNESS: Lend = v3(m.rough, m.rough, m.rough); break;
+            case ORC_MODE_EMISSIVE: Lend = m.emis; break;
+            case ORC_MODE_GEOMETRYNORMAL: {
+                f3 g = geometry_normal(s, h.inst, h.prim);
+                Lend = muls(v3(g.x + 1.0f, g.y + 1.0f, g.z + 1.0f), 0.5f); break;
+            }
+            case ORC_MODE_SHADINGNORMAL: Lend = muls(v3(N.x + 1.0f, N.y + 1.0f, N.z + 1.0f), 0.5f); break;
+            default: Lend = v3(0.0f, 0.0f, 0.0f); break;
+            }
+            break;
+        }
+        f3 result = add3(v3(0.0f, 0.0f, 0.0f), mul3(v3(1.0f, 1.0f, 1.0f), m.emis));   /* :196 */
+        if (fl & ORC_STOCHASTIC) {
+            const float pP = 0.3f, pD = 0.5f, pS = 0.2f;
+            float xi = rnd(seed);                                                          /* :210 */
+            int pick = (xi < pP) ? 0 : ((xi < pP + pD) ? 1 : 2);
+            if (pick == 0) {                                                               /* :216-269 */
+                float Lx[4], Ly[4], Lz[4], dsq[4]; f3 fc[4];
+                for (int i = 0; i < 4; i++) {
+                    Lx[i] = s->ppos[3 * i] - I.x; Ly[i] = s->ppos[3 * i + 1] - I.y; Lz[i] = s->ppos[3 * i + 2] - I.z;
+                    dsq[i] = (Lx[i] * Lx[i] + Ly[i] * Ly[i]) + Lz[i] * Lz[i];
+                    float dist = sqrtf(dsq[i]);
+                    float invD = 1.0f / dist;                  /* _mm_rcp_ps restated exactly */
+                    Lx[i] = Lx[i] * invD; Ly[i] = Ly[i] * invD; Lz[i] = Lz[i] * invD;
+                    float cosa = (N.x * Lx[i] + N.y * Ly[i]) + N.z * Lz[i];
+                    cosa = (cosa > 0.0f) ? cosa : 0.0f;         /* _mm_max_ps(cosa, 0) */
+                    float k = invD * cosa;
+                    fc[i] = v3(s->pcol[3 * i] * k, s->pcol[3 * i + 1] * k, s->pcol[3 * i + 2] * k);
+                }
+                f3 contrib = v3(0.0f, 0.0f, 0.0f);
+                for (int i = 0; i < 4; i++) {
+                    f3 L = v3(Lx[i], Ly[i], Lz[i]);
+                    ray_t sr = make_ray(add3(I, muls(L, EPSILON)), L);
+                    cnt->shadow++;
+                    if (!scene_anyhit(s, sr.O, sr.D, sr.rD, dsq[i] - EPSILON)) contrib = add3(contrib, fc[i]);
+                }
+                contrib = divs(contrib, pP);
+                int wl = (int)(rnd(seed) * 10) % 4;                                        /* :267 */
+                f3 add = v3(0.0f, 0.0f, 0.0f);
+                if (fl & ORC_LIGHTED) add = mul3(eval_combined(N, v3(Lx[wl], Ly[wl], Lz[wl]), V, &m), contrib);
+                result = add3(result, mul3(v3(1.0f, 1.0f, 1.0f), add));
+            } else {                                                                       /* :270-310 */
+                const float* lp = pick == 1 ? s->dpos : s->spos;
+                const float* lc = pick == 1 ? s->dcol : s->scol;
+                f3 L = sub3(v3(lp[0], lp[1], lp[2]), I);
+                float distance = length3(L);
+                L = divs(L, distance);
+                float cosa = smax(0.0f, dot3(N, L));
+                ray_t sr = make_ray(add3(I, muls(L, EPSILON)), L);
+                cnt->shadow++;
+                int occ = scene_anyhit(s, sr.O, sr.D, sr.rD, distance - EPSILON);
+                f3 contrib = v3(0.0f, 0.0f, 0.0f);
+                if (pick == 1) {
+                    if (!occ) contrib = muls(v3(lc[0], lc[1], lc[2]), cosa);
+                    contrib = divs(contrib, pD);
+                } else {
+                    float factor = dot3(L, v3(s->srot[0], s->srot[1], s->srot[2]));
+                    if (!occ) {
+                        if ((double)factor > 0.9) contrib = muls(muls(v3(lc[0], lc[1], lc[2]), (1 / (distance * distance))), cosa);
+                        else contrib = v3(0.0f, 0.0f, 0.0f);
+                    }
+                    contrib = divs(contrib, pS);
+                }
+                f3 add = v3(0.0f, 0.0f, 0.0f);
+                if (fl & ORC_LIGHTED) add = mul3(eval_combined(N, L, V, &m), contrib);
+                result = add3(result, mul3(v3(1.0f, 1.0f, 1.0f), add));
+            }
+        } else {                                                                           /* :312-326 */
+            f3 L = sub3(v3(s->dpos[0], s->dpos[1], s->dpos[2]), I);
+            float distance = length3(L);
+            L = divs(L, distance);
+            float cosa = smax(0.0f, dot3(N, L));
+            ray_t sr = make_ray(add3(I, muls(L, EPSILON)), L);
+            cnt->shadow++;
+            f3 contrib = v3(0.0f, 0.0f, 0.0f); /* uninitialised in the reference when occluded; restated as 0 */
+            if (!scene_anyhit(s, sr.O, sr.D, sr.rD, distance - EPSILON)) contrib = muls(v3(s->dcol[0], s->dcol[1], s->dcol[2]), cosa);
+            f3 add = v3(0.0f, 0.0f, 0.0f);
+            if (fl & ORC_LIGHTED) add = mul3(eval_combined(N, L, V, &m), contrib);
+            result = add3(result, mul3(v3(1.0f, 1.0f, 1.0f), add));
+        }
+        if (depth == P->bounces - 1) { Lend = result; break; }                             /* :329 */
+        /* :331-372 dielectric path: transmissivness is never set (Scene.cpp:193-197 is dead) */
+        int type = 1;
+        f3 thr = v3(1.0f, 1.0f, 1.0f);
+        if (m.metal == 1.0f && m.rough == 0.0f) type = 2;                                  /* :376 */
+        else {
+            float bp = brdf_probability(&m, V, N);                                         /* :380 */
+            if (rnd(seed) < bp) { type = 2; thr = divs(thr, bp); }
+            else { type = 1; thr = divs(thr, 1.0f - bp); }
+        }
+        f3 wgt = v3(1.0f, 1.0f, 1.0f), dir;
+        f2 u; u.x = rnd(seed); u.y = rnd(seed);                                            /* :396 */
+        if (!eval_indirect(u, N, V, &m, type, &dir, &wgt)) { Lend = result; break; }     /* :398 */
+        thr = mul3(thr, wgt);
+        R[nd] = result; TP[nd] = thr; nd++;
+        r = make_ray(add3(I, muls(dir, EPSILON)), dir);                                   /* :404 */
+    }
+    f3 L = Lend;
+    for (int k = nd - 1; k >= 0; k--) L = add3(R[k], mul3(L, TP[k]));                     /* result + Trace(..) * throughput */
+    return L;
+}
+
+/* Camera::GetPrimaryRay, Core/Camera.cpp:113-139 (non-Panini branch) */
+static ray_t primary_ray(const orc_scene* s, float x, float y, int W, int H) {
+    const float u = x * (1.0f / (float)W);
+    const float v = y * (1.0f / (float)H);
+    f3 camPos = v3(s->cam[0], s->cam[1], s->cam[2]);
+    f3 TL = v3(s->cam[3], s->cam[4], s->cam[5]), TR = v3(s->cam[6], s->cam[7], s->cam[8]), BL = v3(s->cam[9], s->cam[10], s->cam[11]);
+    f3 P = add3(add3(TL, smul(u, sub3(TR, TL))), smul(v, sub3(BL, TL)));
+    f3 dir = norm_t8(sub3(P, camPos));
+    return make_ray(camPos, dir);
+}
+
+/* one reference frame for one pixel: Core/Renderer.cpp:58-79 */
+static f3 pixel_frame(const orc_scene* s, const orc_params* P, int x, int y, uint32_t f, float* t1, cnt_t* cnt) {
+    const int W = P->width, H = P->height;
+    uint32_t p = (uint32_t)(y * W + x);
+    uint32_t seed = orc_init_seed(P->seed + p + (uint32_t)W * (uint32_t)H * f);
+    f3 res;
+    *t1 = BVH_FAR;
+    ray_t r1 = primary_ray(s, (float)x, (float)y, W, H);
+    if (P->flags & ORC_AA) {
+        float jx = rnd(&seed), jy = rnd(&seed);
+        ray_t r2 = primary_ray(s, (float)x + jx, (float)y + jy, W, H);
+        f3 s1 = trace(s, P, r1, &seed, t1, cnt);
+        f3 s2 = trace(s, P, r2, &seed, NULL, cnt);
+        res = smul(0.5f, add3(s1, s2));
+    } else {
+        res = trace(s, P, r1, &seed, t1, cnt);
+    }
+    if (P->flags & ORC_GAMMA) res = v3(sqrtf(res.x), sqrtf(res.y), sqrtf(res.z));
+    return res;
+}
+
+static int nframes_of(const orc_params* p) {
+    if (p->spp <= 0) return 0;
+    if (p->flags & ORC_AA) return p->spp / 2 > 0 ? p->spp / 2 : 1;
+    return p->spp;
+}
+
+int orc_render_frames(orc_scene* s, const orc_params* P, float* out, float* tprim, int32_t nthreads, orc_stats* st) {
+    if (!s->built) return -1;
+    if (P->bounces > MAXDEPTH || P->width <= 0 || P->height <= 0) return -2;
+    const int W = P->width, H = P->height, F = nframes_of(P);
+    uint64_t seg = 0, sh = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    for (int f = 0; f < F; f++) {
+#pragma omp parallel for schedule(dynamic) reduction(+:seg, sh)
+        for (int y = 0; y < H; y++) {
+            cnt_t c = {0, 0};
+            for (int x = 0; x < W; x++) {
+                float t1;
+                f3 v = pixel_frame(s, P, x, y, P->frame_index + (uint32_t)f, &t1, &c);
+                size_t o = (size_t)f * W * H + (size_t)y * W + x;
+                out[4 * o] = v.x; out[4 * o + 1] = v.y; out[4 * o + 2] = v.z; out[4 * o + 3] = 0.0f;
+                if (tprim) tprim[o] = t1;
+            }
+            seg += c.seg; sh += c.shadow;
+        }
+    }
+    if (st) { st->segments = seg; st->shadow_rays = sh; st->paths = (uint64_t)W * H * F * ((P->flags & ORC_AA) ? 2 : 1); }
+    return 0;
+}
+
+/* RGBF32_to_RGB8, template/precomp.h:310-315 (scalar path; the SSE path is dead: '_MSC_VER_') */
+static inline uint32_t pack1(float x) {
+    float m = smin(1.0f, x); /* std::min(1, NaN) == 1 */
+    return m > 0.0f ? (uint32_t)(255.0f * m) : 0u; /* negative inputs: UB in the reference, clamped to 0 */
+}
+uint32_t orc_pack_rgb8(const float* v) { return (pack1(v[0]) << 16) + (pack1(v[1]) << 8) + pack1(v[2]); }
+
+/* Core/Renderer.cpp:81-104,137 */
+int orc_render(orc_scene* s, const orc_params* P, float* acc, int32_t* nsamp, float* dist, float* avg, uint32_t* rgb8,
+               int32_t nthreads, orc_stats* st) {
+    const int W = P->width, H = P->height, F = nframes_of(P);
+    size_t np = (size_t)W * H;
+    float* fr = (float*)malloc(sizeof(float) * 4 * np * (F ? F : 1));
+    float* tp = (float*)malloc(sizeof(float) * np * (F ? F : 1));
+    int rc = orc_render_frames(s, P, fr, tp, nthreads, st);
+    if (rc) { free(fr); free(tp); return rc; }
+    for (size_t p = 0; p < np; p++) {
+        float a[4] = {0, 0, 0, 0};
+        for (int f = 0; f < F; f++) {
+            const float* v = fr + 4 * ((size_t)f * np + p);
+            float t1 = tp[(size_t)f * np + p];
+            float* A = acc + 4 * p;
+            if (P->flags & ORC_ACCUMULATE) {
+                if (fabsf(dist[p] - t1) < EPSILON) {
+                    nsamp[p]++;
+                    A[0] += v[0]; A[1] += v[1]; A[2] += v[2];
+                    float inv = 1.f / (float)nsamp[p];
+                    a[0] = A[0] * inv; a[1] = A[1] * inv; a[2] = A[2] * inv; a[3] = A[3] * inv;
+                } else {
+                    nsamp[p] = 1;
+                    A[0] = v[0]; A[1] = v[1]; A[2] = v[2]; A[3] = 0.0f;
+                    a[0] = A[0]; a[1] = A[1]; a[2] = A[2]; a[3] = A[3];
+                }
+                dist[p] = t1;
+            } else {
+                A[0] = v[0]; A[1] = v[1]; A[2] = v[2]; A[3] = 0.0f;
+                a[0] = A[0]; a[1] = A[1]; a[2] = A[2]; a[3] = A[3];
+            }
+        }
+        if (avg) { avg[4 * p] = a[0]; avg[4 * p + 1] = a[1]; avg[4 * p + 2] = a[2]; avg[4 * p + 3] = a[3]; }
+        if (rgb8) rgb8[p] = orc_pack_rgb8(a);
+    }
+    free(fr); free(tp);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ geometry-only queries */
+int orc_primary_hits(orc_scene* s, int32_t W, int32_t H, float* t, float* u, float* v, uint32_t* prim, uint32_t* inst,
+                     int32_t nthreads) {
+    if (!s->built) return -1;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel for schedule(dynamic)
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            ray_t r = primary_ray(s, (float)x, (float)y, W, H);
+            hit_t h; h.t = BVH_FAR; h.u = h.v = 0.0f; h.prim = 0; h.inst = 0;
+            scene_closest(s, r.O, r.D, r.rD, &h);
+            size_t o = (size_t)y * W + x;
+            t[o] = h.t; u[o] = h.u; v[o] = h.v; prim[o] = h.prim; inst[o] = h.inst;
+        }
+    return 0;
+}
+int orc_intersect(orc_scene* s, int32_t n, const float* O, const float* D, const float* tmax, float* t, float* u,
+                  float* v, uint32_t* prim, uint32_t* inst, int32_t nthreads) {
+    if (!s->built) return -1;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++) {
+        ray_t r = make_ray(v3(O[3 * i], O[3 * i + 1], O[3 * i + 2]), v3(D[3 * i], D[3 * i + 1], D[3 * i + 2]));
+        hit_t h; h.t = tmax ? tmax[i] : BVH_FAR; h.u = h.v = 0.0f; h.prim = 0; h.inst = 0;
+        scene_closest(s, r.O, r.D, r.rD, &h);
+        t[i] = h.t; u[i] = h.u; v[i] = h.v; prim[i] = h.prim; inst[i] = h.inst;
+    }
+    return 0;
+}
+int orc_occluded(orc_scene* s, int32_t n, const float* O, const float* D, const float* tmax, int32_t* occ,
+                 int32_t nthreads) {
+    if (!s->built) return -1;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++) {
+        ray_t r = make_ray(v3(O[3 * i], O[3 * i + 1], O[3 * i + 2]), v3(D[3 * i], D[3 * i + 1], D[3 * i + 2]));
+        occ[i] = scene_anyhit(s, r.O, r.D, r.rD, tmax[i]);
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ unit-test entry points */
+static inline mat_t mat_from8(const float* m8) {
+    mat_t m; m.base = v3(m8[0], m8[1], m8[2]); m.metal = m8[3]; m.emis = v3(m8[4], m8[5], m8[6]); m.rough = m8[7];
+    return m;
+}
+void orc_eval_combined_brdf(const float* N, const float* L, const float* V, const float* m8, float* o) {
+    mat_t m = mat_from8(m8);
+    f3 r = eval_combined(v3(N[0], N[1], N[2]), v3(L[0], L[1], L[2]), v3(V[0], V[1], V[2]), &m);
+    o[0] = r.x; o[1] = r.y; o[2] = r.z;
+}
+float orc_brdf_probability(const float* m8, const float* V, const float* N) {
+    mat_t m = mat_from8(m8);
+    return brdf_probability(&m, v3(V[0], V[1], V[2]), v3(N[0], N[1], N[2]));
+}
+int orc_eval_indirect(const float* u2, const float* N, const float* V, const float* m8, int32_t type, float* dir,
+                      float* w) {
+    mat_t m = mat_from8(m8);
+    f2 u = {u2[0], u2[1]};
+    f3 d = v3(0, 0, 0), wt = v3(w[0], w[1], w[2]);
+    int ok = eval_indirect(u, v3(N[0], N[1], N[2]), v3(V[0], V[1], V[2]), &m, type, &d, &wt);
+    dir[0] = d.x; dir[1] = d.y; dir[2] = d.z; w[0] = wt.x; w[1] = wt.y; w[2] = wt.z;
+    return ok;
+}
+void orc_sample_sky(orc_scene* s, const float* D, float* o) {
+    f3 r = sample_sky(s, v3(D[0], D[1], D[2]));
+    o[0] = r.x; o[1] = r.y; o[2] = r.z;
+}
+
+/* Collect the rays Trace fires for every 'stride'-th pixel of the workload (single thread).
+ * Rays are (O, D, tmax) with D as traced (normalised).  Returns 0; counts may exceed capacities. */
+int orc_collect_rays(orc_scene* s, const orc_params* P, int32_t stride, float* closest, int64_t cap_closest,
+                     float* anyhit, int64_t cap_any, int64_t* n_closest, int64_t* n_any) {
+    if (!s->built || stride <= 0) return -1;
+    g_log_closest.buf = closest; g_log_closest.cap = cap_closest; g_log_closest.n = 0;
+    g_log_any.buf = anyhit; g_log_any.cap = cap_any; g_log_any.n = 0;
+    g_logging = 1;
+    const int W = P->width, H = P->height, F = nframes_of(P);
+    cnt_t c = {0, 0};
+    for (int f = 0; f < F; f++)
+        for (int64_t p = 0; p < (int64_t)W * H; p += stride) {
+            float t1;
+            pixel_frame(s, P, (int)(p % W), (int)(p / W), P->frame_index + (uint32_t)f, &t1, &c);
+        }
+    g_logging = 0;
+    *n_closest = g_log_closest.n; *n_any = g_log_any.n;
+    return 0;
+}

@@ -1,0 +1,51 @@
+// bvh_build.h -- host-side BLAS builder producing the device layout.
+//
+// Replaces the reference's BVH8_CPU::BuildHQ chain (Core/tiny_bvh.h:4511-4519 -> BVH::BuildHQ
+// :1968-2284 -> MBVH<8>::ConvertFrom :3706-3781 -> BVH8_CPU::ConvertFrom :4548-4680), which emits a
+// CPU AVX2 layout.  Here: binned-SAH binary BVH over triangle bounds, collapsed to 4-wide nodes whose
+// child bounds are stored SoA (one 128-byte node = one aligned 128-B line: 6 float4 child-bound
+// vectors + int4 child refs) and a separate 48-byte-per-triangle Moeller-Trumbore record
+// {v0,prim | e1 | e2} in leaf order, mirroring BVHTri4Leaf's precomputed edges (tiny_bvh.h:4614-4619).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace prt {
+
+// child ref encoding
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kEmptyChild = 0xFFFFFFFFu;
+inline uint32_t make_leaf(uint32_t first_tri, uint32_t count) { return kLeafBit | (first_tri << 2) | (count - 1); }
+
+struct alignas(16) Node4 {
+  float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
+  uint32_t child[4];
+  uint32_t pad[4];
+};
+static_assert(sizeof(Node4) == 128, "Node4 must be one 128-byte line");
+
+struct alignas(16) TriMT {
+  float v0[3];
+  uint32_t prim;   // mesh-local primitive index (tinybvh Intersection::prim)
+  float e1[3];
+  float pad1;
+  float e2[3];
+  float pad2;
+};
+static_assert(sizeof(TriMT) == 48, "TriMT must be 48 bytes");
+
+struct BuiltBlas {
+  std::vector<Node4> nodes;   // node 0 = root (always interior)
+  std::vector<TriMT> tris;    // leaf order
+  float bmin[3], bmax[3];     // root bounds (exact, not inflated)
+  int depth = 0;
+  int64_t leaves = 0;
+};
+
+// triangles: fat float4 x 3T (Model::triangles).  max_leaf <= 4.
+BuiltBlas build_blas(const float* triangles, int32_t tri_count, int max_leaf = 4);
+
+// Same inflation rule the traversal relies on (see bvh_build.cpp).
+void inflate_box(float* lo, float* hi);
+
+}  // namespace prt

@@ -1,0 +1,668 @@
+// prt_api.cpp -- C-ABI implementation (include/prt.h): device residency of the scene, BLAS build,
+// kernel orchestration.  One host thread per context; all device work on one HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/prt.h"
+#include "bvh_build.h"
+#include "prt_launch.h"
+
+using namespace prt;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess) return fail(PRT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  // (re)allocate to at least n bytes; contents are not preserved
+  hipError_t ensure(size_t n) {
+    if (n <= bytes && p) return hipSuccess;
+    release();
+    hipError_t e = hipMalloc(&p, n ? n : 16);
+    if (e == hipSuccess) bytes = n ? n : 16;
+    return e;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+hipError_t upload(DevBuf& b, const void* src, size_t n) {
+  hipError_t e = b.ensure(n);
+  if (e != hipSuccess) return e;
+  if (n) return hipMemcpy(b.p, src, n, hipMemcpyHostToDevice);
+  return hipSuccess;
+}
+
+// MESA 4x4 inverse (template/tmpl8math.h:701-746 == BLASInstance::InvertTransform, tiny_bvh.h:7883-7905)
+void mesa_inverse(const float* c, float* out) {
+  float inv[16];
+  inv[0] = c[5] * c[10] * c[15] - c[5] * c[11] * c[14] - c[9] * c[6] * c[15] + c[9] * c[7] * c[14] + c[13] * c[6] * c[11] - c[13] * c[7] * c[10];
+  inv[1] = -c[1] * c[10] * c[15] + c[1] * c[11] * c[14] + c[9] * c[2] * c[15] - c[9] * c[3] * c[14] - c[13] * c[2] * c[11] + c[13] * c[3] * c[10];
+  inv[2] = c[1] * c[6] * c[15] - c[1] * c[7] * c[14] - c[5] * c[2] * c[15] + c[5] * c[3] * c[14] + c[13] * c[2] * c[7] - c[13] * c[3] * c[6];
+  inv[3] = -c[1] * c[6] * c[11] + c[1] * c[7] * c[10] + c[5] * c[2] * c[11] - c[5] * c[3] * c[10] - c[9] * c[2] * c[7] + c[9] * c[3] * c[6];
+  inv[4] = -c[4] * c[10] * c[15] + c[4] * c[11] * c[14] + c[8] * c[6] * c[15] - c[8] * c[7] * c[14] - c[12] * c[6] * c[11] + c[12] * c[7] * c[10];
+  inv[5] = c[0] * c[10] * c[15] - c[0] * c[11] * c[14] - c[8] * c[2] * c[15] + c[8] * c[3] * c[14] + c[12] * c[2] * c[11] - c[12] * c[3] * c[10];
+  inv[6] = -c[0] * c[6] * c[15] + c[0] * c[7] * c[14] + c[4] * c[2] * c[15] - c[4] * c[3] * c[14] - c[12] * c[2] * c[7] + c[12] * c[3] * c[6];
+  inv[7] = c[0] * c[6] * c[11] - c[0] * c[7] * c[10] - c[4] * c[2] * c[11] + c[4] * c[3] * c[10] + c[8] * c[2] * c[7] - c[8] * c[3] * c[6];
+  inv[8] = c[4] * c[9] * c[15] - c[4] * c[11] * c[13] - c[8] * c[5] * c[15] + c[8] * c[7] * c[13] + c[12] * c[5] * c[11] - c[12] * c[7] * c[9];
+  inv[9] = -c[0] * c[9] * c[15] + c[0] * c[11] * c[13] + c[8] * c[1] * c[15] - c[8] * c[3] * c[13] - c[12] * c[1] * c[11] + c[12] * c[3] * c[9];
+  inv[10] = c[0] * c[5] * c[15] - c[0] * c[7] * c[13] - c[4] * c[1] * c[15] + c[4] * c[3] * c[13] + c[12] * c[1] * c[7] - c[12] * c[3] * c[5];
+  inv[11] = -c[0] * c[5] * c[11] + c[0] * c[7] * c[9] + c[4] * c[1] * c[11] - c[4] * c[3] * c[9] - c[8] * c[1] * c[7] + c[8] * c[3] * c[5];
+  inv[12] = -c[4] * c[9] * c[14] + c[4] * c[10] * c[13] + c[8] * c[5] * c[14] - c[8] * c[6] * c[13] - c[12] * c[5] * c[10] + c[12] * c[6] * c[9];
+  inv[13] = c[0] * c[9] * c[14] - c[0] * c[10] * c[13] - c[8] * c[1] * c[14] + c[8] * c[2] * c[13] + c[12] * c[1] * c[10] - c[12] * c[2] * c[9];
+  inv[14] = -c[0] * c[5] * c[14] + c[0] * c[6] * c[13] + c[4] * c[1] * c[14] - c[4] * c[2] * c[13] - c[12] * c[1] * c[6] + c[12] * c[2] * c[5];
+  inv[15] = c[0] * c[5] * c[10] - c[0] * c[6] * c[9] - c[4] * c[1] * c[10] + c[4] * c[2] * c[9] + c[8] * c[1] * c[6] - c[8] * c[2] * c[5];
+  const float det = c[0] * inv[0] + c[1] * inv[4] + c[2] * inv[8] + c[3] * inv[12];
+  if (det != 0) {
+    const float invdet = 1.0f / det;
+    for (int i = 0; i < 16; i++) out[i] = inv[i] * invdet;
+  } else {
+    for (int i = 0; i < 16; i++) out[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+  }
+}
+
+struct MeshHost {
+  float bmin[3], bmax[3];
+  int depth;
+  int64_t nodes, leaves;
+  int32_t tris;
+};
+
+}  // namespace
+
+struct prt_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  // textures
+  std::vector<TexDev> tex_host;
+  DevBuf texels, tex;
+  // meshes
+  std::vector<MeshDev> mesh_host;
+  std::vector<MeshHost> mesh_info;
+  DevBuf nodes, tris, fnrm, fuv, vidx, vert, facen, mesh;
+  int max_depth = 0;
+  // instances
+  std::vector<float> inst_xf;
+  std::vector<uint32_t> inst_mesh;
+  DevBuf inst;
+  bool inst_dirty = true;
+  // sky, lights, camera
+  DevBuf sky;
+  int32_t skyw = 0, skyh = 0;
+  prt_lights lights{};
+  bool have_lights = false;
+  prt_camera cam{};
+  bool have_camera = false;
+  // accumulation state (Core/Renderer.h:61-63) and scratch
+  DevBuf acc, nsamp, dist;
+  int32_t accW = 0, accH = 0;
+  DevBuf frames, avg, rgb8, counters, hits;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+};
+
+namespace {
+
+int stack_for(const prt_ctx* c) {
+  const int need = 3 * std::max(0, c->max_depth - 1) + 1;
+  if (need <= 24) return 24;
+  if (need <= 48) return 48;
+  return -1;
+}
+
+int ensure_instances(prt_ctx* c) {
+  if (!c->inst_dirty) return PRT_OK;
+  const int32_t n = (int32_t)c->inst_mesh.size();
+  std::vector<InstDev> host(n);
+  for (int32_t i = 0; i < n; i++) {
+    InstDev& I = host[i];
+    std::memset(&I, 0, sizeof(I));
+    const float* T = &c->inst_xf[16 * (size_t)i];
+    const uint32_t m = c->inst_mesh[i];
+    if (m >= c->mesh_host.size()) return fail(PRT_ERR_INVALID_ARGUMENT, "instance references a missing mesh");
+    mesa_inverse(T, I.inv);
+    for (int r = 0; r < 4; r++)
+      for (int k = 0; k < 4; k++) I.nrm[4 * r + k] = I.inv[4 * k + r];  // Inverted().Transposed()
+    I.mesh = m;
+    const MeshHost& mh = c->mesh_info[m];
+    float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
+    for (int j = 0; j < 8; j++) {  // BLASInstance::Update: world AABB of the 8 root corners
+      const float p[3] = {j & 1 ? mh.bmax[0] : mh.bmin[0], j & 2 ? mh.bmax[1] : mh.bmin[1],
+                          j & 4 ? mh.bmax[2] : mh.bmin[2]};
+      float t[3];
+      for (int r = 0; r < 3; r++) t[r] = T[4 * r] * p[0] + T[4 * r + 1] * p[1] + T[4 * r + 2] * p[2] + T[4 * r + 3];
+      const float w = T[12] * p[0] + T[13] * p[1] + T[14] * p[2] + T[15];
+      if (w != 1)
+        for (int r = 0; r < 3; r++) t[r] = t[r] * (1.f / w);
+      for (int r = 0; r < 3; r++) { lo[r] = std::min(lo[r], t[r]); hi[r] = std::max(hi[r], t[r]); }
+    }
+    for (int r = 0; r < 3; r++) {  // generous inflation: the TLAS test must be conservative
+      const float ext = std::max(std::fabs(lo[r]), std::fabs(hi[r]));
+      const float pad = ext * 1e-5f + 1e-6f;
+      I.bmin[r] = lo[r] - pad;
+      I.bmax[r] = hi[r] + pad;
+    }
+  }
+  HIP_TRY(upload(c->inst, host.data(), sizeof(InstDev) * host.size()));
+  c->inst_dirty = false;
+  return PRT_OK;
+}
+
+int scene_ready(prt_ctx* c, SceneDev& S) {
+  if (c->mesh_host.empty()) return fail(PRT_ERR_NOT_READY, "no meshes: call prt_set_meshes");
+  if (c->inst_mesh.empty()) return fail(PRT_ERR_NOT_READY, "no instances: call prt_set_instances");
+  if ((int)c->inst_mesh.size() > kMaxInstances) return fail(PRT_ERR_UNSUPPORTED, "more than 64 instances");
+  int rc = ensure_instances(c);
+  if (rc) return rc;
+  std::memset(&S, 0, sizeof(S));
+  S.nodes = c->nodes.as<Node4>();
+  S.tris = c->tris.as<TriMT>();
+  S.fnrm = c->fnrm.as<float4>();
+  S.fuv = c->fuv.as<float2>();
+  S.vidx = c->vidx.as<int32_t>();
+  S.vert = c->vert.as<float>();
+  S.facen = c->facen.as<float>();
+  S.texels = c->texels.as<uint32_t>();
+  S.tex = c->tex.as<TexDev>();
+  S.inst = c->inst.as<InstDev>();
+  S.mesh = c->mesh.as<MeshDev>();
+  S.sky = (c->skyw > 0) ? c->sky.as<float>() : nullptr;
+  S.ninst = (int32_t)c->inst_mesh.size();
+  S.skyw = c->skyw;
+  S.skyh = c->skyh;
+  const prt_lights& L = c->lights;
+  std::memcpy(S.ppos, L.point_pos, sizeof(S.ppos));
+  std::memcpy(S.pcol, L.point_color, sizeof(S.pcol));
+  std::memcpy(S.dpos, L.dir_pos, 12);
+  std::memcpy(S.dcol, L.dir_color, 12);
+  std::memcpy(S.spos, L.spot_pos, 12);
+  std::memcpy(S.scol, L.spot_color, 12);
+  std::memcpy(S.srot, L.spot_rot, 12);
+  std::memcpy(S.cam, c->cam.pos, 12);
+  std::memcpy(S.cam + 3, c->cam.top_left, 12);
+  std::memcpy(S.cam + 6, c->cam.top_right, 12);
+  std::memcpy(S.cam + 9, c->cam.bottom_left, 12);
+  return PRT_OK;
+}
+
+int check_params(const prt_render_params* p) {
+  if (!p) return fail(PRT_ERR_INVALID_ARGUMENT, "params is NULL");
+  if (p->width <= 0 || p->height <= 0 || p->width > 16384 || p->height > 16384)
+    return fail(PRT_ERR_INVALID_ARGUMENT, "bad resolution");
+  if (p->spp < 0) return fail(PRT_ERR_INVALID_ARGUMENT, "spp < 0");
+  if ((p->flags & PRT_FLAG_AA) && (p->spp % 2) != 0)
+    return fail(PRT_ERR_INVALID_ARGUMENT, "with PRT_FLAG_AA spp must be even (2 paths per reference frame)");
+  if (p->bounces < 0 || p->bounces > 16) return fail(PRT_ERR_INVALID_ARGUMENT, "bounces must be in [0,16]");
+  if (p->render_mode < 0 || p->render_mode > 6) return fail(PRT_ERR_INVALID_ARGUMENT, "bad render_mode");
+  return PRT_OK;
+}
+
+int32_t frames_of(const prt_render_params* p) {
+  return (p->flags & PRT_FLAG_AA) ? p->spp / 2 : p->spp;
+}
+
+int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
+  if (c->accW == W && c->accH == H && c->acc.p) return PRT_OK;
+  const size_t n = (size_t)W * H;
+  HIP_TRY(c->acc.ensure(n * 16));
+  HIP_TRY(c->nsamp.ensure(n * 4));
+  HIP_TRY(c->dist.ensure(n * 4));
+  HIP_TRY(hipMemsetAsync(c->acc.p, 0, n * 16, c->stream));
+  HIP_TRY(hipMemsetAsync(c->nsamp.p, 0, n * 4, c->stream));
+  std::vector<float> d(n, -1.0f);  // Core/Renderer.h:62 (distances = -1 -> first frame resets)
+  HIP_TRY(hipMemcpyAsync(c->dist.p, d.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->accW = W;
+  c->accH = H;
+  return PRT_OK;
+}
+
+// the shared trace + accumulate sequence for prt_render / prt_render_tiles
+int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4* avg_dev, uint32_t* rgb8_dev,
+               float4* tiles_dev, prt_stats* stats) {
+  SceneDev S;
+  int rc = scene_ready(c, S);
+  if (rc) return rc;
+  if (!c->have_camera) return fail(PRT_ERR_NOT_READY, "no camera: call prt_set_camera");
+  if (!c->have_lights) return fail(PRT_ERR_NOT_READY, "no lights: call prt_set_lights");
+  const int stack = stack_for(c);
+  if (stack < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
+  rc = ensure_state(c, p->width, p->height);
+  if (rc) return rc;
+  const int32_t F = frames_of(p);
+  HIP_TRY(c->frames.ensure(sizeof(float4) * (size_t)M.items * (size_t)std::max(F, 1)));
+  HIP_TRY(c->counters.ensure(sizeof(Counters)));
+  HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
+  TraceArgs A;
+  A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
+  A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F;
+  LaunchCfg L{c->stream, stack};
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  HIP_TRY(launch_trace_frames(L, S, A, M, c->frames.as<float4>(), c->counters.as<Counters>()));
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  HIP_TRY(launch_accumulate(L, M, F, p->flags, c->frames.as<float4>(), c->acc.as<float4>(), c->nsamp.as<int32_t>(),
+                            c->dist.as<float>(), avg_dev, rgb8_dev, tiles_dev));
+  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  if (stats) {
+    Counters h{};
+    HIP_TRY(hipMemcpyAsync(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    float ms = 0, ms_trace = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[2]));
+    HIP_TRY(hipEventElapsedTime(&ms_trace, c->ev[0], c->ev[1]));
+    stats->segments = h.segments;
+    stats->shadow_rays = h.shadow;
+    stats->paths = (uint64_t)M.items * (uint64_t)F * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
+    stats->ms = ms;
+    stats->ms_trace = ms_trace;
+  }
+  return PRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int prt_abi_version(void) { return PRT_ABI_VERSION; }
+const char* prt_last_error(void) { return g_err.c_str(); }
+
+int prt_device_count(int32_t* count) {
+  if (!count) return fail(PRT_ERR_INVALID_ARGUMENT, "count is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  *count = (e == hipSuccess) ? n : 0;
+  return PRT_OK;
+}
+
+int prt_create(const prt_device_desc* desc, prt_ctx** out) {
+  if (!out) return fail(PRT_ERR_INVALID_ARGUMENT, "out is NULL");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(PRT_ERR_NO_DEVICE, "no HIP device visible");
+  const int dev = desc ? desc->device : 0;
+  if (dev < 0 || dev >= n) return fail(PRT_ERR_INVALID_ARGUMENT, "device ordinal out of range");
+  HIP_TRY(hipSetDevice(dev));
+  prt_ctx* c = new prt_ctx();
+  c->device = dev;
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return fail(PRT_ERR_HIP, "hipStreamCreate failed");
+  }
+  c->stream = c->own_stream;
+  for (auto& e : c->ev) {
+    if (hipEventCreate(&e) != hipSuccess) {
+      delete c;
+      return fail(PRT_ERR_HIP, "hipEventCreate failed");
+    }
+  }
+  *out = c;
+  return PRT_OK;
+}
+
+int prt_destroy(prt_ctx* c) {
+  if (!c) return PRT_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&c->texels, &c->tex, &c->nodes, &c->tris, &c->fnrm, &c->fuv, &c->vidx, &c->vert, &c->facen,
+                    &c->mesh, &c->inst, &c->sky, &c->acc, &c->nsamp, &c->dist, &c->frames, &c->avg, &c->rgb8,
+                    &c->counters, &c->hits})
+    b->release();
+  for (auto e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return PRT_OK;
+}
+
+int prt_set_stream(prt_ctx* c, void* s) {
+  if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+  return PRT_OK;
+}
+
+int prt_set_textures(prt_ctx* c, const prt_texture* t, int32_t n) {
+  if (!c || (n > 0 && !t) || n < 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad textures");
+  std::vector<uint32_t> all;
+  std::vector<TexDev> host(n);
+  for (int32_t i = 0; i < n; i++) {
+    if (t[i].width <= 0 || t[i].height <= 0 || !t[i].pixels) return fail(PRT_ERR_INVALID_ARGUMENT, "bad texture");
+    host[i].offset = (uint32_t)all.size();
+    host[i].w = t[i].width;
+    host[i].h = t[i].height;
+    host[i].pad = 0;
+    all.insert(all.end(), t[i].pixels, t[i].pixels + (size_t)t[i].width * t[i].height);
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(upload(c->texels, all.data(), all.size() * 4));
+  HIP_TRY(upload(c->tex, host.data(), host.size() * sizeof(TexDev)));
+  c->tex_host = host;
+  return PRT_OK;
+}
+
+int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
+  if (!c || !m || n <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad meshes");
+  std::vector<Node4> nodes;
+  std::vector<TriMT> tris;
+  std::vector<float4> fnrm;
+  std::vector<float2> fuv;
+  std::vector<int32_t> vidx;
+  std::vector<float> vert, facen;
+  std::vector<MeshDev> mh(n);
+  std::vector<MeshHost> info(n);
+  int maxd = 0;
+  for (int32_t i = 0; i < n; i++) {
+    const prt_mesh& M = m[i];
+    if (M.tri_count <= 0 || M.vertex_count <= 0 || !M.triangles || !M.fixed_normals || !M.fixed_uvs || !M.indices ||
+        !M.vertices || !M.face_normals)
+      return fail(PRT_ERR_INVALID_ARGUMENT, "mesh " + std::to_string(i) + ": missing arrays");
+    const int32_t ntex = (int32_t)c->tex_host.size();
+    if (M.albedo_tex < 0 || M.albedo_tex >= ntex)
+      return fail(PRT_ERR_INVALID_ARGUMENT, "mesh " + std::to_string(i) + ": albedo texture required (Scene.cpp:160)");
+    const int32_t tx[4] = {M.albedo_tex, M.normal_tex, M.metalness_tex, M.emission_tex};
+    const TexDev& A = c->tex_host[M.albedo_tex];
+    for (int k = 1; k < 4; k++) {
+      if (tx[k] >= ntex) return fail(PRT_ERR_INVALID_ARGUMENT, "texture id out of range");
+      // every map is indexed with the albedo dimensions (Scene.cpp:79-85,160-165)
+      if (tx[k] >= 0 && (c->tex_host[tx[k]].w * (int64_t)c->tex_host[tx[k]].h < (int64_t)A.w * A.h ||
+                         c->tex_host[tx[k]].w < A.w))
+        return fail(PRT_ERR_INVALID_ARGUMENT, "texture smaller than the albedo map (indexed with albedo dims)");
+    }
+    for (int64_t k = 0; k < 3 * (int64_t)M.tri_count; k++)
+      if (M.indices[k] < 0 || M.indices[k] >= M.vertex_count) return fail(PRT_ERR_INVALID_ARGUMENT, "index out of range");
+    BuiltBlas b = build_blas(M.triangles, M.tri_count, 4);
+    const uint32_t node_base = (uint32_t)nodes.size(), tri_base = (uint32_t)tris.size();
+    if ((uint64_t)tri_base + b.tris.size() >= (1u << 29)) return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
+    for (Node4& nd : b.nodes) {
+      for (int k = 0; k < 4; k++) {
+        uint32_t& ch = nd.child[k];
+        if (ch == kEmptyChild) continue;
+        if (ch & kLeafBit) ch = make_leaf(((ch >> 2) & 0x1FFFFFFFu) + tri_base, (ch & 3u) + 1u);
+        else ch += node_base;
+      }
+    }
+    nodes.insert(nodes.end(), b.nodes.begin(), b.nodes.end());
+    tris.insert(tris.end(), b.tris.begin(), b.tris.end());
+    mh[i].root = node_base;
+    mh[i].prim_base = (uint32_t)(fuv.size() / 3);
+    mh[i].vert_base = (uint32_t)(vert.size() / 3);
+    mh[i].tri_count = (uint32_t)M.tri_count;
+    for (int k = 0; k < 4; k++) mh[i].tex[k] = tx[k];
+    const size_t T = (size_t)M.tri_count;
+    for (size_t k = 0; k < 3 * T; k++) {
+      fnrm.push_back(make_float4(M.fixed_normals[4 * k], M.fixed_normals[4 * k + 1], M.fixed_normals[4 * k + 2],
+                                 M.fixed_normals[4 * k + 3]));
+      fuv.push_back(make_float2(M.fixed_uvs[2 * k], M.fixed_uvs[2 * k + 1]));
+      vidx.push_back(M.indices[k]);
+    }
+    vert.insert(vert.end(), M.vertices, M.vertices + 3 * (size_t)M.vertex_count);
+    facen.insert(facen.end(), M.face_normals, M.face_normals + 3 * T);
+    for (int k = 0; k < 3; k++) { info[i].bmin[k] = b.bmin[k]; info[i].bmax[k] = b.bmax[k]; }
+    info[i].depth = b.depth;
+    info[i].nodes = (int64_t)b.nodes.size();
+    info[i].leaves = b.leaves;
+    info[i].tris = M.tri_count;
+    maxd = std::max(maxd, b.depth);
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(upload(c->nodes, nodes.data(), nodes.size() * sizeof(Node4)));
+  HIP_TRY(upload(c->tris, tris.data(), tris.size() * sizeof(TriMT)));
+  HIP_TRY(upload(c->fnrm, fnrm.data(), fnrm.size() * sizeof(float4)));
+  HIP_TRY(upload(c->fuv, fuv.data(), fuv.size() * sizeof(float2)));
+  HIP_TRY(upload(c->vidx, vidx.data(), vidx.size() * 4));
+  HIP_TRY(upload(c->vert, vert.data(), vert.size() * 4));
+  HIP_TRY(upload(c->facen, facen.data(), facen.size() * 4));
+  HIP_TRY(upload(c->mesh, mh.data(), mh.size() * sizeof(MeshDev)));
+  c->mesh_host = mh;
+  c->mesh_info = info;
+  c->max_depth = maxd;
+  c->inst_dirty = true;
+  return PRT_OK;
+}
+
+int prt_set_instances(prt_ctx* c, const float* xf, const uint32_t* mi, int32_t n) {
+  if (!c || !xf || !mi || n <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad instances");
+  if (n > kMaxInstances) return fail(PRT_ERR_UNSUPPORTED, "more than 64 instances");
+  c->inst_xf.assign(xf, xf + 16 * (size_t)n);
+  c->inst_mesh.assign(mi, mi + n);
+  c->inst_dirty = true;
+  HIP_TRY(hipSetDevice(c->device));
+  if (!c->mesh_host.empty()) return ensure_instances(c);
+  return PRT_OK;
+}
+
+int prt_set_lights(prt_ctx* c, const prt_lights* l) {
+  if (!c || !l) return fail(PRT_ERR_INVALID_ARGUMENT, "bad lights");
+  c->lights = *l;
+  c->have_lights = true;
+  return PRT_OK;
+}
+
+int prt_set_sky(prt_ctx* c, const float* rgb, int32_t w, int32_t h) {
+  if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  HIP_TRY(hipSetDevice(c->device));
+  if (!rgb || w <= 0 || h <= 0) {
+    c->skyw = c->skyh = 0;
+    return PRT_OK;
+  }
+  HIP_TRY(upload(c->sky, rgb, (size_t)w * h * 3 * 4));
+  c->skyw = w;
+  c->skyh = h;
+  return PRT_OK;
+}
+
+int prt_set_camera(prt_ctx* c, const prt_camera* cam) {
+  if (!c || !cam) return fail(PRT_ERR_INVALID_ARGUMENT, "bad camera");
+  c->cam = *cam;
+  c->have_camera = true;
+  return PRT_OK;
+}
+
+// Camera::Camera (Core/Camera.cpp:29-36): tmpl8 normalize = v * (1/sqrtf(dot))
+int prt_camera_look_at(const float pos[3], const float target[3], float aspect, prt_camera* o) {
+  if (!pos || !target || !o) return fail(PRT_ERR_INVALID_ARGUMENT, "bad look_at arguments");
+  auto nrm = [](V3 v) { return prt::normalize(v); };
+  const V3 P = v3(pos[0], pos[1], pos[2]), Tg = v3(target[0], target[1], target[2]);
+  const V3 ahead = nrm(Tg - P);
+  const V3 right = nrm(cross(ahead, v3(0, 1, 0)));
+  const V3 up = nrm(cross(right, ahead));
+  const V3 a2 = ahead * 2.0f, ar = aspect * right;
+  const V3 TL = P + a2 - ar + up, TR = P + a2 + ar + up, BL = P + a2 - ar - up;
+  for (int k = 0; k < 3; k++) o->pos[k] = pos[k];
+  o->top_left[0] = TL.x; o->top_left[1] = TL.y; o->top_left[2] = TL.z;
+  o->top_right[0] = TR.x; o->top_right[1] = TR.y; o->top_right[2] = TR.z;
+  o->bottom_left[0] = BL.x; o->bottom_left[1] = BL.y; o->bottom_left[2] = BL.z;
+  return PRT_OK;
+}
+
+int prt_reset_accumulation(prt_ctx* c, int32_t full) {
+  if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  if (!c->acc.p) return PRT_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t n = (size_t)c->accW * c->accH;
+  HIP_TRY(hipMemsetAsync(c->acc.p, 0, n * 16, c->stream));
+  if (full) {
+    HIP_TRY(hipMemsetAsync(c->nsamp.p, 0, n * 4, c->stream));
+    std::vector<float> d(n, -1.0f);
+    HIP_TRY(hipMemcpyAsync(c->dist.p, d.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return PRT_OK;
+}
+
+int prt_render(prt_ctx* c, const prt_render_params* p, float* avg_rgba, uint32_t* rgb8, uint32_t out_flags,
+               prt_stats* stats) {
+  if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  int rc = check_params(p);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  const TileMap M = make_tilemap(p->width, p->height, 8, 0, 1);
+  const size_t np = (size_t)p->width * p->height;
+  float4* avg_dev = nullptr;
+  uint32_t* rgb_dev = nullptr;
+  const bool dev_out = (out_flags & PRT_OUT_DEVICE) != 0;
+  if (avg_rgba) {
+    if (dev_out) avg_dev = reinterpret_cast<float4*>(avg_rgba);
+    else { HIP_TRY(c->avg.ensure(np * 16)); avg_dev = c->avg.as<float4>(); }
+  }
+  if (rgb8) {
+    if (dev_out) rgb_dev = rgb8;
+    else { HIP_TRY(c->rgb8.ensure(np * 4)); rgb_dev = c->rgb8.as<uint32_t>(); }
+  }
+  rc = run_render(c, p, M, avg_dev, rgb_dev, nullptr, stats);
+  if (rc) return rc;
+  if (!dev_out) {
+    if (avg_rgba) HIP_TRY(hipMemcpyAsync(avg_rgba, avg_dev, np * 16, hipMemcpyDeviceToHost, c->stream));
+    if (rgb8) HIP_TRY(hipMemcpyAsync(rgb8, rgb_dev, np * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  return PRT_OK;
+}
+
+int prt_tile_buffer_pixels(int32_t W, int32_t H, int32_t ts, int32_t world, int64_t* px) {
+  if (!px || W <= 0 || H <= 0 || ts <= 0 || (ts % 8) != 0 || world <= 0)
+    return fail(PRT_ERR_INVALID_ARGUMENT, "bad tile geometry (tile_size must be a positive multiple of 8)");
+  const TileMap M0 = make_tilemap(W, H, ts, 0, world);  // rank 0 owns the most tiles
+  *px = (int64_t)M0.items;
+  return PRT_OK;
+}
+
+int prt_render_tiles(prt_ctx* c, const prt_render_params* p, int32_t ts, int32_t rank, int32_t world,
+                     float* tiles_dev, prt_stats* stats) {
+  if (!c || !tiles_dev) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/tiles is NULL");
+  int rc = check_params(p);
+  if (rc) return rc;
+  if (ts <= 0 || (ts % 8) != 0 || world <= 0 || rank < 0 || rank >= world)
+    return fail(PRT_ERR_INVALID_ARGUMENT, "bad tile geometry");
+  HIP_TRY(hipSetDevice(c->device));
+  const TileMap M = make_tilemap(p->width, p->height, ts, rank, world);
+  const TileMap M0 = make_tilemap(p->width, p->height, ts, 0, world);
+  if (M0.items > M.items)  // pad the tail of the (equal-size) per-rank buffer
+    HIP_TRY(hipMemsetAsync(reinterpret_cast<float4*>(tiles_dev) + M.items, 0, sizeof(float4) * (M0.items - M.items),
+                           c->stream));
+  return run_render(c, p, M, nullptr, nullptr, reinterpret_cast<float4*>(tiles_dev), stats);
+}
+
+int prt_untile(prt_ctx* c, const float* gathered, int32_t W, int32_t H, int32_t ts, int32_t world, float* avg_dev,
+               uint32_t* rgb8_dev) {
+  if (!c || !gathered) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/gathered is NULL");
+  int64_t per = 0;
+  int rc = prt_tile_buffer_pixels(W, H, ts, world, &per);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  LaunchCfg L{c->stream, 24};
+  HIP_TRY(launch_untile(L, W, H, ts, world, (uint32_t)per, reinterpret_cast<const float4*>(gathered),
+                        reinterpret_cast<float4*>(avg_dev), rgb8_dev));
+  return PRT_OK;
+}
+
+int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t out_flags, prt_stats* stats) {
+  if (!c || !hits || W <= 0 || H <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  SceneDev S;
+  int rc = scene_ready(c, S);
+  if (rc) return rc;
+  if (!c->have_camera) return fail(PRT_ERR_NOT_READY, "no camera");
+  const int stack = stack_for(c);
+  if (stack < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
+  const TileMap M = make_tilemap(W, H, 8, 0, 1);
+  const size_t n = (size_t)W * H;
+  HitOut* out = reinterpret_cast<HitOut*>(hits);
+  const bool dev_out = (out_flags & PRT_OUT_DEVICE) != 0;
+  if (!dev_out) { HIP_TRY(c->hits.ensure(n * sizeof(HitOut))); out = c->hits.as<HitOut>(); }
+  HIP_TRY(c->counters.ensure(sizeof(Counters)));
+  HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
+  LaunchCfg L{c->stream, stack};
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  HIP_TRY(launch_primary_hits(L, S, M, out, c->counters.as<Counters>()));
+  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  if (!dev_out) HIP_TRY(hipMemcpyAsync(hits, out, n * sizeof(HitOut), hipMemcpyDeviceToHost, c->stream));
+  if (stats || !dev_out) HIP_TRY(hipStreamSynchronize(c->stream));
+  if (stats) {
+    Counters h{};
+    HIP_TRY(hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[2]));
+    stats->segments = h.segments;
+    stats->shadow_rays = 0;
+    stats->paths = n;
+    stats->ms = ms;
+    stats->ms_trace = ms;
+  }
+  return PRT_OK;
+}
+
+static int ray_query(prt_ctx* c, int32_t n, const float* O, const float* D, const float* tmax, void* out, bool any) {
+  if (!c || n < 0 || (n > 0 && (!O || !D || !out)) || (any && n > 0 && !tmax))
+    return fail(PRT_ERR_INVALID_ARGUMENT, "bad ray query arguments");
+  if (n == 0) return PRT_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  SceneDev S;
+  int rc = scene_ready(c, S);
+  if (rc) return rc;
+  const int stack = stack_for(c);
+  if (stack < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
+  DevBuf dO, dD, dT, dOut;
+  auto cleanup = [&]() { dO.release(); dD.release(); dT.release(); dOut.release(); };
+  const size_t outb = (size_t)n * (any ? 4 : sizeof(HitOut));
+  if (upload(dO, O, (size_t)n * 12) != hipSuccess || upload(dD, D, (size_t)n * 12) != hipSuccess ||
+      (tmax && upload(dT, tmax, (size_t)n * 4) != hipSuccess) || dOut.ensure(outb) != hipSuccess) {
+    cleanup();
+    return fail(PRT_ERR_OUT_OF_MEMORY, "ray buffers");
+  }
+  LaunchCfg L{c->stream, stack};
+  hipError_t e = any ? launch_occluded(L, S, n, dO.as<float>(), dD.as<float>(), dT.as<float>(), dOut.as<int32_t>())
+                     : launch_intersect(L, S, n, dO.as<float>(), dD.as<float>(), tmax ? dT.as<float>() : nullptr,
+                                        dOut.as<HitOut>());
+  if (e == hipSuccess) e = hipMemcpyAsync(out, dOut.p, outb, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  cleanup();
+  if (e != hipSuccess) return fail(PRT_ERR_HIP, std::string("ray query: ") + hipGetErrorString(e));
+  return PRT_OK;
+}
+
+int prt_intersect(prt_ctx* c, int32_t n, const float* O, const float* D, const float* tmax, prt_hit* hits) {
+  return ray_query(c, n, O, D, tmax, hits, false);
+}
+int prt_occluded(prt_ctx* c, int32_t n, const float* O, const float* D, const float* tmax, int32_t* occ) {
+  return ray_query(c, n, O, D, tmax, occ, true);
+}
+
+int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
+  if (!c || !info) return fail(PRT_ERR_INVALID_ARGUMENT, "bad arguments");
+  std::memset(info, 0, sizeof(*info));
+  for (const MeshHost& m : c->mesh_info) {
+    info->blas_nodes += m.nodes;
+    info->blas_leaves += m.leaves;
+    info->triangles += m.tris;
+  }
+  info->max_depth = c->max_depth;
+  info->device_bytes = (int64_t)(c->nodes.bytes + c->tris.bytes + c->fnrm.bytes + c->fuv.bytes + c->vidx.bytes +
+                                 c->vert.bytes + c->facen.bytes + c->texels.bytes + c->sky.bytes + c->inst.bytes);
+  return PRT_OK;
+}
+
+}  // extern "C"

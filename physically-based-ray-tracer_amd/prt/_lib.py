@@ -1,0 +1,124 @@
+"""ctypes binding of libprt.so (include/prt.h).  Loads the in-tree library and fails loudly when it is
+missing: there is no CPU fallback for the product path."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPATH = os.path.join(HERE, "libprt.so")
+
+PRT_OK = 0
+FLAG_AA, FLAG_ACCUMULATE, FLAG_GAMMA, FLAG_NORMALMAP, FLAG_SKYBOX, FLAG_LIGHTED, FLAG_STOCHASTIC = (1 << i for i in range(7))
+FLAGS_DEFAULT = 0x7F
+OUT_DEVICE = 1
+
+# Renderer::RENDER_STATES (Core/Renderer.h:37-46)
+MODE_BRDF, MODE_BASECOLOR, MODE_GEOMETRYNORMAL, MODE_SHADINGNORMAL, MODE_METAL, MODE_ROUGHNESS, MODE_EMISSIVE = range(7)
+
+# every symbol include/prt.h declares (tests check the library exports all of them)
+EXPORTS = [
+    "prt_abi_version", "prt_last_error", "prt_device_count", "prt_create", "prt_destroy", "prt_set_stream",
+    "prt_set_textures", "prt_set_meshes", "prt_set_instances", "prt_set_lights", "prt_set_sky", "prt_set_camera",
+    "prt_camera_look_at", "prt_render", "prt_reset_accumulation", "prt_tile_buffer_pixels", "prt_render_tiles",
+    "prt_untile", "prt_trace_primary", "prt_intersect", "prt_occluded", "prt_get_scene_info",
+]
+
+
+class PrtError(RuntimeError):
+    pass
+
+
+class DeviceDesc(C.Structure):
+    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32)]
+
+
+class Texture(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("pixels", C.c_void_p)]
+
+
+class Mesh(C.Structure):
+    _fields_ = [("tri_count", C.c_int32), ("vertex_count", C.c_int32), ("triangles", C.c_void_p),
+                ("fixed_normals", C.c_void_p), ("fixed_uvs", C.c_void_p), ("indices", C.c_void_p),
+                ("vertices", C.c_void_p), ("face_normals", C.c_void_p), ("albedo_tex", C.c_int32),
+                ("normal_tex", C.c_int32), ("metalness_tex", C.c_int32), ("emission_tex", C.c_int32)]
+
+
+class Lights(C.Structure):
+    _fields_ = [("point_pos", (C.c_float * 3) * 4), ("point_color", (C.c_float * 3) * 4),
+                ("dir_pos", C.c_float * 3), ("dir_color", C.c_float * 3),
+                ("spot_pos", C.c_float * 3), ("spot_color", C.c_float * 3), ("spot_rot", C.c_float * 3)]
+
+
+class CameraDesc(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("top_left", C.c_float * 3), ("top_right", C.c_float * 3),
+                ("bottom_left", C.c_float * 3)]
+
+
+class RenderParams(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32), ("bounces", C.c_int32),
+                ("flags", C.c_uint32), ("render_mode", C.c_int32), ("frame_index", C.c_uint32), ("seed", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("segments", C.c_uint64), ("shadow_rays", C.c_uint64), ("paths", C.c_uint64), ("ms", C.c_double),
+                ("ms_trace", C.c_double)]
+
+
+class Hit(C.Structure):
+    _fields_ = [("t", C.c_float), ("u", C.c_float), ("v", C.c_float), ("prim", C.c_uint32), ("inst", C.c_uint32)]
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [("blas_nodes", C.c_int64), ("blas_leaves", C.c_int64), ("device_bytes", C.c_int64),
+                ("max_depth", C.c_int32), ("triangles", C.c_int32)]
+
+
+_lib = None
+
+
+def load():
+    """Load libprt.so (built in-tree by __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIBPATH):
+        raise PrtError(f"{LIBPATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+    L = C.CDLL(LIBPATH)
+    vp, i32, u32 = C.c_void_p, C.c_int32, C.c_uint32
+    sig = {
+        "prt_abi_version": ([], C.c_int),
+        "prt_last_error": ([], C.c_char_p),
+        "prt_device_count": ([C.POINTER(i32)], C.c_int),
+        "prt_create": ([C.POINTER(DeviceDesc), C.POINTER(vp)], C.c_int),
+        "prt_destroy": ([vp], C.c_int),
+        "prt_set_stream": ([vp, vp], C.c_int),
+        "prt_set_textures": ([vp, C.POINTER(Texture), i32], C.c_int),
+        "prt_set_meshes": ([vp, C.POINTER(Mesh), i32], C.c_int),
+        "prt_set_instances": ([vp, vp, vp, i32], C.c_int),
+        "prt_set_lights": ([vp, C.POINTER(Lights)], C.c_int),
+        "prt_set_sky": ([vp, vp, i32, i32], C.c_int),
+        "prt_set_camera": ([vp, C.POINTER(CameraDesc)], C.c_int),
+        "prt_camera_look_at": ([vp, vp, C.c_float, C.POINTER(CameraDesc)], C.c_int),
+        "prt_render": ([vp, C.POINTER(RenderParams), vp, vp, u32, C.POINTER(Stats)], C.c_int),
+        "prt_reset_accumulation": ([vp, i32], C.c_int),
+        "prt_tile_buffer_pixels": ([i32, i32, i32, i32, C.POINTER(C.c_int64)], C.c_int),
+        "prt_render_tiles": ([vp, C.POINTER(RenderParams), i32, i32, i32, vp, C.POINTER(Stats)], C.c_int),
+        "prt_untile": ([vp, vp, i32, i32, i32, i32, vp, vp], C.c_int),
+        "prt_trace_primary": ([vp, i32, i32, vp, u32, C.POINTER(Stats)], C.c_int),
+        "prt_intersect": ([vp, i32, vp, vp, vp, vp], C.c_int),
+        "prt_occluded": ([vp, i32, vp, vp, vp, vp], C.c_int),
+        "prt_get_scene_info": ([vp, C.POINTER(SceneInfo)], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != PRT_OK:
+        msg = load().prt_last_error()
+        raise PrtError(f"prt error {rc}: {msg.decode() if msg else ''}")

@@ -1,0 +1,59 @@
+"""CPU tests of the product boundary: libprt.so loads, exports every symbol include/prt.h declares, and
+fails loudly (no CPU fallback) when no GPU is visible."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import prt
+from prt import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_header_symbols_exported():
+    L = prt.load()
+    hdr = open(os.path.join(ROOT, "include", "prt.h")).read()
+    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(prt_\w+)\s*\(", hdr, re.M))
+    assert declared == set(_lib.EXPORTS)
+    for name in declared:
+        assert hasattr(L, name), name
+    assert L.prt_abi_version() == 1
+
+
+def test_camera_basis_matches_oracle(oracle_mod):
+    # Camera::Camera (Core/Camera.cpp:29-36) restated twice (product host code, oracle) must agree bitwise
+    sd = prt.scenes.config_c3()
+    cam = prt.Camera(sd.cam_pos, sd.cam_target, np.float32(1920) / np.float32(1080))
+    osc = oracle_mod.OracleScene(prt.scenes.config_small(4, 4))
+    osc.sd = sd
+    pos, tl, tr, bl = osc.camera_basis(1920, 1080)
+    assert np.array_equal(cam.topLeft, tl) and np.array_equal(cam.topRight, tr) and np.array_equal(cam.bottomLeft, bl)
+
+
+def test_no_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(prt.PrtError):
+        prt.Context(0)
+    L = prt.load()
+    h = C.c_void_p()
+    rc = L.prt_create(C.byref(_lib.DeviceDesc(0, 0)), C.byref(h))
+    assert rc == -2 and b"no HIP device" in L.prt_last_error()
+
+
+def test_tile_geometry():
+    L = prt.load()
+    n = C.c_int64()
+    assert L.prt_tile_buffer_pixels(1920, 1080, 32, 8, C.byref(n)) == 0
+    tiles = 60 * 34
+    assert n.value == ((tiles + 7) // 8) * 1024
+    assert L.prt_tile_buffer_pixels(1920, 1080, 12, 8, C.byref(n)) != 0  # tile size must be a multiple of 8
+
+
+def test_scene_generators_counts():
+    assert prt.scenes.config_c2().tri_count == 10_000
+    assert prt.scenes.heightfield(250, 200).tri_count == 100_000
