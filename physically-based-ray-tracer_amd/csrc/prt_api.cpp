@@ -128,7 +128,7 @@ struct prt_ctx {
 namespace {
 
 int stack_for(const prt_ctx* c) {
-  const int need = 3 * std::max(0, c->max_depth - 1) + 1;
+  const int need = 3 * c->max_depth;  // <= 3 pushes per interior level on the current path
   if (need <= 24) return 24;
   if (need <= 48) return 48;
   return -1;

@@ -118,9 +118,9 @@ __device__ __forceinline__ void blas_closest(const Node4* __restrict__ nodes, co
       float d0 = tn[0], d1 = tn[1], d2 = tn[2], d3 = tn[3];
       uint32_t c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
       PRT_CSWAP(0, 1) PRT_CSWAP(2, 3) PRT_CSWAP(0, 2) PRT_CSWAP(1, 3) PRT_CSWAP(1, 2)
-      if (d3 < kFar) { stk[sp * BLOCK] = c3; sp++; }
-      if (d2 < kFar) { stk[sp * BLOCK] = c2; sp++; }
-      if (d1 < kFar) { stk[sp * BLOCK] = c1; sp++; }
+      if (d3 < kFar && sp < STACK) { stk[sp * BLOCK] = c3; sp++; }
+      if (d2 < kFar && sp < STACK) { stk[sp * BLOCK] = c2; sp++; }
+      if (d1 < kFar && sp < STACK) { stk[sp * BLOCK] = c1; sp++; }
       if (d0 < kFar) { node = c0; continue; }
     } else {
       const uint32_t first = (node >> 2) & 0x1FFFFFFFu, cnt = (node & 3u) + 1u;
@@ -155,9 +155,9 @@ __device__ __forceinline__ bool blas_anyhit(const Node4* __restrict__ nodes, con
       float d0 = tn[0], d1 = tn[1], d2 = tn[2], d3 = tn[3];
       uint32_t c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
       PRT_CSWAP(0, 1) PRT_CSWAP(2, 3) PRT_CSWAP(0, 2) PRT_CSWAP(1, 3) PRT_CSWAP(1, 2)
-      if (d3 < kFar) { stk[sp * BLOCK] = c3; sp++; }
-      if (d2 < kFar) { stk[sp * BLOCK] = c2; sp++; }
-      if (d1 < kFar) { stk[sp * BLOCK] = c1; sp++; }
+      if (d3 < kFar && sp < STACK) { stk[sp * BLOCK] = c3; sp++; }
+      if (d2 < kFar && sp < STACK) { stk[sp * BLOCK] = c2; sp++; }
+      if (d1 < kFar && sp < STACK) { stk[sp * BLOCK] = c1; sp++; }
       if (d0 < kFar) { node = c0; continue; }
     } else {
       const uint32_t first = (node >> 2) & 0x1FFFFFFFu, cnt = (node & 3u) + 1u;

@@ -84,6 +84,12 @@ def load():
         return _lib
     if not os.path.exists(LIBPATH):
         raise PrtError(f"{LIBPATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same SONAME as /opt/rocm's).
+    # Load torch's first so libprt.so binds to it and torch's device memory / streams stay valid.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIBPATH)
     vp, i32, u32 = C.c_void_p, C.c_int32, C.c_uint32
     sig = {

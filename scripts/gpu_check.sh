@@ -1,0 +1,48 @@
+#!/usr/bin/env bash
+# One GPU-box session: smoke -> gpu tests -> short bench (+ optional rocprof).  Each GPU step has its
+# own time limit; a fault / abort / segfault / time limit (rc not in {0,1}) stops the script.
+# usage: scripts/gpu_check.sh [tests|bench|prof|all] [pytest -k expr]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+what=${1:-all}
+kexpr=${2:-}
+
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "!! $name ended with rc=$rc: stopping (no further GPU steps)"
+    exit $rc
+  fi
+  return 0
+}
+
+if [ "$what" = "tests" ] || [ "$what" = "all" ]; then
+  step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
+  if [ -n "$kexpr" ]; then
+    step pytest_gpu 1200 python -m pytest tests -m gpu -x -q -k "$kexpr"
+  else
+    step pytest_gpu 1200 python -m pytest tests -m gpu -q
+  fi
+fi
+if [ "$what" = "bench" ] || [ "$what" = "all" ]; then
+  step bench 900 python bench.py --steps 5 --warmup 1
+fi
+if [ "$what" = "prof" ] || [ "$what" = "benchprof" ]; then
+  export TMPDIR=/tmp
+  if [ "$what" = "benchprof" ]; then
+    step bench 900 python bench.py --steps 5 --warmup 1
+  fi
+  step rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_stats -o run -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline
+  step rocprof_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o run -- \
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
+  step rocprof_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o run -- \
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
+fi
+echo "== done"
