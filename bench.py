@@ -40,6 +40,20 @@ def algorithmic_bytes_per_ray():
     return out, v
 
 
+def measured_traffic(kernel):
+    """HBM bytes per frame of `kernel` from the committed rocprofv3 PMC passes (profiles/traffic_current.json,
+    written by scripts/summarize_prof.py; FETCH_SIZE x2 gfx950 correction, MI355X_MICROARCH.md HBM)."""
+    f = os.path.join(ROOT, "profiles", "traffic_current.json")
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        t = json.load(fh)
+    for name, d in t.get("kernels", {}).items():
+        if name.split("::")[-1].split("<")[0] == kernel and "hbm_bytes_per_frame" in d:
+            return int(d["hbm_bytes_per_frame"])
+    return None
+
+
 def cpu_baseline(sd, threads):
     """The oracle (C restatement, OpenMP over rows) on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -118,13 +132,17 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     seg = shadow = 0
-    ms_trace = []
+    ms_trace, ms_closest, ms_anyhit = [], [], []
+    pipeline = 0
     t0 = time.perf_counter()
     for i in range(args.steps):
         st = step(args.warmup + i)
         seg += st.segments
         shadow += st.shadow_rays
         ms_trace.append(st.ms_trace)
+        ms_closest.append(st.ms_closest)
+        ms_anyhit.append(st.ms_anyhit)
+        pipeline = st.pipeline
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -143,12 +161,19 @@ def main():
         ms_step = elapsed * 1000.0 / args.steps
         value = rays / elapsed / 1e6
         bpr, visits = algorithmic_bytes_per_ray()
-        # dominant kernel: k_trace_frames; algorithmic bytes per launch / its HIP-event duration
-        steps_rays_seg = seg / args.steps
-        steps_rays_sh = shadow / args.steps
-        alg_bytes = steps_rays_seg * bpr["closest"] + steps_rays_sh * bpr["anyhit"]
-        kern_ms = float(np.mean(ms_trace))
+        # roofline of the dominant kernel: algorithmic bytes (reference BVH8_CPU visit counts x SURVEY 8d bytes)
+        # over the kernel's HIP-event time, both summed over the frame's launches of that kernel
+        seg_f, sh_f = seg / args.steps, shadow / args.steps
+        kern = {}
+        if pipeline == 0:
+            kern["k_extend"] = (seg_f * bpr["closest"], float(np.mean(ms_closest)))
+            kern["k_shadow"] = (sh_f * bpr["anyhit"], float(np.mean(ms_anyhit)))
+        else:
+            kern["k_trace_frames"] = (seg_f * bpr["closest"] + sh_f * bpr["anyhit"], float(np.mean(ms_trace)))
+        dom = max(kern, key=lambda k: kern[k][1])
+        alg_bytes, kern_ms = kern[dom]
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+        traffic = measured_traffic(dom)
         out = {
             "metric": "Mrays/s (closest-hit segments + shadow any-hit rays) at 1920x1080, 4 spp, depth 4",
             "value": round(value, 2),
@@ -161,6 +186,7 @@ def main():
             "scaling": "strong",  # one fixed frame is split into pixel tiles over the N GPUs
             "vs_baseline": None,
             "dtype": "f32",
+            "pipeline": "wavefront" if pipeline == 0 else "megakernel",
             "data": "synthetic (seeded procedural heightfield, textures, sky; scenes.py)",
             "config": {"workload": f"{sd.name}: {info.triangles} tris, {W}x{H}, {args.spp} spp, depth {args.bounces}",
                        "global_batch": W * H, "seq_len": args.bounces,
@@ -169,8 +195,11 @@ def main():
                        "shadow_per_step": int(shadow / args.steps),
                        "mpix_per_s": round(W * H / (ms_step / 1e3) / 1e6, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "k_trace_frames", "kernel_ms": round(kern_ms, 3),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": dom, "per": "frame (sum over the kernel's launches)",
+                         "kernel_ms": round(kern_ms, 3), "algorithmic_bytes": round(alg_bytes),
+                         "kernels": {k: {"ms": round(v[1], 3), "alg_GBps": round(v[0] / (v[1] / 1e3) / 1e9, 1)
+                                         if v[1] > 0 else None} for k, v in kern.items()},
                          "bytes_per_ray": {k: round(v, 1) for k, v in bpr.items()}},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -116,6 +116,10 @@ typedef struct {
     uint64_t paths;         /* camera paths traced */
     double   ms;            /* device time of the render (HIP events) */
     double   ms_trace;      /* device time of the path-tracing kernel(s) only */
+    double   ms_closest;    /* device time of the closest-hit traversal launches (wavefront pipeline) */
+    double   ms_anyhit;     /* device time of the shadow any-hit traversal launches (wavefront pipeline) */
+    int32_t  pipeline;      /* 0 = wavefront (default), 1 = megakernel (PRT_PIPELINE=mega) */
+    int32_t  iterations;    /* wavefront iterations launched */
 } prt_stats;
 
 /* closest-hit record, tinybvh::Intersection (Core/tiny_bvh.h:545-567) minus user data */

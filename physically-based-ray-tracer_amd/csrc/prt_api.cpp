@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -123,6 +124,11 @@ struct prt_ctx {
   int32_t accW = 0, accH = 0;
   DevBuf frames, avg, rgb8, counters, hits;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  // wavefront pipeline
+  DevBuf wave;
+  WaveBufs wb{};
+  uint32_t wave_n = 0, wave_levels = 0;
+  WaveTimers wt{};
 };
 
 namespace {
@@ -241,6 +247,37 @@ int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
   return PRT_OK;
 }
 
+// wavefront buffers sized for n items and (bounces-1) (result, throughput) stack levels
+int ensure_wave(prt_ctx* c, uint32_t n, int bounces) {
+  const uint32_t levels = (uint32_t)std::max(1, bounces - 1);
+  if (c->wave_n >= n && c->wave_levels >= levels && c->wave.p) return PRT_OK;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+  const size_t o_seed = take(4ull * n), o_info = take(4ull * n), o_ro = take(16ull * n), o_rd = take(16ull * n),
+               o_R = take(16ull * n * levels), o_T = take(16ull * n * levels), o_s1 = take(16ull * n),
+               o_jit = take(8ull * n), o_hit = take(16ull * n), o_ne = take(16ull * n), o_nb = take(16ull * n),
+               o_nf = take(64ull * n), o_vis = take(4ull * n), o_q0 = take(4ull * n), o_q1 = take(4ull * n),
+               o_sho = take(64ull * n), o_shd = take(64ull * n), o_ctr = take(4ull * 4 * (kMaxIters + 2));
+  HIP_TRY(c->wave.ensure(off));
+  char* b = c->wave.as<char>();
+  WaveBufs& W = c->wb;
+  W.n = n;
+  W.seed = (uint32_t*)(b + o_seed); W.info = (uint32_t*)(b + o_info);
+  W.ro = (float4*)(b + o_ro); W.rd = (float4*)(b + o_rd); W.R = (float4*)(b + o_R); W.T = (float4*)(b + o_T);
+  W.s1 = (float4*)(b + o_s1); W.jit = (float2*)(b + o_jit); W.hit = (float4*)(b + o_hit);
+  W.ne = (float4*)(b + o_ne); W.nb = (float4*)(b + o_nb); W.nf = (float4*)(b + o_nf); W.vis = (uint32_t*)(b + o_vis);
+  W.q0 = (uint32_t*)(b + o_q0); W.q1 = (uint32_t*)(b + o_q1); W.sho = (float4*)(b + o_sho);
+  W.shd = (float4*)(b + o_shd); W.ctr = (uint32_t*)(b + o_ctr);
+  c->wave_n = n;
+  c->wave_levels = levels;
+  return PRT_OK;
+}
+
+bool use_megakernel() {
+  const char* e = std::getenv("PRT_PIPELINE");
+  return e && std::strcmp(e, "mega") == 0;
+}
+
 // the shared trace + accumulate sequence for prt_render / prt_render_tiles
 int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4* avg_dev, uint32_t* rgb8_dev,
                float4* tiles_dev, prt_stats* stats) {
@@ -254,28 +291,59 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   rc = ensure_state(c, p->width, p->height);
   if (rc) return rc;
   const int32_t F = frames_of(p);
-  HIP_TRY(c->frames.ensure(sizeof(float4) * (size_t)M.items * (size_t)std::max(F, 1)));
-  HIP_TRY(c->counters.ensure(sizeof(Counters)));
-  HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
+  const uint64_t n = (uint64_t)M.items * (uint64_t)F;
+  if (n >= (1ull << 30)) return fail(PRT_ERR_UNSUPPORTED, "too many work items in one call (split spp)");
+  HIP_TRY(c->frames.ensure(sizeof(float4) * (size_t)std::max<uint64_t>(n, 1)));
   TraceArgs A;
   A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
   A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F;
   LaunchCfg L{c->stream, stack};
+  const bool mega = use_megakernel();
+  const uint32_t iters = (uint32_t)p->bounces * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
+  if (!mega && iters > (uint32_t)kMaxIters) return fail(PRT_ERR_UNSUPPORTED, "too many wavefront iterations");
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  HIP_TRY(launch_trace_frames(L, S, A, M, c->frames.as<float4>(), c->counters.as<Counters>()));
+  if (mega) {
+    HIP_TRY(c->counters.ensure(sizeof(Counters)));
+    HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
+    HIP_TRY(launch_trace_frames(L, S, A, M, c->frames.as<float4>(), c->counters.as<Counters>()));
+  } else {
+    rc = ensure_wave(c, (uint32_t)n, p->bounces);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4ull * 4 * (kMaxIters + 2), c->stream));
+    HIP_TRY(launch_wavefront(L, S, A, M, c->wb, c->frames.as<float4>(), stats ? &c->wt : nullptr));
+  }
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   HIP_TRY(launch_accumulate(L, M, F, p->flags, c->frames.as<float4>(), c->acc.as<float4>(), c->nsamp.as<int32_t>(),
                             c->dist.as<float>(), avg_dev, rgb8_dev, tiles_dev));
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   if (stats) {
-    Counters h{};
-    HIP_TRY(hipMemcpyAsync(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::memset(stats, 0, sizeof(*stats));
+    if (mega) {
+      Counters h{};
+      HIP_TRY(hipMemcpyAsync(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      stats->segments = h.segments;
+      stats->shadow_rays = h.shadow;
+      stats->pipeline = 1;
+    } else {
+      std::vector<uint32_t> ctr(4 * (kMaxIters + 2));
+      HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      for (uint32_t k = 0; k < iters; k++) {
+        stats->segments += ctr[4 * k];
+        stats->shadow_rays += ctr[4 * k + 1];
+        float a = 0, b = 0;
+        HIP_TRY(hipEventElapsedTime(&a, c->wt.ev[4 * k + 0], c->wt.ev[4 * k + 1]));
+        HIP_TRY(hipEventElapsedTime(&b, c->wt.ev[4 * k + 2], c->wt.ev[4 * k + 3]));
+        stats->ms_closest += a;
+        stats->ms_anyhit += b;
+      }
+      stats->pipeline = 0;
+      stats->iterations = (int32_t)iters;
+    }
     float ms = 0, ms_trace = 0;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[2]));
     HIP_TRY(hipEventElapsedTime(&ms_trace, c->ev[0], c->ev[1]));
-    stats->segments = h.segments;
-    stats->shadow_rays = h.shadow;
     stats->paths = (uint64_t)M.items * (uint64_t)F * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
     stats->ms = ms;
     stats->ms_trace = ms_trace;
@@ -319,6 +387,12 @@ int prt_create(const prt_device_desc* desc, prt_ctx** out) {
       return fail(PRT_ERR_HIP, "hipEventCreate failed");
     }
   }
+  for (auto& e : c->wt.ev) {
+    if (hipEventCreate(&e) != hipSuccess) {
+      delete c;
+      return fail(PRT_ERR_HIP, "hipEventCreate failed");
+    }
+  }
   *out = c;
   return PRT_OK;
 }
@@ -333,6 +407,9 @@ int prt_destroy(prt_ctx* c) {
     b->release();
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto e : c->wt.ev)
+    if (e) (void)hipEventDestroy(e);
+  c->wave.release();
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return PRT_OK;
@@ -606,6 +683,8 @@ int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t 
     HIP_TRY(hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[2]));
+    std::memset(stats, 0, sizeof(*stats));
+    stats->ms_closest = ms;
     stats->segments = h.segments;
     stats->shadow_rays = 0;
     stats->paths = n;

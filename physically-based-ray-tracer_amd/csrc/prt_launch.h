@@ -18,6 +18,36 @@ struct LaunchCfg {
   int stack;  // LDS stack entries per lane: 24 or 48
 };
 
+// wavefront pipeline buffers (SoA over n work items; R/T hold (bounces-1) x n entries)
+struct WaveBufs {
+  uint32_t n;
+  uint32_t* seed;
+  uint32_t* info;   // depth | path << 8 | status << 16 | nee kind << 20
+  float4* ro;
+  float4* rd;
+  float4* R;
+  float4* T;
+  float4* s1;       // path-1 radiance, w = r1.hit.t
+  float2* jit;
+  float4* hit;      // t, u, v, bits(prim | inst << 26)
+  float4* ne;       // emissive (or the path's end value)
+  float4* nb;       // NEE BRDF value
+  float4* nf;       // 4 x n NEE contributions per shadow ray
+  uint32_t* vis;    // 4 visibility bytes per item
+  uint32_t* q0;
+  uint32_t* q1;
+  float4* sho;      // shadow queue: O, tmax
+  float4* shd;      // shadow queue: D, bits(4 * item + slot)
+  uint32_t* ctr;    // per iteration: queue count, shadow count, extend fetch, shadow fetch
+};
+constexpr int kMaxIters = 32;
+struct WaveTimers {
+  hipEvent_t ev[4 * kMaxIters];
+  uint32_t iters;
+};
+
+hipError_t launch_wavefront(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
+                            const WaveBufs& B, float4* out, WaveTimers* tm);
 hipError_t launch_trace_frames(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                                float4* out, Counters* cnt);
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,

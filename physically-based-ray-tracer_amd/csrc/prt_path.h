@@ -1,0 +1,164 @@
+// prt_path.h -- device pieces of Renderer::Trace shared by the megakernel and the wavefront pipeline.
+#pragma once
+#include "prt_kernels.h"
+
+namespace prt {
+
+enum : uint32_t {
+  kAA = 1u << 0, kAccumulate = 1u << 1, kGamma = 1u << 2, kNormalMap = 1u << 3,
+  kSkybox = 1u << 4, kLighted = 1u << 5, kStochastic = 1u << 6
+};
+constexpr int kMaxBounces = 16;
+
+// Camera::GetPrimaryRay (Core/Camera.cpp:113-139, non-Panini branch)
+__device__ __forceinline__ Ray primary_ray(const SceneDev& S, float x, float y, int W, int H) {
+  const float u = x * (1.0f / (float)W);
+  const float v = y * (1.0f / (float)H);
+  const V3 camPos = v3(S.cam[0], S.cam[1], S.cam[2]);
+  const V3 TL = v3(S.cam[3], S.cam[4], S.cam[5]), TR = v3(S.cam[6], S.cam[7], S.cam[8]),
+           BL = v3(S.cam[9], S.cam[10], S.cam[11]);
+  const V3 P = TL + u * (TR - TL) + v * (BL - TL);
+  const V3 dir = normalize(P - camPos);
+  return make_ray(camPos, dir);
+}
+
+// Renderer::Trace debug views (Core/Renderer.cpp:170-194)
+__device__ __forceinline__ V3 debug_view(const SceneDev& S, int mode, const HitAttr& ha, uint32_t inst, uint32_t prim) {
+  switch (mode) {
+    case 1: return ha.m.base;
+    case 4: return v3(ha.m.metal, ha.m.metal, ha.m.metal);
+    case 5: return v3(ha.m.rough, ha.m.rough, ha.m.rough);
+    case 6: return ha.m.emis;
+    case 2: {
+      const V3 g = geometry_normal(S, inst, prim);
+      return v3(g.x + 1.0f, g.y + 1.0f, g.z + 1.0f) * 0.5f;
+    }
+    case 3: return v3(ha.N.x + 1.0f, ha.N.y + 1.0f, ha.N.z + 1.0f) * 0.5f;
+    default: return v3(0.0f, 0.0f, 0.0f);
+  }
+}
+
+// Next-event estimation set-up (Core/Renderer.cpp:198-326) split from its visibility tests.
+// kind: 0 point (4 shadow rays), 1 directional, 2 spot, 3 non-stochastic directional.
+struct NeeSetup {
+  int kind;
+  int nrays;
+  V3 brdf;         // evalCombinedBRDF(...) for the light the reference evaluates (0 when !LIGHTED)
+  V3 f[4];         // per shadow ray: contribution if unoccluded, before the pick-probability division
+  Ray ray[4];
+  float tmax[4];
+};
+
+__device__ __forceinline__ NeeSetup nee_setup(const SceneDev& S, uint32_t fl, V3 I, V3 V, V3 N, const Material& m,
+                                              uint32_t& seed) {
+  NeeSetup ns;
+  if (fl & kStochastic) {
+    const float pP = 0.3f, pD = 0.5f;
+    const float xi = random_float(seed);                                                    // :210
+    const int pick = (xi < pP) ? 0 : ((xi < pP + pD) ? 1 : 2);
+    if (pick == 0) {                                                                        // :216-269
+      float Lx[4], Ly[4], Lz[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        Lx[i] = S.ppos[3 * i] - I.x; Ly[i] = S.ppos[3 * i + 1] - I.y; Lz[i] = S.ppos[3 * i + 2] - I.z;
+        const float dsq = (Lx[i] * Lx[i] + Ly[i] * Ly[i]) + Lz[i] * Lz[i];
+        const float dist = sqrtf(dsq);
+        const float invD = 1.0f / dist;  // _mm_rcp_ps restated as an exact reciprocal
+        Lx[i] = Lx[i] * invD; Ly[i] = Ly[i] * invD; Lz[i] = Lz[i] * invD;
+        float cosa = (N.x * Lx[i] + N.y * Ly[i]) + N.z * Lz[i];
+        cosa = (cosa > 0.0f) ? cosa : 0.0f;  // _mm_max_ps(cosa, 0)
+        const float k = invD * cosa;
+        ns.f[i] = v3(S.pcol[3 * i] * k, S.pcol[3 * i + 1] * k, S.pcol[3 * i + 2] * k);
+        const V3 L = v3(Lx[i], Ly[i], Lz[i]);
+        ns.ray[i] = make_ray(I + L * kEpsilon, L);
+        ns.tmax[i] = dsq - kEpsilon;  // squared distance (Renderer.cpp:257)
+      }
+      const int wl = (int)(random_float(seed) * 10) % 4;                                   // :267
+      ns.brdf = v3(0.0f, 0.0f, 0.0f);
+      if (fl & kLighted) {
+        const float lx = wl == 0 ? Lx[0] : wl == 1 ? Lx[1] : wl == 2 ? Lx[2] : Lx[3];
+        const float ly = wl == 0 ? Ly[0] : wl == 1 ? Ly[1] : wl == 2 ? Ly[2] : Ly[3];
+        const float lz = wl == 0 ? Lz[0] : wl == 1 ? Lz[1] : wl == 2 ? Lz[2] : Lz[3];
+        ns.brdf = eval_combined_brdf(N, v3(lx, ly, lz), V, m);
+      }
+      ns.kind = 0;
+      ns.nrays = 4;
+      return ns;
+    }
+    const float* lp = pick == 1 ? S.dpos : S.spos;                                          // :270-310
+    const float* lc = pick == 1 ? S.dcol : S.scol;
+    V3 L = v3(lp[0], lp[1], lp[2]) - I;
+    const float distance = length(L);
+    L = L / distance;
+    const float cosa = smax(0.0f, dot(N, L));
+    ns.ray[0] = make_ray(I + L * kEpsilon, L);
+    ns.tmax[0] = distance - kEpsilon;
+    if (pick == 1) {
+      ns.f[0] = v3(lc[0], lc[1], lc[2]) * cosa;
+    } else {
+      const float factor = dot(L, v3(S.srot[0], S.srot[1], S.srot[2]));
+      ns.f[0] = ((double)factor > 0.9) ? v3(lc[0], lc[1], lc[2]) * (1 / (distance * distance)) * cosa
+                                       : v3(0.0f, 0.0f, 0.0f);
+    }
+    ns.brdf = (fl & kLighted) ? eval_combined_brdf(N, L, V, m) : v3(0.0f, 0.0f, 0.0f);
+    ns.kind = pick;
+    ns.nrays = 1;
+    return ns;
+  }
+  V3 L = v3(S.dpos[0], S.dpos[1], S.dpos[2]) - I;                                         // :312-326
+  const float distance = length(L);
+  L = L / distance;
+  const float cosa = smax(0.0f, dot(N, L));
+  ns.ray[0] = make_ray(I + L * kEpsilon, L);
+  ns.tmax[0] = distance - kEpsilon;
+  ns.f[0] = v3(S.dcol[0], S.dcol[1], S.dcol[2]) * cosa;
+  ns.brdf = (fl & kLighted) ? eval_combined_brdf(N, L, V, m) : v3(0.0f, 0.0f, 0.0f);
+  ns.kind = 3;
+  ns.nrays = 1;
+  return ns;
+}
+
+// result after NEE: emissive + throughput(=1) * (BRDF * contribution), the reference's float order.
+// vis bit i = shadow ray i unoccluded.
+__device__ __forceinline__ V3 nee_resolve(int kind, uint32_t vis, V3 e, V3 brdf, const V3* f, uint32_t fl) {
+  V3 c = v3(0.0f, 0.0f, 0.0f);
+  if (kind == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (vis & (1u << i)) c = c + f[i];
+    c = c / 0.3f;
+  } else {
+    if (vis & 1u) c = f[0];
+    if (kind == 1) c = c / 0.5f;
+    else if (kind == 2) c = c / 0.2f;
+  }
+  const V3 add = (fl & kLighted) ? brdf * c : v3(0.0f, 0.0f, 0.0f);
+  return e + v3(1.0f, 1.0f, 1.0f) * add;
+}
+
+// lobe pick + BRDF sampling (Core/Renderer.cpp:376-404).  Returns false when the path ends here.
+__device__ __forceinline__ bool sample_bounce(const Material& m, V3 V, V3 N, uint32_t& seed, V3& dir, V3& thr) {
+  int type = 1;
+  thr = v3(1.0f, 1.0f, 1.0f);
+  if (m.metal == 1.0f && m.rough == 0.0f) type = 2;                                         // :376
+  else {
+    const float bp = brdf_probability(m, V, N);                                             // :380
+    if (random_float(seed) < bp) { type = 2; thr = thr / bp; }
+    else { type = 1; thr = thr / (1.0f - bp); }
+  }
+  V3 wgt = v3(1.0f, 1.0f, 1.0f);
+  V2 u;
+  u.x = random_float(seed);                                                                 // :396
+  u.y = random_float(seed);
+  if (!eval_indirect_brdf(u, N, V, m, type, dir, wgt)) return false;                       // :398
+  thr = thr * wgt;
+  return true;
+}
+
+// RGBF32_to_RGB8 (template/precomp.h:310-315, scalar path)
+__device__ __forceinline__ uint32_t pack1(float x) {
+  const float mm = smin(1.0f, x);
+  return mm > 0.0f ? (uint32_t)(255.0f * mm) : 0u;
+}
+
+}  // namespace prt

@@ -1,22 +1,18 @@
-// prt_render.hip -- path-tracing kernels for gfx950 (MI355X).
+// prt_render.hip -- megakernel path tracer + accumulation / untile / geometry-query kernels (gfx950).
 //
 // k_trace_frames: one lane = one (pixel, reference frame) work item, tracing the frame's camera
 //   path(s) in the canonical order (AA jitter, Trace(r1), Trace(r2)) through
-//   the restated Renderer::Trace (Core/Renderer.cpp:150-406): TLAS->BLAS closest hit, hit
-//   attributes, one stochastic NEE light-class sample with shadow any-hit rays, lobe pick, BRDF
-//   sampling, bounce.  The recursion `result + Trace(..) * throughput` is evaluated bottom-up from a
-//   per-lane (result, throughput) stack so float rounding matches the recursive reference exactly.
+//   the restated Renderer::Trace (Core/Renderer.cpp:150-406) with its shadow rays inline.  It is the
+//   reference-shaped baseline (PRT_PIPELINE=mega); the default pipeline is the wavefront one
+//   (prt_wave.hip) and both must produce bit-identical frames.  The recursion
+//   `result + Trace(..) * throughput` is evaluated bottom-up from a per-lane (result, throughput) stack
+//   so float rounding matches the recursive reference exactly.
 // k_accumulate: per pixel, folds the frames into the persistent accumulator with the reference's
 //   distance-keyed progressive mean (Core/Renderer.cpp:81-104) and packs RGB8 (precomp.h:310-315).
 #include "prt_launch.h"
+#include "prt_path.h"
 
 namespace prt {
-
-enum : uint32_t {
-  kAA = 1u << 0, kAccumulate = 1u << 1, kGamma = 1u << 2, kNormalMap = 1u << 3,
-  kSkybox = 1u << 4, kLighted = 1u << 5, kStochastic = 1u << 6
-};
-constexpr int kMaxBounces = 16;
 
 __device__ __forceinline__ void wave_count(Counters* c, uint32_t seg, uint32_t sh) {
   // one atomic per wave: reduce across the 64 lanes first
@@ -28,18 +24,6 @@ __device__ __forceinline__ void wave_count(Counters* c, uint32_t seg, uint32_t s
     atomicAdd(&c->segments, (unsigned long long)seg);
     atomicAdd(&c->shadow, (unsigned long long)sh);
   }
-}
-
-// Camera::GetPrimaryRay (Core/Camera.cpp:113-139, non-Panini branch)
-__device__ __forceinline__ Ray primary_ray(const SceneDev& S, float x, float y, int W, int H) {
-  const float u = x * (1.0f / (float)W);
-  const float v = y * (1.0f / (float)H);
-  const V3 camPos = v3(S.cam[0], S.cam[1], S.cam[2]);
-  const V3 TL = v3(S.cam[3], S.cam[4], S.cam[5]), TR = v3(S.cam[6], S.cam[7], S.cam[8]),
-           BL = v3(S.cam[9], S.cam[10], S.cam[11]);
-  const V3 P = TL + u * (TR - TL) + v * (BL - TL);
-  const V3 dir = normalize(P - camPos);
-  return make_ray(camPos, dir);
 }
 
 // Renderer::Trace, iterative.  Returns radiance; *t_primary = closest-hit t of the first segment.
@@ -59,117 +43,18 @@ __device__ V3 trace_path(const SceneDev& S, const TraceArgs& A, Ray r, uint32_t&
     const V3 I = r.O + h.t * r.D;                                                          // tiny_bvh.h:586
     const V3 V = -r.D;
     const HitAttr ha = hit_attributes(S, h.inst, h.prim, h.u, h.v, (fl & kNormalMap) != 0);
-    const V3 N = ha.N;
-    const Material& m = ha.m;
-    if (A.mode != 0) {                                                                     // :170-194
-      switch (A.mode) {
-        case 1: Lend = m.base; break;
-        case 4: Lend = v3(m.metal, m.metal, m.metal); break;
-        case 5: Lend = v3(m.rough, m.rough, m.rough); break;
-        case 6: Lend = m.emis; break;
-        case 2: {
-          const V3 g = geometry_normal(S, h.inst, h.prim);
-          Lend = v3(g.x + 1.0f, g.y + 1.0f, g.z + 1.0f) * 0.5f;
-          break;
-        }
-        case 3: Lend = v3(N.x + 1.0f, N.y + 1.0f, N.z + 1.0f) * 0.5f; break;
-        default: Lend = v3(0.0f, 0.0f, 0.0f); break;
-      }
-      break;
-    }
-    V3 result = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * m.emis;                  // :196
-    if (fl & kStochastic) {
-      const float pP = 0.3f, pD = 0.5f, pS = 0.2f;
-      const float xi = random_float(seed);                                                 // :210
-      const int pick = (xi < pP) ? 0 : ((xi < pP + pD) ? 1 : 2);
-      if (pick == 0) {                                                                     // :216-269
-        float Lx[4], Ly[4], Lz[4], dsq[4];
-        V3 fc[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          Lx[i] = S.ppos[3 * i] - I.x; Ly[i] = S.ppos[3 * i + 1] - I.y; Lz[i] = S.ppos[3 * i + 2] - I.z;
-          dsq[i] = (Lx[i] * Lx[i] + Ly[i] * Ly[i]) + Lz[i] * Lz[i];
-          const float dist = sqrtf(dsq[i]);
-          const float invD = 1.0f / dist;  // _mm_rcp_ps restated as an exact reciprocal
-          Lx[i] = Lx[i] * invD; Ly[i] = Ly[i] * invD; Lz[i] = Lz[i] * invD;
-          float cosa = (N.x * Lx[i] + N.y * Ly[i]) + N.z * Lz[i];
-          cosa = (cosa > 0.0f) ? cosa : 0.0f;  // _mm_max_ps(cosa, 0)
-          const float k = invD * cosa;
-          fc[i] = v3(S.pcol[3 * i] * k, S.pcol[3 * i + 1] * k, S.pcol[3 * i + 2] * k);
-        }
-        V3 contrib = v3(0.0f, 0.0f, 0.0f);
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const V3 L = v3(Lx[i], Ly[i], Lz[i]);
-          const Ray sr = make_ray(I + L * kEpsilon, L);
-          nshadow++;
-          if (!scene_anyhit<STACK, kBlock>(S, sr, dsq[i] - kEpsilon, stk)) contrib = contrib + fc[i];
-        }
-        contrib = contrib / pP;
-        const int wl = (int)(random_float(seed) * 10) % 4;                                // :267
-        V3 add = v3(0.0f, 0.0f, 0.0f);
-        if (fl & kLighted) {
-          const float lx = wl == 0 ? Lx[0] : wl == 1 ? Lx[1] : wl == 2 ? Lx[2] : Lx[3];
-          const float ly = wl == 0 ? Ly[0] : wl == 1 ? Ly[1] : wl == 2 ? Ly[2] : Ly[3];
-          const float lz = wl == 0 ? Lz[0] : wl == 1 ? Lz[1] : wl == 2 ? Lz[2] : Lz[3];
-          add = eval_combined_brdf(N, v3(lx, ly, lz), V, m) * contrib;
-        }
-        result = result + v3(1.0f, 1.0f, 1.0f) * add;
-      } else {                                                                             // :270-310
-        const float* lp = pick == 1 ? S.dpos : S.spos;
-        const float* lc = pick == 1 ? S.dcol : S.scol;
-        V3 L = v3(lp[0], lp[1], lp[2]) - I;
-        const float distance = length(L);
-        L = L / distance;
-        const float cosa = smax(0.0f, dot(N, L));
-        const Ray sr = make_ray(I + L * kEpsilon, L);
-        nshadow++;
-        const bool occ = scene_anyhit<STACK, kBlock>(S, sr, distance - kEpsilon, stk);
-        V3 contrib = v3(0.0f, 0.0f, 0.0f);
-        if (pick == 1) {
-          if (!occ) contrib = v3(lc[0], lc[1], lc[2]) * cosa;
-          contrib = contrib / pD;
-        } else {
-          const float factor = dot(L, v3(S.srot[0], S.srot[1], S.srot[2]));
-          if (!occ) {
-            if ((double)factor > 0.9) contrib = v3(lc[0], lc[1], lc[2]) * (1 / (distance * distance)) * cosa;
-            else contrib = v3(0.0f, 0.0f, 0.0f);
-          }
-          contrib = contrib / pS;
-        }
-        V3 add = v3(0.0f, 0.0f, 0.0f);
-        if (fl & kLighted) add = eval_combined_brdf(N, L, V, m) * contrib;
-        result = result + v3(1.0f, 1.0f, 1.0f) * add;
-      }
-    } else {                                                                               // :312-326
-      V3 L = v3(S.dpos[0], S.dpos[1], S.dpos[2]) - I;
-      const float distance = length(L);
-      L = L / distance;
-      const float cosa = smax(0.0f, dot(N, L));
-      const Ray sr = make_ray(I + L * kEpsilon, L);
+    if (A.mode != 0) { Lend = debug_view(S, A.mode, ha, h.inst, h.prim); break; }        // :170-194
+    const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
+    const NeeSetup ns = nee_setup(S, fl, I, V, ha.N, ha.m, seed);                         // :198-326
+    uint32_t vis = 0;
+    for (int i = 0; i < ns.nrays; i++) {
       nshadow++;
-      V3 contrib = v3(0.0f, 0.0f, 0.0f);  // uninitialised when occluded in the reference; 0 here
-      if (!scene_anyhit<STACK, kBlock>(S, sr, distance - kEpsilon, stk)) contrib = v3(S.dcol[0], S.dcol[1], S.dcol[2]) * cosa;
-      V3 add = v3(0.0f, 0.0f, 0.0f);
-      if (fl & kLighted) add = eval_combined_brdf(N, L, V, m) * contrib;
-      result = result + v3(1.0f, 1.0f, 1.0f) * add;
+      if (!scene_anyhit<STACK, kBlock>(S, ns.ray[i], ns.tmax[i], stk)) vis |= 1u << i;
     }
-    if (depth == A.bounces - 1) { Lend = result; break; }                                  // :329
-    // :331-372 dielectric path is dead (transmissivness is never set, Scene.cpp:193-197)
-    int type = 1;
-    V3 thr = v3(1.0f, 1.0f, 1.0f);
-    if (m.metal == 1.0f && m.rough == 0.0f) type = 2;                                      // :376
-    else {
-      const float bp = brdf_probability(m, V, N);                                          // :380
-      if (random_float(seed) < bp) { type = 2; thr = thr / bp; }
-      else { type = 1; thr = thr / (1.0f - bp); }
-    }
-    V3 wgt = v3(1.0f, 1.0f, 1.0f), dir;
-    V2 u;
-    u.x = random_float(seed);                                                              // :396
-    u.y = random_float(seed);
-    if (!eval_indirect_brdf(u, N, V, m, type, dir, wgt)) { Lend = result; break; }       // :398
-    thr = thr * wgt;
+    const V3 result = nee_resolve(ns.kind, vis, e, ns.brdf, ns.f, fl);
+    if (depth == A.bounces - 1) { Lend = result; break; }                                 // :329
+    V3 dir, thr;
+    if (!sample_bounce(ha.m, V, ha.N, seed, dir, thr)) { Lend = result; break; }          // :376-399
     R[nd] = result;
     T[nd] = thr;
     nd++;
@@ -213,12 +98,6 @@ __global__ void __launch_bounds__(kBlock) k_trace_frames(SceneDev S, TraceArgs A
     }
   }
   wave_count(cnt, nseg, nsh);
-}
-
-// RGBF32_to_RGB8 (template/precomp.h:310-315, scalar path)
-__device__ __forceinline__ uint32_t pack1(float x) {
-  const float mm = smin(1.0f, x);
-  return mm > 0.0f ? (uint32_t)(255.0f * mm) : 0u;
 }
 
 // Core/Renderer.cpp:81-104,137.  tiles_out != null: write the average in item (tile-compact) order.

@@ -62,7 +62,8 @@ class RenderParams(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("shadow_rays", C.c_uint64), ("paths", C.c_uint64), ("ms", C.c_double),
-                ("ms_trace", C.c_double)]
+                ("ms_trace", C.c_double), ("ms_closest", C.c_double), ("ms_anyhit", C.c_double),
+                ("pipeline", C.c_int32), ("iterations", C.c_int32)]
 
 
 class Hit(C.Structure):

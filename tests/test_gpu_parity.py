@@ -90,6 +90,21 @@ def test_render_c3_reduced(gpu_ctx):
     _compare_render(gpu_ctx, scenes.config_c3(), 320, 180, 4, 4)
 
 
+def test_wavefront_equals_megakernel(gpu_ctx, monkeypatch):
+    """The two pipelines (wavefront default, PRT_PIPELINE=mega) render bit-identical frames."""
+    sd = scenes.multi_instance(scenes.config_small(60, 50))
+    W, H = 128, 96
+    gpu_scene(gpu_ctx, sd, W, H)
+    a_w, r_w, s_w = gpu_ctx.render(W, H, 4, 4)
+    assert s_w.pipeline == 0 and s_w.iterations == 8
+    gpu_ctx.reset_accumulation(full=True)
+    monkeypatch.setenv("PRT_PIPELINE", "mega")
+    a_m, r_m, s_m = gpu_ctx.render(W, H, 4, 4)
+    assert s_m.pipeline == 1
+    assert np.array_equal(a_w, a_m) and np.array_equal(r_w, r_m)
+    assert s_w.segments == s_m.segments and s_w.shadow_rays == s_m.shadow_rays
+
+
 def test_progressive_accumulation(gpu_ctx):
     sd = scenes.config_small(40, 30)
     W, H = 48, 32
