@@ -250,7 +250,10 @@ int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
 // wavefront buffers sized for n items and (bounces-1) (result, throughput) stack levels
 int ensure_wave(prt_ctx* c, uint32_t n, int bounces) {
   const uint32_t levels = (uint32_t)std::max(1, bounces - 1);
-  if (c->wave_n >= n && c->wave_levels >= levels && c->wave.p) return PRT_OK;
+  if (c->wave_n >= n && c->wave_levels >= levels && c->wave.p) {
+    c->wb.n = n;  // capacity stays; the SoA strides (R/T: depth * n + item) follow the current n
+    return PRT_OK;
+  }
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
   const size_t o_seed = take(4ull * n), o_info = take(4ull * n), o_ro = take(16ull * n), o_rd = take(16ull * n),
