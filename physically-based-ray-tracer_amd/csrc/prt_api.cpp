@@ -248,23 +248,31 @@ int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
 }
 
 // wavefront buffers sized for n items and (bounces-1) (result, throughput) stack levels
+constexpr size_t kCtrWords = (size_t)(kMaxIters + 2) * 2 * kNSub * kCtrStride;
 int ensure_wave(prt_ctx* c, uint32_t n, int bounces) {
   const uint32_t levels = (uint32_t)std::max(1, bounces - 1);
+  // sub-queue t receives the 256-entry chunks c == t (mod kNSub): at most ceil(ceil(n/256)/kNSub) of them
+  const uint32_t qcap = 256u * (((n + 255u) / 256u + kNSub - 1) / kNSub);
   if (c->wave_n >= n && c->wave_levels >= levels && c->wave.p) {
     c->wb.n = n;  // capacity stays; the SoA strides (R/T: depth * n + item) follow the current n
+    c->wb.qcap = qcap;
+    c->wb.scap = 4u * qcap;
     return PRT_OK;
   }
+  const size_t qn = (size_t)kNSub * qcap, sn = 4 * qn;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
   const size_t o_seed = take(4ull * n), o_info = take(4ull * n), o_ro = take(16ull * n), o_rd = take(16ull * n),
                o_R = take(16ull * n * levels), o_T = take(16ull * n * levels), o_s1 = take(16ull * n),
                o_jit = take(8ull * n), o_hit = take(16ull * n), o_ne = take(16ull * n), o_nb = take(16ull * n),
-               o_nf = take(64ull * n), o_vis = take(4ull * n), o_q0 = take(4ull * n), o_q1 = take(4ull * n),
-               o_sho = take(64ull * n), o_shd = take(64ull * n), o_ctr = take(4ull * 4 * (kMaxIters + 2));
+               o_nf = take(64ull * n), o_vis = take(4ull * n), o_q0 = take(4 * qn), o_q1 = take(4 * qn),
+               o_sho = take(16 * sn), o_shd = take(16 * sn), o_ctr = take(4 * kCtrWords);
   HIP_TRY(c->wave.ensure(off));
   char* b = c->wave.as<char>();
   WaveBufs& W = c->wb;
   W.n = n;
+  W.qcap = qcap;
+  W.scap = 4u * qcap;
   W.seed = (uint32_t*)(b + o_seed); W.info = (uint32_t*)(b + o_info);
   W.ro = (float4*)(b + o_ro); W.rd = (float4*)(b + o_rd); W.R = (float4*)(b + o_R); W.T = (float4*)(b + o_T);
   W.s1 = (float4*)(b + o_s1); W.jit = (float2*)(b + o_jit); W.hit = (float4*)(b + o_hit);
@@ -312,7 +320,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   } else {
     rc = ensure_wave(c, (uint32_t)n, p->bounces);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4ull * 4 * (kMaxIters + 2), c->stream));
+    HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * kCtrWords, c->stream));
     HIP_TRY(launch_wavefront(L, S, A, M, c->wb, c->frames.as<float4>(), stats ? &c->wt : nullptr));
   }
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
@@ -329,12 +337,14 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
       stats->shadow_rays = h.shadow;
       stats->pipeline = 1;
     } else {
-      std::vector<uint32_t> ctr(4 * (kMaxIters + 2));
+      std::vector<uint32_t> ctr(kCtrWords);
       HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
       for (uint32_t k = 0; k < iters; k++) {
-        stats->segments += ctr[4 * k];
-        stats->shadow_rays += ctr[4 * k + 1];
+        for (uint32_t s = 0; s < kNSub; s++) {
+          stats->segments += ctr[((k * 2 + 0) * kNSub + s) * kCtrStride];
+          stats->shadow_rays += ctr[((k * 2 + 1) * kNSub + s) * kCtrStride];
+        }
         float a = 0, b = 0;
         HIP_TRY(hipEventElapsedTime(&a, c->wt.ev[4 * k + 0], c->wt.ev[4 * k + 1]));
         HIP_TRY(hipEventElapsedTime(&b, c->wt.ev[4 * k + 2], c->wt.ev[4 * k + 3]));

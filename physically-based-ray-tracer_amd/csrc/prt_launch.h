@@ -19,8 +19,12 @@ struct LaunchCfg {
 };
 
 // wavefront pipeline buffers (SoA over n work items; R/T hold (bounces-1) x n entries)
+constexpr uint32_t kNSub = 32;       // sub-queues per queue (one append counter each)
+constexpr uint32_t kCtrStride = 32;  // words between counters (each on its own 128-B line)
 struct WaveBufs {
   uint32_t n;
+  uint32_t qcap;    // capacity of one path sub-queue  (multiple of 256)
+  uint32_t scap;    // capacity of one shadow sub-queue (4 x qcap)
   uint32_t* seed;
   uint32_t* info;   // depth | path << 8 | status << 16 | nee kind << 20
   float4* ro;
@@ -38,7 +42,7 @@ struct WaveBufs {
   uint32_t* q1;
   float4* sho;      // shadow queue: O, tmax
   float4* shd;      // shadow queue: D, bits(4 * item + slot)
-  uint32_t* ctr;    // per iteration: queue count, shadow count, extend fetch, shadow fetch
+  uint32_t* ctr;    // [iteration][path|shadow][sub-queue] counters, kCtrStride apart
 };
 constexpr int kMaxIters = 32;
 struct WaveTimers {

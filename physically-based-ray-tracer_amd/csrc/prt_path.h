@@ -40,82 +40,59 @@ __device__ __forceinline__ V3 debug_view(const SceneDev& S, int mode, const HitA
 
 // Next-event estimation set-up (Core/Renderer.cpp:198-326) split from its visibility tests.
 // kind: 0 point (4 shadow rays), 1 directional, 2 spot, 3 non-stochastic directional.
-struct NeeSetup {
-  int kind;
-  int nrays;
-  V3 brdf;         // evalCombinedBRDF(...) for the light the reference evaluates (0 when !LIGHTED)
-  V3 f[4];         // per shadow ray: contribution if unoccluded, before the pick-probability division
-  Ray ray[4];
-  float tmax[4];
-};
+__device__ __forceinline__ int nee_kind(uint32_t fl, uint32_t& seed) {
+  if (!(fl & kStochastic)) return 3;
+  const float pP = 0.3f, pD = 0.5f;
+  const float xi = random_float(seed);                                                      // :210
+  return (xi < pP) ? 0 : ((xi < pP + pD) ? 1 : 2);
+}
+__device__ __forceinline__ int nee_rays(int kind) { return kind == 0 ? 4 : 1; }
 
-__device__ __forceinline__ NeeSetup nee_setup(const SceneDev& S, uint32_t fl, V3 I, V3 V, V3 N, const Material& m,
-                                              uint32_t& seed) {
-  NeeSetup ns;
-  if (fl & kStochastic) {
-    const float pP = 0.3f, pD = 0.5f;
-    const float xi = random_float(seed);                                                    // :210
-    const int pick = (xi < pP) ? 0 : ((xi < pP + pD) ? 1 : 2);
-    if (pick == 0) {                                                                        // :216-269
-      float Lx[4], Ly[4], Lz[4];
+// Builds the shadow rays of `kind` (emit(k, ray, tmax) per ray, in order), the per-ray unoccluded
+// contribution f[k] (before the pick-probability division) and returns the BRDF value the reference
+// evaluates for this light class (0 when !LIGHTED).  Draws whichLight for point lights.
+template <class Emit>
+__device__ __forceinline__ V3 nee_lights(const SceneDev& S, uint32_t fl, int kind, V3 I, V3 V, V3 N, const Material& m,
+                                         uint32_t& seed, V3* f, Emit&& emit) {
+  if (kind == 0) {                                                                          // :216-269
+    float lx = 0.0f, ly = 0.0f, lz = 0.0f;
+    float Lx[4], Ly[4], Lz[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        Lx[i] = S.ppos[3 * i] - I.x; Ly[i] = S.ppos[3 * i + 1] - I.y; Lz[i] = S.ppos[3 * i + 2] - I.z;
-        const float dsq = (Lx[i] * Lx[i] + Ly[i] * Ly[i]) + Lz[i] * Lz[i];
-        const float dist = sqrtf(dsq);
-        const float invD = 1.0f / dist;  // _mm_rcp_ps restated as an exact reciprocal
-        Lx[i] = Lx[i] * invD; Ly[i] = Ly[i] * invD; Lz[i] = Lz[i] * invD;
-        float cosa = (N.x * Lx[i] + N.y * Ly[i]) + N.z * Lz[i];
-        cosa = (cosa > 0.0f) ? cosa : 0.0f;  // _mm_max_ps(cosa, 0)
-        const float k = invD * cosa;
-        ns.f[i] = v3(S.pcol[3 * i] * k, S.pcol[3 * i + 1] * k, S.pcol[3 * i + 2] * k);
-        const V3 L = v3(Lx[i], Ly[i], Lz[i]);
-        ns.ray[i] = make_ray(I + L * kEpsilon, L);
-        ns.tmax[i] = dsq - kEpsilon;  // squared distance (Renderer.cpp:257)
-      }
-      const int wl = (int)(random_float(seed) * 10) % 4;                                   // :267
-      ns.brdf = v3(0.0f, 0.0f, 0.0f);
-      if (fl & kLighted) {
-        const float lx = wl == 0 ? Lx[0] : wl == 1 ? Lx[1] : wl == 2 ? Lx[2] : Lx[3];
-        const float ly = wl == 0 ? Ly[0] : wl == 1 ? Ly[1] : wl == 2 ? Ly[2] : Ly[3];
-        const float lz = wl == 0 ? Lz[0] : wl == 1 ? Lz[1] : wl == 2 ? Lz[2] : Lz[3];
-        ns.brdf = eval_combined_brdf(N, v3(lx, ly, lz), V, m);
-      }
-      ns.kind = 0;
-      ns.nrays = 4;
-      return ns;
+    for (int i = 0; i < 4; i++) {
+      Lx[i] = S.ppos[3 * i] - I.x; Ly[i] = S.ppos[3 * i + 1] - I.y; Lz[i] = S.ppos[3 * i + 2] - I.z;
+      const float dsq = (Lx[i] * Lx[i] + Ly[i] * Ly[i]) + Lz[i] * Lz[i];
+      const float dist = sqrtf(dsq);
+      const float invD = 1.0f / dist;  // _mm_rcp_ps restated as an exact reciprocal
+      Lx[i] = Lx[i] * invD; Ly[i] = Ly[i] * invD; Lz[i] = Lz[i] * invD;
+      float cosa = (N.x * Lx[i] + N.y * Ly[i]) + N.z * Lz[i];
+      cosa = (cosa > 0.0f) ? cosa : 0.0f;  // _mm_max_ps(cosa, 0)
+      const float k = invD * cosa;
+      f[i] = v3(S.pcol[3 * i] * k, S.pcol[3 * i + 1] * k, S.pcol[3 * i + 2] * k);
+      const V3 L = v3(Lx[i], Ly[i], Lz[i]);
+      emit(i, make_ray(I + L * kEpsilon, L), dsq - kEpsilon);  // tmax = squared distance (:257)
     }
-    const float* lp = pick == 1 ? S.dpos : S.spos;                                          // :270-310
-    const float* lc = pick == 1 ? S.dcol : S.scol;
-    V3 L = v3(lp[0], lp[1], lp[2]) - I;
-    const float distance = length(L);
-    L = L / distance;
-    const float cosa = smax(0.0f, dot(N, L));
-    ns.ray[0] = make_ray(I + L * kEpsilon, L);
-    ns.tmax[0] = distance - kEpsilon;
-    if (pick == 1) {
-      ns.f[0] = v3(lc[0], lc[1], lc[2]) * cosa;
-    } else {
-      const float factor = dot(L, v3(S.srot[0], S.srot[1], S.srot[2]));
-      ns.f[0] = ((double)factor > 0.9) ? v3(lc[0], lc[1], lc[2]) * (1 / (distance * distance)) * cosa
-                                       : v3(0.0f, 0.0f, 0.0f);
-    }
-    ns.brdf = (fl & kLighted) ? eval_combined_brdf(N, L, V, m) : v3(0.0f, 0.0f, 0.0f);
-    ns.kind = pick;
-    ns.nrays = 1;
-    return ns;
+    const int wl = (int)(random_float(seed) * 10) % 4;                                     // :267
+    if (!(fl & kLighted)) return v3(0.0f, 0.0f, 0.0f);
+    lx = wl == 0 ? Lx[0] : wl == 1 ? Lx[1] : wl == 2 ? Lx[2] : Lx[3];
+    ly = wl == 0 ? Ly[0] : wl == 1 ? Ly[1] : wl == 2 ? Ly[2] : Ly[3];
+    lz = wl == 0 ? Lz[0] : wl == 1 ? Lz[1] : wl == 2 ? Lz[2] : Lz[3];
+    return eval_combined_brdf(N, v3(lx, ly, lz), V, m);
   }
-  V3 L = v3(S.dpos[0], S.dpos[1], S.dpos[2]) - I;                                         // :312-326
+  const float* lp = (kind == 2) ? S.spos : S.dpos;                                          // :270-326
+  const float* lc = (kind == 2) ? S.scol : S.dcol;
+  V3 L = v3(lp[0], lp[1], lp[2]) - I;
   const float distance = length(L);
   L = L / distance;
   const float cosa = smax(0.0f, dot(N, L));
-  ns.ray[0] = make_ray(I + L * kEpsilon, L);
-  ns.tmax[0] = distance - kEpsilon;
-  ns.f[0] = v3(S.dcol[0], S.dcol[1], S.dcol[2]) * cosa;
-  ns.brdf = (fl & kLighted) ? eval_combined_brdf(N, L, V, m) : v3(0.0f, 0.0f, 0.0f);
-  ns.kind = 3;
-  ns.nrays = 1;
-  return ns;
+  emit(0, make_ray(I + L * kEpsilon, L), distance - kEpsilon);
+  if (kind == 2) {
+    const float factor = dot(L, v3(S.srot[0], S.srot[1], S.srot[2]));
+    f[0] = ((double)factor > 0.9) ? v3(lc[0], lc[1], lc[2]) * (1 / (distance * distance)) * cosa
+                                  : v3(0.0f, 0.0f, 0.0f);
+  } else {
+    f[0] = v3(lc[0], lc[1], lc[2]) * cosa;
+  }
+  return (fl & kLighted) ? eval_combined_brdf(N, L, V, m) : v3(0.0f, 0.0f, 0.0f);
 }
 
 // result after NEE: emissive + throughput(=1) * (BRDF * contribution), the reference's float order.

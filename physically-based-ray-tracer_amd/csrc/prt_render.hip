@@ -45,13 +45,14 @@ __device__ V3 trace_path(const SceneDev& S, const TraceArgs& A, Ray r, uint32_t&
     const HitAttr ha = hit_attributes(S, h.inst, h.prim, h.u, h.v, (fl & kNormalMap) != 0);
     if (A.mode != 0) { Lend = debug_view(S, A.mode, ha, h.inst, h.prim); break; }        // :170-194
     const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
-    const NeeSetup ns = nee_setup(S, fl, I, V, ha.N, ha.m, seed);                         // :198-326
+    const int kind = nee_kind(fl, seed);                                                  // :198-326
     uint32_t vis = 0;
-    for (int i = 0; i < ns.nrays; i++) {
+    V3 f[4];
+    const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed, f, [&](int k, const Ray& sr, float tmax) {
       nshadow++;
-      if (!scene_anyhit<STACK, kBlock>(S, ns.ray[i], ns.tmax[i], stk)) vis |= 1u << i;
-    }
-    const V3 result = nee_resolve(ns.kind, vis, e, ns.brdf, ns.f, fl);
+      if (!scene_anyhit<STACK, kBlock>(S, sr, tmax, stk)) vis |= 1u << k;
+    });
+    const V3 result = nee_resolve(kind, vis, e, brdf, f, fl);
     if (depth == A.bounces - 1) { Lend = result; break; }                                 // :329
     V3 dir, thr;
     if (!sample_bounce(ha.m, V, ha.N, seed, dir, thr)) { Lend = result; break; }          // :376-399

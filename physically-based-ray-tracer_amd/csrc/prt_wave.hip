@@ -13,9 +13,11 @@
 //     k_resolve  result_d from visibility, (result, throughput) stack, path end: bottom-up
 //                `result + L * throughput`, AA path 2 start, gamma, frame write (:65-79, 404)
 //
-// Traversal kernels are persistent: each wave pulls 64 rays at a time from a device counter, so no
-// host round trip is needed to size grids and slow rays do not hold a whole launch.  Queue appends
-// are wave-aggregated (ballot + one atomic per wave).  All per-item state is SoA in HBM.
+// Queues are split into kNSub sub-queues, each with its own counter on its own 128-B line, so the
+// (block-aggregated, one atomic per 256 entries) appends never pile up on one address.  Consumers
+// need no atomics: a block loads the kNSub counts into an LDS prefix table and walks a static,
+// interleaved set of 64-entry chunks (traversal kernels use one-wave blocks, so a slow wave never
+// holds back its siblings' slots).  All per-item state is SoA in HBM; no host synchronisation.
 #include "prt_launch.h"
 #include "prt_path.h"
 
@@ -24,26 +26,68 @@ namespace prt {
 enum : uint32_t { kStEndValue = 0, kStNeeEnd = 1, kStNeeCont = 2 };
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+__device__ __forceinline__ uint32_t* qcounter(uint32_t* ctr, uint32_t iter, uint32_t which, uint32_t s) {
+  return ctr + ((iter * 2u + which) * kNSub + s) * kCtrStride;
+}
 
-// wave-aggregated append of `n` (0..4) entries per lane; returns this lane's first slot
-__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, uint32_t n) {
+// LDS prefix table of the kNSub sub-queue counts; returns the total.  Call with uniform control flow.
+__device__ __forceinline__ uint32_t load_prefix(const uint32_t* ctr, uint32_t iter, uint32_t which, uint32_t* pref) {
+  if (threadIdx.x < 64) {
+    const uint32_t l = threadIdx.x;
+    uint32_t v = l < kNSub ? ctr[((iter * 2u + which) * kNSub + l) * kCtrStride] : 0u;
+    for (int off = 1; off < 32; off <<= 1) {  // inclusive scan over the first 32 lanes
+      const uint32_t o = __shfl_up(v, off, 64);
+      if (l >= (uint32_t)off) v += o;
+    }
+    if (l < kNSub) pref[l + 1] = v;
+    if (l == 0) pref[0] = 0;
+  }
+  __syncthreads();
+  return pref[kNSub];
+}
+// global index g in [0, total) -> slot in the sub-queue layout (sub-queue s occupies [s*cap, s*cap+cnt_s))
+__device__ __forceinline__ uint32_t map_slot(const uint32_t* pref, uint32_t g, uint32_t cap) {
+  uint32_t lo = 0, hi = kNSub;
+#pragma unroll
+  for (int it = 0; it < 5; it++) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pref[mid] <= g) lo = mid; else hi = mid;
+  }
+  return lo * cap + (g - pref[lo]);
+}
+
+// block-aggregated append of n (0..4) entries per lane into one sub-queue; returns this lane's first
+// index inside that sub-queue.  All threads of the block must call it.  sm: >= 8 words of LDS.
+__device__ __forceinline__ uint32_t block_append(uint32_t* counter, uint32_t n, uint32_t* sm) {
   const uint64_t b1 = __ballot(n & 1u), b2 = __ballot((n >> 1) & 1u), b4 = __ballot((n >> 2) & 1u);
   const uint64_t lt = (1ull << lane_id()) - 1ull;
   const uint32_t before = (uint32_t)__popcll(b1 & lt) + 2u * (uint32_t)__popcll(b2 & lt) + 4u * (uint32_t)__popcll(b4 & lt);
-  const uint32_t total = (uint32_t)__popcll(b1) + 2u * (uint32_t)__popcll(b2) + 4u * (uint32_t)__popcll(b4);
-  uint32_t base = 0;
-  if (lane_id() == 0 && total) base = atomicAdd(counter, total);
-  base = __shfl(base, 0, 64);
-  return base + before;
+  const uint32_t wtot = (uint32_t)__popcll(b1) + 2u * (uint32_t)__popcll(b2) + 4u * (uint32_t)__popcll(b4);
+  const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane_id() == 0) sm[w] = wtot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (uint32_t k = 0; k < nw; k++) tot += sm[k];
+    sm[4] = tot ? atomicAdd(counter, tot) : 0u;
+  }
+  __syncthreads();
+  uint32_t off = sm[4];
+  for (uint32_t k = 0; k < w; k++) off += sm[k];
+  __syncthreads();
+  return off + before;
 }
 
 __device__ __forceinline__ uint32_t pack_hit(uint32_t prim, uint32_t inst) { return prim | (inst << 26); }
 
+// ---- init: items -> primary rays, appended to queue 0 (sub-queue = block % kNSub)
 __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, TileMap M, WaveBufs B,
                                                       float4* __restrict__ out) {
-  const uint32_t stride = gridDim.x * kBlock;
-  for (uint32_t i0 = blockIdx.x * kBlock + (threadIdx.x & ~63u); i0 < B.n; i0 += stride) {
-    const uint32_t i = i0 + lane_id();
+  __shared__ uint32_t sm[8];
+  const uint32_t sub = blockIdx.x % kNSub;
+  uint32_t* cnt = qcounter(B.ctr, 0, 0, sub);
+  for (uint32_t c = blockIdx.x; c * kBlock < B.n; c += gridDim.x) {
+    const uint32_t i = c * kBlock + threadIdx.x;
     bool enq = false;
     if (i < B.n) {
       const uint32_t f = i / M.items, r = i % M.items;
@@ -66,136 +110,154 @@ __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, T
         out[i] = make_float4(0.0f, 0.0f, 0.0f, kFar);  // bounces == 0: Trace returns 0, t1 stays BVH_FAR
       }
     }
-    const uint32_t slot = wave_append(&B.ctr[0], enq ? 1u : 0u);
-    if (enq) B.q0[slot] = i;
+    const uint32_t slot = block_append(cnt, enq ? 1u : 0u, sm);
+    if (enq) B.q0[sub * B.qcap + slot] = i;
   }
 }
 
+// ---- closest hit (one-wave blocks, static interleaved chunks of the live queue)
 template <int STACK>
-__global__ void __launch_bounds__(kBlock) k_extend(SceneDev S, WaveBufs B, uint32_t iter) {
-  __shared__ uint32_t lds_stack[STACK * kBlock];
+__global__ void __launch_bounds__(64) k_extend(SceneDev S, WaveBufs B, uint32_t iter) {
+  __shared__ uint32_t lds_stack[STACK * 64];
+  __shared__ uint32_t pref[kNSub + 1];
   uint32_t* stk = lds_stack + threadIdx.x;
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
-  const uint32_t count = B.ctr[4 * iter + 0];
-  while (true) {
-    uint32_t base = 0;
-    if (lane_id() == 0) base = atomicAdd(&B.ctr[4 * iter + 2], 64u);
-    base = __shfl(base, 0, 64);
-    if (base >= count) break;
-    const uint32_t idx = base + lane_id();
-    if (idx < count) {
-      const uint32_t item = q[idx];
+  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
+  for (uint32_t c = blockIdx.x; c * 64u < total; c += gridDim.x) {
+    const uint32_t g = c * 64u + threadIdx.x;
+    if (g < total) {
+      const uint32_t item = q[map_slot(pref, g, B.qcap)];
       const float4 o = B.ro[item], d = B.rd[item];
       Ray r;
       r.O = v3(o.x, o.y, o.z);
       r.D = v3(d.x, d.y, d.z);
       r.rD = v3(safercp(d.x), safercp(d.y), safercp(d.z));
-      const Hit h = scene_closest<STACK, kBlock>(S, r, kFar, stk);
+      const Hit h = scene_closest<STACK, 64>(S, r, kFar, stk);
       B.hit[item] = make_float4(h.t, h.u, h.v, __uint_as_float(pack_hit(h.prim, h.inst)));
     }
   }
 }
 
+// ---- shading, NEE set-up (shadow rays straight into the shadow queue), BRDF sampling
 __global__ void __launch_bounds__(kBlock) k_shade(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter) {
+  __shared__ uint32_t pref[kNSub + 1];
+  __shared__ uint32_t sm[8];
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
-  const uint32_t count = B.ctr[4 * iter + 0];
+  const uint32_t sub = blockIdx.x % kNSub;
+  uint32_t* shcnt = qcounter(B.ctr, iter, 1, sub);
+  float4* sho = B.sho + (size_t)sub * B.scap;
+  float4* shd = B.shd + (size_t)sub * B.scap;
+  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
   const uint32_t fl = A.flags;
-  const uint32_t stride = gridDim.x * kBlock;
-  for (uint32_t i0 = blockIdx.x * kBlock + (threadIdx.x & ~63u); i0 < count; i0 += stride) {
-    const uint32_t idx = i0 + lane_id();
-    uint32_t nrays = 0, item = 0;
-    NeeSetup ns;
-    if (idx < count) {
-      item = q[idx];
-      uint32_t info = B.info[item];
-      const uint32_t depth = info & 0xFFu, path = (info >> 8) & 1u;
-      const float4 o = B.ro[item], d = B.rd[item], hh = B.hit[item];
-      const V3 O = v3(o.x, o.y, o.z), D = v3(d.x, d.y, d.z);
+  for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    const uint32_t g = c * kBlock + threadIdx.x;
+    uint32_t item = 0, info = 0, depth = 0, status = kStEndValue;
+    int kind = 0;
+    uint32_t nr = 0;
+    float4 hh = make_float4(kFar, 0.0f, 0.0f, 0.0f);
+    V3 O = v3(0.0f, 0.0f, 0.0f), D = v3(0.0f, 0.0f, 1.0f);
+    uint32_t seed = 0;
+    const bool active = g < total;
+    bool shaded = false;
+    if (active) {
+      item = q[map_slot(pref, g, B.qcap)];
+      info = B.info[item];
+      depth = info & 0xFFu;
+      const uint32_t path = (info >> 8) & 1u;
+      const float4 o = B.ro[item], d = B.rd[item];
+      hh = B.hit[item];
+      O = v3(o.x, o.y, o.z);
+      D = v3(d.x, d.y, d.z);
       if (depth == 0 && path == 0) B.s1[item].w = hh.x;                                    // r1.hit.t
-      uint32_t status = kStEndValue, kind = 0;
       if (hh.x >= kFar) {                                                                    // :159
         const V3 L = (fl & kSkybox) ? sample_sky(S, D) : v3(0.0f, 0.0f, 0.0f);
         B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
-      } else {
+      } else if (A.mode != 0) {                                                              // :170-194
         const uint32_t pk = __float_as_uint(hh.w);
-        const uint32_t prim = pk & 0x03FFFFFFu, inst = pk >> 26;
-        const V3 I = O + hh.x * D;                                                           // tiny_bvh.h:586
-        const V3 V = -D;
-        const HitAttr ha = hit_attributes(S, inst, prim, hh.y, hh.z, (fl & kNormalMap) != 0);
-        if (A.mode != 0) {
-          const V3 L = debug_view(S, A.mode, ha, inst, prim);
-          B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
-        } else {
-          uint32_t seed = B.seed[item];
-          const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;            // :196
-          ns = nee_setup(S, fl, I, V, ha.N, ha.m, seed);
-          nrays = (uint32_t)ns.nrays;
-          kind = (uint32_t)ns.kind;
-          B.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
-          B.nb[item] = make_float4(ns.brdf.x, ns.brdf.y, ns.brdf.z, 0.0f);
-          for (uint32_t k = 0; k < nrays; k++) B.nf[4 * (size_t)item + k] = make_float4(ns.f[k].x, ns.f[k].y, ns.f[k].z, 0.0f);
-          B.vis[item] = 0u;
-          status = kStNeeEnd;
-          if ((int)depth != A.bounces - 1) {                                                 // :329
-            V3 dir, thr;
-            if (sample_bounce(ha.m, V, ha.N, seed, dir, thr)) {
-              status = kStNeeCont;
-              B.T[(size_t)depth * B.n + item] = make_float4(thr.x, thr.y, thr.z, 0.0f);
-              const Ray nr = make_ray(I + dir * kEpsilon, dir);                              // :404
-              B.ro[item] = make_float4(nr.O.x, nr.O.y, nr.O.z, 0.0f);
-              B.rd[item] = make_float4(nr.D.x, nr.D.y, nr.D.z, 0.0f);
-            }
-          }
-          B.seed[item] = seed;
+        const HitAttr ha = hit_attributes(S, pk >> 26, pk & 0x03FFFFFFu, hh.y, hh.z, (fl & kNormalMap) != 0);
+        const V3 L = debug_view(S, A.mode, ha, pk >> 26, pk & 0x03FFFFFFu);
+        B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
+      } else {
+        seed = B.seed[item];
+        kind = nee_kind(fl, seed);                                                           // :198-214
+        nr = (uint32_t)nee_rays(kind);
+        shaded = true;
+      }
+    }
+    // reserve the shadow-ray slots of the whole block at once (one atomic per 256 items)
+    const uint32_t s0 = block_append(shcnt, nr, sm);
+    if (shaded) {
+      const uint32_t pk = __float_as_uint(hh.w);
+      const uint32_t prim = pk & 0x03FFFFFFu, inst = pk >> 26;
+      const V3 I = O + hh.x * D;                                                             // tiny_bvh.h:586
+      const V3 V = -D;
+      const HitAttr ha = hit_attributes(S, inst, prim, hh.y, hh.z, (fl & kNormalMap) != 0);
+      const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
+      V3 f[4];
+      const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed, f, [&](int k, const Ray& sr, float tmax) {
+        sho[s0 + k] = make_float4(sr.O.x, sr.O.y, sr.O.z, tmax);
+        shd[s0 + k] = make_float4(sr.D.x, sr.D.y, sr.D.z, __uint_as_float(4u * item + (uint32_t)k));
+      });
+      B.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
+      B.nb[item] = make_float4(brdf.x, brdf.y, brdf.z, 0.0f);
+      for (uint32_t k = 0; k < nr; k++) B.nf[4 * (size_t)item + k] = make_float4(f[k].x, f[k].y, f[k].z, 0.0f);
+      B.vis[item] = 0u;
+      status = kStNeeEnd;
+      if ((int)depth != A.bounces - 1) {                                                     // :329
+        V3 dir, thr;
+        if (sample_bounce(ha.m, V, ha.N, seed, dir, thr)) {                                  // :376-399
+          status = kStNeeCont;
+          B.T[(size_t)depth * B.n + item] = make_float4(thr.x, thr.y, thr.z, 0.0f);
+          const Ray nr2 = make_ray(I + dir * kEpsilon, dir);                                 // :404
+          B.ro[item] = make_float4(nr2.O.x, nr2.O.y, nr2.O.z, 0.0f);
+          B.rd[item] = make_float4(nr2.D.x, nr2.D.y, nr2.D.z, 0.0f);
         }
       }
-      info = (info & 0x1FFu) | (status << 16) | (kind << 20);
-      B.info[item] = info;
+      B.seed[item] = seed;
     }
-    const uint32_t s = wave_append(&B.ctr[4 * iter + 1], nrays);
-    for (uint32_t k = 0; k < nrays; k++) {
-      B.sho[s + k] = make_float4(ns.ray[k].O.x, ns.ray[k].O.y, ns.ray[k].O.z, ns.tmax[k]);
-      B.shd[s + k] = make_float4(ns.ray[k].D.x, ns.ray[k].D.y, ns.ray[k].D.z, __uint_as_float(4u * item + k));
-    }
+    if (active) B.info[item] = (info & 0x1FFu) | (status << 16) | ((uint32_t)kind << 20);
   }
 }
 
+// ---- any hit for the shadow queue
 template <int STACK>
-__global__ void __launch_bounds__(kBlock) k_shadow(SceneDev S, WaveBufs B, uint32_t iter) {
-  __shared__ uint32_t lds_stack[STACK * kBlock];
+__global__ void __launch_bounds__(64) k_shadow(SceneDev S, WaveBufs B, uint32_t iter) {
+  __shared__ uint32_t lds_stack[STACK * 64];
+  __shared__ uint32_t pref[kNSub + 1];
   uint32_t* stk = lds_stack + threadIdx.x;
-  const uint32_t count = B.ctr[4 * iter + 1];
   uint8_t* vis8 = reinterpret_cast<uint8_t*>(B.vis);
-  while (true) {
-    uint32_t base = 0;
-    if (lane_id() == 0) base = atomicAdd(&B.ctr[4 * iter + 3], 64u);
-    base = __shfl(base, 0, 64);
-    if (base >= count) break;
-    const uint32_t idx = base + lane_id();
-    if (idx < count) {
-      const float4 o = B.sho[idx], d = B.shd[idx];
+  const uint32_t total = load_prefix(B.ctr, iter, 1, pref);
+  for (uint32_t c = blockIdx.x; c * 64u < total; c += gridDim.x) {
+    const uint32_t g = c * 64u + threadIdx.x;
+    if (g < total) {
+      const uint32_t slot = map_slot(pref, g, B.scap);
+      const float4 o = B.sho[slot], d = B.shd[slot];
       Ray r;
       r.O = v3(o.x, o.y, o.z);
       r.D = v3(d.x, d.y, d.z);
       r.rD = v3(safercp(d.x), safercp(d.y), safercp(d.z));
-      if (!scene_anyhit<STACK, kBlock>(S, r, o.w, stk)) vis8[__float_as_uint(d.w)] = 1;
+      if (!scene_anyhit<STACK, 64>(S, r, o.w, stk)) vis8[__float_as_uint(d.w)] = 1;
     }
   }
 }
 
+// ---- NEE resolve, (result, throughput) stack, path end, AA path 2, frame write
 __global__ void __launch_bounds__(kBlock) k_resolve(SceneDev S, TraceArgs A, TileMap M, WaveBufs B, uint32_t iter,
                                                     float4* __restrict__ out) {
+  __shared__ uint32_t pref[kNSub + 1];
+  __shared__ uint32_t sm[8];
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
   uint32_t* qn = (iter & 1) ? B.q0 : B.q1;
-  const uint32_t count = B.ctr[4 * iter + 0];
+  const uint32_t sub = blockIdx.x % kNSub;
+  uint32_t* ncnt = qcounter(B.ctr, iter + 1, 0, sub);
+  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
   const uint32_t fl = A.flags;
-  const uint32_t stride = gridDim.x * kBlock;
-  for (uint32_t i0 = blockIdx.x * kBlock + (threadIdx.x & ~63u); i0 < count; i0 += stride) {
-    const uint32_t idx = i0 + lane_id();
+  for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    const uint32_t g = c * kBlock + threadIdx.x;
     bool enq = false;
     uint32_t item = 0;
-    if (idx < count) {
-      item = q[idx];
+    if (g < total) {
+      item = q[map_slot(pref, g, B.qcap)];
       const uint32_t info = B.info[item];
       const uint32_t depth = info & 0xFFu, path = (info >> 8) & 1u, status = (info >> 16) & 3u,
                      kind = (info >> 20) & 3u;
@@ -251,35 +313,30 @@ __global__ void __launch_bounds__(kBlock) k_resolve(SceneDev S, TraceArgs A, Til
         }
       }
     }
-    const uint32_t slot = wave_append(&B.ctr[4 * (iter + 1) + 0], enq ? 1u : 0u);
-    if (enq) qn[slot] = item;
+    const uint32_t slot = block_append(ncnt, enq ? 1u : 0u, sm);
+    if (enq) qn[sub * B.qcap + slot] = item;
   }
 }
 
 // ---- host launcher: the whole frame batch, no host synchronisation inside
-static inline unsigned blocks_for(uint64_t n, unsigned cap) {
-  const uint64_t b = (n + kBlock - 1) / kBlock;
-  return (unsigned)(b < cap ? (b ? b : 1) : cap);
-}
-
 hipError_t launch_wavefront(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                             const WaveBufs& B, float4* out, WaveTimers* tm) {
   if (B.n == 0) return hipSuccess;
-  const unsigned persist = 256u * 8u;  // persistent traversal grid (waves pull work from a counter)
-  const unsigned gs = blocks_for(B.n, 4096u);
-  hipLaunchKernelGGL(k_wave_init, dim3(gs), dim3(kBlock), 0, c.stream, S, A, M, B, out);
+  const unsigned gtrav = 256u * 16u;  // one-wave blocks, static interleaved chunks
+  const unsigned gprod = 256u * 4u;   // producer blocks (multiple of kNSub)
+  hipLaunchKernelGGL(k_wave_init, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, out);
   const uint32_t iters = (uint32_t)A.bounces * ((A.flags & kAA) ? 2u : 1u);
   for (uint32_t it = 0; it < iters; it++) {
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 0], c.stream);
-    if (c.stack <= 24) hipLaunchKernelGGL(k_extend<24>, dim3(persist), dim3(kBlock), 0, c.stream, S, B, it);
-    else hipLaunchKernelGGL(k_extend<48>, dim3(persist), dim3(kBlock), 0, c.stream, S, B, it);
+    if (c.stack <= 24) hipLaunchKernelGGL(k_extend<24>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    else hipLaunchKernelGGL(k_extend<48>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
-    hipLaunchKernelGGL(k_shade, dim3(gs), dim3(kBlock), 0, c.stream, S, A, B, it);
+    hipLaunchKernelGGL(k_shade, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 2], c.stream);
-    if (c.stack <= 24) hipLaunchKernelGGL(k_shadow<24>, dim3(persist), dim3(kBlock), 0, c.stream, S, B, it);
-    else hipLaunchKernelGGL(k_shadow<48>, dim3(persist), dim3(kBlock), 0, c.stream, S, B, it);
+    if (c.stack <= 24) hipLaunchKernelGGL(k_shadow<24>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    else hipLaunchKernelGGL(k_shadow<48>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 3], c.stream);
-    hipLaunchKernelGGL(k_resolve, dim3(gs), dim3(kBlock), 0, c.stream, S, A, M, B, it, out);
+    hipLaunchKernelGGL(k_resolve, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it, out);
   }
   if (tm) tm->iters = iters;
   return hipGetLastError();
