@@ -248,7 +248,8 @@ int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
 }
 
 // wavefront buffers sized for n items and (bounces-1) (result, throughput) stack levels
-constexpr size_t kCtrWords = (size_t)(kMaxIters + 2) * 2 * kNSub * kCtrStride;
+// queue counters [iter][path|shadow][kNSub] + traversal fetch counters [iter][path|shadow][8 parts]
+constexpr size_t kCtrWords = (size_t)(kMaxIters + 2) * 2 * (kNSub + 8) * kCtrStride;
 int ensure_wave(prt_ctx* c, uint32_t n, int bounces) {
   const uint32_t levels = (uint32_t)std::max(1, bounces - 1);
   // sub-queue t receives the 256-entry chunks c == t (mod kNSub): at most ceil(ceil(n/256)/kNSub) of them

@@ -56,6 +56,35 @@ __device__ __forceinline__ uint32_t map_slot(const uint32_t* pref, uint32_t g, u
   return lo * cap + (g - pref[lo]);
 }
 
+// Dynamic work fetch for the traversal kernels without a hot counter: the live range [0, total) is cut
+// into kParts contiguous parts, each with its own fetch counter; a wave starts on the part of its XCD
+// (HW_REG_XCC_ID) and steals from the others once that part is drained.  Returns false when all parts
+// are drained.  Wave-uniform.
+constexpr uint32_t kParts = 8;
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 7u;
+}
+__device__ __forceinline__ bool fetch_chunk(uint32_t* fctr, uint32_t total, uint32_t& part, uint32_t& base) {
+  for (uint32_t tries = 0; tries < kParts; tries++) {
+    const uint32_t lo = (uint32_t)(((uint64_t)total * part) / kParts);
+    const uint32_t hi = (uint32_t)(((uint64_t)total * (part + 1)) / kParts);
+    uint32_t off = 0;
+    if (lane_id() == 0) off = (hi > lo) ? atomicAdd(fctr + part * kCtrStride, 64u) : 0xFFFFFFFFu;
+    off = __shfl(off, 0, 64);
+    if (off != 0xFFFFFFFFu && off < hi - lo) {
+      base = lo + off;
+      return true;
+    }
+    part = (part + 1) & (kParts - 1);
+  }
+  return false;
+}
+__device__ __forceinline__ uint32_t* fetch_counters(uint32_t* ctr, uint32_t iter, uint32_t which) {
+  return ctr + ((size_t)(kMaxIters + 2) * 2 * kNSub + (iter * 2u + which) * kParts) * kCtrStride;
+}
+
 // block-aggregated append of n (0..4) entries per lane into one sub-queue; returns this lane's first
 // index inside that sub-queue.  All threads of the block must call it.  sm: >= 8 words of LDS.
 __device__ __forceinline__ uint32_t block_append(uint32_t* counter, uint32_t n, uint32_t* sm) {
@@ -123,9 +152,12 @@ __global__ void __launch_bounds__(64) k_extend(SceneDev S, WaveBufs B, uint32_t 
   uint32_t* stk = lds_stack + threadIdx.x;
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
   const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
-  for (uint32_t c = blockIdx.x; c * 64u < total; c += gridDim.x) {
-    const uint32_t g = c * 64u + threadIdx.x;
-    if (g < total) {
+  uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
+  uint32_t part = xcc_id(), base = 0;
+  while (fetch_chunk(fctr, total, part, base)) {
+    const uint32_t g = base + threadIdx.x;
+    const uint32_t hi = (uint32_t)(((uint64_t)total * (part + 1)) / kParts);
+    if (g < hi) {
       const uint32_t item = q[map_slot(pref, g, B.qcap)];
       const float4 o = B.ro[item], d = B.rd[item];
       Ray r;
@@ -227,9 +259,12 @@ __global__ void __launch_bounds__(64) k_shadow(SceneDev S, WaveBufs B, uint32_t 
   uint32_t* stk = lds_stack + threadIdx.x;
   uint8_t* vis8 = reinterpret_cast<uint8_t*>(B.vis);
   const uint32_t total = load_prefix(B.ctr, iter, 1, pref);
-  for (uint32_t c = blockIdx.x; c * 64u < total; c += gridDim.x) {
-    const uint32_t g = c * 64u + threadIdx.x;
-    if (g < total) {
+  uint32_t* fctr = fetch_counters(B.ctr, iter, 1);
+  uint32_t part = xcc_id(), base = 0;
+  while (fetch_chunk(fctr, total, part, base)) {
+    const uint32_t g = base + threadIdx.x;
+    const uint32_t hi = (uint32_t)(((uint64_t)total * (part + 1)) / kParts);
+    if (g < hi) {
       const uint32_t slot = map_slot(pref, g, B.scap);
       const float4 o = B.sho[slot], d = B.shd[slot];
       Ray r;
