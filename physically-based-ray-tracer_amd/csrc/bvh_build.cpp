@@ -238,4 +238,152 @@ BuiltBlas build_blas(const float* triangles, int32_t T, int max_leaf) {
   return out;
 }
 
+namespace {
+
+// per-axis power-of-two scale so that ext / 2^e <= 255; returns the biased exponent (e + 127)
+uint8_t grid_exponent(double ext) {
+  if (!(ext > 0)) return 1;
+  int e = (int)std::ceil(std::log2(ext / 255.0));
+  while (std::ldexp(255.0, e) < ext) e++;
+  while (e > -126 && std::ldexp(255.0, e - 1) >= ext) e--;
+  return (uint8_t)std::min(254, std::max(1, e + 127));
+}
+
+}  // namespace
+
+BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf) {
+  BuiltBlas8 out;
+  Builder B;
+  B.tri = triangles;
+  B.max_leaf = std::max(1, std::min(4, max_leaf));
+  B.build(T);
+  for (int k = 0; k < 3; k++) { out.bmin[k] = B.nodes[0].box.lo[k]; out.bmax[k] = B.nodes[0].box.hi[k]; }
+  out.tris.reserve(T);
+  struct Item { int32_t n2; uint32_t n8; int depth; };
+  std::vector<Item> work;
+  out.nodes.push_back(Node8());
+  work.push_back({0, 0, 1});
+  while (!work.empty()) {
+    const Item it = work.back();
+    work.pop_back();
+    out.depth = std::max(out.depth, it.depth);
+    // gather up to 8 children by opening the largest-area interior child
+    int32_t ch[8];
+    int nc = 0;
+    const Node2& root = B.nodes[it.n2];
+    if (root.leaf()) {
+      ch[nc++] = it.n2;
+    } else {
+      ch[nc++] = root.left;
+      ch[nc++] = root.right;
+      while (nc < 8) {
+        int bi = -1;
+        float ba = -1.0f;
+        for (int i = 0; i < nc; i++) {
+          const Node2& c = B.nodes[ch[i]];
+          if (!c.leaf() && c.box.area() > ba) { ba = c.box.area(); bi = i; }
+        }
+        if (bi < 0) break;
+        const Node2& c = B.nodes[ch[bi]];
+        ch[bi] = c.left;
+        ch[nc++] = c.right;
+      }
+    }
+    // inflated child boxes and the node grid
+    float clo[8][3], chi[8][3];
+    double nlo[3] = {1e300, 1e300, 1e300}, nhi[3] = {-1e300, -1e300, -1e300};
+    for (int i = 0; i < nc; i++) {
+      const Node2& c = B.nodes[ch[i]];
+      for (int k = 0; k < 3; k++) { clo[i][k] = c.box.lo[k]; chi[i][k] = c.box.hi[k]; }
+      inflate_box(clo[i], chi[i]);
+      for (int k = 0; k < 3; k++) { nlo[k] = std::min(nlo[k], (double)clo[i][k]); nhi[k] = std::max(nhi[k], (double)chi[i][k]); }
+    }
+    // octant slot assignment: slot s holds the child that comes first for rays of octant s
+    int slot_of[8], child_in[8];
+    for (int s = 0; s < 8; s++) child_in[s] = -1;
+    {
+      double pc[3];
+      for (int k = 0; k < 3; k++) pc[k] = 0.5 * (nlo[k] + nhi[k]);
+      double cost[8][8];
+      for (int i = 0; i < nc; i++)
+        for (int s = 0; s < 8; s++) {
+          double d = 0;
+          for (int k = 0; k < 3; k++) {
+            const double cc = 0.5 * ((double)clo[i][k] + (double)chi[i][k]) - pc[k];
+            d += ((s >> k) & 1) ? -cc : cc;
+          }
+          cost[i][s] = d;
+        }
+      bool used_c[8] = {false}, used_s[8] = {false};
+      for (int n = 0; n < nc; n++) {
+        double best = 1e300;
+        int bi = -1, bs = -1;
+        for (int i = 0; i < nc; i++)
+          if (!used_c[i])
+            for (int s = 0; s < 8; s++)
+              if (!used_s[s] && cost[i][s] < best) { best = cost[i][s]; bi = i; bs = s; }
+        used_c[bi] = used_s[bs] = true;
+        slot_of[bi] = bs;
+        child_in[bs] = bi;
+      }
+    }
+    Node8 nd;
+    std::memset(&nd, 0, sizeof(nd));
+    nd.px = (float)nlo[0]; nd.py = (float)nlo[1]; nd.pz = (float)nlo[2];
+    const double p[3] = {(double)nd.px, (double)nd.py, (double)nd.pz};
+    uint8_t e[3];
+    for (int k = 0; k < 3; k++) e[k] = grid_exponent(nhi[k] - p[k]);
+    nd.ex = e[0]; nd.ey = e[1]; nd.ez = e[2];
+    const double sc[3] = {std::ldexp(1.0, (int)e[0] - 127), std::ldexp(1.0, (int)e[1] - 127),
+                          std::ldexp(1.0, (int)e[2] - 127)};
+    // interior children are stored contiguously in slot order; leaf triangles likewise
+    nd.child_base = (uint32_t)out.nodes.size();
+    nd.tri_base = (uint32_t)out.tris.size();
+    uint32_t ninterior = 0;
+    for (int s = 0; s < 8; s++)
+      if (child_in[s] >= 0 && !B.nodes[ch[child_in[s]]].leaf()) ninterior++;
+    out.nodes.resize(out.nodes.size() + ninterior);
+    uint32_t nextchild = nd.child_base, tri_off = 0;
+    for (int s = 0; s < 8; s++) {
+      const int i = child_in[s];
+      if (i < 0) {  // empty slot: inverted box never hits
+        nd.qlox[s] = nd.qloy[s] = nd.qloz[s] = 255;
+        nd.qhix[s] = nd.qhiy[s] = nd.qhiz[s] = 0;
+        continue;
+      }
+      uint8_t* qlo[3] = {&nd.qlox[s], &nd.qloy[s], &nd.qloz[s]};
+      uint8_t* qhi[3] = {&nd.qhix[s], &nd.qhiy[s], &nd.qhiz[s]};
+      for (int k = 0; k < 3; k++) {
+        const double lo = std::floor(((double)clo[i][k] - p[k]) / sc[k]);
+        const double hi = std::ceil(((double)chi[i][k] - p[k]) / sc[k]);
+        *qlo[k] = (uint8_t)std::min(255.0, std::max(0.0, lo));
+        *qhi[k] = (uint8_t)std::min(255.0, std::max(0.0, hi));
+      }
+      const Node2& c = B.nodes[ch[i]];
+      if (c.leaf()) {
+        for (int32_t j = c.first; j < c.first + c.count; j++) {
+          const uint32_t pr = B.idx[j];
+          const float* a = triangles + 12 * (size_t)pr;
+          TriMT t;
+          for (int k = 0; k < 3; k++) {
+            t.v0[k] = a[k];
+            t.e1[k] = a[4 + k] - a[k];   // e1 = v1 - v0, e2 = v2 - v0 (tiny_bvh.h:4614-4616)
+            t.e2[k] = a[8 + k] - a[k];
+          }
+          t.prim = pr; t.pad1 = 0; t.pad2 = 0;
+          out.tris.push_back(t);
+        }
+        nd.meta[s] = (uint8_t)((tri_off << 3) | (uint32_t)c.count);
+        tri_off += (uint32_t)c.count;
+        out.leaves++;
+      } else {
+        nd.imask |= (uint8_t)(1u << s);
+        work.push_back({ch[i], nextchild++, it.depth + 1});
+      }
+    }
+    out.nodes[it.n8] = nd;
+  }
+  return out;
+}
+
 }  // namespace prt

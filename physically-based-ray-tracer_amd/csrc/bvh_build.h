@@ -45,6 +45,32 @@ struct BuiltBlas {
 // triangles: fat float4 x 3T (Model::triangles).  max_leaf <= 4.
 BuiltBlas build_blas(const float* triangles, int32_t tri_count, int max_leaf = 4);
 
+// ---- 8-wide compressed node (CWBVH-style, Ylitie et al. 2017 "Efficient Incoherent Ray Traversal on GPUs
+// Through Compressed Wide BVHs"; own encoding).  80 bytes = 5 x 16-B loads per visit:
+//   [0]  px py pz | ex ey ez imask      grid origin, per-axis power-of-two scale 2^(e-127), interior mask
+//   [1]  child_base tri_base meta[8]    interior slot k -> child_base + popc(imask & ((1<<k)-1));
+//                                       leaf slot k: meta = (tri offset << 3) | count (count 1..4)
+//   [2-4] qlo{x,y,z}[8] qhi{x,y,z}[8]   child bounds quantised outward on the node grid
+// Children sit in slots chosen per octant (slot s holds the child nearest for rays of octant s), so
+// visiting slots in the order (i ^ ray_octant) is approximately front to back without sorting.
+struct alignas(16) Node8 {
+  float px, py, pz;
+  uint8_t ex, ey, ez, imask;
+  uint32_t child_base, tri_base;
+  uint8_t meta[8];
+  uint8_t qlox[8], qloy[8], qloz[8], qhix[8], qhiy[8], qhiz[8];
+};
+static_assert(sizeof(Node8) == 80, "Node8 must be 80 bytes");
+
+struct BuiltBlas8 {
+  std::vector<Node8> nodes;   // node 0 = root
+  std::vector<TriMT> tris;    // grouped per node (leaf children's triangles contiguous)
+  float bmin[3], bmax[3];
+  int depth = 0;
+  int64_t leaves = 0;
+};
+BuiltBlas8 build_blas8(const float* triangles, int32_t tri_count, int max_leaf = 3);
+
 // Same inflation rule the traversal relies on (see bvh_build.cpp).
 void inflate_box(float* lo, float* hi);
 

@@ -105,8 +105,9 @@ struct prt_ctx {
   // meshes
   std::vector<MeshDev> mesh_host;
   std::vector<MeshHost> mesh_info;
-  DevBuf nodes, tris, fnrm, fuv, vidx, vert, facen, mesh;
+  DevBuf nodes, nodes8, tris, fnrm, fuv, vidx, vert, facen, mesh;
   int max_depth = 0;
+  int layout = 8;  // BLAS node layout of the uploaded meshes: 8 = Node8 (default), 4 = Node4 (PRT_BVH=4)
   // instances
   std::vector<float> inst_xf;
   std::vector<uint32_t> inst_mesh;
@@ -133,11 +134,15 @@ struct prt_ctx {
 
 namespace {
 
-int stack_for(const prt_ctx* c) {
-  const int need = 3 * c->max_depth;  // <= 3 pushes per interior level on the current path
-  if (need <= 24) return 24;
-  if (need <= 48) return 48;
-  return -1;
+// The LDS traversal stacks are sized for Trav<L>::kMaxDepth node levels (prt_traverse8.h).
+int layout_for(const prt_ctx* c) {
+  const int maxd = c->layout == 4 ? Trav<4>::kMaxDepth : Trav<8>::kMaxDepth;
+  return c->max_depth <= maxd ? c->layout : -1;
+}
+
+int layout_from_env() {
+  const char* e = std::getenv("PRT_BVH");
+  return (e && std::strcmp(e, "4") == 0) ? 4 : 8;
 }
 
 int ensure_instances(prt_ctx* c) {
@@ -186,6 +191,7 @@ int scene_ready(prt_ctx* c, SceneDev& S) {
   if (rc) return rc;
   std::memset(&S, 0, sizeof(S));
   S.nodes = c->nodes.as<Node4>();
+  S.nodes8 = c->nodes8.as<Node8>();
   S.tris = c->tris.as<TriMT>();
   S.fnrm = c->fnrm.as<float4>();
   S.fuv = c->fuv.as<float2>();
@@ -298,8 +304,8 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   if (rc) return rc;
   if (!c->have_camera) return fail(PRT_ERR_NOT_READY, "no camera: call prt_set_camera");
   if (!c->have_lights) return fail(PRT_ERR_NOT_READY, "no lights: call prt_set_lights");
-  const int stack = stack_for(c);
-  if (stack < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
+  const int layout = layout_for(c);
+  if (layout < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
   rc = ensure_state(c, p->width, p->height);
   if (rc) return rc;
   const int32_t F = frames_of(p);
@@ -309,7 +315,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   TraceArgs A;
   A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
   A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F;
-  LaunchCfg L{c->stream, stack};
+  LaunchCfg L{c->stream, layout};
   const bool mega = use_megakernel();
   const uint32_t iters = (uint32_t)p->bounces * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
   if (!mega && iters > (uint32_t)kMaxIters) return fail(PRT_ERR_UNSUPPORTED, "too many wavefront iterations");
@@ -415,7 +421,7 @@ int prt_destroy(prt_ctx* c) {
   if (!c) return PRT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->texels, &c->tex, &c->nodes, &c->tris, &c->fnrm, &c->fuv, &c->vidx, &c->vert, &c->facen,
+  for (DevBuf* b : {&c->texels, &c->tex, &c->nodes, &c->nodes8, &c->tris, &c->fnrm, &c->fuv, &c->vidx, &c->vert, &c->facen,
                     &c->mesh, &c->inst, &c->sky, &c->acc, &c->nsamp, &c->dist, &c->frames, &c->avg, &c->rgb8,
                     &c->counters, &c->hits})
     b->release();
@@ -456,7 +462,9 @@ int prt_set_textures(prt_ctx* c, const prt_texture* t, int32_t n) {
 
 int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
   if (!c || !m || n <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad meshes");
+  const int layout = layout_from_env();
   std::vector<Node4> nodes;
+  std::vector<Node8> nodes8;
   std::vector<TriMT> tris;
   std::vector<float4> fnrm;
   std::vector<float2> fuv;
@@ -484,20 +492,42 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
     }
     for (int64_t k = 0; k < 3 * (int64_t)M.tri_count; k++)
       if (M.indices[k] < 0 || M.indices[k] >= M.vertex_count) return fail(PRT_ERR_INVALID_ARGUMENT, "index out of range");
-    BuiltBlas b = build_blas(M.triangles, M.tri_count, 4);
-    const uint32_t node_base = (uint32_t)nodes.size(), tri_base = (uint32_t)tris.size();
-    if ((uint64_t)tri_base + b.tris.size() >= (1u << 29)) return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
-    for (Node4& nd : b.nodes) {
-      for (int k = 0; k < 4; k++) {
-        uint32_t& ch = nd.child[k];
-        if (ch == kEmptyChild) continue;
-        if (ch & kLeafBit) ch = make_leaf(((ch >> 2) & 0x1FFFFFFFu) + tri_base, (ch & 3u) + 1u);
-        else ch += node_base;
+    const uint32_t tri_base = (uint32_t)tris.size();
+    float bmin[3], bmax[3];
+    int depth = 0;
+    int64_t nnodes = 0, nleaves = 0;
+    if (layout == 4) {
+      BuiltBlas b = build_blas(M.triangles, M.tri_count, 4);
+      const uint32_t node_base = (uint32_t)nodes.size();
+      if ((uint64_t)tri_base + b.tris.size() >= (1u << 29)) return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
+      for (Node4& nd : b.nodes) {
+        for (int k = 0; k < 4; k++) {
+          uint32_t& ch = nd.child[k];
+          if (ch == kEmptyChild) continue;
+          if (ch & kLeafBit) ch = make_leaf(((ch >> 2) & 0x1FFFFFFFu) + tri_base, (ch & 3u) + 1u);
+          else ch += node_base;
+        }
       }
+      nodes.insert(nodes.end(), b.nodes.begin(), b.nodes.end());
+      tris.insert(tris.end(), b.tris.begin(), b.tris.end());
+      mh[i].root = node_base;
+      std::memcpy(bmin, b.bmin, sizeof(bmin)); std::memcpy(bmax, b.bmax, sizeof(bmax));
+      depth = b.depth; nnodes = (int64_t)b.nodes.size(); nleaves = b.leaves;
+    } else {
+      BuiltBlas8 b = build_blas8(M.triangles, M.tri_count, 3);
+      const uint32_t node_base = (uint32_t)nodes8.size();
+      if ((uint64_t)tri_base + b.tris.size() >= (1ull << 32) || (uint64_t)node_base + b.nodes.size() >= (1ull << 32))
+        return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
+      for (Node8& nd : b.nodes) {
+        nd.child_base += node_base;
+        nd.tri_base += tri_base;
+      }
+      nodes8.insert(nodes8.end(), b.nodes.begin(), b.nodes.end());
+      tris.insert(tris.end(), b.tris.begin(), b.tris.end());
+      mh[i].root = node_base;
+      std::memcpy(bmin, b.bmin, sizeof(bmin)); std::memcpy(bmax, b.bmax, sizeof(bmax));
+      depth = b.depth; nnodes = (int64_t)b.nodes.size(); nleaves = b.leaves;
     }
-    nodes.insert(nodes.end(), b.nodes.begin(), b.nodes.end());
-    tris.insert(tris.end(), b.tris.begin(), b.tris.end());
-    mh[i].root = node_base;
     mh[i].prim_base = (uint32_t)(fuv.size() / 3);
     mh[i].vert_base = (uint32_t)(vert.size() / 3);
     mh[i].tri_count = (uint32_t)M.tri_count;
@@ -511,15 +541,18 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
     }
     vert.insert(vert.end(), M.vertices, M.vertices + 3 * (size_t)M.vertex_count);
     facen.insert(facen.end(), M.face_normals, M.face_normals + 3 * T);
-    for (int k = 0; k < 3; k++) { info[i].bmin[k] = b.bmin[k]; info[i].bmax[k] = b.bmax[k]; }
-    info[i].depth = b.depth;
-    info[i].nodes = (int64_t)b.nodes.size();
-    info[i].leaves = b.leaves;
+    for (int k = 0; k < 3; k++) { info[i].bmin[k] = bmin[k]; info[i].bmax[k] = bmax[k]; }
+    info[i].depth = depth;
+    info[i].nodes = nnodes;
+    info[i].leaves = nleaves;
     info[i].tris = M.tri_count;
-    maxd = std::max(maxd, b.depth);
+    maxd = std::max(maxd, depth);
   }
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(upload(c->nodes, nodes.data(), nodes.size() * sizeof(Node4)));
+  c->nodes.release();
+  c->nodes8.release();
+  if (layout == 4) HIP_TRY(upload(c->nodes, nodes.data(), nodes.size() * sizeof(Node4)));
+  else HIP_TRY(upload(c->nodes8, nodes8.data(), nodes8.size() * sizeof(Node8)));
   HIP_TRY(upload(c->tris, tris.data(), tris.size() * sizeof(TriMT)));
   HIP_TRY(upload(c->fnrm, fnrm.data(), fnrm.size() * sizeof(float4)));
   HIP_TRY(upload(c->fuv, fuv.data(), fuv.size() * sizeof(float2)));
@@ -530,6 +563,7 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
   c->mesh_host = mh;
   c->mesh_info = info;
   c->max_depth = maxd;
+  c->layout = layout;
   c->inst_dirty = true;
   return PRT_OK;
 }
@@ -664,7 +698,7 @@ int prt_untile(prt_ctx* c, const float* gathered, int32_t W, int32_t H, int32_t 
   int rc = prt_tile_buffer_pixels(W, H, ts, world, &per);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
-  LaunchCfg L{c->stream, 24};
+  LaunchCfg L{c->stream, c->layout};
   HIP_TRY(launch_untile(L, W, H, ts, world, (uint32_t)per, reinterpret_cast<const float4*>(gathered),
                         reinterpret_cast<float4*>(avg_dev), rgb8_dev));
   return PRT_OK;
@@ -677,8 +711,8 @@ int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t 
   int rc = scene_ready(c, S);
   if (rc) return rc;
   if (!c->have_camera) return fail(PRT_ERR_NOT_READY, "no camera");
-  const int stack = stack_for(c);
-  if (stack < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
+  const int layout = layout_for(c);
+  if (layout < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
   const TileMap M = make_tilemap(W, H, 8, 0, 1);
   const size_t n = (size_t)W * H;
   HitOut* out = reinterpret_cast<HitOut*>(hits);
@@ -686,7 +720,7 @@ int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t 
   if (!dev_out) { HIP_TRY(c->hits.ensure(n * sizeof(HitOut))); out = c->hits.as<HitOut>(); }
   HIP_TRY(c->counters.ensure(sizeof(Counters)));
   HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
-  LaunchCfg L{c->stream, stack};
+  LaunchCfg L{c->stream, layout};
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   HIP_TRY(launch_primary_hits(L, S, M, out, c->counters.as<Counters>()));
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
@@ -716,8 +750,8 @@ static int ray_query(prt_ctx* c, int32_t n, const float* O, const float* D, cons
   SceneDev S;
   int rc = scene_ready(c, S);
   if (rc) return rc;
-  const int stack = stack_for(c);
-  if (stack < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
+  const int layout = layout_for(c);
+  if (layout < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
   DevBuf dO, dD, dT, dOut;
   auto cleanup = [&]() { dO.release(); dD.release(); dT.release(); dOut.release(); };
   const size_t outb = (size_t)n * (any ? 4 : sizeof(HitOut));
@@ -726,7 +760,7 @@ static int ray_query(prt_ctx* c, int32_t n, const float* O, const float* D, cons
     cleanup();
     return fail(PRT_ERR_OUT_OF_MEMORY, "ray buffers");
   }
-  LaunchCfg L{c->stream, stack};
+  LaunchCfg L{c->stream, layout};
   hipError_t e = any ? launch_occluded(L, S, n, dO.as<float>(), dD.as<float>(), dT.as<float>(), dOut.as<int32_t>())
                      : launch_intersect(L, S, n, dO.as<float>(), dD.as<float>(), tmax ? dT.as<float>() : nullptr,
                                         dOut.as<HitOut>());
@@ -753,7 +787,7 @@ int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
     info->triangles += m.tris;
   }
   info->max_depth = c->max_depth;
-  info->device_bytes = (int64_t)(c->nodes.bytes + c->tris.bytes + c->fnrm.bytes + c->fuv.bytes + c->vidx.bytes +
+  info->device_bytes = (int64_t)(c->nodes.bytes + c->nodes8.bytes + c->tris.bytes + c->fnrm.bytes + c->fuv.bytes + c->vidx.bytes +
                                  c->vert.bytes + c->facen.bytes + c->texels.bytes + c->sky.bytes + c->inst.bytes);
   return PRT_OK;
 }

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "prt_kernels.h"
+#include "prt_traverse8.h"
 
 namespace prt {
 
@@ -15,7 +16,7 @@ struct HitOut {
 };
 struct LaunchCfg {
   hipStream_t stream;
-  int stack;  // LDS stack entries per lane: 24 or 48
+  int layout;  // BLAS layout: 4 (Node4) or 8 (Node8, default)
 };
 
 // wavefront pipeline buffers (SoA over n work items; R/T hold (bounces-1) x n entries)

@@ -27,7 +27,7 @@ __device__ __forceinline__ void wave_count(Counters* c, uint32_t seg, uint32_t s
 }
 
 // Renderer::Trace, iterative.  Returns radiance; *t_primary = closest-hit t of the first segment.
-template <int STACK>
+template <int BV>
 __device__ V3 trace_path(const SceneDev& S, const TraceArgs& A, Ray r, uint32_t& seed, float* t_primary,
                          uint32_t& nseg, uint32_t& nshadow, uint32_t* stk) {
   V3 R[kMaxBounces], T[kMaxBounces];
@@ -36,7 +36,7 @@ __device__ V3 trace_path(const SceneDev& S, const TraceArgs& A, Ray r, uint32_t&
   const uint32_t fl = A.flags;
   for (int depth = 0;; depth++) {
     if (depth >= A.bounces) { Lend = v3(0.0f, 0.0f, 0.0f); break; }                   // :152
-    const Hit h = scene_closest<STACK, kBlock>(S, r, kFar, stk);                         // :157
+    const Hit h = Trav<BV>::template closest<kBlock>(S, r, kFar, stk);                         // :157
     nseg++;
     if (depth == 0 && t_primary) *t_primary = h.t;
     if (h.t >= kFar) { Lend = (fl & kSkybox) ? sample_sky(S, r.D) : v3(0.0f, 0.0f, 0.0f); break; }  // :159
@@ -50,7 +50,7 @@ __device__ V3 trace_path(const SceneDev& S, const TraceArgs& A, Ray r, uint32_t&
     V3 f[4];
     const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed, f, [&](int k, const Ray& sr, float tmax) {
       nshadow++;
-      if (!scene_anyhit<STACK, kBlock>(S, sr, tmax, stk)) vis |= 1u << k;
+      if (!Trav<BV>::template anyhit<kBlock>(S, sr, tmax, stk)) vis |= 1u << k;
     });
     const V3 result = nee_resolve(kind, vis, e, brdf, f, fl);
     if (depth == A.bounces - 1) { Lend = result; break; }                                 // :329
@@ -66,10 +66,10 @@ __device__ V3 trace_path(const SceneDev& S, const TraceArgs& A, Ray r, uint32_t&
   return L;
 }
 
-template <int STACK>
+template <int BV>
 __global__ void __launch_bounds__(kBlock) k_trace_frames(SceneDev S, TraceArgs A, TileMap M, float4* __restrict__ out,
                                                          Counters* __restrict__ cnt) {
-  __shared__ uint32_t lds_stack[STACK * kBlock];
+  __shared__ uint32_t lds_stack[Trav<BV>::kWords * kBlock];
   uint32_t* stk = lds_stack + threadIdx.x;
   const uint64_t item = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t total = (uint64_t)M.items * (uint64_t)A.frames;
@@ -86,11 +86,11 @@ __global__ void __launch_bounds__(kBlock) k_trace_frames(SceneDev S, TraceArgs A
       if (A.flags & kAA) {                                                                 // :59-66
         const float jx = random_float(seed), jy = random_float(seed);
         const Ray r2 = primary_ray(S, (float)x + jx, (float)y + jy, A.W, A.H);
-        const V3 s1 = trace_path<STACK>(S, A, r1, seed, &t1, nseg, nsh, stk);
-        const V3 s2 = trace_path<STACK>(S, A, r2, seed, nullptr, nseg, nsh, stk);
+        const V3 s1 = trace_path<BV>(S, A, r1, seed, &t1, nseg, nsh, stk);
+        const V3 s2 = trace_path<BV>(S, A, r2, seed, nullptr, nseg, nsh, stk);
         res = 0.5f * (s1 + s2);
       } else {
-        res = trace_path<STACK>(S, A, r1, seed, &t1, nseg, nsh, stk);
+        res = trace_path<BV>(S, A, r1, seed, &t1, nseg, nsh, stk);
       }
       if (A.flags & kGamma) res = v3(sqrtf(res.x), sqrtf(res.y), sqrtf(res.z));          // :73-79
       out[item] = make_float4(res.x, res.y, res.z, t1);
@@ -168,10 +168,10 @@ __global__ void __launch_bounds__(kBlock) k_untile(int32_t W, int32_t H, int32_t
 
 // ---- geometry-only kernels
 
-template <int STACK>
+template <int BV>
 __global__ void __launch_bounds__(kBlock) k_primary_hits(SceneDev S, TileMap M, HitOut* __restrict__ out,
                                                          Counters* __restrict__ cnt) {
-  __shared__ uint32_t lds_stack[STACK * kBlock];
+  __shared__ uint32_t lds_stack[Trav<BV>::kWords * kBlock];
   uint32_t* stk = lds_stack + threadIdx.x;
   const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
   uint32_t nseg = 0;
@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(kBlock) k_primary_hits(SceneDev S, TileMap M, 
     int32_t x, y;
     if (item_pixel(M, r, x, y)) {
       const Ray ray = primary_ray(S, (float)x, (float)y, M.W, M.H);
-      const Hit h = scene_closest<STACK, kBlock>(S, ray, kFar, stk);
+      const Hit h = Trav<BV>::template closest<kBlock>(S, ray, kFar, stk);
       nseg = 1;
       HitOut o;
       o.t = h.t; o.u = h.u; o.v = h.v; o.prim = h.prim; o.inst = h.inst;
@@ -189,31 +189,31 @@ __global__ void __launch_bounds__(kBlock) k_primary_hits(SceneDev S, TileMap M, 
   wave_count(cnt, nseg, 0);
 }
 
-template <int STACK>
+template <int BV>
 __global__ void __launch_bounds__(kBlock) k_intersect(SceneDev S, int32_t n, const float* __restrict__ O,
                                                       const float* __restrict__ D, const float* __restrict__ tmax,
                                                       HitOut* __restrict__ out) {
-  __shared__ uint32_t lds_stack[STACK * kBlock];
+  __shared__ uint32_t lds_stack[Trav<BV>::kWords * kBlock];
   uint32_t* stk = lds_stack + threadIdx.x;
   const int32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const Ray r = make_ray(v3(O[3 * i], O[3 * i + 1], O[3 * i + 2]), v3(D[3 * i], D[3 * i + 1], D[3 * i + 2]));
-  const Hit h = scene_closest<STACK, kBlock>(S, r, tmax ? tmax[i] : kFar, stk);
+  const Hit h = Trav<BV>::template closest<kBlock>(S, r, tmax ? tmax[i] : kFar, stk);
   HitOut o;
   o.t = h.t; o.u = h.u; o.v = h.v; o.prim = h.prim; o.inst = h.inst;
   out[i] = o;
 }
 
-template <int STACK>
+template <int BV>
 __global__ void __launch_bounds__(kBlock) k_occluded(SceneDev S, int32_t n, const float* __restrict__ O,
                                                      const float* __restrict__ D, const float* __restrict__ tmax,
                                                      int32_t* __restrict__ out) {
-  __shared__ uint32_t lds_stack[STACK * kBlock];
+  __shared__ uint32_t lds_stack[Trav<BV>::kWords * kBlock];
   uint32_t* stk = lds_stack + threadIdx.x;
   const int32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const Ray r = make_ray(v3(O[3 * i], O[3 * i + 1], O[3 * i + 2]), v3(D[3 * i], D[3 * i + 1], D[3 * i + 2]));
-  out[i] = scene_anyhit<STACK, kBlock>(S, r, tmax[i], stk) ? 1 : 0;
+  out[i] = Trav<BV>::template anyhit<kBlock>(S, r, tmax[i], stk) ? 1 : 0;
 }
 
 // ---- launchers (host)
@@ -223,10 +223,10 @@ hipError_t launch_trace_frames(const LaunchCfg& c, const SceneDev& S, const Trac
                                float4* out, Counters* cnt) {
   const uint64_t total = (uint64_t)M.items * (uint64_t)A.frames;
   if (total == 0) return hipSuccess;
-  if (c.stack <= 24)
-    hipLaunchKernelGGL(k_trace_frames<24>, dim3(grid_of(total)), dim3(kBlock), 0, c.stream, S, A, M, out, cnt);
+  if (c.layout == 4)
+    hipLaunchKernelGGL(k_trace_frames<4>, dim3(grid_of(total)), dim3(kBlock), 0, c.stream, S, A, M, out, cnt);
   else
-    hipLaunchKernelGGL(k_trace_frames<48>, dim3(grid_of(total)), dim3(kBlock), 0, c.stream, S, A, M, out, cnt);
+    hipLaunchKernelGGL(k_trace_frames<8>, dim3(grid_of(total)), dim3(kBlock), 0, c.stream, S, A, M, out, cnt);
   return hipGetLastError();
 }
 
@@ -249,30 +249,30 @@ hipError_t launch_untile(const LaunchCfg& c, int32_t W, int32_t H, int32_t ts, i
 
 hipError_t launch_primary_hits(const LaunchCfg& c, const SceneDev& S, const TileMap& M, HitOut* out, Counters* cnt) {
   if (M.items == 0) return hipSuccess;
-  if (c.stack <= 24)
-    hipLaunchKernelGGL(k_primary_hits<24>, dim3(grid_of(M.items)), dim3(kBlock), 0, c.stream, S, M, out, cnt);
+  if (c.layout == 4)
+    hipLaunchKernelGGL(k_primary_hits<4>, dim3(grid_of(M.items)), dim3(kBlock), 0, c.stream, S, M, out, cnt);
   else
-    hipLaunchKernelGGL(k_primary_hits<48>, dim3(grid_of(M.items)), dim3(kBlock), 0, c.stream, S, M, out, cnt);
+    hipLaunchKernelGGL(k_primary_hits<8>, dim3(grid_of(M.items)), dim3(kBlock), 0, c.stream, S, M, out, cnt);
   return hipGetLastError();
 }
 
 hipError_t launch_intersect(const LaunchCfg& c, const SceneDev& S, int32_t n, const float* O, const float* D,
                             const float* tmax, HitOut* out) {
   if (n <= 0) return hipSuccess;
-  if (c.stack <= 24)
-    hipLaunchKernelGGL(k_intersect<24>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
+  if (c.layout == 4)
+    hipLaunchKernelGGL(k_intersect<4>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
   else
-    hipLaunchKernelGGL(k_intersect<48>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
+    hipLaunchKernelGGL(k_intersect<8>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
   return hipGetLastError();
 }
 
 hipError_t launch_occluded(const LaunchCfg& c, const SceneDev& S, int32_t n, const float* O, const float* D,
                            const float* tmax, int32_t* out) {
   if (n <= 0) return hipSuccess;
-  if (c.stack <= 24)
-    hipLaunchKernelGGL(k_occluded<24>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
+  if (c.layout == 4)
+    hipLaunchKernelGGL(k_occluded<4>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
   else
-    hipLaunchKernelGGL(k_occluded<48>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
+    hipLaunchKernelGGL(k_occluded<8>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
   return hipGetLastError();
 }
 

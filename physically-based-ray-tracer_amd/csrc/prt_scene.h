@@ -44,6 +44,7 @@ constexpr int kMaxInstances = 64;
 
 struct SceneDev {
   const Node4* nodes;
+  const Node8* nodes8;  // Node8 BLASes (layout 8); root indices in MeshDev.root refer to the active layout
   const TriMT* tris;
   const float4* fnrm;
   const float2* fuv;

@@ -1,0 +1,178 @@
+// prt_traverse8.h -- 8-wide compressed-BVH traversal (one lane = one ray), the default BLAS layout.
+//
+// Same contract as prt_traverse.h (hit rule, conservative boxes); the node format is Node8
+// (bvh_build.h).  Per visited node: 5 x 16-B loads, 8 quantised child slabs, leaf children's
+// triangles tested on the spot, interior hits kept as one (child_base, ordered 8-bit mask) group.
+// The current group lives in registers; a group is pushed to the LDS stack only when a new node
+// has interior hits while the current group still has unvisited children, so the stack never holds
+// more than one entry per tree level.
+#pragma once
+#include "prt_traverse.h"
+
+namespace prt {
+
+// ray-invariant slab set-up for one node
+struct Slab8 {
+  float ax, ay, az;  // (p - O) * rD
+  float bx, by, bz;  // 2^(e-127) * rD  (exact: power-of-two scale)
+};
+
+__device__ __forceinline__ float byte_f(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xFFu); }
+
+// hit mask (physical slots) of the 8 children; near/far plane choice by the sign of rD
+__device__ __forceinline__ uint32_t node8_hits(const uint4& a, const uint4& c, const uint4& d, const uint4& e,
+                                               const V3& O, const V3& rD, float tlimit) {
+  const float sx = __uint_as_float((a.w & 0xFFu) << 23), sy = __uint_as_float(((a.w >> 8) & 0xFFu) << 23),
+              sz = __uint_as_float(((a.w >> 16) & 0xFFu) << 23);
+  const float ax = (__uint_as_float(a.x) - O.x) * rD.x, ay = (__uint_as_float(a.y) - O.y) * rD.y,
+              az = (__uint_as_float(a.z) - O.z) * rD.z;
+  const float bx = sx * rD.x, by = sy * rD.y, bz = sz * rD.z;
+  // near / far quantised planes per axis: words (lo0-3, lo4-7) / (hi0-3, hi4-7)
+  const bool px = rD.x >= 0.0f, py = rD.y >= 0.0f, pz = rD.z >= 0.0f;
+  const uint32_t nx0 = px ? c.x : d.z, nx1 = px ? c.y : d.w, fx0 = px ? d.z : c.x, fx1 = px ? d.w : c.y;
+  const uint32_t ny0 = py ? c.z : e.x, ny1 = py ? c.w : e.y, fy0 = py ? e.x : c.z, fy1 = py ? e.y : c.w;
+  const uint32_t nz0 = pz ? d.x : e.z, nz1 = pz ? d.y : e.w, fz0 = pz ? e.z : d.x, fz1 = pz ? e.w : d.y;
+  uint32_t hits = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int b = k & 3;
+    const uint32_t wnx = k < 4 ? nx0 : nx1, wny = k < 4 ? ny0 : ny1, wnz = k < 4 ? nz0 : nz1;
+    const uint32_t wfx = k < 4 ? fx0 : fx1, wfy = k < 4 ? fy0 : fy1, wfz = k < 4 ? fz0 : fz1;
+    const float tnx = __builtin_fmaf(byte_f(wnx, b), bx, ax), tfx = __builtin_fmaf(byte_f(wfx, b), bx, ax);
+    const float tny = __builtin_fmaf(byte_f(wny, b), by, ay), tfy = __builtin_fmaf(byte_f(wfy, b), by, ay);
+    const float tnz = __builtin_fmaf(byte_f(wnz, b), bz, az), tfz = __builtin_fmaf(byte_f(wfz, b), bz, az);
+    const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f)) * kNearPad;
+    const float tf = fminf(fminf(tfx, tfy), tfz) * kFarPad;
+    if (tn <= tf && tn <= tlimit) hits |= 1u << k;
+  }
+  return hits;
+}
+
+// physical-slot mask -> traversal-order mask (bit k ^ oct)
+__device__ __forceinline__ uint32_t order_mask(uint32_t m, uint32_t oct) {
+  if (oct & 1u) m = ((m & 0x55u) << 1) | ((m >> 1) & 0x55u);
+  if (oct & 2u) m = ((m & 0x33u) << 2) | ((m >> 2) & 0x33u);
+  if (oct & 4u) m = ((m & 0x0Fu) << 4) | ((m >> 4) & 0x0Fu);
+  return m;
+}
+
+template <int STACK, int BLOCK, bool ANY>
+__device__ __forceinline__ bool blas_traverse8(const Node8* __restrict__ nodes, const TriMT* __restrict__ tris,
+                                               uint32_t root, const V3& O, const V3& D, const V3& rD, uint32_t inst,
+                                               Hit& h, uint32_t* __restrict__ stk) {
+  const uint32_t oct = (rD.x < 0.0f ? 1u : 0u) | (rD.y < 0.0f ? 2u : 0u) | (rD.z < 0.0f ? 4u : 0u);
+  uint32_t gbase = 0, gmask = 0, gimask = 0;  // current group: unvisited interior children (ordered bits)
+  uint32_t node = root;
+  int sp = 0;
+  while (true) {
+    {
+      const uint4* np = reinterpret_cast<const uint4*>(nodes + node);
+      const uint4 a = np[0], b = np[1], c = np[2], d = np[3], e = np[4];
+      const uint32_t imask = a.w >> 24;
+      const uint32_t hits = node8_hits(a, c, d, e, O, rD, h.t);
+      uint32_t lhit = hits & ~imask;
+      while (lhit) {  // leaf children: test their triangles now
+        const uint32_t k = __builtin_ctz(lhit);
+        lhit &= lhit - 1u;
+        const uint32_t meta = ((k < 4 ? b.z : b.w) >> (8 * (k & 3))) & 0xFFu;
+        const uint32_t first = b.y + (meta >> 3), cnt = meta & 7u;
+        for (uint32_t i = 0; i < cnt; i++) {
+          float t, u, v;
+          uint32_t prim;
+          if (mt_test(tris + first + i, O, D, t, u, v, prim)) {
+            if (ANY) {
+              if (t < h.t) return true;  // tiny_bvh.h:6594 (h.t holds tmax)
+            } else if (t < h.t || (t == h.t && (inst < h.inst || (inst == h.inst && prim < h.prim)))) {
+              h.t = t; h.u = u; h.v = v; h.prim = prim; h.inst = inst;
+            }
+          }
+        }
+      }
+      const uint32_t ihit = hits & imask;
+      if (ihit) {
+        if (gmask && sp < STACK) {
+          stk[(2 * sp) * BLOCK] = gbase;
+          stk[(2 * sp + 1) * BLOCK] = gmask | (gimask << 8);
+          sp++;
+        }
+        gbase = b.x;
+        gmask = order_mask(ihit, oct);
+        gimask = imask;
+      }
+    }
+    if (!gmask) {
+      if (sp == 0) break;
+      sp--;
+      gbase = stk[(2 * sp) * BLOCK];
+      const uint32_t m = stk[(2 * sp + 1) * BLOCK];
+      gmask = m & 0xFFu;
+      gimask = m >> 8;
+    }
+    const uint32_t bit = __builtin_ctz(gmask);
+    gmask &= gmask - 1u;
+    const uint32_t k = bit ^ oct;
+    node = gbase + __builtin_popcount(gimask & ((1u << k) - 1u));
+  }
+  return false;
+}
+
+template <int STACK, int BLOCK>
+__device__ __forceinline__ Hit scene_closest8(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
+  Hit h;
+  h.t = tmax; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;
+  for (int i = 0; i < S.ninst; i++) {
+    const InstDev& I = S.inst[i];
+    if (slab1(I.bmin, I.bmax, r.O, r.rD, h.t) >= kFar) continue;
+    const V3 Oi = xform_point(r.O, I.inv), Di = xform_vector(r.D, I.inv);
+    const V3 rDi = v3(safercp(Di.x), safercp(Di.y), safercp(Di.z));
+    blas_traverse8<STACK, BLOCK, false>(S.nodes8, S.tris, S.mesh[I.mesh].root, Oi, Di, rDi, (uint32_t)i, h, stk);
+  }
+  return h;
+}
+
+template <int STACK, int BLOCK>
+__device__ __forceinline__ bool scene_anyhit8(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
+  for (int i = 0; i < S.ninst; i++) {
+    const InstDev& I = S.inst[i];
+    if (slab1(I.bmin, I.bmax, r.O, r.rD, tmax) >= kFar) continue;
+    const V3 Oi = xform_point(r.O, I.inv), Di = xform_vector(r.D, I.inv);
+    const V3 rDi = v3(safercp(Di.x), safercp(Di.y), safercp(Di.z));
+    Hit h;
+    h.t = tmax;
+    if (blas_traverse8<STACK, BLOCK, true>(S.nodes8, S.tris, S.mesh[I.mesh].root, Oi, Di, rDi, 0u, h, stk)) return true;
+  }
+  return false;
+}
+
+// BLAS layout selection for the kernels: 4 = Node4 (128-B fp32 nodes, per-node LDS stack of 48
+// entries), 8 = Node8 (80-B compressed nodes, 16 two-word group entries).  kWords = LDS words / lane.
+template <int LAYOUT>
+struct Trav;
+template <>
+struct Trav<4> {
+  static constexpr int kWords = 48;
+  static constexpr int kMaxDepth = 16;  // 3 pushes per level
+  template <int BLOCK>
+  __device__ static __forceinline__ Hit closest(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
+    return scene_closest<48, BLOCK>(S, r, tmax, stk);
+  }
+  template <int BLOCK>
+  __device__ static __forceinline__ bool anyhit(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
+    return scene_anyhit<48, BLOCK>(S, r, tmax, stk);
+  }
+};
+template <>
+struct Trav<8> {
+  static constexpr int kWords = 32;
+  static constexpr int kMaxDepth = 16;  // one group per level
+  template <int BLOCK>
+  __device__ static __forceinline__ Hit closest(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
+    return scene_closest8<16, BLOCK>(S, r, tmax, stk);
+  }
+  template <int BLOCK>
+  __device__ static __forceinline__ bool anyhit(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
+    return scene_anyhit8<16, BLOCK>(S, r, tmax, stk);
+  }
+};
+
+}  // namespace prt

@@ -145,9 +145,9 @@ __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, T
 }
 
 // ---- closest hit (one-wave blocks, static interleaved chunks of the live queue)
-template <int STACK>
+template <int BV>
 __global__ void __launch_bounds__(64) k_extend(SceneDev S, WaveBufs B, uint32_t iter) {
-  __shared__ uint32_t lds_stack[STACK * 64];
+  __shared__ uint32_t lds_stack[Trav<BV>::kWords * 64];
   __shared__ uint32_t pref[kNSub + 1];
   uint32_t* stk = lds_stack + threadIdx.x;
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(64) k_extend(SceneDev S, WaveBufs B, uint32_t 
       r.O = v3(o.x, o.y, o.z);
       r.D = v3(d.x, d.y, d.z);
       r.rD = v3(safercp(d.x), safercp(d.y), safercp(d.z));
-      const Hit h = scene_closest<STACK, 64>(S, r, kFar, stk);
+      const Hit h = Trav<BV>::template closest<64>(S, r, kFar, stk);
       B.hit[item] = make_float4(h.t, h.u, h.v, __uint_as_float(pack_hit(h.prim, h.inst)));
     }
   }
@@ -252,9 +252,9 @@ __global__ void __launch_bounds__(kBlock) k_shade(SceneDev S, TraceArgs A, WaveB
 }
 
 // ---- any hit for the shadow queue
-template <int STACK>
+template <int BV>
 __global__ void __launch_bounds__(64) k_shadow(SceneDev S, WaveBufs B, uint32_t iter) {
-  __shared__ uint32_t lds_stack[STACK * 64];
+  __shared__ uint32_t lds_stack[Trav<BV>::kWords * 64];
   __shared__ uint32_t pref[kNSub + 1];
   uint32_t* stk = lds_stack + threadIdx.x;
   uint8_t* vis8 = reinterpret_cast<uint8_t*>(B.vis);
@@ -271,7 +271,7 @@ __global__ void __launch_bounds__(64) k_shadow(SceneDev S, WaveBufs B, uint32_t 
       r.O = v3(o.x, o.y, o.z);
       r.D = v3(d.x, d.y, d.z);
       r.rD = v3(safercp(d.x), safercp(d.y), safercp(d.z));
-      if (!scene_anyhit<STACK, 64>(S, r, o.w, stk)) vis8[__float_as_uint(d.w)] = 1;
+      if (!Trav<BV>::template anyhit<64>(S, r, o.w, stk)) vis8[__float_as_uint(d.w)] = 1;
     }
   }
 }
@@ -363,13 +363,13 @@ hipError_t launch_wavefront(const LaunchCfg& c, const SceneDev& S, const TraceAr
   const uint32_t iters = (uint32_t)A.bounces * ((A.flags & kAA) ? 2u : 1u);
   for (uint32_t it = 0; it < iters; it++) {
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 0], c.stream);
-    if (c.stack <= 24) hipLaunchKernelGGL(k_extend<24>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
-    else hipLaunchKernelGGL(k_extend<48>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    if (c.layout == 4) hipLaunchKernelGGL(k_extend<4>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    else hipLaunchKernelGGL(k_extend<8>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
     hipLaunchKernelGGL(k_shade, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 2], c.stream);
-    if (c.stack <= 24) hipLaunchKernelGGL(k_shadow<24>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
-    else hipLaunchKernelGGL(k_shadow<48>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    if (c.layout == 4) hipLaunchKernelGGL(k_shadow<4>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    else hipLaunchKernelGGL(k_shadow<8>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 3], c.stream);
     hipLaunchKernelGGL(k_resolve, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it, out);
   }

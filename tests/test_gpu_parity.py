@@ -12,9 +12,12 @@ from prt import scenes
 pytestmark = pytest.mark.gpu
 
 
-def test_basic_float_ops_bitexact(gpu_ctx):
-    """sqrt / division / transcendental rounding used by the shading path agree with the CPU: checked
+@pytest.mark.parametrize("bvh", ["8", "4"])
+def test_basic_float_ops_bitexact(gpu_ctx, monkeypatch, bvh):
+    """Both BLAS layouts (PRT_BVH=8 compressed 8-wide, default; PRT_BVH=4 fp32 4-wide).
+    sqrt / division / transcendental rounding used by the shading path agree with the CPU: checked
     indirectly through BRDF-heavy renders below; here the primary-ray hits (pure +,-,*,/,sqrt)."""
+    monkeypatch.setenv("PRT_BVH", bvh)
     sd = scenes.config_c2()
     W, H = 1280, 720
     gpu_scene(gpu_ctx, sd, W, H)
@@ -30,7 +33,9 @@ def test_basic_float_ops_bitexact(gpu_ctx):
     assert st.segments == W * H
 
 
-def test_random_rays_closest_and_anyhit(gpu_ctx):
+@pytest.mark.parametrize("bvh", ["8", "4"])
+def test_random_rays_closest_and_anyhit(gpu_ctx, monkeypatch, bvh):
+    monkeypatch.setenv("PRT_BVH", bvh)
     sd = scenes.multi_instance(scenes.config_small(120, 90))
     gpu_scene(gpu_ctx, sd, 64, 64)
     osc = oracle.OracleScene(sd)
@@ -103,6 +108,21 @@ def test_wavefront_equals_megakernel(gpu_ctx, monkeypatch):
     assert s_m.pipeline == 1
     assert np.array_equal(a_w, a_m) and np.array_equal(r_w, r_m)
     assert s_w.segments == s_m.segments and s_w.shadow_rays == s_m.shadow_rays
+
+
+def test_bvh_layouts_render_identical(gpu_ctx, monkeypatch):
+    """The hit rule is BVH-independent (conservative boxes + lexicographic tie-break), so the Node8
+    and Node4 BLAS layouts must render bit-identical frames on the C3 scene."""
+    sd = scenes.config_c3()
+    W, H = 256, 144
+    out = {}
+    for bvh in ("8", "4"):
+        monkeypatch.setenv("PRT_BVH", bvh)
+        gpu_scene(gpu_ctx, sd, W, H)
+        gpu_ctx.reset_accumulation(full=True)
+        out[bvh] = gpu_ctx.render(W, H, 4, 4)
+    assert np.array_equal(out["8"][0], out["4"][0]) and np.array_equal(out["8"][1], out["4"][1])
+    assert out["8"][2].segments == out["4"][2].segments
 
 
 def test_progressive_accumulation(gpu_ctx):
