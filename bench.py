@@ -41,7 +41,7 @@ def algorithmic_bytes_per_ray():
 
 
 def measured_traffic(kernel):
-    """HBM bytes per frame of `kernel` from the committed rocprofv3 PMC passes (profiles/traffic_current.json,
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/traffic_current.json,
     written by scripts/summarize_prof.py; FETCH_SIZE x2 gfx950 correction, MI355X_MICROARCH.md HBM)."""
     f = os.path.join(ROOT, "profiles", "traffic_current.json")
     if not os.path.exists(f):
@@ -49,8 +49,8 @@ def measured_traffic(kernel):
     with open(f) as fh:
         t = json.load(fh)
     for name, d in t.get("kernels", {}).items():
-        if name.split("::")[-1].split("<")[0] == kernel and "hbm_bytes_per_frame" in d:
-            return int(d["hbm_bytes_per_frame"])
+        if name.split("::")[-1].split("<")[0] == kernel and "hbm_bytes_per_launch" in d:
+            return int(d["hbm_bytes_per_launch"])
     return None
 
 
@@ -110,20 +110,14 @@ def main():
     avg = torch.zeros((H * W, 4), dtype=torch.float32, device=dev)
     rgb = torch.zeros(H * W, dtype=torch.int32, device=dev)
     if world > 1:
-        per = ctx.tile_buffer_pixels(W, H, args.tile, world)
-        tiles = torch.zeros((per, 4), dtype=torch.float32, device=dev)
-        gathered = torch.zeros((world, per, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+        shard = prt.tiles.ShardedFrame(ctx, dist, W, H, args.tile, device=dev)
 
     def step(i):
         if world == 1:
             _, _, st = ctx.render(W, H, args.spp, args.bounces, frame_index=2 * i, avg=avg.data_ptr(),
                                   rgb8=rgb.data_ptr(), device_out=True, stats=True)
         else:
-            st = ctx.render_tiles(W, H, args.spp, args.bounces, args.tile, rank, world, tiles.data_ptr(),
-                                  frame_index=2 * i, stats=True)
-            dist.gather(tiles, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                ctx.untile(gathered.data_ptr(), W, H, args.tile, world, avg.data_ptr(), rgb.data_ptr())
+            st = shard.render(args.spp, args.bounces, avg.data_ptr(), rgb.data_ptr(), frame_index=2 * i)
         return st
 
     for i in range(args.warmup):
@@ -133,7 +127,7 @@ def main():
     torch.cuda.synchronize()
     seg = shadow = 0
     ms_trace, ms_closest, ms_anyhit = [], [], []
-    pipeline = 0
+    pipeline = iters = 0
     t0 = time.perf_counter()
     for i in range(args.steps):
         st = step(args.warmup + i)
@@ -143,6 +137,7 @@ def main():
         ms_closest.append(st.ms_closest)
         ms_anyhit.append(st.ms_anyhit)
         pipeline = st.pipeline
+        iters = st.iterations
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -161,13 +156,15 @@ def main():
         ms_step = elapsed * 1000.0 / args.steps
         value = rays / elapsed / 1e6
         bpr, visits = algorithmic_bytes_per_ray()
-        # roofline of the dominant kernel: algorithmic bytes (reference BVH8_CPU visit counts x SURVEY 8d bytes)
-        # over the kernel's HIP-event time, both summed over the frame's launches of that kernel
+        # roofline of the dominant kernel, per launch: algorithmic bytes (reference BVH8_CPU visit counts x
+        # SURVEY 8d bytes) of the rays one launch processes over the kernel's average launch duration (HIP events
+        # recorded on the render stream around every launch; ms_closest / ms_anyhit sum them per frame)
         seg_f, sh_f = seg / args.steps, shadow / args.steps
+        launches = max(1, iters) if pipeline == 0 else 1
         kern = {}
         if pipeline == 0:
-            kern["k_extend"] = (seg_f * bpr["closest"], float(np.mean(ms_closest)))
-            kern["k_shadow"] = (sh_f * bpr["anyhit"], float(np.mean(ms_anyhit)))
+            kern["k_extend"] = (seg_f * bpr["closest"] / launches, float(np.mean(ms_closest)) / launches)
+            kern["k_shadow"] = (sh_f * bpr["anyhit"] / launches, float(np.mean(ms_anyhit)) / launches)
         else:
             kern["k_trace_frames"] = (seg_f * bpr["closest"] + sh_f * bpr["anyhit"], float(np.mean(ms_trace)))
         dom = max(kern, key=lambda k: kern[k][1])
@@ -196,9 +193,9 @@ def main():
                        "mpix_per_s": round(W * H / (ms_step / 1e3) / 1e6, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": dom, "per": "frame (sum over the kernel's launches)",
-                         "kernel_ms": round(kern_ms, 3), "algorithmic_bytes": round(alg_bytes),
-                         "kernels": {k: {"ms": round(v[1], 3), "alg_GBps": round(v[0] / (v[1] / 1e3) / 1e9, 1)
+                         "kernel": dom, "per": f"launch (avg of {launches} launches per frame)",
+                         "launch_ms": round(kern_ms, 4), "algorithmic_bytes": round(alg_bytes),
+                         "kernels": {k: {"launch_ms": round(v[1], 4), "alg_GBps": round(v[0] / (v[1] / 1e3) / 1e9, 1)
                                          if v[1] > 0 else None} for k, v in kern.items()},
                          "bytes_per_ray": {k: round(v, 1) for k, v in bpr.items()}},
         }

@@ -167,6 +167,10 @@ int prt_reset_accumulation(prt_ctx* ctx, int32_t full);
  * [local_tile][tile_size*tile_size] (pixels outside the image are written as 0).
  * prt_tile_buffer_pixels() gives the element count (per rank, equal on all ranks: the max). */
 int prt_tile_buffer_pixels(int32_t width, int32_t height, int32_t tile_size, int32_t world, int64_t* pixels);
+/* host-only: image pixel index (y*width + x) of every element of rank's tile buffer, -1 where the tile
+ * overhangs the image; pixel_of_slot holds prt_tile_buffer_pixels() entries.  No device needed. */
+int prt_tile_pixel_map(int32_t width, int32_t height, int32_t tile_size, int32_t rank, int32_t world,
+                       int32_t* pixel_of_slot);
 int prt_render_tiles(prt_ctx* ctx, const prt_render_params* params, int32_t tile_size, int32_t rank,
                      int32_t world, float* tiles_rgba_device, prt_stats* stats);
 /* rank-0 side: gathered [world][tile_buffer_pixels] float4 device buffer -> W*H avg_rgba + rgb8 (device) */

@@ -675,6 +675,19 @@ int prt_tile_buffer_pixels(int32_t W, int32_t H, int32_t ts, int32_t world, int6
   return PRT_OK;
 }
 
+int prt_tile_pixel_map(int32_t W, int32_t H, int32_t ts, int32_t rank, int32_t world, int32_t* out) {
+  int64_t per = 0;
+  int rc = prt_tile_buffer_pixels(W, H, ts, world, &per);
+  if (rc) return rc;
+  if (!out || rank < 0 || rank >= world) return fail(PRT_ERR_INVALID_ARGUMENT, "bad rank / output");
+  const TileMap M = make_tilemap(W, H, ts, rank, world);
+  for (int64_t r = 0; r < per; r++) {
+    int32_t x = 0, y = 0;
+    out[r] = ((uint64_t)r < M.items && item_pixel(M, (uint32_t)r, x, y)) ? y * W + x : -1;
+  }
+  return PRT_OK;
+}
+
 int prt_render_tiles(prt_ctx* c, const prt_render_params* p, int32_t ts, int32_t rank, int32_t world,
                      float* tiles_dev, prt_stats* stats) {
   if (!c || !tiles_dev) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/tiles is NULL");

@@ -20,7 +20,8 @@ MODE_BRDF, MODE_BASECOLOR, MODE_GEOMETRYNORMAL, MODE_SHADINGNORMAL, MODE_METAL, 
 EXPORTS = [
     "prt_abi_version", "prt_last_error", "prt_device_count", "prt_create", "prt_destroy", "prt_set_stream",
     "prt_set_textures", "prt_set_meshes", "prt_set_instances", "prt_set_lights", "prt_set_sky", "prt_set_camera",
-    "prt_camera_look_at", "prt_render", "prt_reset_accumulation", "prt_tile_buffer_pixels", "prt_render_tiles",
+    "prt_camera_look_at", "prt_render", "prt_reset_accumulation", "prt_tile_buffer_pixels", "prt_tile_pixel_map",
+    "prt_render_tiles",
     "prt_untile", "prt_trace_primary", "prt_intersect", "prt_occluded", "prt_get_scene_info",
 ]
 
@@ -110,6 +111,7 @@ def load():
         "prt_render": ([vp, C.POINTER(RenderParams), vp, vp, u32, C.POINTER(Stats)], C.c_int),
         "prt_reset_accumulation": ([vp, i32], C.c_int),
         "prt_tile_buffer_pixels": ([i32, i32, i32, i32, C.POINTER(C.c_int64)], C.c_int),
+        "prt_tile_pixel_map": ([i32, i32, i32, i32, i32, C.c_void_p], C.c_int),
         "prt_render_tiles": ([vp, C.POINTER(RenderParams), i32, i32, i32, vp, C.POINTER(Stats)], C.c_int),
         "prt_untile": ([vp, vp, i32, i32, i32, i32, vp, vp], C.c_int),
         "prt_trace_primary": ([vp, i32, i32, vp, u32, C.POINTER(Stats)], C.c_int),
