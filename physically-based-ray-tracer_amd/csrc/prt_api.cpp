@@ -140,6 +140,13 @@ int layout_for(const prt_ctx* c) {
   return c->max_depth <= maxd ? c->layout : -1;
 }
 
+int trav_from_env() {
+  const char* e = std::getenv("PRT_TRAV");
+  if (e && std::strcmp(e, "lockstep") == 0) return 1;
+  if (e && std::strcmp(e, "refill32") == 0) return 32;
+  return 16;
+}
+
 int layout_from_env() {
   const char* e = std::getenv("PRT_BVH");
   return (e && std::strcmp(e, "4") == 0) ? 4 : 8;
@@ -315,7 +322,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   TraceArgs A;
   A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
   A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F;
-  LaunchCfg L{c->stream, layout};
+  LaunchCfg L{c->stream, layout, trav_from_env()};
   const bool mega = use_megakernel();
   const uint32_t iters = (uint32_t)p->bounces * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
   if (!mega && iters > (uint32_t)kMaxIters) return fail(PRT_ERR_UNSUPPORTED, "too many wavefront iterations");
@@ -711,7 +718,7 @@ int prt_untile(prt_ctx* c, const float* gathered, int32_t W, int32_t H, int32_t 
   int rc = prt_tile_buffer_pixels(W, H, ts, world, &per);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
-  LaunchCfg L{c->stream, c->layout};
+  LaunchCfg L{c->stream, c->layout, trav_from_env()};
   HIP_TRY(launch_untile(L, W, H, ts, world, (uint32_t)per, reinterpret_cast<const float4*>(gathered),
                         reinterpret_cast<float4*>(avg_dev), rgb8_dev));
   return PRT_OK;
@@ -733,7 +740,7 @@ int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t 
   if (!dev_out) { HIP_TRY(c->hits.ensure(n * sizeof(HitOut))); out = c->hits.as<HitOut>(); }
   HIP_TRY(c->counters.ensure(sizeof(Counters)));
   HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
-  LaunchCfg L{c->stream, layout};
+  LaunchCfg L{c->stream, layout, trav_from_env()};
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   HIP_TRY(launch_primary_hits(L, S, M, out, c->counters.as<Counters>()));
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
@@ -773,7 +780,7 @@ static int ray_query(prt_ctx* c, int32_t n, const float* O, const float* D, cons
     cleanup();
     return fail(PRT_ERR_OUT_OF_MEMORY, "ray buffers");
   }
-  LaunchCfg L{c->stream, layout};
+  LaunchCfg L{c->stream, layout, trav_from_env()};
   hipError_t e = any ? launch_occluded(L, S, n, dO.as<float>(), dD.as<float>(), dT.as<float>(), dOut.as<int32_t>())
                      : launch_intersect(L, S, n, dO.as<float>(), dD.as<float>(), tmax ? dT.as<float>() : nullptr,
                                         dOut.as<HitOut>());

@@ -17,6 +17,8 @@ struct HitOut {
 struct LaunchCfg {
   hipStream_t stream;
   int layout;  // BLAS layout: 4 (Node4) or 8 (Node8, default)
+  int trav;    // Node8 wavefront traversal: 16 / 32 = persistent lanes refilled at that many idle lanes
+               // (default 16), 1 = lock-step one-ray-per-lane kernels (PRT_TRAV=lockstep)
 };
 
 // wavefront pipeline buffers (SoA over n work items; R/T hold (bounces-1) x n entries)

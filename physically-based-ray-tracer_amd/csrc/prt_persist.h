@@ -1,0 +1,151 @@
+// prt_persist.h -- persistent-lane Node8 traversal for the wavefront queues (default traversal kernels).
+//
+// The lock-step loop of prt_traverse8.h runs a wave until its slowest of 64 rays is done, and every
+// node visit waits for the lane with the most leaf triangles.  On the C4 secondary rays that leaves
+// about a third of the lanes busy (scripts/trav_stats.cpp: lane efficiency 0.34 closest, 0.43 any-hit).
+// Here every lane is a small state machine and one loop iteration does, per lane:
+//   refill     lanes without a ray take the next queue entries (once >= kRefill lanes are idle; one
+//              atomic per wave on an XCD-partitioned fetch counter, see prt_wave.hip)
+//   instance   lanes done with a BLAS enter the next instance whose world box the ray hits (TLAS loop)
+//   node       lanes with no pending triangles visit one Node8 node (8 quantised child slabs), keep its
+//              hit leaf children as pending and step to the next interior child / pop the LDS stack
+//   triangle   lanes with pending leaf triangles test one of them (Moeller-Trumbore, prt_traverse.h)
+// so node visits and triangle tests of different lanes share iterations instead of serialising.
+// Results are those of blas_traverse8: the hit rule is order-independent (closest t, then smaller
+// (instance, prim)) and the box tests are conservative, so visiting order cannot change a hit.
+#pragma once
+#include "prt_traverse8.h"
+
+namespace prt {
+
+constexpr uint32_t kNoNode = 0xFFFFFFFFu;
+
+// Persistent traversal of one wave (blockDim.x == 64).  Ray source and sink are callbacks:
+//   fetch(uint32_t* base, uint32_t want) -> uint32_t got   (wave-uniform; called by all lanes)
+//   load(uint32_t g, V3& O, V3& D, float& tmax, uint32_t& tag)  queue entry g -> world ray
+//   finish(uint32_t tag, const Hit& h, bool hit)        closest: h; any-hit: hit = occluded
+template <bool ANY, int STACK, int REFILL, class Fetch, class Load, class Finish>
+__device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
+                                                 Load load, Finish finish) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t lanes_below = (1ull << lane) - 1ull;
+  bool active = false, drained = false;
+  uint32_t tag = 0;
+  V3 Ow = v3(0.0f, 0.0f, 0.0f), Dw = v3(0.0f, 0.0f, 1.0f);  // world ray (instance loop)
+  V3 O = Ow, D = Dw, rD = Dw;                                  // instance-space ray
+  uint32_t oct = 0;
+  Hit h;
+  h.t = kFar; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;
+  int inst = -1;
+  uint32_t node = kNoNode, gbase = 0, gmask = 0, gimask = 0;
+  int sp = 0;
+  uint32_t lhit = 0, ltri = 0, lmeta0 = 0, lmeta1 = 0, tcur = 0, tcnt = 0;  // pending leaf triangles
+  while (true) {
+    // ---- refill idle lanes from the queue
+    const uint64_t idle = __ballot(!active);
+    if (!drained && __popcll(idle) >= (uint32_t)REFILL) {
+      uint32_t base = 0;
+      const uint32_t want = (uint32_t)__popcll(idle);
+      const uint32_t got = fetch(&base, want);
+      if (got == 0) drained = true;
+      if (!active) {
+        const uint32_t rank = (uint32_t)__popcll(idle & lanes_below);
+        if (rank < got) {
+          float tmax;
+          load(base + rank, Ow, Dw, tmax, tag);
+          h.t = tmax; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;
+          inst = -1;
+          node = kNoNode;
+          lhit = 0; tcnt = 0;
+          active = true;
+        }
+      }
+    }
+    if (__ballot(active) == 0) {
+      if (drained) break;
+      continue;
+    }
+    // ---- enter the next instance (TLAS: linear loop over the instance boxes, tiny_bvh.h:2500-2565)
+    if (active && node == kNoNode && lhit == 0 && tcnt == 0) {
+      const V3 rDw = v3(safercp(Dw.x), safercp(Dw.y), safercp(Dw.z));
+      int i = inst + 1;
+      while (i < S.ninst && slab1(S.inst[i].bmin, S.inst[i].bmax, Ow, rDw, h.t) >= kFar) i++;
+      if (i >= S.ninst) {
+        finish(tag, h, false);
+        active = false;
+      } else {
+        const InstDev& I = S.inst[i];
+        inst = i;
+        O = xform_point(Ow, I.inv);
+        D = xform_vector(Dw, I.inv);
+        rD = v3(safercp(D.x), safercp(D.y), safercp(D.z));
+        oct = (rD.x < 0.0f ? 1u : 0u) | (rD.y < 0.0f ? 2u : 0u) | (rD.z < 0.0f ? 4u : 0u);
+        node = S.mesh[I.mesh].root;
+        gmask = 0;
+        sp = 0;
+      }
+    }
+    // ---- one node visit for lanes without pending triangles
+    if (active && node != kNoNode && lhit == 0 && tcnt == 0) {
+      const uint4* np = reinterpret_cast<const uint4*>(S.nodes8 + node);
+      const uint4 a = np[0], b = np[1], c = np[2], d = np[3], e = np[4];
+      const uint32_t imask = a.w >> 24;
+      const uint32_t hits = node8_hits(a, c, d, e, O, rD, h.t);
+      lhit = hits & ~imask;
+      ltri = b.y; lmeta0 = b.z; lmeta1 = b.w;
+      const uint32_t ihit = hits & imask;
+      if (ihit) {
+        if (gmask && sp < STACK) {
+          stk[(2 * sp) * 64] = gbase;
+          stk[(2 * sp + 1) * 64] = gmask | (gimask << 8);
+          sp++;
+        }
+        gbase = b.x;
+        gmask = order_mask(ihit, oct);
+        gimask = imask;
+      }
+      if (!gmask && sp > 0) {
+        sp--;
+        gbase = stk[(2 * sp) * 64];
+        const uint32_t m = stk[(2 * sp + 1) * 64];
+        gmask = m & 0xFFu;
+        gimask = m >> 8;
+      }
+      if (gmask) {
+        const uint32_t bit = __builtin_ctz(gmask);
+        gmask &= gmask - 1u;
+        const uint32_t k = bit ^ oct;
+        node = gbase + __builtin_popcount(gimask & ((1u << k) - 1u));
+      } else {
+        node = kNoNode;
+      }
+    }
+    // ---- one triangle test for lanes with pending leaf triangles
+    if (active && (lhit | tcnt)) {
+      if (tcnt == 0) {
+        const uint32_t k = __builtin_ctz(lhit);
+        lhit &= lhit - 1u;
+        const uint32_t meta = ((k < 4 ? lmeta0 : lmeta1) >> (8 * (k & 3))) & 0xFFu;
+        tcur = ltri + (meta >> 3);
+        tcnt = meta & 7u;
+      }
+      float t, u, v;
+      uint32_t prim;
+      const bool hit = mt_test(S.tris + tcur, O, D, t, u, v, prim);
+      tcur++;
+      tcnt--;
+      if (ANY) {
+        if (hit && t < h.t) {  // tiny_bvh.h:6594 (h.t holds tmax)
+          finish(tag, h, true);
+          active = false;
+          node = kNoNode; lhit = 0; tcnt = 0;
+        }
+      } else if (hit && (t < h.t || (t == h.t && ((uint32_t)inst < h.inst ||
+                                                  ((uint32_t)inst == h.inst && prim < h.prim))))) {
+        h.t = t; h.u = u; h.v = v; h.prim = prim; h.inst = (uint32_t)inst;
+      }
+    }
+  }
+}
+
+}  // namespace prt

@@ -20,6 +20,7 @@
 // holds back its siblings' slots).  All per-item state is SoA in HBM; no host synchronisation.
 #include "prt_launch.h"
 #include "prt_path.h"
+#include "prt_persist.h"
 
 namespace prt {
 
@@ -276,6 +277,73 @@ __global__ void __launch_bounds__(64) k_shadow(SceneDev S, WaveBufs B, uint32_t 
   }
 }
 
+// ---- persistent-lane variants (Node8): lanes refill from the queue as their rays finish (prt_persist.h)
+// wave-uniform fetch of up to `want` consecutive live-range entries from the XCD-partitioned counters
+__device__ __forceinline__ uint32_t fetch_some(uint32_t* fctr, uint32_t total, uint32_t& part, uint32_t* base,
+                                               uint32_t want) {
+  for (uint32_t tries = 0; tries < kParts; tries++) {
+    const uint32_t lo = (uint32_t)(((uint64_t)total * part) / kParts);
+    const uint32_t hi = (uint32_t)(((uint64_t)total * (part + 1)) / kParts);
+    uint32_t off = 0;
+    if (lane_id() == 0) off = (hi > lo) ? atomicAdd(fctr + part * kCtrStride, want) : 0xFFFFFFFFu;
+    off = __shfl(off, 0, 64);
+    if (off != 0xFFFFFFFFu && off < hi - lo) {
+      *base = lo + off;
+      return min(want, hi - lo - off);
+    }
+    part = (part + 1) & (kParts - 1);
+  }
+  return 0;
+}
+
+template <int REFILL>
+__global__ void __launch_bounds__(64) k_extend_p(SceneDev S, WaveBufs B, uint32_t iter) {
+  __shared__ uint32_t lds_stack[Trav<8>::kWords * 64];
+  __shared__ uint32_t pref[kNSub + 1];
+  const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
+  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
+  uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
+  uint32_t part = xcc_id();
+  trav8_persistent<false, 16, REFILL>(
+      S, lds_stack + threadIdx.x,
+      [&](uint32_t* base, uint32_t want) { return fetch_some(fctr, total, part, base, want); },
+      [&](uint32_t g, V3& O, V3& D, float& tmax, uint32_t& tag) {
+        const uint32_t item = q[map_slot(pref, g, B.qcap)];
+        const float4 o = B.ro[item], d = B.rd[item];
+        O = v3(o.x, o.y, o.z);
+        D = v3(d.x, d.y, d.z);
+        tmax = kFar;
+        tag = item;
+      },
+      [&](uint32_t item, const Hit& h, bool) {
+        B.hit[item] = make_float4(h.t, h.u, h.v, __uint_as_float(pack_hit(h.prim, h.inst)));
+      });
+}
+
+template <int REFILL>
+__global__ void __launch_bounds__(64) k_shadow_p(SceneDev S, WaveBufs B, uint32_t iter) {
+  __shared__ uint32_t lds_stack[Trav<8>::kWords * 64];
+  __shared__ uint32_t pref[kNSub + 1];
+  uint8_t* vis8 = reinterpret_cast<uint8_t*>(B.vis);
+  const uint32_t total = load_prefix(B.ctr, iter, 1, pref);
+  uint32_t* fctr = fetch_counters(B.ctr, iter, 1);
+  uint32_t part = xcc_id();
+  trav8_persistent<true, 16, REFILL>(
+      S, lds_stack + threadIdx.x,
+      [&](uint32_t* base, uint32_t want) { return fetch_some(fctr, total, part, base, want); },
+      [&](uint32_t g, V3& O, V3& D, float& tmax, uint32_t& tag) {
+        const uint32_t slot = map_slot(pref, g, B.scap);
+        const float4 o = B.sho[slot], d = B.shd[slot];
+        O = v3(o.x, o.y, o.z);
+        D = v3(d.x, d.y, d.z);
+        tmax = o.w;
+        tag = __float_as_uint(d.w);
+      },
+      [&](uint32_t tag, const Hit&, bool occluded) {
+        if (!occluded) vis8[tag] = 1;
+      });
+}
+
 // ---- NEE resolve, (result, throughput) stack, path end, AA path 2, frame write
 __global__ void __launch_bounds__(kBlock) k_resolve(SceneDev S, TraceArgs A, TileMap M, WaveBufs B, uint32_t iter,
                                                     float4* __restrict__ out) {
@@ -359,17 +427,22 @@ hipError_t launch_wavefront(const LaunchCfg& c, const SceneDev& S, const TraceAr
   if (B.n == 0) return hipSuccess;
   const unsigned gtrav = 256u * 16u;  // one-wave blocks, static interleaved chunks
   const unsigned gprod = 256u * 4u;   // producer blocks (multiple of kNSub)
+  const unsigned gpers = 256u * 20u;  // persistent one-wave blocks: 20 resident per CU (8 KB LDS, <= 96 VGPRs)
   hipLaunchKernelGGL(k_wave_init, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, out);
   const uint32_t iters = (uint32_t)A.bounces * ((A.flags & kAA) ? 2u : 1u);
   for (uint32_t it = 0; it < iters; it++) {
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 0], c.stream);
     if (c.layout == 4) hipLaunchKernelGGL(k_extend<4>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
-    else hipLaunchKernelGGL(k_extend<8>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    else if (c.trav == 1) hipLaunchKernelGGL(k_extend<8>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    else if (c.trav == 32) hipLaunchKernelGGL(k_extend_p<32>, dim3(gpers), dim3(64), 0, c.stream, S, B, it);
+    else hipLaunchKernelGGL(k_extend_p<16>, dim3(gpers), dim3(64), 0, c.stream, S, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
     hipLaunchKernelGGL(k_shade, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 2], c.stream);
     if (c.layout == 4) hipLaunchKernelGGL(k_shadow<4>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
-    else hipLaunchKernelGGL(k_shadow<8>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    else if (c.trav == 1) hipLaunchKernelGGL(k_shadow<8>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    else if (c.trav == 32) hipLaunchKernelGGL(k_shadow_p<32>, dim3(gpers), dim3(64), 0, c.stream, S, B, it);
+    else hipLaunchKernelGGL(k_shadow_p<16>, dim3(gpers), dim3(64), 0, c.stream, S, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 3], c.stream);
     hipLaunchKernelGGL(k_resolve, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it, out);
   }

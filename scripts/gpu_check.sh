@@ -45,4 +45,14 @@ if [ "$what" = "prof" ] || [ "$what" = "benchprof" ]; then
   step rocprof_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o run -- \
     python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
 fi
+if [ "$what" = "pmc" ]; then
+  # scripts/gpu_check.sh pmc "<counter list>" <tag>: one extra --pmc pass (kernel-trace only, no sys/hip trace)
+  export TMPDIR=/tmp
+  tag=${3:-pmc}
+  step "pmc_$tag" 900 rocprofv3 --pmc $kexpr --output-format csv -d "gpurun_out/pmc_$tag" -o run -- \
+    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline
+fi
+if [ "$what" = "listpmc" ]; then
+  step listpmc 300 rocprofv3 -L
+fi
 echo "== done"

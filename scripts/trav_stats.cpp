@@ -1,0 +1,235 @@
+// trav_stats.cpp -- host replica of the Node8 BLAS traversal (prt_traverse8.h) with visit counters and a
+// lock-step wave64 model, to size traversal-kernel changes before spending GPU time.  Diagnostic only.
+//
+// input:  <tris.bin>  float32 fat triangles (Model::triangles layout: 3 x float4 per triangle)
+//         <rays.bin>  float32 records {Ox,Oy,Oz,Dx,Dy,Dz,tmax,kind} (kind 0 = closest, 1 = any-hit),
+//                     in the order a wavefront queue would hand them to waves
+// output: per kind: mean node visits, leaf-triangle tests, stack pushes per ray; lock-step wave cost
+//         (iterations = max over lanes) and lane efficiency with and without per-lane ray refill.
+//
+// build:  g++ -O2 -I physically-based-ray-tracer_amd/csrc scripts/trav_stats.cpp \
+//             physically-based-ray-tracer_amd/csrc/bvh_build.cpp -o /tmp/trav_stats
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "bvh_build.h"
+
+using namespace prt;
+
+namespace {
+
+struct V { float x, y, z; };
+const float kFar = 1e30f, kNearPad = 0.99999f, kFarPad = 1.00001f;
+float safercp(float x) { return x > 1e-12f ? 1.0f / x : (x < -1e-12f ? 1.0f / x : kFar); }
+
+bool mt(const TriMT& T, V O, V D, float& t) {
+  const float hx = D.y * T.e2[2] - D.z * T.e2[1], hy = D.z * T.e2[0] - D.x * T.e2[2], hz = D.x * T.e2[1] - D.y * T.e2[0];
+  const float sx = O.x - T.v0[0], sy = O.y - T.v0[1], sz = O.z - T.v0[2];
+  const float det = T.e1[0] * hx + T.e1[1] * hy + T.e1[2] * hz;
+  if (!(det <= -1e-6f || det >= 1e-6f)) return false;
+  const float id = 1.0f / det;
+  const float u = (sx * hx + sy * hy + sz * hz) * id;
+  const float qx = sy * T.e1[2] - sz * T.e1[1], qy = sz * T.e1[0] - sx * T.e1[2], qz = sx * T.e1[1] - sy * T.e1[0];
+  const float v = (D.x * qx + D.y * qy + D.z * qz) * id;
+  t = (T.e2[0] * qx + T.e2[1] * qy + T.e2[2] * qz) * id;
+  return u >= 0 && u <= 1 && v >= 0 && u + v <= 1 && t > 0;
+}
+
+uint32_t order_mask(uint32_t m, uint32_t oct) {
+  if (oct & 1u) m = ((m & 0x55u) << 1) | ((m >> 1) & 0x55u);
+  if (oct & 2u) m = ((m & 0x33u) << 2) | ((m >> 2) & 0x33u);
+  if (oct & 4u) m = ((m & 0x0Fu) << 4) | ((m >> 4) & 0x0Fu);
+  return m;
+}
+
+// one lane's traversal as a list of iterations: tri tests done in each node visit
+struct Trace { std::vector<uint8_t> tris_per_visit; int pushes = 0; float t = kFar; };
+
+Trace traverse(const BuiltBlas8& B, V O, V D, float tmax, bool any) {
+  Trace tr;
+  const V rD = {safercp(D.x), safercp(D.y), safercp(D.z)};
+  const uint32_t oct = (rD.x < 0 ? 1u : 0u) | (rD.y < 0 ? 2u : 0u) | (rD.z < 0 ? 4u : 0u);
+  uint32_t gbase = 0, gmask = 0, gimask = 0, node = 0;
+  std::vector<std::pair<uint32_t, uint32_t>> stk;
+  float ht = tmax;
+  while (true) {
+    const Node8& n = B.nodes[node];
+    const float sc[3] = {std::ldexp(1.0f, (int)n.ex - 127), std::ldexp(1.0f, (int)n.ey - 127),
+                         std::ldexp(1.0f, (int)n.ez - 127)};
+    const float ax = (n.px - O.x) * rD.x, ay = (n.py - O.y) * rD.y, az = (n.pz - O.z) * rD.z;
+    const float bx = sc[0] * rD.x, by = sc[1] * rD.y, bz = sc[2] * rD.z;
+    uint32_t hits = 0;
+    for (int k = 0; k < 8; k++) {
+      const float lx = std::fma((float)(rD.x >= 0 ? n.qlox[k] : n.qhix[k]), bx, ax);
+      const float hx = std::fma((float)(rD.x >= 0 ? n.qhix[k] : n.qlox[k]), bx, ax);
+      const float ly = std::fma((float)(rD.y >= 0 ? n.qloy[k] : n.qhiy[k]), by, ay);
+      const float hy = std::fma((float)(rD.y >= 0 ? n.qhiy[k] : n.qloy[k]), by, ay);
+      const float lz = std::fma((float)(rD.z >= 0 ? n.qloz[k] : n.qhiz[k]), bz, az);
+      const float hz = std::fma((float)(rD.z >= 0 ? n.qhiz[k] : n.qloz[k]), bz, az);
+      const float tn = std::max(std::max(lx, ly), std::max(lz, 0.0f)) * kNearPad;
+      const float tf = std::min(std::min(hx, hy), hz) * kFarPad;
+      if (tn <= tf && tn <= ht) hits |= 1u << k;
+    }
+    int ntri = 0;
+    bool done = false;
+    uint32_t lhit = hits & ~(uint32_t)n.imask;
+    while (lhit && !done) {
+      const int k = __builtin_ctz(lhit);
+      lhit &= lhit - 1;
+      const uint32_t first = n.tri_base + (n.meta[k] >> 3), cnt = n.meta[k] & 7u;
+      for (uint32_t i = 0; i < cnt; i++) {
+        float t;
+        ntri++;
+        if (mt(B.tris[first + i], O, D, t) && t < ht) {
+          ht = t;
+          if (any) { done = true; break; }
+        }
+      }
+    }
+    tr.tris_per_visit.push_back((uint8_t)std::min(ntri, 255));
+    if (done) break;
+    const uint32_t ihit = hits & n.imask;
+    if (ihit) {
+      if (gmask) { stk.push_back({gbase, gmask | (gimask << 8)}); tr.pushes++; }
+      gbase = n.child_base;
+      gmask = order_mask(ihit, oct);
+      gimask = n.imask;
+    }
+    if (!gmask) {
+      if (stk.empty()) break;
+      gbase = stk.back().first;
+      gmask = stk.back().second & 0xFFu;
+      gimask = stk.back().second >> 8;
+      stk.pop_back();
+    }
+    const uint32_t bit = __builtin_ctz(gmask);
+    gmask &= gmask - 1;
+    const uint32_t k = bit ^ oct;
+    node = gbase + __builtin_popcount(gimask & ((1u << k) - 1u));
+  }
+  tr.t = ht;
+  return tr;
+}
+
+// lock-step wave64 cost model: an iteration costs c_node + c_tri * max over active lanes of their tri tests.
+// refill_at: a lane that finishes takes the next ray from the stream once >= refill_at lanes are idle
+// (64 = only when the whole wave is idle, i.e. the current kernel).
+void wave_model(const std::vector<Trace>& tr, int refill_at, double c_node, double c_tri, double c_refill) {
+  size_t next = 0;
+  double cost = 0, useful = 0;
+  long iters = 0, lane_iters = 0;
+  struct Lane { const Trace* t = nullptr; size_t pos = 0; };
+  std::vector<Lane> lanes(64);
+  auto refill = [&]() {
+    for (auto& l : lanes)
+      if (!l.t && next < tr.size()) { l.t = &tr[next++]; l.pos = 0; }
+    cost += c_refill;
+  };
+  refill();
+  while (true) {
+    int active = 0, maxtri = 0;
+    for (auto& l : lanes)
+      if (l.t) {
+        active++;
+        const int nt = l.t->tris_per_visit[l.pos];
+        maxtri = std::max(maxtri, nt);
+        useful += c_node + c_tri * nt;
+        lane_iters++;
+      }
+    if (!active) break;
+    iters++;
+    cost += c_node + c_tri * maxtri;
+    int idle = 0;
+    for (auto& l : lanes) {
+      if (l.t && ++l.pos == l.t->tris_per_visit.size()) l.t = nullptr;
+      if (!l.t) idle++;
+    }
+    if (idle >= refill_at && next < tr.size()) refill();
+  }
+  std::printf("    refill_at=%2d: wave iterations/ray %.2f  lane efficiency %.3f  cost/ray %.1f (useful %.1f)\n",
+              refill_at, (double)iters * 64 / tr.size(), (double)lane_iters / (iters * 64.0), cost * 64 / tr.size(),
+              useful / tr.size());
+}
+
+// decoupled model: per iteration a lane may visit one node (only when it has no pending triangles left
+// from an earlier visit) and test up to tri_per_iter pending triangles; cost = c_node x [any lane visits]
+// + c_tri x tri_per_iter x [any lane tests].
+void wave_model_decoupled(const std::vector<Trace>& tr, int refill_at, int tri_per_iter, double c_node, double c_tri,
+                          double c_refill) {
+  size_t next = 0;
+  double cost = 0;
+  long iters = 0;
+  struct Lane { const Trace* t = nullptr; size_t pos = 0; int pend = 0; };
+  std::vector<Lane> lanes(64);
+  auto refill = [&]() {
+    for (auto& l : lanes)
+      if (!l.t && next < tr.size()) { l.t = &tr[next++]; l.pos = 0; l.pend = 0; }
+    cost += c_refill;
+  };
+  refill();
+  while (true) {
+    bool any_visit = false, any_tri = false, any = false;
+    for (auto& l : lanes) {
+      if (!l.t) continue;
+      any = true;
+      if (l.pend == 0 && l.pos < l.t->tris_per_visit.size()) {
+        l.pend = l.t->tris_per_visit[l.pos++];
+        any_visit = true;
+      }
+      if (l.pend > 0) { l.pend = std::max(0, l.pend - tri_per_iter); any_tri = true; }
+    }
+    if (!any) break;
+    iters++;
+    cost += (any_visit ? c_node : 0) + (any_tri ? c_tri * tri_per_iter : 0);
+    int idle = 0;
+    for (auto& l : lanes) {
+      if (l.t && l.pend == 0 && l.pos == l.t->tris_per_visit.size()) l.t = nullptr;
+      if (!l.t) idle++;
+    }
+    if (idle >= refill_at && next < tr.size()) refill();
+  }
+  std::printf("    decoupled refill_at=%2d tri/iter=%d: cost/ray %.1f\n", refill_at, tri_per_iter, cost * 64 / tr.size());
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 3) { std::fprintf(stderr, "usage: trav_stats tris.bin rays.bin\n"); return 1; }
+  FILE* f = std::fopen(argv[1], "rb");
+  std::vector<float> tri;
+  float buf[4096];
+  size_t n;
+  while ((n = std::fread(buf, 4, 4096, f)) > 0) tri.insert(tri.end(), buf, buf + n);
+  std::fclose(f);
+  const int T = (int)(tri.size() / 12);
+  const BuiltBlas8 B = build_blas8(tri.data(), T, 3);
+  std::printf("tris %d  nodes %zu  depth %d\n", T, B.nodes.size(), B.depth);
+  f = std::fopen(argv[2], "rb");
+  std::vector<float> rays;
+  while ((n = std::fread(buf, 4, 4096, f)) > 0) rays.insert(rays.end(), buf, buf + n);
+  std::fclose(f);
+  const size_t R = rays.size() / 8;
+  for (int kind = 0; kind < 2; kind++) {
+    std::vector<Trace> tr;
+    double visits = 0, tris = 0, pushes = 0;
+    for (size_t i = 0; i < R; i++) {
+      const float* r = &rays[8 * i];
+      if ((int)r[7] != kind) continue;
+      tr.push_back(traverse(B, {r[0], r[1], r[2]}, {r[3], r[4], r[5]}, r[6], kind == 1));
+      visits += tr.back().tris_per_visit.size();
+      for (uint8_t c : tr.back().tris_per_visit) tris += c;
+      pushes += tr.back().pushes;
+    }
+    if (tr.empty()) continue;
+    std::printf("%s rays %zu: node visits %.2f  tri tests %.2f  pushes %.2f per ray\n", kind ? "any-hit" : "closest",
+                tr.size(), visits / tr.size(), tris / tr.size(), pushes / tr.size());
+    for (int ra : {64, 32, 16, 8}) wave_model(tr, ra, 130.0, 35.0, 40.0);
+    for (int ra : {64, 32, 16})
+      for (int tpi : {1, 2, 3}) wave_model_decoupled(tr, ra, tpi, 130.0, 35.0, 40.0);
+  }
+  return 0;
+}
