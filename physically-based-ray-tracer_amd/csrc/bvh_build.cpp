@@ -241,18 +241,51 @@ BuiltBlas build_blas(const float* triangles, int32_t T, int max_leaf) {
 namespace {
 
 // per-axis power-of-two scale so that ext / 2^e <= 255; returns the biased exponent (e + 127)
-uint8_t grid_exponent(double ext) {
+// smallest biased exponent e with qmax * 2^(e-127) >= ext (the node grid step is a power of two, so
+// origin + q * step and (origin - O) * rD + q * (step * rD) lose no precision in the step factor)
+uint8_t grid_exponent(double ext, double qmax) {
   if (!(ext > 0)) return 1;
-  int e = (int)std::ceil(std::log2(ext / 255.0));
-  while (std::ldexp(255.0, e) < ext) e++;
-  while (e > -126 && std::ldexp(255.0, e - 1) >= ext) e--;
+  int e = (int)std::ceil(std::log2(ext / qmax));
+  while (std::ldexp(qmax, e) < ext) e++;
+  while (e > -126 && std::ldexp(qmax, e - 1) >= ext) e--;
   return (uint8_t)std::min(254, std::max(1, e + 127));
 }
 
-}  // namespace
+// per-format child-bound storage: Node8 = 8-bit grid coordinates, Node8H = fp16 integers on an 11-bit grid
+struct Fmt8 {
+  static constexpr double kQMax = 255.0;
+  static void set(Node8& n, int s, const double* lo, const double* hi) {
+    uint8_t* ql[3] = {&n.qlox[s], &n.qloy[s], &n.qloz[s]};
+    uint8_t* qh[3] = {&n.qhix[s], &n.qhiy[s], &n.qhiz[s]};
+    for (int k = 0; k < 3; k++) { *ql[k] = (uint8_t)lo[k]; *qh[k] = (uint8_t)hi[k]; }
+  }
+  static void empty(Node8& n, int s) {
+    n.qlox[s] = n.qloy[s] = n.qloz[s] = 255;
+    n.qhix[s] = n.qhiy[s] = n.qhiz[s] = 0;
+  }
+};
+uint16_t f16_of_int(int q) {  // exact fp16 encoding of an integer 0..2047
+  if (q == 0) return 0;
+  int e = 0;
+  while ((q >> e) > 1) e++;
+  const uint32_t mant = e >= 10 ? ((uint32_t)q >> (e - 10)) & 0x3FFu : ((uint32_t)q << (10 - e)) & 0x3FFu;
+  return (uint16_t)(((uint32_t)(e + 15) << 10) | mant);
+}
+struct Fmt8H {
+  static constexpr double kQMax = 2047.0;
+  static void set(Node8H& n, int s, const double* lo, const double* hi) {
+    uint16_t* ql[3] = {&n.qlox[s], &n.qloy[s], &n.qloz[s]};
+    uint16_t* qh[3] = {&n.qhix[s], &n.qhiy[s], &n.qhiz[s]};
+    for (int k = 0; k < 3; k++) { *ql[k] = f16_of_int((int)lo[k]); *qh[k] = f16_of_int((int)hi[k]); }
+  }
+  static void empty(Node8H& n, int s) {
+    n.qlox[s] = n.qloy[s] = n.qloz[s] = f16_of_int(2047);
+    n.qhix[s] = n.qhiy[s] = n.qhiz[s] = 0;
+  }
+};
 
-BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf) {
-  BuiltBlas8 out;
+template <class NodeT, class Fmt, class Out>
+void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out) {
   Builder B;
   B.tri = triangles;
   B.max_leaf = std::max(1, std::min(4, max_leaf));
@@ -261,7 +294,7 @@ BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf) {
   out.tris.reserve(T);
   struct Item { int32_t n2; uint32_t n8; int depth; };
   std::vector<Item> work;
-  out.nodes.push_back(Node8());
+  out.nodes.push_back(NodeT());
   work.push_back({0, 0, 1});
   while (!work.empty()) {
     const Item it = work.back();
@@ -299,7 +332,7 @@ BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf) {
       for (int k = 0; k < 3; k++) { nlo[k] = std::min(nlo[k], (double)clo[i][k]); nhi[k] = std::max(nhi[k], (double)chi[i][k]); }
     }
     // octant slot assignment: slot s holds the child that comes first for rays of octant s
-    int slot_of[8], child_in[8];
+    int child_in[8];
     for (int s = 0; s < 8; s++) child_in[s] = -1;
     {
       double pc[3];
@@ -323,16 +356,15 @@ BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf) {
             for (int s = 0; s < 8; s++)
               if (!used_s[s] && cost[i][s] < best) { best = cost[i][s]; bi = i; bs = s; }
         used_c[bi] = used_s[bs] = true;
-        slot_of[bi] = bs;
         child_in[bs] = bi;
       }
     }
-    Node8 nd;
+    NodeT nd;
     std::memset(&nd, 0, sizeof(nd));
     nd.px = (float)nlo[0]; nd.py = (float)nlo[1]; nd.pz = (float)nlo[2];
     const double p[3] = {(double)nd.px, (double)nd.py, (double)nd.pz};
     uint8_t e[3];
-    for (int k = 0; k < 3; k++) e[k] = grid_exponent(nhi[k] - p[k]);
+    for (int k = 0; k < 3; k++) e[k] = grid_exponent(nhi[k] - p[k], Fmt::kQMax);
     nd.ex = e[0]; nd.ey = e[1]; nd.ez = e[2];
     const double sc[3] = {std::ldexp(1.0, (int)e[0] - 127), std::ldexp(1.0, (int)e[1] - 127),
                           std::ldexp(1.0, (int)e[2] - 127)};
@@ -347,18 +379,15 @@ BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf) {
     for (int s = 0; s < 8; s++) {
       const int i = child_in[s];
       if (i < 0) {  // empty slot: inverted box never hits
-        nd.qlox[s] = nd.qloy[s] = nd.qloz[s] = 255;
-        nd.qhix[s] = nd.qhiy[s] = nd.qhiz[s] = 0;
+        Fmt::empty(nd, s);
         continue;
       }
-      uint8_t* qlo[3] = {&nd.qlox[s], &nd.qloy[s], &nd.qloz[s]};
-      uint8_t* qhi[3] = {&nd.qhix[s], &nd.qhiy[s], &nd.qhiz[s]};
+      double qlo[3], qhi[3];
       for (int k = 0; k < 3; k++) {
-        const double lo = std::floor(((double)clo[i][k] - p[k]) / sc[k]);
-        const double hi = std::ceil(((double)chi[i][k] - p[k]) / sc[k]);
-        *qlo[k] = (uint8_t)std::min(255.0, std::max(0.0, lo));
-        *qhi[k] = (uint8_t)std::min(255.0, std::max(0.0, hi));
+        qlo[k] = std::min(Fmt::kQMax, std::max(0.0, std::floor(((double)clo[i][k] - p[k]) / sc[k])));
+        qhi[k] = std::min(Fmt::kQMax, std::max(0.0, std::ceil(((double)chi[i][k] - p[k]) / sc[k])));
       }
+      Fmt::set(nd, s, qlo, qhi);
       const Node2& c = B.nodes[ch[i]];
       if (c.leaf()) {
         for (int32_t j = c.first; j < c.first + c.count; j++) {
@@ -383,6 +412,19 @@ BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf) {
     }
     out.nodes[it.n8] = nd;
   }
+}
+
+}  // namespace
+
+BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf) {
+  BuiltBlas8 out;
+  build_wide8<Node8, Fmt8>(triangles, T, max_leaf, out);
+  return out;
+}
+
+BuiltBlas8H build_blas8h(const float* triangles, int32_t T, int max_leaf) {
+  BuiltBlas8H out;
+  build_wide8<Node8H, Fmt8H>(triangles, T, max_leaf, out);
   return out;
 }
 

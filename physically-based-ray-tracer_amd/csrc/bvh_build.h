@@ -71,6 +71,29 @@ struct BuiltBlas8 {
 };
 BuiltBlas8 build_blas8(const float* triangles, int32_t tri_count, int max_leaf = 3);
 
+// ---- the same tree with fp16 child bounds on an 11-bit grid: 128 bytes = one aligned cache line.
+//   [0]  px py pz | ex ey ez imask      as Node8 (grid step 2^(e-127), q in 0..2047)
+//   [1]  child_base tri_base meta[8]    as Node8
+//   [2-7] qlox qhix qloy qhiy qloz qhiz [8] fp16 integers; a ray loads the near/far block per axis by
+//        its direction sign and feeds the halves straight into v_fma_mix_f32 (no conversions)
+struct alignas(128) Node8H {
+  float px, py, pz;
+  uint8_t ex, ey, ez, imask;
+  uint32_t child_base, tri_base;
+  uint8_t meta[8];
+  uint16_t qlox[8], qhix[8], qloy[8], qhiy[8], qloz[8], qhiz[8];
+};
+static_assert(sizeof(Node8H) == 128, "Node8H must be one 128-byte line");
+
+struct BuiltBlas8H {
+  std::vector<Node8H> nodes;
+  std::vector<TriMT> tris;
+  float bmin[3], bmax[3];
+  int depth = 0;
+  int64_t leaves = 0;
+};
+BuiltBlas8H build_blas8h(const float* triangles, int32_t tri_count, int max_leaf = 3);
+
 // Same inflation rule the traversal relies on (see bvh_build.cpp).
 void inflate_box(float* lo, float* hi);
 

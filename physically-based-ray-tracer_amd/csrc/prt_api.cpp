@@ -105,9 +105,9 @@ struct prt_ctx {
   // meshes
   std::vector<MeshDev> mesh_host;
   std::vector<MeshHost> mesh_info;
-  DevBuf nodes, nodes8, tris, fnrm, fuv, vidx, vert, facen, mesh;
+  DevBuf nodes, nodes8, nodes8h, tris, stri, mesh;
   int max_depth = 0;
-  int layout = 8;  // BLAS node layout of the uploaded meshes: 8 = Node8 (default), 4 = Node4 (PRT_BVH=4)
+  int layout = 8;  // BLAS node layout of the uploaded meshes: 8 = Node8, 9 = Node8H, 4 = Node4 (PRT_BVH)
   // instances
   std::vector<float> inst_xf;
   std::vector<uint32_t> inst_mesh;
@@ -136,20 +136,31 @@ namespace {
 
 // The LDS traversal stacks are sized for Trav<L>::kMaxDepth node levels (prt_traverse8.h).
 int layout_for(const prt_ctx* c) {
-  const int maxd = c->layout == 4 ? Trav<4>::kMaxDepth : Trav<8>::kMaxDepth;
+  const int maxd = c->layout == 4 ? Trav<4>::kMaxDepth : c->layout == 9 ? Trav<9>::kMaxDepth : Trav<8>::kMaxDepth;
   return c->max_depth <= maxd ? c->layout : -1;
 }
 
 int trav_from_env() {
   const char* e = std::getenv("PRT_TRAV");
   if (e && std::strcmp(e, "lockstep") == 0) return 1;
-  if (e && std::strcmp(e, "refill32") == 0) return 32;
-  return 16;
+  if (e && std::strcmp(e, "refill16") == 0) return 16;
+  return 32;
+}
+
+// waves/SIMD of the persistent traversal kernels: the LDS stack must hold max_depth - 1 groups
+int occ_for(const prt_ctx* c) {
+  const char* e = std::getenv("PRT_OCC");
+  int want = e ? std::atoi(e) : 6;
+  if (want >= 8 && c->max_depth <= 9) return 8;
+  if (want >= 6 && c->max_depth <= 13) return 6;
+  return 5;
 }
 
 int layout_from_env() {
   const char* e = std::getenv("PRT_BVH");
-  return (e && std::strcmp(e, "4") == 0) ? 4 : 8;
+  if (e && std::strcmp(e, "4") == 0) return 4;
+  if (e && std::strcmp(e, "8h") == 0) return 9;
+  return 8;
 }
 
 int ensure_instances(prt_ctx* c) {
@@ -199,12 +210,9 @@ int scene_ready(prt_ctx* c, SceneDev& S) {
   std::memset(&S, 0, sizeof(S));
   S.nodes = c->nodes.as<Node4>();
   S.nodes8 = c->nodes8.as<Node8>();
+  S.nodes8h = c->nodes8h.as<Node8H>();
   S.tris = c->tris.as<TriMT>();
-  S.fnrm = c->fnrm.as<float4>();
-  S.fuv = c->fuv.as<float2>();
-  S.vidx = c->vidx.as<int32_t>();
-  S.vert = c->vert.as<float>();
-  S.facen = c->facen.as<float>();
+  S.stri = c->stri.as<ShadeTri>();
   S.texels = c->texels.as<uint32_t>();
   S.tex = c->tex.as<TexDev>();
   S.inst = c->inst.as<InstDev>();
@@ -322,7 +330,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   TraceArgs A;
   A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
   A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F;
-  LaunchCfg L{c->stream, layout, trav_from_env()};
+  LaunchCfg L{c->stream, layout, trav_from_env(), occ_for(c)};
   const bool mega = use_megakernel();
   const uint32_t iters = (uint32_t)p->bounces * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
   if (!mega && iters > (uint32_t)kMaxIters) return fail(PRT_ERR_UNSUPPORTED, "too many wavefront iterations");
@@ -428,7 +436,7 @@ int prt_destroy(prt_ctx* c) {
   if (!c) return PRT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->texels, &c->tex, &c->nodes, &c->nodes8, &c->tris, &c->fnrm, &c->fuv, &c->vidx, &c->vert, &c->facen,
+  for (DevBuf* b : {&c->texels, &c->tex, &c->nodes, &c->nodes8, &c->nodes8h, &c->tris, &c->stri,
                     &c->mesh, &c->inst, &c->sky, &c->acc, &c->nsamp, &c->dist, &c->frames, &c->avg, &c->rgb8,
                     &c->counters, &c->hits})
     b->release();
@@ -472,11 +480,9 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
   const int layout = layout_from_env();
   std::vector<Node4> nodes;
   std::vector<Node8> nodes8;
+  std::vector<Node8H> nodes8h;
   std::vector<TriMT> tris;
-  std::vector<float4> fnrm;
-  std::vector<float2> fuv;
-  std::vector<int32_t> vidx;
-  std::vector<float> vert, facen;
+  std::vector<ShadeTri> stri;
   std::vector<MeshDev> mh(n);
   std::vector<MeshHost> info(n);
   int maxd = 0;
@@ -521,33 +527,50 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
       std::memcpy(bmin, b.bmin, sizeof(bmin)); std::memcpy(bmax, b.bmax, sizeof(bmax));
       depth = b.depth; nnodes = (int64_t)b.nodes.size(); nleaves = b.leaves;
     } else {
-      BuiltBlas8 b = build_blas8(M.triangles, M.tri_count, 3);
-      const uint32_t node_base = (uint32_t)nodes8.size();
-      if ((uint64_t)tri_base + b.tris.size() >= (1ull << 32) || (uint64_t)node_base + b.nodes.size() >= (1ull << 32))
-        return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
-      for (Node8& nd : b.nodes) {
-        nd.child_base += node_base;
-        nd.tri_base += tri_base;
-      }
-      nodes8.insert(nodes8.end(), b.nodes.begin(), b.nodes.end());
-      tris.insert(tris.end(), b.tris.begin(), b.tris.end());
-      mh[i].root = node_base;
-      std::memcpy(bmin, b.bmin, sizeof(bmin)); std::memcpy(bmax, b.bmax, sizeof(bmax));
-      depth = b.depth; nnodes = (int64_t)b.nodes.size(); nleaves = b.leaves;
+      // 8-wide layouts: rebase child / triangle offsets into the concatenated arrays
+      auto append = [&](auto&& built, auto& all) -> bool {
+        const uint32_t node_base = (uint32_t)all.size();
+        if ((uint64_t)tri_base + built.tris.size() >= (1ull << 32) ||
+            (uint64_t)node_base + built.nodes.size() >= (1ull << 32))
+          return false;
+        for (auto& nd : built.nodes) {
+          nd.child_base += node_base;
+          nd.tri_base += tri_base;
+        }
+        all.insert(all.end(), built.nodes.begin(), built.nodes.end());
+        tris.insert(tris.end(), built.tris.begin(), built.tris.end());
+        mh[i].root = node_base;
+        std::memcpy(bmin, built.bmin, sizeof(bmin));
+        std::memcpy(bmax, built.bmax, sizeof(bmax));
+        depth = built.depth; nnodes = (int64_t)built.nodes.size(); nleaves = built.leaves;
+        return true;
+      };
+      const bool ok = layout == 9 ? append(build_blas8h(M.triangles, M.tri_count, 3), nodes8h)
+                                  : append(build_blas8(M.triangles, M.tri_count, 3), nodes8);
+      if (!ok) return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
     }
-    mh[i].prim_base = (uint32_t)(fuv.size() / 3);
-    mh[i].vert_base = (uint32_t)(vert.size() / 3);
+    mh[i].prim_base = (uint32_t)stri.size();
+    mh[i].vert_base = 0;
     mh[i].tri_count = (uint32_t)M.tri_count;
     for (int k = 0; k < 4; k++) mh[i].tex[k] = tx[k];
     const size_t T = (size_t)M.tri_count;
-    for (size_t k = 0; k < 3 * T; k++) {
-      fnrm.push_back(make_float4(M.fixed_normals[4 * k], M.fixed_normals[4 * k + 1], M.fixed_normals[4 * k + 2],
-                                 M.fixed_normals[4 * k + 3]));
-      fuv.push_back(make_float2(M.fixed_uvs[2 * k], M.fixed_uvs[2 * k + 1]));
-      vidx.push_back(M.indices[k]);
+    for (size_t p = 0; p < T; p++) {
+      ShadeTri st;
+      std::memset(&st, 0, sizeof(st));
+      for (int k = 0; k < 3; k++) {
+        const size_t c3 = 3 * p + k;
+        const float* vp = M.vertices + 3 * (size_t)M.indices[c3];
+        for (int j = 0; j < 3; j++) {
+          st.n[3 * k + j] = M.fixed_normals[4 * c3 + j];
+          st.p[3 * k + j] = vp[j];
+          st.fn[j] = M.face_normals[3 * p + j];
+        }
+        st.uv[2 * k] = M.fixed_uvs[2 * c3];
+        st.uv[2 * k + 1] = M.fixed_uvs[2 * c3 + 1];
+      }
+      stri.push_back(st);
     }
-    vert.insert(vert.end(), M.vertices, M.vertices + 3 * (size_t)M.vertex_count);
-    facen.insert(facen.end(), M.face_normals, M.face_normals + 3 * T);
+
     for (int k = 0; k < 3; k++) { info[i].bmin[k] = bmin[k]; info[i].bmax[k] = bmax[k]; }
     info[i].depth = depth;
     info[i].nodes = nnodes;
@@ -558,14 +581,12 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
   HIP_TRY(hipSetDevice(c->device));
   c->nodes.release();
   c->nodes8.release();
+  c->nodes8h.release();
   if (layout == 4) HIP_TRY(upload(c->nodes, nodes.data(), nodes.size() * sizeof(Node4)));
+  else if (layout == 9) HIP_TRY(upload(c->nodes8h, nodes8h.data(), nodes8h.size() * sizeof(Node8H)));
   else HIP_TRY(upload(c->nodes8, nodes8.data(), nodes8.size() * sizeof(Node8)));
   HIP_TRY(upload(c->tris, tris.data(), tris.size() * sizeof(TriMT)));
-  HIP_TRY(upload(c->fnrm, fnrm.data(), fnrm.size() * sizeof(float4)));
-  HIP_TRY(upload(c->fuv, fuv.data(), fuv.size() * sizeof(float2)));
-  HIP_TRY(upload(c->vidx, vidx.data(), vidx.size() * 4));
-  HIP_TRY(upload(c->vert, vert.data(), vert.size() * 4));
-  HIP_TRY(upload(c->facen, facen.data(), facen.size() * 4));
+  HIP_TRY(upload(c->stri, stri.data(), stri.size() * sizeof(ShadeTri)));
   HIP_TRY(upload(c->mesh, mh.data(), mh.size() * sizeof(MeshDev)));
   c->mesh_host = mh;
   c->mesh_info = info;
@@ -718,7 +739,7 @@ int prt_untile(prt_ctx* c, const float* gathered, int32_t W, int32_t H, int32_t 
   int rc = prt_tile_buffer_pixels(W, H, ts, world, &per);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
-  LaunchCfg L{c->stream, c->layout, trav_from_env()};
+  LaunchCfg L{c->stream, c->layout, trav_from_env(), occ_for(c)};
   HIP_TRY(launch_untile(L, W, H, ts, world, (uint32_t)per, reinterpret_cast<const float4*>(gathered),
                         reinterpret_cast<float4*>(avg_dev), rgb8_dev));
   return PRT_OK;
@@ -740,7 +761,7 @@ int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t 
   if (!dev_out) { HIP_TRY(c->hits.ensure(n * sizeof(HitOut))); out = c->hits.as<HitOut>(); }
   HIP_TRY(c->counters.ensure(sizeof(Counters)));
   HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
-  LaunchCfg L{c->stream, layout, trav_from_env()};
+  LaunchCfg L{c->stream, layout, trav_from_env(), occ_for(c)};
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   HIP_TRY(launch_primary_hits(L, S, M, out, c->counters.as<Counters>()));
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
@@ -780,7 +801,7 @@ static int ray_query(prt_ctx* c, int32_t n, const float* O, const float* D, cons
     cleanup();
     return fail(PRT_ERR_OUT_OF_MEMORY, "ray buffers");
   }
-  LaunchCfg L{c->stream, layout, trav_from_env()};
+  LaunchCfg L{c->stream, layout, trav_from_env(), occ_for(c)};
   hipError_t e = any ? launch_occluded(L, S, n, dO.as<float>(), dD.as<float>(), dT.as<float>(), dOut.as<int32_t>())
                      : launch_intersect(L, S, n, dO.as<float>(), dD.as<float>(), tmax ? dT.as<float>() : nullptr,
                                         dOut.as<HitOut>());
@@ -807,8 +828,7 @@ int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
     info->triangles += m.tris;
   }
   info->max_depth = c->max_depth;
-  info->device_bytes = (int64_t)(c->nodes.bytes + c->nodes8.bytes + c->tris.bytes + c->fnrm.bytes + c->fuv.bytes + c->vidx.bytes +
-                                 c->vert.bytes + c->facen.bytes + c->texels.bytes + c->sky.bytes + c->inst.bytes);
+  info->device_bytes = (int64_t)(c->nodes.bytes + c->nodes8.bytes + c->nodes8h.bytes + c->tris.bytes + c->stri.bytes + c->texels.bytes + c->sky.bytes + c->inst.bytes);
   return PRT_OK;
 }
 

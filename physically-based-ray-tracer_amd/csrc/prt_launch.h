@@ -17,8 +17,9 @@ struct HitOut {
 struct LaunchCfg {
   hipStream_t stream;
   int layout;  // BLAS layout: 4 (Node4) or 8 (Node8, default)
-  int trav;    // Node8 wavefront traversal: 16 / 32 = persistent lanes refilled at that many idle lanes
-               // (default 16), 1 = lock-step one-ray-per-lane kernels (PRT_TRAV=lockstep)
+  int trav;    // 8-wide wavefront traversal: 32 / 16 = persistent lanes refilled at that many idle lanes
+               // (default 32; PRT_TRAV=refill16), 1 = lock-step one-ray-per-lane kernels (PRT_TRAV=lockstep)
+  int occ;     // persistent traversal waves/SIMD: 5 (16-group LDS stack), 6 (12 groups), 8 (8 groups)
 };
 
 // wavefront pipeline buffers (SoA over n work items; R/T hold (bounces-1) x n entries)

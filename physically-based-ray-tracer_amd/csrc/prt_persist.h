@@ -22,17 +22,19 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 
 // Persistent traversal of one wave (blockDim.x == 64).  Ray source and sink are callbacks:
 //   fetch(uint32_t* base, uint32_t want) -> uint32_t got   (wave-uniform; called by all lanes)
-//   load(uint32_t g, V3& O, V3& D, float& tmax, uint32_t& tag)  queue entry g -> world ray
-//   finish(uint32_t tag, const Hit& h, bool hit)        closest: h; any-hit: hit = occluded
-template <bool ANY, int STACK, int REFILL, class Fetch, class Load, class Finish>
+//   load(uint32_t g, V3& O, V3& D, float& tmax) -> handle  queue entry g -> world ray + a handle
+//   reload(uint32_t handle, V3& O, V3& D)                  world ray again (next instance of the TLAS loop)
+//   finish(uint32_t handle, const Hit& h, bool hit)        closest: h; any-hit: hit = occluded
+// The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
+// register budget of 6-8 waves/SIMD.
+template <bool ANY, bool HALF, int STACK, int REFILL, class Fetch, class Load, class Reload, class Finish>
 __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
-                                                 Load load, Finish finish) {
+                                                 Load load, Reload reload, Finish finish) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   bool active = false, drained = false;
-  uint32_t tag = 0;
-  V3 Ow = v3(0.0f, 0.0f, 0.0f), Dw = v3(0.0f, 0.0f, 1.0f);  // world ray (instance loop)
-  V3 O = Ow, D = Dw, rD = Dw;                                  // instance-space ray
+  uint32_t handle = 0;
+  V3 O = v3(0.0f, 0.0f, 0.0f), D = v3(0.0f, 0.0f, 1.0f), rD = D;  // instance-space ray
   uint32_t oct = 0;
   Hit h;
   h.t = kFar; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;
@@ -40,6 +42,24 @@ __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __
   uint32_t node = kNoNode, gbase = 0, gmask = 0, gimask = 0;
   int sp = 0;
   uint32_t lhit = 0, ltri = 0, lmeta0 = 0, lmeta1 = 0, tcur = 0, tcnt = 0;  // pending leaf triangles
+  // enter the first instance >= i0 whose world box the ray hits before h.t (tiny_bvh.h:2500-2565 TLAS
+  // walk as a linear loop over <= 64 instance boxes); false when there is none
+  auto enter = [&](int i0, const V3& Ow, const V3& Dw) -> bool {
+    const V3 rDw = v3(safercp(Dw.x), safercp(Dw.y), safercp(Dw.z));
+    int i = i0;
+    while (i < S.ninst && slab1(S.inst[i].bmin, S.inst[i].bmax, Ow, rDw, h.t) >= kFar) i++;
+    if (i >= S.ninst) return false;
+    const InstDev& I = S.inst[i];
+    inst = i;
+    O = xform_point(Ow, I.inv);
+    D = xform_vector(Dw, I.inv);
+    rD = v3(safercp(D.x), safercp(D.y), safercp(D.z));
+    oct = (rD.x < 0.0f ? 1u : 0u) | (rD.y < 0.0f ? 2u : 0u) | (rD.z < 0.0f ? 4u : 0u);
+    node = S.mesh[I.mesh].root;
+    gmask = 0;
+    sp = 0;
+    return true;
+  };
   while (true) {
     // ---- refill idle lanes from the queue
     const uint64_t idle = __ballot(!active);
@@ -51,13 +71,13 @@ __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __
       if (!active) {
         const uint32_t rank = (uint32_t)__popcll(idle & lanes_below);
         if (rank < got) {
+          V3 Ow, Dw;
           float tmax;
-          load(base + rank, Ow, Dw, tmax, tag);
+          handle = load(base + rank, Ow, Dw, tmax);
           h.t = tmax; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;
-          inst = -1;
-          node = kNoNode;
           lhit = 0; tcnt = 0;
-          active = true;
+          if (enter(0, Ow, Dw)) active = true;
+          else finish(handle, h, false);
         }
       }
     }
@@ -65,32 +85,36 @@ __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __
       if (drained) break;
       continue;
     }
-    // ---- enter the next instance (TLAS: linear loop over the instance boxes, tiny_bvh.h:2500-2565)
+    // ---- BLAS done: next instance, or the ray is finished
     if (active && node == kNoNode && lhit == 0 && tcnt == 0) {
-      const V3 rDw = v3(safercp(Dw.x), safercp(Dw.y), safercp(Dw.z));
-      int i = inst + 1;
-      while (i < S.ninst && slab1(S.inst[i].bmin, S.inst[i].bmax, Ow, rDw, h.t) >= kFar) i++;
-      if (i >= S.ninst) {
-        finish(tag, h, false);
+      bool more = false;
+      if (inst + 1 < S.ninst) {
+        V3 Ow, Dw;
+        reload(handle, Ow, Dw);
+        more = enter(inst + 1, Ow, Dw);
+      }
+      if (!more) {
+        finish(handle, h, false);
         active = false;
-      } else {
-        const InstDev& I = S.inst[i];
-        inst = i;
-        O = xform_point(Ow, I.inv);
-        D = xform_vector(Dw, I.inv);
-        rD = v3(safercp(D.x), safercp(D.y), safercp(D.z));
-        oct = (rD.x < 0.0f ? 1u : 0u) | (rD.y < 0.0f ? 2u : 0u) | (rD.z < 0.0f ? 4u : 0u);
-        node = S.mesh[I.mesh].root;
-        gmask = 0;
-        sp = 0;
       }
     }
     // ---- one node visit for lanes without pending triangles
     if (active && node != kNoNode && lhit == 0 && tcnt == 0) {
-      const uint4* np = reinterpret_cast<const uint4*>(S.nodes8 + node);
-      const uint4 a = np[0], b = np[1], c = np[2], d = np[3], e = np[4];
+      uint4 a, b;
+      uint32_t hits;
+      if (HALF) {  // Node8H: one 128-B line
+        const uint4* np = reinterpret_cast<const uint4*>(S.nodes8h + node);
+        a = np[0];
+        b = np[1];
+        hits = node8h_hits(np, a, O, rD, h.t);
+      } else {     // Node8: 80 B
+        const uint4* np = reinterpret_cast<const uint4*>(S.nodes8 + node);
+        a = np[0];
+        b = np[1];
+        const uint4 c = np[2], d = np[3], e = np[4];
+        hits = node8_hits(a, c, d, e, O, rD, h.t);
+      }
       const uint32_t imask = a.w >> 24;
-      const uint32_t hits = node8_hits(a, c, d, e, O, rD, h.t);
       lhit = hits & ~imask;
       ltri = b.y; lmeta0 = b.z; lmeta1 = b.w;
       const uint32_t ihit = hits & imask;
@@ -136,7 +160,7 @@ __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __
       tcnt--;
       if (ANY) {
         if (hit && t < h.t) {  // tiny_bvh.h:6594 (h.t holds tmax)
-          finish(tag, h, true);
+          finish(handle, h, true);
           active = false;
           node = kNoNode; lhit = 0; tcnt = 0;
         }

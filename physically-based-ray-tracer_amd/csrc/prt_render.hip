@@ -219,14 +219,19 @@ __global__ void __launch_bounds__(kBlock) k_occluded(SceneDev S, int32_t n, cons
 // ---- launchers (host)
 static inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// launch kernel template K<layout> (4 = Node4, 8 = Node8, 9 = Node8H)
+#define PRT_BY_LAYOUT(layout, K, ...)                           \
+  do {                                                          \
+    if ((layout) == 4) hipLaunchKernelGGL(K<4>, __VA_ARGS__);   \
+    else if ((layout) == 9) hipLaunchKernelGGL(K<9>, __VA_ARGS__); \
+    else hipLaunchKernelGGL(K<8>, __VA_ARGS__);                 \
+  } while (0)
+
 hipError_t launch_trace_frames(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                                float4* out, Counters* cnt) {
   const uint64_t total = (uint64_t)M.items * (uint64_t)A.frames;
   if (total == 0) return hipSuccess;
-  if (c.layout == 4)
-    hipLaunchKernelGGL(k_trace_frames<4>, dim3(grid_of(total)), dim3(kBlock), 0, c.stream, S, A, M, out, cnt);
-  else
-    hipLaunchKernelGGL(k_trace_frames<8>, dim3(grid_of(total)), dim3(kBlock), 0, c.stream, S, A, M, out, cnt);
+  PRT_BY_LAYOUT(c.layout, k_trace_frames, dim3(grid_of(total)), dim3(kBlock), 0, c.stream, S, A, M, out, cnt);
   return hipGetLastError();
 }
 
@@ -249,30 +254,21 @@ hipError_t launch_untile(const LaunchCfg& c, int32_t W, int32_t H, int32_t ts, i
 
 hipError_t launch_primary_hits(const LaunchCfg& c, const SceneDev& S, const TileMap& M, HitOut* out, Counters* cnt) {
   if (M.items == 0) return hipSuccess;
-  if (c.layout == 4)
-    hipLaunchKernelGGL(k_primary_hits<4>, dim3(grid_of(M.items)), dim3(kBlock), 0, c.stream, S, M, out, cnt);
-  else
-    hipLaunchKernelGGL(k_primary_hits<8>, dim3(grid_of(M.items)), dim3(kBlock), 0, c.stream, S, M, out, cnt);
+  PRT_BY_LAYOUT(c.layout, k_primary_hits, dim3(grid_of(M.items)), dim3(kBlock), 0, c.stream, S, M, out, cnt);
   return hipGetLastError();
 }
 
 hipError_t launch_intersect(const LaunchCfg& c, const SceneDev& S, int32_t n, const float* O, const float* D,
                             const float* tmax, HitOut* out) {
   if (n <= 0) return hipSuccess;
-  if (c.layout == 4)
-    hipLaunchKernelGGL(k_intersect<4>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
-  else
-    hipLaunchKernelGGL(k_intersect<8>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
+  PRT_BY_LAYOUT(c.layout, k_intersect, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
   return hipGetLastError();
 }
 
 hipError_t launch_occluded(const LaunchCfg& c, const SceneDev& S, int32_t n, const float* O, const float* D,
                            const float* tmax, int32_t* out) {
   if (n <= 0) return hipSuccess;
-  if (c.layout == 4)
-    hipLaunchKernelGGL(k_occluded<4>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
-  else
-    hipLaunchKernelGGL(k_occluded<8>, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
+  PRT_BY_LAYOUT(c.layout, k_occluded, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
   return hipGetLastError();
 }
 

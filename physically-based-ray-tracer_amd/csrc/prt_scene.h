@@ -2,11 +2,9 @@
 //
 //   nodes   Node4[]    128 B each, all meshes' BLASes concatenated (bvh_build.h)
 //   tris    TriMT[]    48 B each, leaf order, MT-ready {v0,prim | e1 | e2}
-//   fnrm    float4[3T] Model::fixedNormals, prim order (global prim = mesh.prim_base + prim)
-//   fuv     float2[3T] Model::fixedTextureCoords
-//   vidx    int32[3T]  Model::indices (mesh-local vertex ids)
-//   vert    float[3V]  Model::vertices (global vertex = mesh.vert_base + id)
-//   facen   float[3T]  Model::faceNormals
+//   stri    ShadeTri[T] everything shading reads for one primitive in one 128-B line, prim order
+//                       (global prim = mesh.prim_base + prim): Model::fixedNormals, fixedTextureCoords,
+//                       the object-space corner positions vertices[indices[3p+k]], faceNormals
 //   texels  uint32[]   every texture's 0x00RRGGBB pixels back to back
 //   inst    InstDev[]  inverse transform (rays), inverse-transpose (normals), world AABB
 #pragma once
@@ -26,10 +24,20 @@ struct InstDev {
   uint32_t pad;
 };
 
+// one primitive's shading inputs (Core/Scene.cpp:47-218 reads them from five arrays; here one line)
+struct alignas(16) ShadeTri {
+  float n[9];    // fixedNormals[3p..3p+2].xyz
+  float uv[6];   // fixedTextureCoords[3p..3p+2]
+  float p[9];    // vertices[indices[3p+k]], k = 0..2 (normal-map tangent frame, Scene.cpp:93-103)
+  float fn[3];   // faceNormals[p]
+  uint32_t pad[5];
+};
+static_assert(sizeof(ShadeTri) == 128, "ShadeTri must be one 128-byte line");
+
 struct MeshDev {
   uint32_t root;       // Node4 index of the BLAS root
   uint32_t prim_base;  // offset into the per-triangle shading arrays
-  uint32_t vert_base;  // offset (in vertices) into vert
+  uint32_t vert_base;  // unused (kept for layout)
   uint32_t tri_count;
   int32_t tex[4];      // albedo, normal, metalness, emission (-1 = none)
 };
@@ -44,13 +52,10 @@ constexpr int kMaxInstances = 64;
 
 struct SceneDev {
   const Node4* nodes;
-  const Node8* nodes8;  // Node8 BLASes (layout 8); root indices in MeshDev.root refer to the active layout
+  const Node8* nodes8;    // Node8 BLASes (layout 8); root indices in MeshDev.root refer to the active layout
+  const Node8H* nodes8h;  // Node8H BLASes (layout 9)
   const TriMT* tris;
-  const float4* fnrm;
-  const float2* fuv;
-  const int32_t* vidx;
-  const float* vert;
-  const float* facen;
+  const ShadeTri* stri;
   const uint32_t* texels;
   const TexDev* tex;
   const InstDev* inst;

@@ -168,8 +168,8 @@ __device__ __forceinline__ uint32_t texel_index(const TexDev& A, float2 uv) {
 __device__ __forceinline__ V3 geometry_normal(const SceneDev& S, uint32_t inst, uint32_t prim) {  // :47-58
   const InstDev& I = S.inst[inst];
   const MeshDev& M = S.mesh[I.mesh];
-  const float* f = S.facen + 3 * (size_t)(M.prim_base + prim);
-  return xform_vector(v3(f[0], f[1], f[2]), I.nrm);
+  const float4 f = reinterpret_cast<const float4*>(S.stri + M.prim_base + prim)[6];
+  return xform_vector(v3(f.x, f.y, f.z), I.nrm);
 }
 
 __device__ __forceinline__ HitAttr hit_attributes(const SceneDev& S, uint32_t inst, uint32_t prim, float u, float v,
@@ -177,23 +177,21 @@ __device__ __forceinline__ HitAttr hit_attributes(const SceneDev& S, uint32_t in
   HitAttr out;
   const InstDev& I = S.inst[inst];
   const MeshDev& M = S.mesh[I.mesh];
-  const size_t gp = (size_t)M.prim_base + prim;
+  const float4* st = reinterpret_cast<const float4*>(S.stri + M.prim_base + prim);
   const float w = 1.0f - u - v;
-  const float2 uv0 = S.fuv[3 * gp], uv1 = S.fuv[3 * gp + 1], uv2 = S.fuv[3 * gp + 2];
+  const float4 s0 = st[0], s1 = st[1], s2 = st[2], s3 = st[3];  // n0 n1 n2 | uv0 uv1 uv2 | p0.x
+  const float2 uv0 = make_float2(s2.y, s2.z), uv1 = make_float2(s2.w, s3.x), uv2 = make_float2(s3.y, s3.z);
   float2 uv;
   uv.x = v * uv2.x + u * uv1.x + w * uv0.x;
   uv.y = v * uv2.y + u * uv1.y + w * uv0.y;
   const TexDev A = S.tex[M.tex[0]];
   const uint32_t px = texel_index(A, uv);
-  const float4 n0 = S.fnrm[3 * gp], n1 = S.fnrm[3 * gp + 1], n2 = S.fnrm[3 * gp + 2];
+  const V3 n0 = v3(s0.x, s0.y, s0.z), n1 = v3(s0.w, s1.x, s1.y), n2 = v3(s1.z, s1.w, s2.x);
   // ---- GetShadingNormal (:60-138)
   if (M.tex[1] >= 0 && normalmapped) {
     const V3 nc = texel_normal(S.texels[S.tex[M.tex[1]].offset + px]);
-    const int32_t* vi = S.vidx + 3 * gp;
-    const float* P0 = S.vert + 3 * (size_t)(M.vert_base + vi[0]);
-    const float* P1 = S.vert + 3 * (size_t)(M.vert_base + vi[1]);
-    const float* P2 = S.vert + 3 * (size_t)(M.vert_base + vi[2]);
-    const V3 p0 = v3(P0[0], P0[1], P0[2]), p1 = v3(P1[0], P1[1], P1[2]), p2 = v3(P2[0], P2[1], P2[2]);
+    const float4 s4 = st[4], s5 = st[5];  // p0.yz p1.xy | p1.z p2
+    const V3 p0 = v3(s3.w, s4.x, s4.y), p1 = v3(s4.z, s4.w, s5.x), p2 = v3(s5.y, s5.z, s5.w);
     const V3 edge1 = p1 - p0, edge2 = p2 - p0;
     const float d1x = uv1.x - uv0.x, d1y = uv1.y - uv0.y, d2x = uv2.x - uv0.x, d2y = uv2.y - uv0.y;
     const float det = d1x * d2y - d1y * d2x;

@@ -296,50 +296,61 @@ __device__ __forceinline__ uint32_t fetch_some(uint32_t* fctr, uint32_t total, u
   return 0;
 }
 
-template <int REFILL>
-__global__ void __launch_bounds__(64) k_extend_p(SceneDev S, WaveBufs B, uint32_t iter) {
-  __shared__ uint32_t lds_stack[Trav<8>::kWords * 64];
+template <bool HALF, int REFILL, int STACK, int WAVES>
+__global__ void __launch_bounds__(64, WAVES) k_extend_p(SceneDev S, WaveBufs B, uint32_t iter) {
+  __shared__ uint32_t lds_stack[2 * STACK * 64];
   __shared__ uint32_t pref[kNSub + 1];
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
   const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
   uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
   uint32_t part = xcc_id();
-  trav8_persistent<false, 16, REFILL>(
+  trav8_persistent<false, HALF, STACK, REFILL>(
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) { return fetch_some(fctr, total, part, base, want); },
-      [&](uint32_t g, V3& O, V3& D, float& tmax, uint32_t& tag) {
+      [&](uint32_t g, V3& O, V3& D, float& tmax) -> uint32_t {
         const uint32_t item = q[map_slot(pref, g, B.qcap)];
         const float4 o = B.ro[item], d = B.rd[item];
         O = v3(o.x, o.y, o.z);
         D = v3(d.x, d.y, d.z);
         tmax = kFar;
-        tag = item;
+        return item;
+      },
+      [&](uint32_t item, V3& O, V3& D) {
+        const float4 o = B.ro[item], d = B.rd[item];
+        O = v3(o.x, o.y, o.z);
+        D = v3(d.x, d.y, d.z);
       },
       [&](uint32_t item, const Hit& h, bool) {
         B.hit[item] = make_float4(h.t, h.u, h.v, __uint_as_float(pack_hit(h.prim, h.inst)));
       });
 }
 
-template <int REFILL>
-__global__ void __launch_bounds__(64) k_shadow_p(SceneDev S, WaveBufs B, uint32_t iter) {
-  __shared__ uint32_t lds_stack[Trav<8>::kWords * 64];
+template <bool HALF, int REFILL, int STACK, int WAVES>
+__global__ void __launch_bounds__(64, WAVES) k_shadow_p(SceneDev S, WaveBufs B, uint32_t iter) {
+  __shared__ uint32_t lds_stack[2 * STACK * 64];
   __shared__ uint32_t pref[kNSub + 1];
   uint8_t* vis8 = reinterpret_cast<uint8_t*>(B.vis);
   const uint32_t total = load_prefix(B.ctr, iter, 1, pref);
   uint32_t* fctr = fetch_counters(B.ctr, iter, 1);
   uint32_t part = xcc_id();
-  trav8_persistent<true, 16, REFILL>(
+  trav8_persistent<true, HALF, STACK, REFILL>(
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) { return fetch_some(fctr, total, part, base, want); },
-      [&](uint32_t g, V3& O, V3& D, float& tmax, uint32_t& tag) {
+      [&](uint32_t g, V3& O, V3& D, float& tmax) -> uint32_t {
         const uint32_t slot = map_slot(pref, g, B.scap);
         const float4 o = B.sho[slot], d = B.shd[slot];
         O = v3(o.x, o.y, o.z);
         D = v3(d.x, d.y, d.z);
         tmax = o.w;
-        tag = __float_as_uint(d.w);
+        return slot;
       },
-      [&](uint32_t tag, const Hit&, bool occluded) {
+      [&](uint32_t slot, V3& O, V3& D) {
+        const float4 o = B.sho[slot], d = B.shd[slot];
+        O = v3(o.x, o.y, o.z);
+        D = v3(d.x, d.y, d.z);
+      },
+      [&](uint32_t slot, const Hit&, bool occluded) {
+        const uint32_t tag = __float_as_uint(B.shd[slot].w);
         if (!occluded) vis8[tag] = 1;
       });
 }
@@ -421,28 +432,51 @@ __global__ void __launch_bounds__(kBlock) k_resolve(SceneDev S, TraceArgs A, Til
   }
 }
 
+// persistent traversal launch: LDS stack depth and waves/SIMD by c.occ (the BVH depth was checked against
+// the stack on the host), refill threshold by c.trav; grid = the resident wave count
+template <bool ANY, int REFILL, int STACK, int WAVES>
+void launch_p1(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it) {
+  const dim3 grid(256u * 4u * WAVES);
+  if (c.layout == 9) {
+    if (ANY) hipLaunchKernelGGL((k_shadow_p<true, REFILL, STACK, WAVES>), grid, dim3(64), 0, c.stream, S, B, it);
+    else hipLaunchKernelGGL((k_extend_p<true, REFILL, STACK, WAVES>), grid, dim3(64), 0, c.stream, S, B, it);
+  } else {
+    if (ANY) hipLaunchKernelGGL((k_shadow_p<false, REFILL, STACK, WAVES>), grid, dim3(64), 0, c.stream, S, B, it);
+    else hipLaunchKernelGGL((k_extend_p<false, REFILL, STACK, WAVES>), grid, dim3(64), 0, c.stream, S, B, it);
+  }
+}
+template <bool ANY>
+void launch_persistent(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it) {
+  if (c.occ == 8) {
+    if (c.trav == 32) launch_p1<ANY, 32, 8, 8>(c, S, B, it); else launch_p1<ANY, 16, 8, 8>(c, S, B, it);
+  } else if (c.occ == 6) {
+    if (c.trav == 32) launch_p1<ANY, 32, 12, 6>(c, S, B, it); else launch_p1<ANY, 16, 12, 6>(c, S, B, it);
+  } else {
+    if (c.trav == 32) launch_p1<ANY, 32, 16, 5>(c, S, B, it); else launch_p1<ANY, 16, 16, 5>(c, S, B, it);
+  }
+}
+
 // ---- host launcher: the whole frame batch, no host synchronisation inside
 hipError_t launch_wavefront(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                             const WaveBufs& B, float4* out, WaveTimers* tm) {
   if (B.n == 0) return hipSuccess;
   const unsigned gtrav = 256u * 16u;  // one-wave blocks, static interleaved chunks
   const unsigned gprod = 256u * 4u;   // producer blocks (multiple of kNSub)
-  const unsigned gpers = 256u * 20u;  // persistent one-wave blocks: 20 resident per CU (8 KB LDS, <= 96 VGPRs)
   hipLaunchKernelGGL(k_wave_init, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, out);
   const uint32_t iters = (uint32_t)A.bounces * ((A.flags & kAA) ? 2u : 1u);
   for (uint32_t it = 0; it < iters; it++) {
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 0], c.stream);
     if (c.layout == 4) hipLaunchKernelGGL(k_extend<4>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    else if (c.trav == 1 && c.layout == 9) hipLaunchKernelGGL(k_extend<9>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
     else if (c.trav == 1) hipLaunchKernelGGL(k_extend<8>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
-    else if (c.trav == 32) hipLaunchKernelGGL(k_extend_p<32>, dim3(gpers), dim3(64), 0, c.stream, S, B, it);
-    else hipLaunchKernelGGL(k_extend_p<16>, dim3(gpers), dim3(64), 0, c.stream, S, B, it);
+    else launch_persistent<false>(c, S, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
     hipLaunchKernelGGL(k_shade, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 2], c.stream);
     if (c.layout == 4) hipLaunchKernelGGL(k_shadow<4>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
+    else if (c.trav == 1 && c.layout == 9) hipLaunchKernelGGL(k_shadow<9>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
     else if (c.trav == 1) hipLaunchKernelGGL(k_shadow<8>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
-    else if (c.trav == 32) hipLaunchKernelGGL(k_shadow_p<32>, dim3(gpers), dim3(64), 0, c.stream, S, B, it);
-    else hipLaunchKernelGGL(k_shadow_p<16>, dim3(gpers), dim3(64), 0, c.stream, S, B, it);
+    else launch_persistent<true>(c, S, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 3], c.stream);
     hipLaunchKernelGGL(k_resolve, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it, out);
   }
