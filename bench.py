@@ -40,6 +40,19 @@ def algorithmic_bytes_per_ray():
     return out, v
 
 
+def own_layout_bytes_per_ray():
+    """The build's own Node8 layout priced with its own visit counts (profiles/node8_visits_c4.json, from
+    scripts/measure_node8_visits.py): 80 B per node visit + 48 B per triangle test + ray in / result out."""
+    f = os.path.join(ROOT, "profiles", "node8_visits_c4.json")
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        v = json.load(fh)
+    c, a = v["all_closest"], v["all_anyhit"]
+    return {"closest": v["node_bytes"] * c["node_visits"] + v["tri_bytes"] * c["tri_tests"] + 4 + 32 + 16,
+            "anyhit": v["node_bytes"] * a["node_visits"] + v["tri_bytes"] * a["tri_tests"] + 32 + 1}
+
+
 def measured_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/traffic_current.json,
     written by scripts/summarize_prof.py; FETCH_SIZE x2 gfx950 correction, MI355X_MICROARCH.md HBM)."""
@@ -49,7 +62,8 @@ def measured_traffic(kernel):
     with open(f) as fh:
         t = json.load(fh)
     for name, d in t.get("kernels", {}).items():
-        if name.split("::")[-1].split("<")[0] == kernel and "hbm_bytes_per_launch" in d:
+        base = name.split("::")[-1].split("<")[0]
+        if base in (kernel, kernel + "_p") and "hbm_bytes_per_launch" in d:
             return int(d["hbm_bytes_per_launch"])
     return None
 
@@ -171,6 +185,13 @@ def main():
         alg_bytes, kern_ms = kern[dom]
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
         traffic = measured_traffic(dom)
+        own = own_layout_bytes_per_ray()
+        own_block = None
+        if own is not None and pipeline == 0:
+            own_b = (seg_f * own["closest"] if dom == "k_extend" else sh_f * own["anyhit"]) / launches
+            own_block = {"bytes_per_ray": {k: round(v, 1) for k, v in own.items()}, "algorithmic_bytes": round(own_b),
+                         "achieved": round(own_b / (kern_ms / 1e3) / 1e9, 1),
+                         "frac": round(own_b / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
         out = {
             "metric": "Mrays/s (closest-hit segments + shadow any-hit rays) at 1920x1080, 4 spp, depth 4",
             "value": round(value, 2),
@@ -197,7 +218,9 @@ def main():
                          "launch_ms": round(kern_ms, 4), "algorithmic_bytes": round(alg_bytes),
                          "kernels": {k: {"launch_ms": round(v[1], 4), "alg_GBps": round(v[0] / (v[1] / 1e3) / 1e9, 1)
                                          if v[1] > 0 else None} for k, v in kern.items()},
-                         "bytes_per_ray": {k: round(v, 1) for k, v in bpr.items()}},
+                         "bytes_per_ray": {k: round(v, 1) for k, v in bpr.items()},
+                         "own_layout": own_block,
+                         "traffic_GBps": round(traffic / (kern_ms / 1e3) / 1e9, 1) if traffic else None},
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)

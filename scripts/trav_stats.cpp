@@ -4,8 +4,9 @@
 // input:  <tris.bin>  float32 fat triangles (Model::triangles layout: 3 x float4 per triangle)
 //         <rays.bin>  float32 records {Ox,Oy,Oz,Dx,Dy,Dz,tmax,kind} (kind 0 = closest, 1 = any-hit),
 //                     in the order a wavefront queue would hand them to waves
-// output: per kind: mean node visits, leaf-triangle tests, stack pushes per ray; lock-step wave cost
-//         (iterations = max over lanes) and lane efficiency with and without per-lane ray refill.
+// output: per kind: mean node visits, leaf-triangle tests, stack pushes per ray (stdout; one JSON line per
+//         kind on stderr); with --models the lock-step wave cost (iterations = max over lanes), lane
+//         efficiency with and without per-lane ray refill, and the decoupled node/triangle model.
 //
 // build:  g++ -O2 -I physically-based-ray-tracer_amd/csrc scripts/trav_stats.cpp \
 //             physically-based-ray-tracer_amd/csrc/bvh_build.cpp -o /tmp/trav_stats
@@ -198,7 +199,7 @@ void wave_model_decoupled(const std::vector<Trace>& tr, int refill_at, int tri_p
 }  // namespace
 
 int main(int argc, char** argv) {
-  if (argc < 3) { std::fprintf(stderr, "usage: trav_stats tris.bin rays.bin\n"); return 1; }
+  if (argc < 3) { std::fprintf(stderr, "usage: trav_stats tris.bin rays.bin [--models]\n"); return 1; }
   FILE* f = std::fopen(argv[1], "rb");
   std::vector<float> tri;
   float buf[4096];
@@ -227,9 +228,13 @@ int main(int argc, char** argv) {
     if (tr.empty()) continue;
     std::printf("%s rays %zu: node visits %.2f  tri tests %.2f  pushes %.2f per ray\n", kind ? "any-hit" : "closest",
                 tr.size(), visits / tr.size(), tris / tr.size(), pushes / tr.size());
-    for (int ra : {64, 32, 16, 8}) wave_model(tr, ra, 130.0, 35.0, 40.0);
-    for (int ra : {64, 32, 16})
-      for (int tpi : {1, 2, 3}) wave_model_decoupled(tr, ra, tpi, 130.0, 35.0, 40.0);
+    std::fprintf(stderr, "{\"kind\": \"%s\", \"rays\": %zu, \"node_visits\": %.4f, \"tri_tests\": %.4f}\n",
+                 kind ? "anyhit" : "closest", tr.size(), visits / tr.size(), tris / tr.size());
+    if (argc > 3 && std::strcmp(argv[3], "--models") == 0) {
+      for (int ra : {64, 32, 16, 8}) wave_model(tr, ra, 130.0, 35.0, 40.0);
+      for (int ra : {64, 32, 16})
+        for (int tpi : {1, 2, 3}) wave_model_decoupled(tr, ra, tpi, 130.0, 35.0, 40.0);
+    }
   }
   return 0;
 }
