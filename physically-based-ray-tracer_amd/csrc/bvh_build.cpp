@@ -2,7 +2,9 @@
 #include "bvh_build.h"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace prt {
@@ -284,6 +286,72 @@ struct Fmt8H {
   }
 };
 
+// SAH-optimal collapse of the binary tree into 8-wide nodes (Ylitie, Karras, Laine 2017, sec. 3.1, restated):
+// C(n, i) = cheapest cost of representing binary subtree n by at most i slots of its parent, where one slot
+// is either a leaf (<= max_leaf triangles, cost A(n) * c_tri * count) or a wide node (A(n) * c_node + the
+// best distribution of its 8 slots over the two binary children).  Costs are area-weighted (SAH).
+struct WideDp {
+  std::vector<std::array<float, 9>> C;     // C[n][i], i = 1..8
+  std::vector<std::array<int8_t, 9>> Dk;   // best left share k of D(n, j) = C(l, k) + C(r, j - k), j = 2..8
+  std::vector<std::array<uint8_t, 9>> prev;  // C(n, i) == C(n, i - 1) (use fewer slots)
+  std::vector<uint8_t> leaf1;              // the single-slot form of n is a leaf
+
+  void compute(const Builder& B, float c_node, float c_tri) {
+    const size_t N = B.nodes.size();
+    C.assign(N, {});
+    Dk.assign(N, {});
+    prev.assign(N, {});
+    leaf1.assign(N, 0);
+    for (size_t n = N; n-- > 0;) {  // children are stored after their parent
+      const Node2& x = B.nodes[n];
+      const float A = std::max(x.box.area(), 1e-30f);
+      const float leafc = x.count <= B.max_leaf ? A * c_tri * (float)x.count : 3e38f;
+      if (x.leaf()) {
+        for (int i = 1; i <= 8; i++) { C[n][i] = leafc; prev[n][i] = i > 1; }
+        leaf1[n] = 1;
+        continue;
+      }
+      float D[9];
+      for (int j = 2; j <= 8; j++) {
+        D[j] = 3e38f;
+        for (int k = 1; k < j; k++) {
+          const float c = C[x.left][k] + C[x.right][j - k];
+          if (c < D[j]) { D[j] = c; Dk[n][j] = (int8_t)k; }
+        }
+      }
+      const float intc = A * c_node + D[8];
+      leaf1[n] = leafc <= intc;
+      C[n][1] = std::min(leafc, intc);
+      for (int i = 2; i <= 8; i++) {
+        prev[n][i] = C[n][i - 1] <= D[i];
+        C[n][i] = prev[n][i] ? C[n][i - 1] : D[i];
+      }
+    }
+  }
+  // the slots (binary node ids) that subtree n occupies when given at most i slots
+  void collect(const Builder& B, int32_t n, int i, int32_t* out, int& nc) const {
+    if (i == 1 || B.nodes[n].leaf()) { out[nc++] = n; return; }
+    if (prev[n][i]) { collect(B, n, i - 1, out, nc); return; }
+    const int k = Dk[n][i];
+    collect(B, B.nodes[n].left, k, out, nc);
+    collect(B, B.nodes[n].right, i - k, out, nc);
+  }
+  // the <= 8 children of the wide node made from binary node n
+  int expand(const Builder& B, int32_t n, int32_t* out) const {
+    int nc = 0;
+    if (B.nodes[n].leaf()) { out[nc++] = n; return nc; }
+    const int k = Dk[n][8];
+    collect(B, B.nodes[n].left, k, out, nc);
+    collect(B, B.nodes[n].right, 8 - k, out, nc);
+    return nc;
+  }
+};
+
+// relative SAH costs of an 8-wide node visit and of one triangle test in the traversal kernels
+// (measured optimum on C4 at 1 : 1 with the persistent kernels; PRT_COLLAPSE_TRI_COST overrides, and
+// PRT_COLLAPSE=greedy restores the area-greedy collapse)
+constexpr float kWideNodeCost = 1.0f, kWideTriCost = 1.0f;  // tri cost swept 0.15-5 on C4: flat above 1
+
 template <class NodeT, class Fmt, class Out>
 void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out) {
   Builder B;
@@ -292,6 +360,14 @@ void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out) {
   B.build(T);
   for (int k = 0; k < 3; k++) { out.bmin[k] = B.nodes[0].box.lo[k]; out.bmax[k] = B.nodes[0].box.hi[k]; }
   out.tris.reserve(T);
+  const char* ce = std::getenv("PRT_COLLAPSE");
+  const bool greedy = ce && std::strcmp(ce, "greedy") == 0;
+  WideDp dp;
+  if (!greedy) {
+    const char* cr = std::getenv("PRT_COLLAPSE_TRI_COST");
+    dp.compute(B, kWideNodeCost, cr ? (float)std::atof(cr) : kWideTriCost);
+  }
+  auto is_leaf = [&](int32_t n) { return greedy ? B.nodes[n].leaf() : dp.leaf1[n] != 0; };
   struct Item { int32_t n2; uint32_t n8; int depth; };
   std::vector<Item> work;
   out.nodes.push_back(NodeT());
@@ -300,11 +376,12 @@ void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out) {
     const Item it = work.back();
     work.pop_back();
     out.depth = std::max(out.depth, it.depth);
-    // gather up to 8 children by opening the largest-area interior child
     int32_t ch[8];
     int nc = 0;
     const Node2& root = B.nodes[it.n2];
-    if (root.leaf()) {
+    if (!greedy) {
+      nc = dp.expand(B, it.n2, ch);
+    } else if (root.leaf()) {  // greedy: open the largest-area interior child until 8 children
       ch[nc++] = it.n2;
     } else {
       ch[nc++] = root.left;
@@ -373,7 +450,7 @@ void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out) {
     nd.tri_base = (uint32_t)out.tris.size();
     uint32_t ninterior = 0;
     for (int s = 0; s < 8; s++)
-      if (child_in[s] >= 0 && !B.nodes[ch[child_in[s]]].leaf()) ninterior++;
+      if (child_in[s] >= 0 && !is_leaf(ch[child_in[s]])) ninterior++;
     out.nodes.resize(out.nodes.size() + ninterior);
     uint32_t nextchild = nd.child_base, tri_off = 0;
     for (int s = 0; s < 8; s++) {
@@ -389,7 +466,7 @@ void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out) {
       }
       Fmt::set(nd, s, qlo, qhi);
       const Node2& c = B.nodes[ch[i]];
-      if (c.leaf()) {
+      if (is_leaf(ch[i])) {
         for (int32_t j = c.first; j < c.first + c.count; j++) {
           const uint32_t pr = B.idx[j];
           const float* a = triangles + 12 * (size_t)pr;

@@ -8,7 +8,7 @@
 //         kind on stderr); with --models the lock-step wave cost (iterations = max over lanes), lane
 //         efficiency with and without per-lane ray refill, and the decoupled node/triangle model.
 //
-// build:  g++ -O2 -I physically-based-ray-tracer_amd/csrc scripts/trav_stats.cpp \
+// build:  g++ -O2 -I physically-based-ray-tracer_amd/csrc scripts/trav_stats.cpp
 //             physically-based-ray-tracer_amd/csrc/bvh_build.cpp -o /tmp/trav_stats
 #include <algorithm>
 #include <cmath>
