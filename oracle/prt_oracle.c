@@ -78,6 +78,9 @@ static inline f3 reflect3(f3 i, f3 n) { return sub3(i, muls(smul(2.0f, n), dot3(
 
 /* correctly-rounded float transcendentals (see header comment) */
 static inline float cr_pow(float x, float y) { return (float)pow((double)x, (double)y); }
+/* pow(x, 5) of the Fresnel term (BRDF.cpp:84-87) as x^5 in double rounded once to float: the correctly
+ * rounded x^5 but within 2^-50 of a float rounding boundary (same expression as the GPU's pow5) */
+static inline float pow5f(float x) { const double d = (double)x, d2 = d * d; return (float)(d2 * d2 * d); }
 static inline float cr_sin(float x) { return (float)sin((double)x); }
 static inline float cr_cos(float x) { return (float)cos((double)x); }
 static inline float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
@@ -549,7 +552,7 @@ static inline f3 specular_f0(f3 base, float metal) {                            
 static inline f3 diffuse_refl(f3 base, float metal) { return muls(base, 1.0f - metal); }              /* :32-35 */
 static inline float shadowed_f90(f3 F0) { const float t = (1.0f / MIN_DIELECTRICS_F0); return smin(1.0f, t * luminance(F0)); } /* :100-104 */
 static inline f3 fresnel(f3 f0, float f90, float NdotS) {                                            /* :84-87 */
-    float p = cr_pow(1.0f - NdotS, 5.0f);
+    float p = pow5f(1.0f - NdotS);
     return add3(f0, muls(v3(f90 - f0.x, f90 - f0.y, f90 - f0.z), p));
 }
 static inline float ggx_d(float a2, float NdotH) {                                                    /* :218-222 */

@@ -116,6 +116,7 @@ struct prt_ctx {
   // sky, lights, camera
   DevBuf sky;
   int32_t skyw = 0, skyh = 0;
+  DevBuf srgb;  // 256-entry sRGB -> linear table of the albedo decode
   prt_lights lights{};
   bool have_lights = false;
   prt_camera cam{};
@@ -213,6 +214,7 @@ int scene_ready(prt_ctx* c, SceneDev& S) {
   S.nodes8h = c->nodes8h.as<Node8H>();
   S.tris = c->tris.as<TriMT>();
   S.stri = c->stri.as<ShadeTri>();
+  S.srgb = c->srgb.as<float>();
   S.texels = c->texels.as<uint32_t>();
   S.tex = c->tex.as<TexDev>();
   S.inst = c->inst.as<InstDev>();
@@ -416,6 +418,19 @@ int prt_create(const prt_device_desc* desc, prt_ctx** out) {
     return fail(PRT_ERR_HIP, "hipStreamCreate failed");
   }
   c->stream = c->own_stream;
+  {
+    // srgbToLinear of every albedo byte (Scene.cpp:171 on texel/255, BRDF.cpp srgbToLinear); the same
+    // float ops and double-precision pow rounded once as the oracle, evaluated on the host
+    float lut[256];
+    for (int b = 0; b < 256; b++) {
+      const float x = (float)b * (1.0f / 255.0f);
+      lut[b] = (x <= 0.04045f) ? (x / 12.92f) : (float)std::pow((double)((x + 0.055f) / 1.055f), (double)2.4f);
+    }
+    if (upload(c->srgb, lut, sizeof(lut)) != hipSuccess) {
+      delete c;
+      return fail(PRT_ERR_HIP, "srgb table upload failed");
+    }
+  }
   for (auto& e : c->ev) {
     if (hipEventCreate(&e) != hipSuccess) {
       delete c;
@@ -437,7 +452,7 @@ int prt_destroy(prt_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->texels, &c->tex, &c->nodes, &c->nodes8, &c->nodes8h, &c->tris, &c->stri,
-                    &c->mesh, &c->inst, &c->sky, &c->acc, &c->nsamp, &c->dist, &c->frames, &c->avg, &c->rgb8,
+                    &c->mesh, &c->inst, &c->sky, &c->srgb, &c->acc, &c->nsamp, &c->dist, &c->frames, &c->avg, &c->rgb8,
                     &c->counters, &c->hits})
     b->release();
   for (auto e : c->ev)

@@ -59,6 +59,13 @@ PRT_HD float lerpf(float a, float b, float t) { return a + t * (b - a); }
 PRT_HD V3 reflect(V3 i, V3 n) { return i - (2.0f * n) * dot(n, i); }              // tmpl8math.h:547
 
 PRT_HD float cr_pow(float x, float y) { return (float)pow((double)x, (double)y); }
+// pow(x, 5) (BRDF.cpp:84-87 Fresnel): x^5 in double (three roundings, <= 3 ulp of double) rounded once to
+// float -- the correctly rounded float x^5 except within 2^-50 of a float rounding boundary; the oracle
+// evaluates the identical double expression
+PRT_HD float pow5(float x) {
+  const double d = (double)x, d2 = d * d;
+  return (float)(d2 * d2 * d);
+}
 PRT_HD float cr_sin(float x) { return (float)sin((double)x); }
 PRT_HD float cr_cos(float x) { return (float)cos((double)x); }
 PRT_HD float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }

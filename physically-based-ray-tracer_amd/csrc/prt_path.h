@@ -48,35 +48,34 @@ __device__ __forceinline__ int nee_kind(uint32_t fl, uint32_t& seed) {
 }
 __device__ __forceinline__ int nee_rays(int kind) { return kind == 0 ? 4 : 1; }
 
-// Builds the shadow rays of `kind` (emit(k, ray, tmax) per ray, in order), the per-ray unoccluded
-// contribution f[k] (before the pick-probability division) and returns the BRDF value the reference
-// evaluates for this light class (0 when !LIGHTED).  Draws whichLight for point lights.
+// Builds the shadow rays of `kind` (emit(k, ray, tmax, f_k) per ray, in order, with f_k the ray's
+// unoccluded contribution before the pick-probability division) and returns the BRDF value the reference
+// evaluates for this light class (0 when !LIGHTED).  Draws whichLight for point lights: the reference
+// draws it after tracing the four shadow rays (:267), which consume no random numbers, so drawing it
+// first keeps the stream and lets only the chosen light direction stay live.
 template <class Emit>
 __device__ __forceinline__ V3 nee_lights(const SceneDev& S, uint32_t fl, int kind, V3 I, V3 V, V3 N, const Material& m,
-                                         uint32_t& seed, V3* f, Emit&& emit) {
+                                         uint32_t& seed, Emit&& emit) {
   if (kind == 0) {                                                                          // :216-269
-    float lx = 0.0f, ly = 0.0f, lz = 0.0f;
-    float Lx[4], Ly[4], Lz[4];
+    const int wl = (int)(random_float(seed) * 10) % 4;                                     // :267
+    V3 Lw = v3(0.0f, 0.0f, 0.0f);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      Lx[i] = S.ppos[3 * i] - I.x; Ly[i] = S.ppos[3 * i + 1] - I.y; Lz[i] = S.ppos[3 * i + 2] - I.z;
-      const float dsq = (Lx[i] * Lx[i] + Ly[i] * Ly[i]) + Lz[i] * Lz[i];
+      float Lx = S.ppos[3 * i] - I.x, Ly = S.ppos[3 * i + 1] - I.y, Lz = S.ppos[3 * i + 2] - I.z;
+      const float dsq = (Lx * Lx + Ly * Ly) + Lz * Lz;
       const float dist = sqrtf(dsq);
       const float invD = 1.0f / dist;  // _mm_rcp_ps restated as an exact reciprocal
-      Lx[i] = Lx[i] * invD; Ly[i] = Ly[i] * invD; Lz[i] = Lz[i] * invD;
-      float cosa = (N.x * Lx[i] + N.y * Ly[i]) + N.z * Lz[i];
+      Lx = Lx * invD; Ly = Ly * invD; Lz = Lz * invD;
+      float cosa = (N.x * Lx + N.y * Ly) + N.z * Lz;
       cosa = (cosa > 0.0f) ? cosa : 0.0f;  // _mm_max_ps(cosa, 0)
       const float k = invD * cosa;
-      f[i] = v3(S.pcol[3 * i] * k, S.pcol[3 * i + 1] * k, S.pcol[3 * i + 2] * k);
-      const V3 L = v3(Lx[i], Ly[i], Lz[i]);
-      emit(i, make_ray(I + L * kEpsilon, L), dsq - kEpsilon);  // tmax = squared distance (:257)
+      const V3 L = v3(Lx, Ly, Lz);
+      if (i == wl) Lw = L;
+      emit(i, make_ray(I + L * kEpsilon, L), dsq - kEpsilon,                                // tmax = squared distance (:257)
+           v3(S.pcol[3 * i] * k, S.pcol[3 * i + 1] * k, S.pcol[3 * i + 2] * k));
     }
-    const int wl = (int)(random_float(seed) * 10) % 4;                                     // :267
     if (!(fl & kLighted)) return v3(0.0f, 0.0f, 0.0f);
-    lx = wl == 0 ? Lx[0] : wl == 1 ? Lx[1] : wl == 2 ? Lx[2] : Lx[3];
-    ly = wl == 0 ? Ly[0] : wl == 1 ? Ly[1] : wl == 2 ? Ly[2] : Ly[3];
-    lz = wl == 0 ? Lz[0] : wl == 1 ? Lz[1] : wl == 2 ? Lz[2] : Lz[3];
-    return eval_combined_brdf(N, v3(lx, ly, lz), V, m);
+    return eval_combined_brdf(N, Lw, V, m);
   }
   const float* lp = (kind == 2) ? S.spos : S.dpos;                                          // :270-326
   const float* lc = (kind == 2) ? S.scol : S.dcol;
@@ -84,14 +83,15 @@ __device__ __forceinline__ V3 nee_lights(const SceneDev& S, uint32_t fl, int kin
   const float distance = length(L);
   L = L / distance;
   const float cosa = smax(0.0f, dot(N, L));
-  emit(0, make_ray(I + L * kEpsilon, L), distance - kEpsilon);
+  V3 f0;
   if (kind == 2) {
     const float factor = dot(L, v3(S.srot[0], S.srot[1], S.srot[2]));
-    f[0] = ((double)factor > 0.9) ? v3(lc[0], lc[1], lc[2]) * (1 / (distance * distance)) * cosa
-                                  : v3(0.0f, 0.0f, 0.0f);
+    f0 = ((double)factor > 0.9) ? v3(lc[0], lc[1], lc[2]) * (1 / (distance * distance)) * cosa
+                                : v3(0.0f, 0.0f, 0.0f);
   } else {
-    f[0] = v3(lc[0], lc[1], lc[2]) * cosa;
+    f0 = v3(lc[0], lc[1], lc[2]) * cosa;
   }
+  emit(0, make_ray(I + L * kEpsilon, L), distance - kEpsilon, f0);
   return (fl & kLighted) ? eval_combined_brdf(N, L, V, m) : v3(0.0f, 0.0f, 0.0f);
 }
 

@@ -48,7 +48,8 @@ __device__ V3 trace_path(const SceneDev& S, const TraceArgs& A, Ray r, uint32_t&
     const int kind = nee_kind(fl, seed);                                                  // :198-326
     uint32_t vis = 0;
     V3 f[4];
-    const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed, f, [&](int k, const Ray& sr, float tmax) {
+    const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed, [&](int k, const Ray& sr, float tmax, V3 fk) {
+      f[k] = fk;
       nshadow++;
       if (!Trav<BV>::template anyhit<kBlock>(S, sr, tmax, stk)) vis |= 1u << k;
     });

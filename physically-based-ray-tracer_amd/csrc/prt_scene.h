@@ -61,6 +61,7 @@ struct SceneDev {
   const InstDev* inst;
   const MeshDev* mesh;
   const float* sky;
+  const float* srgb;  // srgbToLinear(byte / 255) for byte 0..255
   int32_t ninst;
   int32_t skyw, skyh;
   int32_t pad0;

@@ -35,7 +35,7 @@ __device__ __forceinline__ float shadowed_f90(V3 F0) {                          
   return smin(1.0f, t * luminance(F0));
 }
 __device__ __forceinline__ V3 fresnel_schlick(V3 f0, float f90, float NdotS) {  // :84-87
-  const float p = cr_pow(1.0f - NdotS, 5.0f);
+  const float p = pow5(1.0f - NdotS);
   return f0 + v3(f90 - f0.x, f90 - f0.y, f90 - f0.z) * p;
 }
 __device__ __forceinline__ float ggx_d(float a2, float NdotH) {  // :218-222
@@ -209,8 +209,8 @@ __device__ __forceinline__ HitAttr hit_attributes(const SceneDev& S, uint32_t in
     out.N = xform_vector(it, I.nrm);  // not normalised (Scene.cpp:134-136)
   }
   // ---- GetMaterialBRDF (:140-218)
-  const V3 c = texel_color(S.texels[A.offset + px]);
-  out.m.base = v3(srgb1(c.x), srgb1(c.y), srgb1(c.z));
+  const uint32_t ct = S.texels[A.offset + px];  // srgb1(texel_color(ct)) per channel, tabulated
+  out.m.base = v3(S.srgb[(ct >> 16) & 0xFFu], S.srgb[(ct >> 8) & 0xFFu], S.srgb[ct & 0xFFu]);
   out.m.metal = 0.0f;
   out.m.rough = 0.0f;
   out.m.emis = v3(0.0f, 0.0f, 0.0f);

@@ -24,7 +24,7 @@
 
 namespace prt {
 
-enum : uint32_t { kStEndValue = 0, kStNeeEnd = 1, kStNeeCont = 2 };
+enum : uint32_t { kStEndValue = 0, kStNeeEnd = 1, kStNeeCont = 2, kStMiss = 3 };
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ uint32_t* qcounter(uint32_t* ctr, uint32_t iter, uint32_t which, uint32_t s) {
@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(64) k_extend(SceneDev S, WaveBufs B, uint32_t 
   }
 }
 
-// ---- shading, NEE set-up (shadow rays straight into the shadow queue), BRDF sampling
+// ---- shading, NEE set-up (shadow rays straight into the shadow queue), BRDF sampling (render mode 0)
 __global__ void __launch_bounds__(kBlock) k_shade(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter) {
   __shared__ uint32_t pref[kNSub + 1];
   __shared__ uint32_t sm[8];
@@ -184,56 +184,41 @@ __global__ void __launch_bounds__(kBlock) k_shade(SceneDev S, TraceArgs A, WaveB
   const uint32_t fl = A.flags;
   for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
     const uint32_t g = c * kBlock + threadIdx.x;
-    uint32_t item = 0, info = 0, depth = 0, status = kStEndValue;
+    uint32_t item = 0, info = 0, seed = 0, nr = 0;
     int kind = 0;
-    uint32_t nr = 0;
     float4 hh = make_float4(kFar, 0.0f, 0.0f, 0.0f);
-    V3 O = v3(0.0f, 0.0f, 0.0f), D = v3(0.0f, 0.0f, 1.0f);
-    uint32_t seed = 0;
     const bool active = g < total;
-    bool shaded = false;
     if (active) {
       item = q[map_slot(pref, g, B.qcap)];
       info = B.info[item];
-      depth = info & 0xFFu;
-      const uint32_t path = (info >> 8) & 1u;
-      const float4 o = B.ro[item], d = B.rd[item];
       hh = B.hit[item];
-      O = v3(o.x, o.y, o.z);
-      D = v3(d.x, d.y, d.z);
-      if (depth == 0 && path == 0) B.s1[item].w = hh.x;                                    // r1.hit.t
-      if (hh.x >= kFar) {                                                                    // :159
-        const V3 L = (fl & kSkybox) ? sample_sky(S, D) : v3(0.0f, 0.0f, 0.0f);
-        B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
-      } else if (A.mode != 0) {                                                              // :170-194
-        const uint32_t pk = __float_as_uint(hh.w);
-        const HitAttr ha = hit_attributes(S, pk >> 26, pk & 0x03FFFFFFu, hh.y, hh.z, (fl & kNormalMap) != 0);
-        const V3 L = debug_view(S, A.mode, ha, pk >> 26, pk & 0x03FFFFFFu);
-        B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
-      } else {
+      if ((info & 0x1FFu) == 0) B.s1[item].w = hh.x;                                        // r1.hit.t
+      if (hh.x < kFar) {  // misses (:159) are resolved in k_resolve: the sky lookup's double-precision
+                          // atan2 / acos would otherwise set this kernel's register budget
         seed = B.seed[item];
         kind = nee_kind(fl, seed);                                                           // :198-214
         nr = (uint32_t)nee_rays(kind);
-        shaded = true;
       }
     }
     // reserve the shadow-ray slots of the whole block at once (one atomic per 256 items)
     const uint32_t s0 = block_append(shcnt, nr, sm);
-    if (shaded) {
+    uint32_t status = kStMiss;
+    if (nr) {
+      const uint32_t depth = info & 0xFFu;
+      const float4 o = B.ro[item], d = B.rd[item];
+      const V3 D = v3(d.x, d.y, d.z);
       const uint32_t pk = __float_as_uint(hh.w);
-      const uint32_t prim = pk & 0x03FFFFFFu, inst = pk >> 26;
-      const V3 I = O + hh.x * D;                                                             // tiny_bvh.h:586
+      const V3 I = v3(o.x, o.y, o.z) + hh.x * D;                                             // tiny_bvh.h:586
       const V3 V = -D;
-      const HitAttr ha = hit_attributes(S, inst, prim, hh.y, hh.z, (fl & kNormalMap) != 0);
+      const HitAttr ha = hit_attributes(S, pk >> 26, pk & 0x03FFFFFFu, hh.y, hh.z, (fl & kNormalMap) != 0);
       const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
-      V3 f[4];
-      const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed, f, [&](int k, const Ray& sr, float tmax) {
+      B.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
+      const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed, [&](int k, const Ray& sr, float tmax, V3 fk) {
         sho[s0 + k] = make_float4(sr.O.x, sr.O.y, sr.O.z, tmax);
         shd[s0 + k] = make_float4(sr.D.x, sr.D.y, sr.D.z, __uint_as_float(4u * item + (uint32_t)k));
+        B.nf[4 * (size_t)item + k] = make_float4(fk.x, fk.y, fk.z, 0.0f);
       });
-      B.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
       B.nb[item] = make_float4(brdf.x, brdf.y, brdf.z, 0.0f);
-      for (uint32_t k = 0; k < nr; k++) B.nf[4 * (size_t)item + k] = make_float4(f[k].x, f[k].y, f[k].z, 0.0f);
       B.vis[item] = 0u;
       status = kStNeeEnd;
       if ((int)depth != A.bounces - 1) {                                                     // :329
@@ -249,6 +234,57 @@ __global__ void __launch_bounds__(kBlock) k_shade(SceneDev S, TraceArgs A, WaveB
       B.seed[item] = seed;
     }
     if (active) B.info[item] = (info & 0x1FFu) | (status << 16) | ((uint32_t)kind << 20);
+  }
+}
+
+// ---- misses of this iteration (:159): sky radiance (or 0) ends the path.  Kept out of k_shade and
+// k_resolve: the sky lookup's double-precision atan2 / acos would set their register budgets.
+__global__ void __launch_bounds__(kBlock) k_miss(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter) {
+  __shared__ uint32_t pref[kNSub + 1];
+  const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
+  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
+  for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    const uint32_t g = c * kBlock + threadIdx.x;
+    if (g >= total) continue;
+    const uint32_t item = q[map_slot(pref, g, B.qcap)];
+    const uint32_t info = B.info[item];
+    if (((info >> 16) & 3u) != kStMiss) continue;
+    V3 L = v3(0.0f, 0.0f, 0.0f);
+    if (A.flags & kSkybox) {
+      const float4 d = B.rd[item];
+      L = sample_sky(S, v3(d.x, d.y, d.z));
+    }
+    B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
+    B.info[item] = info & ~(3u << 16);  // kStEndValue
+  }
+}
+
+// ---- debug render modes (Core/Renderer.cpp:170-194): the hit's debug colour ends the path
+__global__ void __launch_bounds__(kBlock) k_shade_debug(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter) {
+  __shared__ uint32_t pref[kNSub + 1];
+  const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
+  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
+  const uint32_t fl = A.flags;
+  for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    const uint32_t g = c * kBlock + threadIdx.x;
+    if (g >= total) continue;
+    const uint32_t item = q[map_slot(pref, g, B.qcap)];
+    const uint32_t info = B.info[item];
+    const float4 hh = B.hit[item];
+    if ((info & 0x1FFu) == 0) B.s1[item].w = hh.x;
+    V3 L = v3(0.0f, 0.0f, 0.0f);
+    if (hh.x >= kFar) {
+      if (fl & kSkybox) {
+        const float4 d = B.rd[item];
+        L = sample_sky(S, v3(d.x, d.y, d.z));
+      }
+    } else {
+      const uint32_t pk = __float_as_uint(hh.w);
+      const HitAttr ha = hit_attributes(S, pk >> 26, pk & 0x03FFFFFFu, hh.y, hh.z, (fl & kNormalMap) != 0);
+      L = debug_view(S, A.mode, ha, pk >> 26, pk & 0x03FFFFFFu);
+    }
+    B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
+    B.info[item] = info & 0x1FFu;  // status kStEndValue
   }
 }
 
@@ -378,7 +414,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(SceneDev S, TraceArgs A, Til
       const float4 ne = B.ne[item];
       V3 L = v3(ne.x, ne.y, ne.z);
       bool path_end = true;
-      if (status != kStEndValue) {
+      if (status == kStNeeEnd || status == kStNeeCont) {
         const float4 nb = B.nb[item];
         const uint32_t vw = B.vis[item];
         const uint32_t vis = ((vw & 0xFFu) ? 1u : 0u) | ((vw & 0xFF00u) ? 2u : 0u) | ((vw & 0xFF0000u) ? 4u : 0u) |
@@ -471,7 +507,11 @@ hipError_t launch_wavefront(const LaunchCfg& c, const SceneDev& S, const TraceAr
     else if (c.trav == 1) hipLaunchKernelGGL(k_extend<8>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
     else launch_persistent<false>(c, S, B, it);
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
-    hipLaunchKernelGGL(k_shade, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
+    if (A.mode != 0) hipLaunchKernelGGL(k_shade_debug, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
+    else {
+      hipLaunchKernelGGL(k_shade, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
+      hipLaunchKernelGGL(k_miss, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
+    }
     if (tm) (void)hipEventRecord(tm->ev[4 * it + 2], c.stream);
     if (c.layout == 4) hipLaunchKernelGGL(k_shadow<4>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
     else if (c.trav == 1 && c.layout == 9) hipLaunchKernelGGL(k_shadow<9>, dim3(gtrav), dim3(64), 0, c.stream, S, B, it);
