@@ -364,16 +364,23 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
       std::vector<uint32_t> ctr(kCtrWords);
       HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
+      const bool dump = std::getenv("PRT_DEBUG_QUEUES") != nullptr;
       for (uint32_t k = 0; k < iters; k++) {
+        uint64_t qs = 0, qa = 0;
         for (uint32_t s = 0; s < kNSub; s++) {
-          stats->segments += ctr[((k * 2 + 0) * kNSub + s) * kCtrStride];
-          stats->shadow_rays += ctr[((k * 2 + 1) * kNSub + s) * kCtrStride];
+          qs += ctr[((k * 2 + 0) * kNSub + s) * kCtrStride];
+          qa += ctr[((k * 2 + 1) * kNSub + s) * kCtrStride];
         }
+        stats->segments += qs;
+        stats->shadow_rays += qa;
         float a = 0, b = 0;
         HIP_TRY(hipEventElapsedTime(&a, c->wt.ev[4 * k + 0], c->wt.ev[4 * k + 1]));
         HIP_TRY(hipEventElapsedTime(&b, c->wt.ev[4 * k + 2], c->wt.ev[4 * k + 3]));
         stats->ms_closest += a;
         stats->ms_anyhit += b;
+        if (dump)
+          std::fprintf(stderr, "prt: iteration %u: %llu closest rays %.3f ms, %llu shadow rays %.3f ms\n", k,
+                       (unsigned long long)qs, a, (unsigned long long)qa, b);
       }
       stats->pipeline = 0;
       stats->iterations = (int32_t)iters;
@@ -437,8 +444,8 @@ int prt_create(const prt_device_desc* desc, prt_ctx** out) {
       return fail(PRT_ERR_HIP, "hipEventCreate failed");
     }
   }
-  for (auto& e : c->wt.ev) {
-    if (hipEventCreate(&e) != hipSuccess) {
+  for (auto& e : c->wt.ev) {  // per-launch timers only: no system-scope fence / cache writeback per record
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess && hipEventCreate(&e) != hipSuccess) {
       delete c;
       return fail(PRT_ERR_HIP, "hipEventCreate failed");
     }

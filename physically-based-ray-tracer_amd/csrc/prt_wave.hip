@@ -320,8 +320,15 @@ __device__ __forceinline__ uint32_t fetch_some(uint32_t* fctr, uint32_t total, u
   for (uint32_t tries = 0; tries < kParts; tries++) {
     const uint32_t lo = (uint32_t)(((uint64_t)total * part) / kParts);
     const uint32_t hi = (uint32_t)(((uint64_t)total * (part + 1)) / kParts);
-    uint32_t off = 0;
-    if (lane_id() == 0) off = (hi > lo) ? atomicAdd(fctr + part * kCtrStride, want) : 0xFFFFFFFFu;
+    uint32_t off = 0xFFFFFFFFu;
+    if (lane_id() == 0 && hi > lo) {
+      // the wave's current part: straight to the atomic.  Other parts (stealing, end of launch): a plain
+      // relaxed read first, so a drained part costs no atomic and the end of a launch does not queue
+      // every wave's failing atomics on eight addresses
+      uint32_t* ctr = fctr + part * kCtrStride;
+      if (tries == 0 || __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hi - lo)
+        off = atomicAdd(ctr, want);
+    }
     off = __shfl(off, 0, 64);
     if (off != 0xFFFFFFFFu && off < hi - lo) {
       *base = lo + off;
@@ -338,6 +345,7 @@ __global__ void __launch_bounds__(64, WAVES) k_extend_p(SceneDev S, WaveBufs B, 
   __shared__ uint32_t pref[kNSub + 1];
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
   const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
+  if (blockIdx.x * 64u >= total) return;  // small queues: only as many waves as 64-ray chunks
   uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
   uint32_t part = xcc_id();
   trav8_persistent<false, HALF, STACK, REFILL>(
@@ -367,6 +375,7 @@ __global__ void __launch_bounds__(64, WAVES) k_shadow_p(SceneDev S, WaveBufs B, 
   __shared__ uint32_t pref[kNSub + 1];
   uint8_t* vis8 = reinterpret_cast<uint8_t*>(B.vis);
   const uint32_t total = load_prefix(B.ctr, iter, 1, pref);
+  if (blockIdx.x * 64u >= total) return;
   uint32_t* fctr = fetch_counters(B.ctr, iter, 1);
   uint32_t part = xcc_id();
   trav8_persistent<true, HALF, STACK, REFILL>(
