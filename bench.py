@@ -63,7 +63,7 @@ def measured_traffic(kernel):
         t = json.load(fh)
     for name, d in t.get("kernels", {}).items():
         base = name.split("::")[-1].split("<")[0]
-        if base in (kernel, kernel + "_p") and "hbm_bytes_per_launch" in d:
+        if base in (kernel, kernel + "_p", kernel + "2") and "hbm_bytes_per_launch" in d:
             return int(d["hbm_bytes_per_launch"])
     return None
 
@@ -174,9 +174,12 @@ def main():
         # SURVEY 8d bytes) of the rays one launch processes over the kernel's average launch duration (HIP events
         # recorded on the render stream around every launch; ms_closest / ms_anyhit sum them per frame)
         seg_f, sh_f = seg / args.steps, shadow / args.steps
-        launches = max(1, iters) if pipeline == 0 else 1
+        launches = max(1, iters) if pipeline in (0, 2) else 1
         kern = {}
-        if pipeline == 0:
+        if pipeline == 2:  # merged pipeline: one traversal launch per iteration (closest + shadow rays)
+            kern["k_trace"] = ((seg_f * bpr["closest"] + sh_f * bpr["anyhit"]) / launches,
+                               float(np.mean(ms_closest)) / launches)
+        elif pipeline == 0:
             kern["k_extend"] = (seg_f * bpr["closest"] / launches, float(np.mean(ms_closest)) / launches)
             kern["k_shadow"] = (sh_f * bpr["anyhit"] / launches, float(np.mean(ms_anyhit)) / launches)
         else:
@@ -187,8 +190,9 @@ def main():
         traffic = measured_traffic(dom)
         own = own_layout_bytes_per_ray()
         own_block = None
-        if own is not None and pipeline == 0:
-            own_b = (seg_f * own["closest"] if dom == "k_extend" else sh_f * own["anyhit"]) / launches
+        if own is not None and pipeline in (0, 2):
+            own_b = ((seg_f * own["closest"] if dom in ("k_extend", "k_trace") else 0.0) +
+                     (sh_f * own["anyhit"] if dom in ("k_shadow", "k_trace") else 0.0)) / launches
             own_block = {"bytes_per_ray": {k: round(v, 1) for k, v in own.items()}, "algorithmic_bytes": round(own_b),
                          "achieved": round(own_b / (kern_ms / 1e3) / 1e9, 1),
                          "frac": round(own_b / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
@@ -204,7 +208,7 @@ def main():
             "scaling": "strong",  # one fixed frame is split into pixel tiles over the N GPUs
             "vs_baseline": None,
             "dtype": "f32",
-            "pipeline": "wavefront" if pipeline == 0 else "megakernel",
+            "pipeline": {0: "wavefront", 1: "megakernel", 2: "wavefront-merged"}[pipeline],
             "data": "synthetic (seeded procedural heightfield, textures, sky; scenes.py)",
             "config": {"workload": f"{sd.name}: {info.triangles} tris, {W}x{H}, {args.spp} spp, depth {args.bounces}",
                        "global_batch": W * H, "seq_len": args.bounces,

@@ -286,7 +286,7 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces) {
   const size_t qn = (size_t)kNSub * qcap, sn = 4 * qn;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
-  const size_t o_seed = take(4ull * n), o_info = take(4ull * n), o_ro = take(16ull * n), o_rd = take(16ull * n),
+  const size_t o_seed = take(4ull * n), o_info = take(4ull * n), o_rinfo = take(4ull * n), o_ro = take(16ull * n), o_rd = take(16ull * n),
                o_R = take(16ull * n * levels), o_T = take(16ull * n * levels), o_s1 = take(16ull * n),
                o_jit = take(8ull * n), o_hit = take(16ull * n), o_ne = take(16ull * n), o_nb = take(16ull * n),
                o_nf = take(64ull * n), o_vis = take(4ull * n), o_q0 = take(4 * qn), o_q1 = take(4 * qn),
@@ -297,7 +297,7 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces) {
   W.n = n;
   W.qcap = qcap;
   W.scap = 4u * qcap;
-  W.seed = (uint32_t*)(b + o_seed); W.info = (uint32_t*)(b + o_info);
+  W.seed = (uint32_t*)(b + o_seed); W.info = (uint32_t*)(b + o_info); W.rinfo = (uint32_t*)(b + o_rinfo);
   W.ro = (float4*)(b + o_ro); W.rd = (float4*)(b + o_rd); W.R = (float4*)(b + o_R); W.T = (float4*)(b + o_T);
   W.s1 = (float4*)(b + o_s1); W.jit = (float2*)(b + o_jit); W.hit = (float4*)(b + o_hit);
   W.ne = (float4*)(b + o_ne); W.nb = (float4*)(b + o_nb); W.nf = (float4*)(b + o_nf); W.vis = (uint32_t*)(b + o_vis);
@@ -308,9 +308,13 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces) {
   return PRT_OK;
 }
 
-bool use_megakernel() {
+// PRT_PIPELINE: "mega" = one megakernel per pixel-frame, "wave1" = wavefront with separate extend /
+// shadow launches (prt_wave.hip), default = merged-trace wavefront (prt_wave2.hip)
+int pipeline_from_env() {
   const char* e = std::getenv("PRT_PIPELINE");
-  return e && std::strcmp(e, "mega") == 0;
+  if (e && std::strcmp(e, "mega") == 0) return 1;
+  if (e && std::strcmp(e, "wave1") == 0) return 0;
+  return 2;
 }
 
 // the shared trace + accumulate sequence for prt_render / prt_render_tiles
@@ -333,7 +337,10 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
   A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F;
   LaunchCfg L{c->stream, layout, trav_from_env(), occ_for(c)};
-  const bool mega = use_megakernel();
+  // the merged pipeline runs the persistent 8-wide traversal only: Node4 and the lock-step kernels use wave1
+  int pipe = pipeline_from_env();
+  if (pipe == 2 && (layout == 4 || L.trav == 1)) pipe = 0;
+  const bool mega = pipe == 1;
   const uint32_t iters = (uint32_t)p->bounces * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
   if (!mega && iters > (uint32_t)kMaxIters) return fail(PRT_ERR_UNSUPPORTED, "too many wavefront iterations");
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
@@ -345,7 +352,8 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     rc = ensure_wave(c, (uint32_t)n, p->bounces);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * kCtrWords, c->stream));
-    HIP_TRY(launch_wavefront(L, S, A, M, c->wb, c->frames.as<float4>(), stats ? &c->wt : nullptr));
+    if (pipe == 2) HIP_TRY(launch_wavefront2(L, S, A, M, c->wb, c->frames.as<float4>(), stats ? &c->wt : nullptr));
+    else HIP_TRY(launch_wavefront(L, S, A, M, c->wb, c->frames.as<float4>(), stats ? &c->wt : nullptr));
   }
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   HIP_TRY(launch_accumulate(L, M, F, p->flags, c->frames.as<float4>(), c->acc.as<float4>(), c->nsamp.as<int32_t>(),
@@ -375,15 +383,20 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
         stats->shadow_rays += qa;
         float a = 0, b = 0;
         HIP_TRY(hipEventElapsedTime(&a, c->wt.ev[4 * k + 0], c->wt.ev[4 * k + 1]));
-        HIP_TRY(hipEventElapsedTime(&b, c->wt.ev[4 * k + 2], c->wt.ev[4 * k + 3]));
+        if (pipe == 0) HIP_TRY(hipEventElapsedTime(&b, c->wt.ev[4 * k + 2], c->wt.ev[4 * k + 3]));
         stats->ms_closest += a;
         stats->ms_anyhit += b;
         if (dump)
           std::fprintf(stderr, "prt: iteration %u: %llu closest rays %.3f ms, %llu shadow rays %.3f ms\n", k,
                        (unsigned long long)qs, a, (unsigned long long)qa, b);
       }
-      stats->pipeline = 0;
-      stats->iterations = (int32_t)iters;
+      if (pipe == 2) {  // one merged trace launch per iteration plus the final shadow-only one
+        float a = 0;
+        HIP_TRY(hipEventElapsedTime(&a, c->wt.ev[4 * iters + 0], c->wt.ev[4 * iters + 1]));
+        stats->ms_closest += a;
+      }
+      stats->pipeline = pipe;
+      stats->iterations = (int32_t)(pipe == 2 ? iters + 1 : iters);
     }
     float ms = 0, ms_trace = 0;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[2]));

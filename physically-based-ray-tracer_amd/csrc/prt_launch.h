@@ -31,6 +31,7 @@ struct WaveBufs {
   uint32_t scap;    // capacity of one shadow sub-queue (4 x qcap)
   uint32_t* seed;
   uint32_t* info;   // depth | path << 8 | status << 16 | nee kind << 20
+  uint32_t* rinfo;  // merged pipeline: what k_resolve2 finishes (depth | path << 8 | status << 16 | kind << 20)
   float4* ro;
   float4* rd;
   float4* R;
@@ -56,6 +57,11 @@ struct WaveTimers {
 
 hipError_t launch_wavefront(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                             const WaveBufs& B, float4* out, WaveTimers* tm);
+hipError_t launch_wave_init(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
+                            const WaveBufs& B, float4* out);
+// merged pipeline (prt_wave2.hip): one traversal launch per iteration for P(i) closest + S(i-1) any-hit
+hipError_t launch_wavefront2(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
+                             const WaveBufs& B, float4* out, WaveTimers* tm);
 hipError_t launch_trace_frames(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                                float4* out, Counters* cnt);
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,

@@ -20,19 +20,22 @@ namespace prt {
 
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 
-// Persistent traversal of one wave (blockDim.x == 64).  Ray source and sink are callbacks:
+// Persistent traversal of one wave (blockDim.x == 64).  MODE 0: closest hit, 1: any hit, 2: each ray says
+// (mixed queues).  Ray source and sink are callbacks:
 //   fetch(uint32_t* base, uint32_t want) -> uint32_t got   (wave-uniform; called by all lanes)
-//   load(uint32_t g, V3& O, V3& D, float& tmax) -> handle  queue entry g -> world ray + a handle
-//   reload(uint32_t handle, V3& O, V3& D)                  world ray again (next instance of the TLAS loop)
-//   finish(uint32_t handle, const Hit& h, bool hit)        closest: h; any-hit: hit = occluded
+//   load(uint32_t g, V3& O, V3& D, float& tmax, bool& any) -> handle   queue entry g -> world ray, a handle
+//                                                                       and (MODE 2) its query kind
+//   reload(uint32_t handle, bool any, V3& O, V3& D)        world ray again (next instance of the TLAS loop)
+//   finish(uint32_t handle, const Hit& h, bool any, bool hit)  closest: h; any-hit: hit = occluded
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
-template <bool ANY, bool HALF, int STACK, int REFILL, class Fetch, class Load, class Reload, class Finish>
+template <int MODE, bool HALF, int STACK, int REFILL, class Fetch, class Load, class Reload, class Finish>
 __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                  Load load, Reload reload, Finish finish) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   bool active = false, drained = false;
+  bool any = MODE == 1;
   uint32_t handle = 0;
   V3 O = v3(0.0f, 0.0f, 0.0f), D = v3(0.0f, 0.0f, 1.0f), rD = D;  // instance-space ray
   uint32_t oct = 0;
@@ -73,11 +76,13 @@ __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __
         if (rank < got) {
           V3 Ow, Dw;
           float tmax;
-          handle = load(base + rank, Ow, Dw, tmax);
+          bool a = MODE == 1;
+          handle = load(base + rank, Ow, Dw, tmax, a);
+          if (MODE == 2) any = a;
           h.t = tmax; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;
           lhit = 0; tcnt = 0;
           if (enter(0, Ow, Dw)) active = true;
-          else finish(handle, h, false);
+          else finish(handle, h, any, false);
         }
       }
     }
@@ -90,11 +95,11 @@ __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __
       bool more = false;
       if (inst + 1 < S.ninst) {
         V3 Ow, Dw;
-        reload(handle, Ow, Dw);
+        reload(handle, any, Ow, Dw);
         more = enter(inst + 1, Ow, Dw);
       }
       if (!more) {
-        finish(handle, h, false);
+        finish(handle, h, any, false);
         active = false;
       }
     }
@@ -158,9 +163,9 @@ __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __
       const bool hit = mt_test(S.tris + tcur, O, D, t, u, v, prim);
       tcur++;
       tcnt--;
-      if (ANY) {
+      if (MODE == 1 || (MODE == 2 && any)) {
         if (hit && t < h.t) {  // tiny_bvh.h:6594 (h.t holds tmax)
-          finish(handle, h, true);
+          finish(handle, h, true, true);
           active = false;
           node = kNoNode; lhit = 0; tcnt = 0;
         }

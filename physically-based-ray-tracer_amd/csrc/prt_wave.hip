@@ -21,94 +21,9 @@
 #include "prt_launch.h"
 #include "prt_path.h"
 #include "prt_persist.h"
+#include "prt_queue.h"
 
 namespace prt {
-
-enum : uint32_t { kStEndValue = 0, kStNeeEnd = 1, kStNeeCont = 2, kStMiss = 3 };
-
-__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
-__device__ __forceinline__ uint32_t* qcounter(uint32_t* ctr, uint32_t iter, uint32_t which, uint32_t s) {
-  return ctr + ((iter * 2u + which) * kNSub + s) * kCtrStride;
-}
-
-// LDS prefix table of the kNSub sub-queue counts; returns the total.  Call with uniform control flow.
-__device__ __forceinline__ uint32_t load_prefix(const uint32_t* ctr, uint32_t iter, uint32_t which, uint32_t* pref) {
-  if (threadIdx.x < 64) {
-    const uint32_t l = threadIdx.x;
-    uint32_t v = l < kNSub ? ctr[((iter * 2u + which) * kNSub + l) * kCtrStride] : 0u;
-    for (int off = 1; off < 32; off <<= 1) {  // inclusive scan over the first 32 lanes
-      const uint32_t o = __shfl_up(v, off, 64);
-      if (l >= (uint32_t)off) v += o;
-    }
-    if (l < kNSub) pref[l + 1] = v;
-    if (l == 0) pref[0] = 0;
-  }
-  __syncthreads();
-  return pref[kNSub];
-}
-// global index g in [0, total) -> slot in the sub-queue layout (sub-queue s occupies [s*cap, s*cap+cnt_s))
-__device__ __forceinline__ uint32_t map_slot(const uint32_t* pref, uint32_t g, uint32_t cap) {
-  uint32_t lo = 0, hi = kNSub;
-#pragma unroll
-  for (int it = 0; it < 5; it++) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (pref[mid] <= g) lo = mid; else hi = mid;
-  }
-  return lo * cap + (g - pref[lo]);
-}
-
-// Dynamic work fetch for the traversal kernels without a hot counter: the live range [0, total) is cut
-// into kParts contiguous parts, each with its own fetch counter; a wave starts on the part of its XCD
-// (HW_REG_XCC_ID) and steals from the others once that part is drained.  Returns false when all parts
-// are drained.  Wave-uniform.
-constexpr uint32_t kParts = 8;
-__device__ __forceinline__ uint32_t xcc_id() {
-  uint32_t v;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-  return v & 7u;
-}
-__device__ __forceinline__ bool fetch_chunk(uint32_t* fctr, uint32_t total, uint32_t& part, uint32_t& base) {
-  for (uint32_t tries = 0; tries < kParts; tries++) {
-    const uint32_t lo = (uint32_t)(((uint64_t)total * part) / kParts);
-    const uint32_t hi = (uint32_t)(((uint64_t)total * (part + 1)) / kParts);
-    uint32_t off = 0;
-    if (lane_id() == 0) off = (hi > lo) ? atomicAdd(fctr + part * kCtrStride, 64u) : 0xFFFFFFFFu;
-    off = __shfl(off, 0, 64);
-    if (off != 0xFFFFFFFFu && off < hi - lo) {
-      base = lo + off;
-      return true;
-    }
-    part = (part + 1) & (kParts - 1);
-  }
-  return false;
-}
-__device__ __forceinline__ uint32_t* fetch_counters(uint32_t* ctr, uint32_t iter, uint32_t which) {
-  return ctr + ((size_t)(kMaxIters + 2) * 2 * kNSub + (iter * 2u + which) * kParts) * kCtrStride;
-}
-
-// block-aggregated append of n (0..4) entries per lane into one sub-queue; returns this lane's first
-// index inside that sub-queue.  All threads of the block must call it.  sm: >= 8 words of LDS.
-__device__ __forceinline__ uint32_t block_append(uint32_t* counter, uint32_t n, uint32_t* sm) {
-  const uint64_t b1 = __ballot(n & 1u), b2 = __ballot((n >> 1) & 1u), b4 = __ballot((n >> 2) & 1u);
-  const uint64_t lt = (1ull << lane_id()) - 1ull;
-  const uint32_t before = (uint32_t)__popcll(b1 & lt) + 2u * (uint32_t)__popcll(b2 & lt) + 4u * (uint32_t)__popcll(b4 & lt);
-  const uint32_t wtot = (uint32_t)__popcll(b1) + 2u * (uint32_t)__popcll(b2) + 4u * (uint32_t)__popcll(b4);
-  const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if (lane_id() == 0) sm[w] = wtot;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t tot = 0;
-    for (uint32_t k = 0; k < nw; k++) tot += sm[k];
-    sm[4] = tot ? atomicAdd(counter, tot) : 0u;
-  }
-  __syncthreads();
-  uint32_t off = sm[4];
-  for (uint32_t k = 0; k < w; k++) off += sm[k];
-  __syncthreads();
-  return off + before;
-}
-
-__device__ __forceinline__ uint32_t pack_hit(uint32_t prim, uint32_t inst) { return prim | (inst << 26); }
 
 // ---- init: items -> primary rays, appended to queue 0 (sub-queue = block % kNSub)
 __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, TileMap M, WaveBufs B,
@@ -314,31 +229,6 @@ __global__ void __launch_bounds__(64) k_shadow(SceneDev S, WaveBufs B, uint32_t 
 }
 
 // ---- persistent-lane variants (Node8): lanes refill from the queue as their rays finish (prt_persist.h)
-// wave-uniform fetch of up to `want` consecutive live-range entries from the XCD-partitioned counters
-__device__ __forceinline__ uint32_t fetch_some(uint32_t* fctr, uint32_t total, uint32_t& part, uint32_t* base,
-                                               uint32_t want) {
-  for (uint32_t tries = 0; tries < kParts; tries++) {
-    const uint32_t lo = (uint32_t)(((uint64_t)total * part) / kParts);
-    const uint32_t hi = (uint32_t)(((uint64_t)total * (part + 1)) / kParts);
-    uint32_t off = 0xFFFFFFFFu;
-    if (lane_id() == 0 && hi > lo) {
-      // the wave's current part: straight to the atomic.  Other parts (stealing, end of launch): a plain
-      // relaxed read first, so a drained part costs no atomic and the end of a launch does not queue
-      // every wave's failing atomics on eight addresses
-      uint32_t* ctr = fctr + part * kCtrStride;
-      if (tries == 0 || __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hi - lo)
-        off = atomicAdd(ctr, want);
-    }
-    off = __shfl(off, 0, 64);
-    if (off != 0xFFFFFFFFu && off < hi - lo) {
-      *base = lo + off;
-      return min(want, hi - lo - off);
-    }
-    part = (part + 1) & (kParts - 1);
-  }
-  return 0;
-}
-
 template <bool HALF, int REFILL, int STACK, int WAVES>
 __global__ void __launch_bounds__(64, WAVES) k_extend_p(SceneDev S, WaveBufs B, uint32_t iter) {
   __shared__ uint32_t lds_stack[2 * STACK * 64];
@@ -348,10 +238,10 @@ __global__ void __launch_bounds__(64, WAVES) k_extend_p(SceneDev S, WaveBufs B, 
   if (blockIdx.x * 64u >= total) return;  // small queues: only as many waves as 64-ray chunks
   uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
   uint32_t part = xcc_id();
-  trav8_persistent<false, HALF, STACK, REFILL>(
+  trav8_persistent<0, HALF, STACK, REFILL>(
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) { return fetch_some(fctr, total, part, base, want); },
-      [&](uint32_t g, V3& O, V3& D, float& tmax) -> uint32_t {
+      [&](uint32_t g, V3& O, V3& D, float& tmax, bool&) -> uint32_t {
         const uint32_t item = q[map_slot(pref, g, B.qcap)];
         const float4 o = B.ro[item], d = B.rd[item];
         O = v3(o.x, o.y, o.z);
@@ -359,12 +249,12 @@ __global__ void __launch_bounds__(64, WAVES) k_extend_p(SceneDev S, WaveBufs B, 
         tmax = kFar;
         return item;
       },
-      [&](uint32_t item, V3& O, V3& D) {
+      [&](uint32_t item, bool, V3& O, V3& D) {
         const float4 o = B.ro[item], d = B.rd[item];
         O = v3(o.x, o.y, o.z);
         D = v3(d.x, d.y, d.z);
       },
-      [&](uint32_t item, const Hit& h, bool) {
+      [&](uint32_t item, const Hit& h, bool, bool) {
         B.hit[item] = make_float4(h.t, h.u, h.v, __uint_as_float(pack_hit(h.prim, h.inst)));
       });
 }
@@ -378,10 +268,10 @@ __global__ void __launch_bounds__(64, WAVES) k_shadow_p(SceneDev S, WaveBufs B, 
   if (blockIdx.x * 64u >= total) return;
   uint32_t* fctr = fetch_counters(B.ctr, iter, 1);
   uint32_t part = xcc_id();
-  trav8_persistent<true, HALF, STACK, REFILL>(
+  trav8_persistent<1, HALF, STACK, REFILL>(
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) { return fetch_some(fctr, total, part, base, want); },
-      [&](uint32_t g, V3& O, V3& D, float& tmax) -> uint32_t {
+      [&](uint32_t g, V3& O, V3& D, float& tmax, bool&) -> uint32_t {
         const uint32_t slot = map_slot(pref, g, B.scap);
         const float4 o = B.sho[slot], d = B.shd[slot];
         O = v3(o.x, o.y, o.z);
@@ -389,12 +279,12 @@ __global__ void __launch_bounds__(64, WAVES) k_shadow_p(SceneDev S, WaveBufs B, 
         tmax = o.w;
         return slot;
       },
-      [&](uint32_t slot, V3& O, V3& D) {
+      [&](uint32_t slot, bool, V3& O, V3& D) {
         const float4 o = B.sho[slot], d = B.shd[slot];
         O = v3(o.x, o.y, o.z);
         D = v3(d.x, d.y, d.z);
       },
-      [&](uint32_t slot, const Hit&, bool occluded) {
+      [&](uint32_t slot, const Hit&, bool, bool occluded) {
         const uint32_t tag = __float_as_uint(B.shd[slot].w);
         if (!occluded) vis8[tag] = 1;
       });
@@ -499,6 +389,12 @@ void launch_persistent(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B,
   } else {
     if (c.trav == 32) launch_p1<ANY, 32, 16, 5>(c, S, B, it); else launch_p1<ANY, 16, 16, 5>(c, S, B, it);
   }
+}
+
+hipError_t launch_wave_init(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
+                            const WaveBufs& B, float4* out) {
+  hipLaunchKernelGGL(k_wave_init, dim3(256u * 4u), dim3(kBlock), 0, c.stream, S, A, M, B, out);
+  return hipGetLastError();
 }
 
 // ---- host launcher: the whole frame batch, no host synchronisation inside

@@ -1,0 +1,311 @@
+// prt_wave2.hip -- merged-trace wavefront pipeline (default) for gfx950.
+//
+// Same estimator, RNG stream and per-item state as prt_wave.hip; the difference is where the path's
+// next ray is decided.  Every random number of a path is drawn in the shading stage, so the shading
+// of iteration i already knows the ray of iteration i+1 (the sampled bounce, or the AA path-2 primary
+// ray when path 1 ends) and queues it at once.  The closest-hit rays of iteration i+1 and the shadow
+// rays of iteration i are then traced by ONE persistent launch, and the NEE resolve of iteration i
+// (which needs those shadow results) runs after it:
+//
+//   k_wave_init                                   P(0) = primary rays r1
+//   for i = 0 .. iters:
+//     k_trace2(i)    closest hits of P(i)  +  any hits of S(i-1)         (one launch, mixed lanes)
+//     k_resolve2(i-1) NEE result of iteration i-1, (result, throughput) stack, path end, frame write
+//     k_miss2(i)     sky radiance of this iteration's misses (before shading rewrites the ray)
+//     k_shade2(i)    hit attributes, NEE set-up -> S(i), BRDF sample or path-2 start -> P(i+1)
+//
+// Hazards (all kernels on one stream): P(i+1) reuses P(i-1)'s buffer after k_resolve2(i-1) read it;
+// S(i) reuses S(i-1)'s buffer after k_trace2(i) read it; k_resolve2(i-1) reads ne/nb/nf/vis/R/T of its
+// items before k_miss2(i) / k_shade2(i) overwrite them; rinfo keeps iteration i-1's status while info
+// already holds the state of the queued next ray.
+#include "prt_launch.h"
+#include "prt_path.h"
+#include "prt_persist.h"
+#include "prt_queue.h"
+
+namespace prt {
+
+// ---- one traversal launch: closest hits of P(iter) (iter < iters) + any hits of S(iter - 1) (iter > 0)
+template <bool HALF, int REFILL, int STACK, int WAVES>
+__global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, uint32_t iter, uint32_t iters) {
+  __shared__ uint32_t lds_stack[2 * STACK * 64];
+  __shared__ uint32_t prefP[kNSub + 1], prefS[kNSub + 1];
+  uint8_t* vis8 = reinterpret_cast<uint8_t*>(B.vis);
+  const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
+  const uint32_t nP = iter < iters ? load_prefix(B.ctr, iter, 0, prefP) : 0u;
+  const uint32_t nS = iter > 0 ? load_prefix(B.ctr, iter - 1, 1, prefS) : 0u;
+  const uint32_t total = nP + nS;
+  if (blockIdx.x * 64u >= total) return;
+  uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
+  uint32_t part = xcc_id();
+  trav8_persistent<2, HALF, STACK, REFILL>(
+      S, lds_stack + threadIdx.x,
+      [&](uint32_t* base, uint32_t want) { return fetch_some(fctr, total, part, base, want); },
+      [&](uint32_t g, V3& O, V3& D, float& tmax, bool& any) -> uint32_t {
+        float4 o, d;
+        uint32_t h;
+        if (g < nP) {
+          h = q[map_slot(prefP, g, B.qcap)];
+          o = B.ro[h];
+          d = B.rd[h];
+          tmax = kFar;
+          any = false;
+        } else {
+          h = map_slot(prefS, g - nP, B.scap);
+          o = B.sho[h];
+          d = B.shd[h];
+          tmax = o.w;
+          any = true;
+        }
+        O = v3(o.x, o.y, o.z);
+        D = v3(d.x, d.y, d.z);
+        return h;
+      },
+      [&](uint32_t h, bool any, V3& O, V3& D) {
+        const float4 o = any ? B.sho[h] : B.ro[h], d = any ? B.shd[h] : B.rd[h];
+        O = v3(o.x, o.y, o.z);
+        D = v3(d.x, d.y, d.z);
+      },
+      [&](uint32_t h, const Hit& hit, bool any, bool occluded) {
+        if (any) {
+          if (!occluded) vis8[__float_as_uint(B.shd[h].w)] = 1;
+        } else {
+          B.hit[h] = make_float4(hit.t, hit.u, hit.v, __uint_as_float(hit.prim | (hit.inst << 26)));
+        }
+      });
+}
+
+// ---- misses of P(iter) (:159): sky radiance (or 0) into ne, before k_shade2 replaces the ray
+__global__ void __launch_bounds__(kBlock) k_miss2(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter) {
+  __shared__ uint32_t pref[kNSub + 1];
+  const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
+  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
+  for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    const uint32_t g = c * kBlock + threadIdx.x;
+    if (g >= total) continue;
+    const uint32_t item = q[map_slot(pref, g, B.qcap)];
+    if (B.hit[item].x < kFar) continue;
+    V3 L = v3(0.0f, 0.0f, 0.0f);
+    if (A.flags & kSkybox) {
+      const float4 d = B.rd[item];
+      L = sample_sky(S, v3(d.x, d.y, d.z));
+    }
+    B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
+  }
+}
+
+// the path of `item` ends at this iteration: with AA and path 1, queue path 2's primary ray (its jitter was
+// drawn at init, :61) -- returns true when a ray was set up for P(iter + 1)
+__device__ __forceinline__ bool start_path2(const SceneDev& S, const TraceArgs& A, const TileMap& M,
+                                            const WaveBufs& B, uint32_t item, uint32_t path) {
+  if (path != 0 || !(A.flags & kAA)) return false;
+  const uint32_t r = item % M.items;
+  int32_t x, y;
+  item_pixel(M, r, x, y);
+  const float2 j = B.jit[item];
+  const Ray r2 = primary_ray(S, (float)x + j.x, (float)y + j.y, A.W, A.H);
+  B.ro[item] = make_float4(r2.O.x, r2.O.y, r2.O.z, 0.0f);
+  B.rd[item] = make_float4(r2.D.x, r2.D.y, r2.D.z, 0.0f);
+  B.info[item] = 1u << 8;
+  return true;
+}
+
+// ---- shading of P(iter): NEE set-up -> S(iter), BRDF sample or path-2 start -> P(iter + 1)
+__global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, TileMap M, WaveBufs B, uint32_t iter) {
+  __shared__ uint32_t pref[kNSub + 1];
+  __shared__ uint32_t sm[8];
+  const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
+  uint32_t* qn = (iter & 1) ? B.q0 : B.q1;
+  const uint32_t sub = blockIdx.x % kNSub;
+  uint32_t* shcnt = qcounter(B.ctr, iter, 1, sub);
+  uint32_t* ncnt = qcounter(B.ctr, iter + 1, 0, sub);
+  float4* sho = B.sho + (size_t)sub * B.scap;
+  float4* shd = B.shd + (size_t)sub * B.scap;
+  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
+  const uint32_t fl = A.flags;
+  for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    const uint32_t g = c * kBlock + threadIdx.x;
+    uint32_t item = 0, info = 0, seed = 0, nr = 0;
+    int kind = 0;
+    float4 hh = make_float4(kFar, 0.0f, 0.0f, 0.0f);
+    const bool active = g < total;
+    if (active) {
+      item = q[map_slot(pref, g, B.qcap)];
+      info = B.info[item];
+      hh = B.hit[item];
+      if ((info & 0x1FFu) == 0) B.s1[item].w = hh.x;                                        // r1.hit.t
+      if (hh.x < kFar) {
+        seed = B.seed[item];
+        kind = nee_kind(fl, seed);                                                           // :198-214
+        nr = (uint32_t)nee_rays(kind);
+      }
+    }
+    const uint32_t s0 = block_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic
+    const uint32_t depth = info & 0xFFu, path = (info >> 8) & 1u;
+    uint32_t status = kStMiss;
+    bool next = false;
+    if (nr) {
+      const float4 o = B.ro[item], d = B.rd[item];
+      const V3 D = v3(d.x, d.y, d.z);
+      const uint32_t pk = __float_as_uint(hh.w);
+      const V3 I = v3(o.x, o.y, o.z) + hh.x * D;                                             // tiny_bvh.h:586
+      const V3 V = -D;
+      const HitAttr ha = hit_attributes(S, pk >> 26, pk & 0x03FFFFFFu, hh.y, hh.z, (fl & kNormalMap) != 0);
+      const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
+      B.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
+      const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed, [&](int k, const Ray& sr, float tmax, V3 fk) {
+        sho[s0 + k] = make_float4(sr.O.x, sr.O.y, sr.O.z, tmax);
+        shd[s0 + k] = make_float4(sr.D.x, sr.D.y, sr.D.z, __uint_as_float(4u * item + (uint32_t)k));
+        B.nf[4 * (size_t)item + k] = make_float4(fk.x, fk.y, fk.z, 0.0f);
+      });
+      B.nb[item] = make_float4(brdf.x, brdf.y, brdf.z, 0.0f);
+      B.vis[item] = 0u;
+      status = kStNeeEnd;
+      if ((int)depth != A.bounces - 1) {                                                     // :329
+        V3 dir, thr;
+        if (sample_bounce(ha.m, V, ha.N, seed, dir, thr)) {                                  // :376-399
+          status = kStNeeCont;
+          B.T[(size_t)depth * B.n + item] = make_float4(thr.x, thr.y, thr.z, 0.0f);
+          const Ray nr2 = make_ray(I + dir * kEpsilon, dir);                                 // :404
+          B.ro[item] = make_float4(nr2.O.x, nr2.O.y, nr2.O.z, 0.0f);
+          B.rd[item] = make_float4(nr2.D.x, nr2.D.y, nr2.D.z, 0.0f);
+          B.info[item] = (depth + 1u) | (path << 8);
+          next = true;
+        }
+      }
+      B.seed[item] = seed;
+    }
+    if (active) {
+      B.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20);
+      if (status != kStNeeCont) next = start_path2(S, A, M, B, item, path);
+    }
+    const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
+    if (next) qn[sub * B.qcap + slot] = item;
+  }
+}
+
+// ---- debug render modes (:170-194): the hit's debug colour (or the sky) ends the path
+__global__ void __launch_bounds__(kBlock) k_shade2_debug(SceneDev S, TraceArgs A, TileMap M, WaveBufs B,
+                                                         uint32_t iter) {
+  __shared__ uint32_t pref[kNSub + 1];
+  __shared__ uint32_t sm[8];
+  const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
+  uint32_t* qn = (iter & 1) ? B.q0 : B.q1;
+  const uint32_t sub = blockIdx.x % kNSub;
+  uint32_t* ncnt = qcounter(B.ctr, iter + 1, 0, sub);
+  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
+  for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    const uint32_t g = c * kBlock + threadIdx.x;
+    bool next = false;
+    uint32_t item = 0;
+    if (g < total) {
+      item = q[map_slot(pref, g, B.qcap)];
+      const uint32_t info = B.info[item];
+      const float4 hh = B.hit[item];
+      if ((info & 0x1FFu) == 0) B.s1[item].w = hh.x;
+      if (hh.x < kFar) {  // misses keep k_miss2's sky value
+        const uint32_t pk = __float_as_uint(hh.w);
+        const HitAttr ha = hit_attributes(S, pk >> 26, pk & 0x03FFFFFFu, hh.y, hh.z, (A.flags & kNormalMap) != 0);
+        const V3 L = debug_view(S, A.mode, ha, pk >> 26, pk & 0x03FFFFFFu);
+        B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
+      }
+      B.rinfo[item] = info & 0x1FFu;  // kStEndValue
+      next = start_path2(S, A, M, B, item, (info >> 8) & 1u);
+    }
+    const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
+    if (next) qn[sub * B.qcap + slot] = item;
+  }
+}
+
+// ---- NEE resolve of P(iter) (after k_trace2(iter + 1) traced S(iter)), stack, path end, frame write
+__global__ void __launch_bounds__(kBlock) k_resolve2(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter,
+                                                     float4* __restrict__ out) {
+  __shared__ uint32_t pref[kNSub + 1];
+  const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
+  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
+  const uint32_t fl = A.flags;
+  for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    const uint32_t g = c * kBlock + threadIdx.x;
+    if (g >= total) continue;
+    const uint32_t item = q[map_slot(pref, g, B.qcap)];
+    const uint32_t ri = B.rinfo[item];
+    const uint32_t depth = ri & 0xFFu, path = (ri >> 8) & 1u, status = (ri >> 16) & 3u, kind = (ri >> 20) & 3u;
+    const float4 ne = B.ne[item];
+    V3 L = v3(ne.x, ne.y, ne.z);
+    if (status == kStNeeEnd || status == kStNeeCont) {
+      const float4 nb = B.nb[item];
+      const uint32_t vw = B.vis[item];
+      const uint32_t vis = ((vw & 0xFFu) ? 1u : 0u) | ((vw & 0xFF00u) ? 2u : 0u) | ((vw & 0xFF0000u) ? 4u : 0u) |
+                           ((vw & 0xFF000000u) ? 8u : 0u);
+      V3 f[4];
+      const uint32_t nr = kind == 0 ? 4u : 1u;
+      for (uint32_t k = 0; k < 4; k++) {
+        if (k < nr) {
+          const float4 fk = B.nf[4 * (size_t)item + k];
+          f[k] = v3(fk.x, fk.y, fk.z);
+        } else {
+          f[k] = v3(0.0f, 0.0f, 0.0f);
+        }
+      }
+      const V3 result = nee_resolve((int)kind, vis, L, v3(nb.x, nb.y, nb.z), f, fl);
+      if (status == kStNeeCont) {  // the path goes on: result joins the stack
+        B.R[(size_t)depth * B.n + item] = make_float4(result.x, result.y, result.z, 0.0f);
+        continue;
+      }
+      L = result;
+    }
+    for (int k = (int)depth - 1; k >= 0; k--) {                                              // result + Trace(..) * throughput
+      const float4 Rk = B.R[(size_t)k * B.n + item], Tk = B.T[(size_t)k * B.n + item];
+      L = v3(Rk.x, Rk.y, Rk.z) + L * v3(Tk.x, Tk.y, Tk.z);
+    }
+    const float4 s1 = B.s1[item];
+    if (path == 0 && (fl & kAA)) {  // path 2 was queued by k_shade2; keep path 1's radiance
+      B.s1[item] = make_float4(L.x, L.y, L.z, s1.w);
+    } else {
+      V3 res = (fl & kAA) ? 0.5f * (v3(s1.x, s1.y, s1.z) + L) : L;                           // :65
+      if (fl & kGamma) res = v3(sqrtf(res.x), sqrtf(res.y), sqrtf(res.z));                  // :73-79
+      out[item] = make_float4(res.x, res.y, res.z, s1.w);
+    }
+  }
+}
+
+template <int REFILL, int STACK, int WAVES>
+void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
+  const dim3 grid(256u * 4u * WAVES);
+  if (c.layout == 9)
+    hipLaunchKernelGGL((k_trace2<true, REFILL, STACK, WAVES>), grid, dim3(64), 0, c.stream, S, B, it, iters);
+  else
+    hipLaunchKernelGGL((k_trace2<false, REFILL, STACK, WAVES>), grid, dim3(64), 0, c.stream, S, B, it, iters);
+}
+static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
+  if (c.occ == 8) {
+    if (c.trav == 16) launch_t2<16, 8, 8>(c, S, B, it, iters); else launch_t2<32, 8, 8>(c, S, B, it, iters);
+  } else if (c.occ == 6) {
+    if (c.trav == 16) launch_t2<16, 12, 6>(c, S, B, it, iters); else launch_t2<32, 12, 6>(c, S, B, it, iters);
+  } else {
+    if (c.trav == 16) launch_t2<16, 16, 5>(c, S, B, it, iters); else launch_t2<32, 16, 5>(c, S, B, it, iters);
+  }
+}
+
+hipError_t launch_wavefront2(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
+                             const WaveBufs& B, float4* out, WaveTimers* tm) {
+  if (B.n == 0) return hipSuccess;
+  const unsigned gprod = 256u * 4u;  // producer blocks (multiple of kNSub)
+  hipError_t e = launch_wave_init(c, S, A, M, B, out);
+  if (e != hipSuccess) return e;
+  const uint32_t iters = (uint32_t)A.bounces * ((A.flags & kAA) ? 2u : 1u);
+  for (uint32_t it = 0; it <= iters; it++) {
+    if (tm) (void)hipEventRecord(tm->ev[4 * it + 0], c.stream);
+    launch_trace2(c, S, B, it, iters);
+    if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
+    if (it > 0) hipLaunchKernelGGL(k_resolve2, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it - 1, out);
+    if (it == iters) break;
+    hipLaunchKernelGGL(k_miss2, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
+    if (A.mode != 0) hipLaunchKernelGGL(k_shade2_debug, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
+    else hipLaunchKernelGGL(k_shade2, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
+  }
+  if (tm) tm->iters = iters + 1;
+  return hipGetLastError();
+}
+
+}  // namespace prt

@@ -95,19 +95,25 @@ def test_render_c3_reduced(gpu_ctx):
     _compare_render(gpu_ctx, scenes.config_c3(), 320, 180, 4, 4)
 
 
-def test_wavefront_equals_megakernel(gpu_ctx, monkeypatch):
-    """The two pipelines (wavefront default, PRT_PIPELINE=mega) render bit-identical frames."""
+@pytest.mark.parametrize("flags", [oracle.DEFAULT_FLAGS, oracle.DEFAULT_FLAGS & ~oracle.AA])
+def test_pipelines_identical(gpu_ctx, monkeypatch, flags):
+    """The three pipelines -- merged-trace wavefront (default), wavefront with separate extend / shadow
+    launches (PRT_PIPELINE=wave1) and the megakernel (PRT_PIPELINE=mega) -- render bit-identical frames."""
     sd = scenes.multi_instance(scenes.config_small(60, 50))
     W, H = 128, 96
     gpu_scene(gpu_ctx, sd, W, H)
-    a_w, r_w, s_w = gpu_ctx.render(W, H, 4, 4)
-    assert s_w.pipeline == 0 and s_w.iterations == 8
-    gpu_ctx.reset_accumulation(full=True)
-    monkeypatch.setenv("PRT_PIPELINE", "mega")
-    a_m, r_m, s_m = gpu_ctx.render(W, H, 4, 4)
-    assert s_m.pipeline == 1
-    assert np.array_equal(a_w, a_m) and np.array_equal(r_w, r_m)
-    assert s_w.segments == s_m.segments and s_w.shadow_rays == s_m.shadow_rays
+    out = {}
+    for pipe, code, iters in (("", 2, 9 if flags & oracle.AA else 5), ("wave1", 0, 8 if flags & oracle.AA else 4),
+                              ("mega", 1, 0)):
+        if pipe:
+            monkeypatch.setenv("PRT_PIPELINE", pipe)
+        gpu_ctx.reset_accumulation(full=True)
+        a, r, st = gpu_ctx.render(W, H, 4, 4, flags)
+        assert st.pipeline == code and st.iterations == iters
+        out[code] = (a, r, st)
+    for code in (0, 1):
+        assert np.array_equal(out[2][0], out[code][0]) and np.array_equal(out[2][1], out[code][1])
+        assert out[2][2].segments == out[code][2].segments and out[2][2].shadow_rays == out[code][2].shadow_rays
 
 
 def test_bvh_layouts_render_identical(gpu_ctx, monkeypatch):
