@@ -1,0 +1,206 @@
+// prt_renderer.hpp -- C++ host mirror of the reference's Renderer / Scene / Camera API surface
+// (Core/Renderer.h:12-112, Core/Scene.h:12-80, Core/Camera.h:11-37, Core/Model.h:36-44) on top of the C ABI
+// in prt.h.  Header-only C++17; link libprt.so.  The names and meanings of the public members follow the
+// reference so a Renderer::Tick port reads like the original; the hot path (Tick's pixel loop +
+// Renderer::Trace, Core/Renderer.cpp:43-141,150-406) runs on the GPU through prt_render().
+//
+// Differences from the reference, all outside the hot path: the Scene is filled by the caller (the
+// reference's assimp / JSON loading, Core/Scene.cpp:10-28,279-340, stays where it is), physics and UI
+// are not part of this header, and errors surface as prt::Error exceptions instead of crashes.
+#pragma once
+#include <array>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "prt.h"
+
+namespace prt {
+
+class Error : public std::runtime_error {
+ public:
+  Error(int code, const std::string& what) : std::runtime_error(what), code(code) {}
+  int code;
+};
+
+inline void check(int rc) {
+  if (rc != PRT_OK) throw Error(rc, std::string("prt error ") + std::to_string(rc) + ": " + prt_last_error());
+}
+
+// Model (Core/Model.h:36-44): the fat per-corner arrays the hot path reads, owned here.
+struct Model {
+  std::vector<float> triangles;           // float4 x 3T (Model::triangles)
+  std::vector<float> fixedNormals;        // float4 x 3T
+  std::vector<float> fixedTextureCoords;  // float2 x 3T
+  std::vector<int32_t> indices;           // 3T
+  std::vector<float> vertices;            // float3 x V
+  std::vector<float> faceNormals;         // float3 x T
+  int32_t albedoTexture = -1, normalTexture = -1, metalnessTexture = -1, emissionTexture = -1;  // Scene::textures ids
+  int32_t TriCount() const { return (int32_t)(indices.size() / 3); }
+};
+
+// Surface (template/surface.h:49-94): packed 0x00RRGGBB pixels
+struct Texture {
+  int32_t width = 0, height = 0;
+  std::vector<uint32_t> pixels;
+};
+
+// GameObject + BLASInstance (Core/GameObject.h, Core/tiny_bvh.h:1243-1256): row-major 4x4 and model index
+struct GameObject {
+  std::array<float, 16> transform{1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  uint32_t modelIndex = 0;
+};
+
+class Scene {
+ public:
+  std::vector<Model> models;
+  std::vector<Texture> textures;
+  std::vector<GameObject> gameobjects;
+  prt_lights lights{};              // Renderer point-light SoA + directionalLights[0] + spotlights[0]
+  std::vector<float> skyPixels;     // Camera::skyPixels, float RGB equirect (empty = no sky)
+  int32_t skyWidth = 0, skyHeight = 0;
+
+  // everything the hot path reads, copied to HBM (Scene::Init + BuildTLAS, Core/Scene.cpp:10-28,220-223)
+  void Upload(prt_ctx* ctx) const {
+    std::vector<prt_texture> tex;
+    for (const Texture& t : textures) tex.push_back({t.width, t.height, t.pixels.data()});
+    check(prt_set_textures(ctx, tex.data(), (int32_t)tex.size()));
+    std::vector<prt_mesh> ms;
+    for (const Model& m : models) {
+      prt_mesh d{};
+      d.tri_count = m.TriCount();
+      d.vertex_count = (int32_t)(m.vertices.size() / 3);
+      d.triangles = m.triangles.data();
+      d.fixed_normals = m.fixedNormals.data();
+      d.fixed_uvs = m.fixedTextureCoords.data();
+      d.indices = m.indices.data();
+      d.vertices = m.vertices.data();
+      d.face_normals = m.faceNormals.data();
+      d.albedo_tex = m.albedoTexture;
+      d.normal_tex = m.normalTexture;
+      d.metalness_tex = m.metalnessTexture;
+      d.emission_tex = m.emissionTexture;
+      ms.push_back(d);
+    }
+    check(prt_set_meshes(ctx, ms.data(), (int32_t)ms.size()));
+    UploadInstances(ctx);
+    check(prt_set_lights(ctx, &lights));
+    check(prt_set_sky(ctx, skyPixels.empty() ? nullptr : skyPixels.data(), skyWidth, skyHeight));
+  }
+  // GameObject::Synchronise moved an instance: new transforms, TLAS rebuilt (Core/Renderer.cpp:33-41)
+  void UploadInstances(prt_ctx* ctx) const {
+    std::vector<float> xf;
+    std::vector<uint32_t> mi;
+    for (const GameObject& g : gameobjects) {
+      xf.insert(xf.end(), g.transform.begin(), g.transform.end());
+      mi.push_back(g.modelIndex);
+    }
+    check(prt_set_instances(ctx, xf.data(), mi.data(), (int32_t)mi.size()));
+  }
+};
+
+// Camera (Core/Camera.h:15-17): position, target and the screen plane GetPrimaryRay interpolates
+class Camera {
+ public:
+  float camPos[3] = {0, 0, -1}, camTarget[3] = {0, 0, 0};
+  float aspect = 1.0f;
+  float topLeft[3] = {}, topRight[3] = {}, bottomLeft[3] = {};
+
+  Camera() = default;
+  Camera(const float pos[3], const float target[3], float aspect_) : aspect(aspect_) {
+    for (int k = 0; k < 3; k++) { camPos[k] = pos[k]; camTarget[k] = target[k]; }
+    Update();
+  }
+  // the basis of Camera::Camera / HandleInput (Core/Camera.cpp:29-36)
+  void Update() {
+    prt_camera c{};
+    check(prt_camera_look_at(camPos, camTarget, aspect, &c));
+    for (int k = 0; k < 3; k++) { topLeft[k] = c.top_left[k]; topRight[k] = c.top_right[k]; bottomLeft[k] = c.bottom_left[k]; }
+  }
+  prt_camera Plane() const {
+    prt_camera c{};
+    for (int k = 0; k < 3; k++) {
+      c.pos[k] = camPos[k]; c.top_left[k] = topLeft[k]; c.top_right[k] = topRight[k]; c.bottom_left[k] = bottomLeft[k];
+    }
+    return c;
+  }
+};
+
+// Renderer (Core/Renderer.h:12-112): the public switches of the reference and Tick()
+class Renderer {
+ public:
+  enum class RENDER_STATES { BRDF, BASECOLOR, GEOMETRYNORMAL, SHADINGNORMAL, METAL, ROUGHNESS, EMMISIVE };
+
+  bool accumulates = true;
+  int bounces = 2;
+  RENDER_STATES renderingMode = RENDER_STATES::BRDF;
+  bool LIGHTED = true, GAMMACORRECTED = true, NORMALMAPPED = true, SKYBOX = true, AA = true, isStochastic = true;
+
+  Scene scene;
+  Camera camera;
+  std::vector<float> accumulator;  // float4 x W*H: accumulator / samplesPerPixel (the displayed average)
+  std::vector<uint32_t> screen;    // 0x00RRGGBB x W*H (RGBF32_to_RGB8 of the average)
+
+  Renderer(int32_t width, int32_t height, int32_t device = 0) : width_(width), height_(height) {
+    prt_device_desc d{device, 0};
+    check(prt_create(&d, &ctx_));
+    accumulator.assign(4 * (size_t)width * height, 0.0f);
+    screen.assign((size_t)width * height, 0u);
+  }
+  ~Renderer() { prt_destroy(ctx_); }
+  Renderer(const Renderer&) = delete;
+  Renderer& operator=(const Renderer&) = delete;
+
+  // Renderer::Init (Core/Renderer.cpp:7-16): scene + camera to the device, fresh accumulation state
+  void Init() {
+    scene.Upload(ctx_);
+    const prt_camera c = camera.Plane();
+    check(prt_set_camera(ctx_, &c));
+    check(prt_reset_accumulation(ctx_, 1));
+    frame_ = 0;
+  }
+
+  // Renderer::Tick (Core/Renderer.cpp:22-148): `frames` reference frames (2 camera paths per pixel each
+  // with AA) folded into the progressive accumulator; accumulator / screen hold the result afterwards
+  void Tick(float deltaTime = 0.0f, int32_t frames = 1) {
+    (void)deltaTime;
+    prt_render_params p{};
+    p.width = width_;
+    p.height = height_;
+    p.spp = frames * (AA ? 2 : 1);
+    p.bounces = bounces;
+    p.flags = Flags();
+    p.render_mode = (int32_t)renderingMode;
+    p.frame_index = frame_;
+    p.seed = 0;
+    check(prt_render(ctx_, &p, accumulator.data(), screen.data(), 0u, &stats_));
+    frame_ += (uint32_t)frames;
+  }
+
+  // Camera::HandleInput returned true: new screen plane, accumulator memset (Core/Renderer.cpp:147)
+  void CameraMoved() {
+    const prt_camera c = camera.Plane();
+    check(prt_set_camera(ctx_, &c));
+    check(prt_reset_accumulation(ctx_, 0));
+  }
+
+  uint32_t Flags() const {
+    return (AA ? PRT_FLAG_AA : 0u) | (accumulates ? PRT_FLAG_ACCUMULATE : 0u) | (GAMMACORRECTED ? PRT_FLAG_GAMMA : 0u) |
+           (NORMALMAPPED ? PRT_FLAG_NORMALMAP : 0u) | (SKYBOX ? PRT_FLAG_SKYBOX : 0u) | (LIGHTED ? PRT_FLAG_LIGHTED : 0u) |
+           (isStochastic ? PRT_FLAG_STOCHASTIC : 0u);
+  }
+  const prt_stats& LastStats() const { return stats_; }
+  prt_ctx* Context() const { return ctx_; }
+  int32_t Width() const { return width_; }
+  int32_t Height() const { return height_; }
+
+ private:
+  prt_ctx* ctx_ = nullptr;
+  int32_t width_, height_;
+  uint32_t frame_ = 0;
+  prt_stats stats_{};
+};
+
+}  // namespace prt

@@ -41,3 +41,38 @@ def random_rays(sd, n, seed=1):
     tgt[:, 1] = rng.uniform(-0.5, 0.5, n).astype(np.float32)
     D = (tgt - O).astype(np.float32)
     return O, D
+
+
+def dump_scene(sd, W, H, path):
+    """Binary scene file read by tests/cpp/render_scene.cpp (the C++ host mirror, include/prt_renderer.hpp).
+    Little-endian: b"PRTS", int32 W, H; camera pos[3], target[3], aspect (f32); lights: 39 f32 in prt_lights
+    order; sky: int32 w, h + w*h*3 f32; textures: int32 n + per texture int32 w, h + w*h u32; meshes:
+    int32 n + per mesh int32 T, V, 4 texture ids + triangles 12T f32, normals 12T f32, uvs 6T f32,
+    indices 3T i32, vertices 3V f32, face normals 3T f32; instances: int32 n + per instance 16 f32, u32 mesh."""
+    import struct
+    F = np.float32
+    with open(path, "wb") as f:
+        f.write(b"PRTS")
+        f.write(struct.pack("<ii", W, H))
+        f.write(np.asarray(sd.cam_pos, F).tobytes() + np.asarray(sd.cam_target, F).tobytes())
+        f.write(np.array([np.float32(W) / np.float32(H)], F).tobytes())
+        L = sd.lights
+        f.write(np.concatenate([np.asarray(a, F).ravel() for a in (L.point_pos, L.point_col, L.dir_pos, L.dir_col,
+                                                                     L.spot_pos, L.spot_col, L.spot_rot)]).tobytes())
+        if sd.sky is None:
+            f.write(struct.pack("<ii", 0, 0))
+        else:
+            f.write(struct.pack("<ii", sd.sky.shape[1], sd.sky.shape[0]) + np.ascontiguousarray(sd.sky, F).tobytes())
+        f.write(struct.pack("<i", len(sd.textures)))
+        for t in sd.textures:
+            f.write(struct.pack("<ii", t.shape[1], t.shape[0]) + np.ascontiguousarray(t, np.uint32).tobytes())
+        f.write(struct.pack("<i", len(sd.meshes)))
+        for m in sd.meshes:
+            f.write(struct.pack("<iiiiii", m.tri_count, m.vertices.size // 3, m.albedo, m.normal, m.metalness,
+                                m.emission))
+            for a, dt in ((m.triangles, F), (m.fixed_normals, F), (m.fixed_uvs, F), (m.indices, np.int32),
+                          (m.vertices, F), (m.face_normals, F)):
+                f.write(np.ascontiguousarray(a, dt).tobytes())
+        f.write(struct.pack("<i", len(sd.instances)))
+        for mi, xf in sd.instances:
+            f.write(np.ascontiguousarray(xf, F).tobytes() + struct.pack("<I", mi))
