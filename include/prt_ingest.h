@@ -1,0 +1,21 @@
+/*
+ * prt_ingest.h -- host-side helpers of the scene ingest (physically-based-ray-tracer_amd/prt/ingest.py),
+ * built into libprt_ingest.so.  Not part of the hot-path ABI (prt.h): the reference's own loaders
+ * (assimp, stb_image, Core/Model.cpp, template/surface.cpp) feed prt.h directly in a C++ integration.
+ */
+#ifndef PRT_INGEST_H
+#define PRT_INGEST_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* PNG scanline reconstruction (filters 0-4) of an inflated IDAT stream: raw = height x (1 + width*bpp)
+ * bytes, out = height x width*bpp.  Returns 0, -1 on bad arguments / short input, -2 on a bad filter. */
+int prt_png_unfilter(const uint8_t* raw, int64_t raw_len, int32_t width, int32_t height, int32_t bpp, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,346 @@
+"""Scene ingest: the reference's assets -> the arrays the hot path reads.
+
+The reference loads models with assimp (Core/Model.cpp:165-218: aiProcess_Triangulate |
+aiProcess_GenSmoothNormals | aiProcess_FlipUVs, mesh 0 only), textures with stb_image into 0x00RRGGBB
+Surfaces (template/surface.cpp:47-66, maps found by the "<model>_<type><ext>" convention), game objects
+and lights from JSON (Core/GameObject.cpp, Core/PhysicsObject.cpp, Core/LightTransform.cpp) and the
+camera from prefabs/camera.json (Core/Camera.cpp:13-16).  This module restates that host-side loading
+for glTF 2.0 (.gltf + .bin, .glb) and PNG, producing scenes.SceneData for prt.Scene.from_data and the
+oracle.  It is not on the hot path.
+
+Parity: assimp and Bullet are only present as prebuilt Windows binaries, so this ingest is
+"parity unpinned": it follows their published semantics (triangulation of glTF triangle lists / strips /
+fans in file order, V flipped as v' = 1 - v, file normals kept, smooth normals generated only when a mesh
+has none) and is checked against the counts the survey recorded (SciFiHelmet: 23,358 triangles, 70,074
+vertices; scene1's ship rotated ~pi about Y).
+"""
+from __future__ import annotations
+
+import json
+import os
+import struct
+import zlib
+
+import numpy as np
+
+from .scenes import F32, Lights, Mesh, SceneData
+
+# ---------------------------------------------------------------- PNG (stb_image subset)
+
+
+_INGEST_LIB = None
+
+
+def _unfilter(raw: bytes, w: int, h: int, bpp: int) -> np.ndarray:
+    """PNG scanline reconstruction in libprt_ingest.so (include/prt_ingest.h)."""
+    import ctypes as C
+    global _INGEST_LIB
+    if _INGEST_LIB is None:
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprt_ingest.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: build with make -C physically-based-ray-tracer_amd/csrc")
+        _INGEST_LIB = C.CDLL(path)
+        _INGEST_LIB.prt_png_unfilter.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
+        _INGEST_LIB.prt_png_unfilter.restype = C.c_int
+    src = np.frombuffer(raw, np.uint8)
+    out = np.empty((h, w * bpp), np.uint8)
+    rc = _INGEST_LIB.prt_png_unfilter(src.ctypes.data, src.size, w, h, bpp, out.ctypes.data)
+    if rc != 0:
+        raise ValueError(f"PNG scanline reconstruction failed ({rc})")
+    return out
+
+
+def load_png(path: str) -> np.ndarray:
+    """8-bit non-interlaced PNG -> (h, w) uint32 0x00RRGGBB, exactly Surface::LoadFromFile's packing
+    (grey replicated, channels 0..2 of RGB(A))."""
+    data = open(path, "rb").read()
+    if data[:8] != b"\x89PNG\r\n\x1a\n":
+        raise ValueError(f"{path}: not a PNG")
+    pos, idat, hdr = 8, [], None
+    while pos < len(data):
+        n, kind = struct.unpack(">I4s", data[pos:pos + 8])
+        body = data[pos + 8:pos + 8 + n]
+        pos += 12 + n
+        if kind == b"IHDR":
+            hdr = struct.unpack(">IIBBBBB", body)
+        elif kind == b"IDAT":
+            idat.append(body)
+        elif kind == b"IEND":
+            break
+    w, h, depth, ctype, _, _, interlace = hdr
+    if depth != 8 or interlace != 0 or ctype not in (0, 2, 4, 6):
+        raise ValueError(f"{path}: unsupported PNG (depth {depth}, colour type {ctype}, interlace {interlace})")
+    n = {0: 1, 2: 3, 4: 2, 6: 4}[ctype]
+    px = _unfilter(zlib.decompress(b"".join(idat)), w, h, n).reshape(h, w, n).astype(np.uint32)
+    if n <= 2:  # grey (+alpha)
+        g = px[..., 0]
+        return (g + (g << 8) + (g << 16)).astype(np.uint32)
+    return ((px[..., 0] << 16) + (px[..., 1] << 8) + px[..., 2]).astype(np.uint32)
+
+
+# ---------------------------------------------------------------- glTF 2.0
+
+_CT = {5120: np.int8, 5121: np.uint8, 5122: np.int16, 5123: np.uint16, 5125: np.uint32, 5126: np.float32}
+_NC = {"SCALAR": 1, "VEC2": 2, "VEC3": 3, "VEC4": 4}
+
+
+def _read_gltf(path: str):
+    raw = open(path, "rb").read()
+    if raw[:4] == b"glTF":  # GLB: JSON chunk + optional BIN chunk
+        pos, doc, binc = 12, None, None
+        while pos < len(raw):
+            n, kind = struct.unpack("<II", raw[pos:pos + 8])
+            chunk = raw[pos + 8:pos + 8 + n]
+            pos += 8 + n
+            if kind == 0x4E4F534A:
+                doc = json.loads(chunk)
+            elif kind == 0x004E4942:
+                binc = chunk
+        buffers = [binc if "uri" not in b else open(os.path.join(os.path.dirname(path), b["uri"]), "rb").read()
+                   for b in doc["buffers"]]
+    else:
+        doc = json.loads(raw)
+        buffers = []
+        for b in doc["buffers"]:
+            uri = b["uri"]
+            if uri.startswith("data:"):
+                import base64
+                buffers.append(base64.b64decode(uri.split(",", 1)[1]))
+            else:
+                buffers.append(open(os.path.join(os.path.dirname(path), uri), "rb").read())
+    return doc, buffers
+
+
+def _accessor(doc, buffers, i: int) -> np.ndarray:
+    a = doc["accessors"][i]
+    dt = np.dtype(_CT[a["componentType"]])
+    nc = _NC[a["type"]]
+    count = a["count"]
+    if "bufferView" not in a:
+        return np.zeros((count, nc), dt)
+    bv = doc["bufferViews"][a["bufferView"]]
+    buf = buffers[bv["buffer"]]
+    off = bv.get("byteOffset", 0) + a.get("byteOffset", 0)
+    stride = bv.get("byteStride", 0) or dt.itemsize * nc
+    if stride == dt.itemsize * nc:
+        return np.frombuffer(buf, dt, count * nc, off).reshape(count, nc).copy()
+    out = np.empty((count, nc), dt)
+    for k in range(count):
+        out[k] = np.frombuffer(buf, dt, nc, off + k * stride)
+    return out
+
+
+def _triangulate(idx: np.ndarray, mode: int) -> np.ndarray:
+    """aiProcess_Triangulate for glTF primitive modes 4 (list), 5 (strip), 6 (fan)."""
+    if mode == 4:
+        return idx[: len(idx) // 3 * 3].reshape(-1, 3)
+    if mode == 5:
+        tris = [(idx[k], idx[k + 1], idx[k + 2]) if k % 2 == 0 else (idx[k + 1], idx[k], idx[k + 2])
+                for k in range(len(idx) - 2)]
+        return np.asarray(tris, np.uint32).reshape(-1, 3)
+    if mode == 6:
+        return np.asarray([(idx[0], idx[k], idx[k + 1]) for k in range(1, len(idx) - 1)], np.uint32).reshape(-1, 3)
+    raise ValueError(f"glTF primitive mode {mode} has no triangles")
+
+
+def _normalize(v: np.ndarray) -> np.ndarray:
+    """tmpl8 normalize in float32: v * (1 / sqrtf((x*x + y*y) + z*z))."""
+    v = v.astype(F32)
+    d = (v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1]) + v[:, 2] * v[:, 2]
+    inv = (np.float32(1.0) / np.sqrt(d)).astype(F32)
+    return (v * inv[:, None]).astype(F32)
+
+
+def _smooth_normals(P: np.ndarray, tri: np.ndarray) -> np.ndarray:
+    """aiProcess_GenSmoothNormals for meshes without normals: face normals averaged over the faces that
+    share a vertex position (assimp joins positions within an epsilon; exact equality here)."""
+    fn = np.cross(P[tri[:, 1]] - P[tri[:, 0]], P[tri[:, 2]] - P[tri[:, 0]]).astype(F32)
+    ln = np.linalg.norm(fn, axis=1)
+    fn = np.where(ln[:, None] > 0, fn / np.maximum(ln, 1e-30)[:, None], 0).astype(F32)
+    _, key = np.unique(P, axis=0, return_inverse=True)
+    key = key.reshape(-1)
+    acc = np.zeros((key.max() + 1, 3), np.float64)
+    for c in range(3):
+        np.add.at(acc, key[tri[:, c]], fn)
+    n = acc[key]
+    return (n / np.maximum(np.linalg.norm(n, axis=1), 1e-30)[:, None]).astype(F32)
+
+
+def load_model(path: str) -> Mesh:
+    """Model(fullPath) (Core/Model.cpp:4-16,25-119,165-218): mesh 0 of the file (assimp's first aiMesh is
+    the first primitive of the first glTF mesh), corners in face order, V flipped."""
+    doc, buffers = _read_gltf(path)
+    prim = doc["meshes"][0]["primitives"][0]
+    at = prim["attributes"]
+    P = _accessor(doc, buffers, at["POSITION"]).astype(F32)
+    n = P.shape[0]
+    if "indices" in prim:
+        idx = _accessor(doc, buffers, prim["indices"]).reshape(-1).astype(np.uint32)
+    else:
+        idx = np.arange(n, dtype=np.uint32)
+    tri = _triangulate(idx, prim.get("mode", 4)).astype(np.int64)
+    N = _accessor(doc, buffers, at["NORMAL"]).astype(F32) if "NORMAL" in at else _smooth_normals(P, tri)
+    if "TEXCOORD_0" in at:
+        UV = _accessor(doc, buffers, at["TEXCOORD_0"]).astype(F32)
+        UV[:, 1] = np.float32(1.0) - UV[:, 1]  # aiProcess_FlipUVs
+    else:
+        UV = np.zeros((n, 2), F32)
+    T = tri.shape[0]
+    corner = tri.reshape(-1)
+    triangles = np.zeros((3 * T, 4), F32)
+    triangles[:, :3] = P[corner]
+    fixed_normals = np.zeros((3 * T, 4), F32)
+    fixed_normals[:, :3] = N[corner]
+    fixed_uvs = UV[corner]
+    v0, v1, v2 = P[tri[:, 0]], P[tri[:, 1]], P[tri[:, 2]]
+    e1, e2 = (v1 - v0).astype(F32), (v2 - v0).astype(F32)
+    cr = np.stack([e1[:, 1] * e2[:, 2] - e1[:, 2] * e2[:, 1], e1[:, 2] * e2[:, 0] - e1[:, 0] * e2[:, 2],
+                   e1[:, 0] * e2[:, 1] - e1[:, 1] * e2[:, 0]], axis=1).astype(F32)  # tmpl8 cross
+    return Mesh(triangles.reshape(-1), fixed_normals.reshape(-1), fixed_uvs.reshape(-1).astype(F32),
+                corner.astype(np.int32), P.reshape(-1), _normalize(cr).reshape(-1))
+
+
+def model_textures(path: str, ext: str = ".png") -> dict:
+    """Model::Load's LoadTexture convention (Core/Model.cpp:180-201): <dir>/<stem>_<type><ext>, PNG only."""
+    d, stem = os.path.dirname(path), os.path.splitext(os.path.basename(path))[0]
+    out = {}
+    for kind in ("albedo", "normal", "metalness", "emission"):
+        f = os.path.join(d, f"{stem}_{kind}{ext}")
+        if os.path.exists(f):
+            out[kind] = load_png(f)
+    return out
+
+
+# ---------------------------------------------------------------- game objects, lights, camera
+
+_PI_F = np.float32(3.141592653589)  # the PI macro in effect in these translation units (Core/BRDF.h:27)
+
+
+def _f(x):
+    return np.float32(x)
+
+
+def instance_transform(pos, rot_deg) -> np.ndarray:
+    """The transform chain of a JSON game object, restated in float32:
+    PhysicsObject::Update (Core/PhysicsObject.cpp:116-140) sets the body rotation with
+    btQuaternion::setEulerZYX(rx, ry, rz in radians) (lib/bullet/LinearMath/btQuaternion.h:140-155);
+    PhysicsObject::Synchronise (:173-186) reads it back with getEulerZYX (:161-200) and stores
+    (-yaw, pitch, -roll); GameObject::Synchronise (Core/GameObject.cpp:53-66) builds glm::quat from those
+    Euler angles, hands it to tmpl8 quat(w, x, y, z) as (glm.x, glm.y, glm.z, glm.w) -- components
+    rotated by one place -- and composes Translate(position) * quat.toMatrix() * Scale(1)
+    (template/tmpl8math.h:856-865).  Bullet's basis round trip (quaternion -> btMatrix3x3 -> quaternion)
+    is the identity up to float rounding and is not restated."""
+    rx, ry, rz = (_f(r) * _PI_F / _f(180.0) for r in rot_deg)
+    hy, hp, hr = _f(rx * _f(0.5)), _f(ry * _f(0.5)), _f(rz * _f(0.5))  # yawZ, pitchY, rollX
+    cy, sy, cp, sp, cr, sr = (np.cos(hy), np.sin(hy), np.cos(hp), np.sin(hp), np.cos(hr), np.sin(hr))
+    qx = sr * cp * cy - cr * sp * sy
+    qy = cr * sp * cy + sr * cp * sy
+    qz = cr * cp * sy - sr * sp * cy
+    qw = cr * cp * cy + sr * sp * sy
+    sqx, sqy, sqz, squ = qx * qx, qy * qy, qz * qz, qw * qw
+    sarg = _f(-2.0) * (qx * qz - qw * qy)
+    if sarg <= _f(-0.99999):
+        pitch, roll, yaw = _f(-0.5) * _PI_F, _f(0.0), _f(2.0) * np.arctan2(qx, -qy)
+    elif sarg >= _f(0.99999):
+        pitch, roll, yaw = _f(0.5) * _PI_F, _f(0.0), _f(2.0) * np.arctan2(-qx, qy)
+    else:
+        pitch = np.arcsin(sarg)
+        roll = np.arctan2(_f(2.0) * (qy * qz + qw * qx), squ - sqx - sqy + sqz)
+        yaw = np.arctan2(_f(2.0) * (qx * qy + qw * qz), squ + sqx - sqy - sqz)
+    e = np.array([-yaw, pitch, -roll], F32)  # GameObject::rotation
+    c, s = np.cos(e * _f(0.5)).astype(F32), np.sin(e * _f(0.5)).astype(F32)
+    gw = c[0] * c[1] * c[2] + s[0] * s[1] * s[2]  # glm quat(vec3 eulerAngles)
+    gx = s[0] * c[1] * c[2] - c[0] * s[1] * s[2]
+    gy = c[0] * s[1] * c[2] + s[0] * c[1] * s[2]
+    gz = c[0] * c[1] * s[2] - s[0] * s[1] * c[2]
+    w, x, y, z = gx, gy, gz, gw  # quat templateQuat(glmQuat.x, glmQuat.y, glmQuat.z, glmQuat.w) -> (w, x, y, z)
+    two = _f(2.0)
+    R = np.eye(4, dtype=F32)
+    R[0, 0] = _f(1) - two * y * y - two * z * z
+    R[0, 1] = two * x * y - two * w * z
+    R[0, 2] = two * x * z + two * w * y
+    R[1, 0] = two * x * y + two * w * z
+    R[1, 1] = _f(1) - two * x * x - two * z * z
+    R[1, 2] = two * y * z - two * w * x
+    R[2, 0] = two * x * z - two * w * y
+    R[2, 1] = two * y * z + two * w * x
+    R[2, 2] = _f(1) - two * x * x - two * y * y
+    M = R.copy()
+    M[0, 3], M[1, 3], M[2, 3] = (_f(p) for p in pos)  # Translate(position) * R (translation column untouched)
+    return M
+
+
+def load_game_objects(directory: str):
+    """Scene::FindSerialized(gameObjectsPath, ".json", 0) (Core/Scene.cpp:279-317): every *.json with a
+    modelIndex is one game object / BLAS instance, in directory order (sorted here)."""
+    out = []
+    for name in sorted(os.listdir(directory)):
+        if not name.endswith(".json"):
+            continue
+        d = json.load(open(os.path.join(directory, name)))
+        if "modelIndex" not in d:
+            continue
+        pos = (d.get("positionX", 0.0), d.get("positionY", 0.0), d.get("positionZ", 0.0))
+        rot = (d.get("rotationX", 0.0), d.get("rotationY", 0.0), d.get("rotationZ", 0.0))
+        out.append((int(d["modelIndex"]), instance_transform(pos, rot), name))
+    return out
+
+
+def _light(path):
+    d = json.load(open(path))
+    p = np.array([d["pX"], d["pY"], d["pZ"]], F32)
+    c = np.array([d["cX"], d["cY"], d["cZ"]], F32)
+    r = np.array([d.get("rX", 0.0), d.get("rY", 0.0), d.get("rZ", 0.0)], F32)
+    return p, c, r
+
+
+def load_lights(scene_dir: str) -> Lights:
+    """The lights the hot path reads: the four SIMD point lights stay zero (Renderer::InitLights copies
+    arrays that Scene::Init never fills, Core/Renderer.cpp:408-417), directionalLights[0] and
+    spotlights[0] from their JSON (Core/LightTransform.cpp:4-23; Scene.cpp:26-27)."""
+    z3 = np.zeros(3, F32)
+    dp = dc = sp = sc = sr = z3
+    dd = os.path.join(scene_dir, "directionallights")
+    if os.path.isdir(dd):
+        files = sorted(f for f in os.listdir(dd) if f.endswith(".json"))
+        if files:
+            dp, dc, _ = _light(os.path.join(dd, files[0]))
+    sdir = os.path.join(scene_dir, "spotlights")
+    if os.path.isdir(sdir):
+        files = sorted(f for f in os.listdir(sdir) if f.endswith(".json"))
+        if files:
+            sp, sc, sr = _light(os.path.join(sdir, files[0]))
+    return Lights(np.zeros((4, 3), F32), np.zeros((4, 3), F32), dp, dc, sp, sc, sr)
+
+
+def load_camera(path: str):
+    """prefabs/camera.json (Core/Camera.cpp:13-16): camPos, camTarget."""
+    d = json.load(open(path))
+    return (np.array([d["pX"], d["pY"], d["pZ"]], F32), np.array([d["tX"], d["tY"], d["tZ"]], F32))
+
+
+def load_scene(model_paths, scene_dir: str, camera_json: str, textures_ext: str = ".png",
+               fallback_albedo: int = 0xB0B0B0, fallback_metalness: int | None = (128 << 8),
+               name: str = "ingested") -> SceneData:
+    """Scene::Init (Core/Scene.cpp:10-28) for the given models + scene directory.  Missing maps: the
+    reference dereferences the albedo map unconditionally (Scene.cpp:160), so a 1x1 `fallback_albedo` is
+    used when a model has none; `fallback_metalness` (G = roughness, B = metal) likewise (None = no map)."""
+    meshes, textures = [], []
+
+    def tex(arr):
+        textures.append(np.ascontiguousarray(arr, np.uint32))
+        return len(textures) - 1
+    for mp in model_paths:
+        m = load_model(mp)
+        maps = model_textures(mp, textures_ext)
+        m.albedo = tex(maps["albedo"]) if "albedo" in maps else tex(np.full((1, 1), fallback_albedo, np.uint32))
+        m.normal = tex(maps["normal"]) if "normal" in maps else -1
+        if "metalness" in maps:
+            m.metalness = tex(maps["metalness"])
+        elif fallback_metalness is not None:
+            m.metalness = tex(np.full((1, 1), fallback_metalness, np.uint32))
+        m.emission = tex(maps["emission"]) if "emission" in maps else -1
+        meshes.append(m)
+    inst = [(mi, xf) for mi, xf, _ in load_game_objects(scene_dir)]
+    cam_pos, cam_target = load_camera(camera_json)
+    return SceneData(meshes, textures, inst, load_lights(scene_dir), None, cam_pos, cam_target, name)

@@ -18,6 +18,7 @@ sky) are replaced by these procedural maps.
 from __future__ import annotations
 
 import dataclasses
+import os
 import numpy as np
 
 F32 = np.float32
@@ -230,3 +231,23 @@ def multi_instance(base: SceneData) -> SceneData:
         return M.astype(F32)
     inst = list(base.instances) + [(0, trs((1.5, 0.6, 2.0), 0.7, 0.35)), (0, trs((-1.8, 0.9, 1.0), -0.4, 0.25))]
     return dataclasses.replace(base, instances=inst, name=base.name + "+inst")
+
+
+REFERENCE_ROOT = os.environ.get("PRT_REFERENCE_ROOT", "/root/reference")
+
+
+def config_c1(root: str = REFERENCE_ROOT) -> SceneData:
+    """C1 (BASELINE configs[0]): scene1 as the reference ships it -- SciFiHelmet (23,358 triangles) as
+    model 0, the XShip game object (~pi about Y), scene1's directional + spot light, zero point lights,
+    prefabs/camera.json; render at 256x256, 1 spp (AA off), depth 1, SKYBOX off.  The helmet's maps are
+    missing blobs in the reference tree, so 1x1 maps stand in (albedo 0xB0B0B0; G = roughness 128,
+    B = metal 0).  Needs the reference's asset files (`root`, PRT_REFERENCE_ROOT); see prt/ingest.py."""
+    from . import ingest
+    model = os.path.join(root, "Core", "assets", "prefabs", "models", "SciFiHelmet", "SciFiHelmet.gltf")
+    if not os.path.exists(model):
+        raise FileNotFoundError(f"C1 needs the reference assets ({model})")
+    return ingest.load_scene([model], os.path.join(root, "assets", "scene1"),
+                             os.path.join(root, "Core", "assets", "prefabs", "camera.json"), name="c1-scene1-helmet")
+
+
+C1_FLAGS = 0x7F & ~(1 << 4) & ~(1 << 0)  # reference defaults without SKYBOX (C1) and AA (1 spp)
