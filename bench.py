@@ -179,6 +179,8 @@ def main():
         if pipeline == 2:  # merged pipeline: one traversal launch per iteration (closest + shadow rays)
             kern["k_trace"] = ((seg_f * bpr["closest"] + sh_f * bpr["anyhit"]) / launches,
                                float(np.mean(ms_closest)) / launches)
+        elif pipeline == 3:  # streaming engine: one persistent launch per frame (traversal + shading)
+            kern["k_stream"] = (seg_f * bpr["closest"] + sh_f * bpr["anyhit"], float(np.mean(ms_closest)))
         elif pipeline == 0:
             kern["k_extend"] = (seg_f * bpr["closest"] / launches, float(np.mean(ms_closest)) / launches)
             kern["k_shadow"] = (sh_f * bpr["anyhit"] / launches, float(np.mean(ms_anyhit)) / launches)
@@ -190,9 +192,9 @@ def main():
         traffic = measured_traffic(dom)
         own = own_layout_bytes_per_ray()
         own_block = None
-        if own is not None and pipeline in (0, 2):
-            own_b = ((seg_f * own["closest"] if dom in ("k_extend", "k_trace") else 0.0) +
-                     (sh_f * own["anyhit"] if dom in ("k_shadow", "k_trace") else 0.0)) / launches
+        if own is not None and pipeline in (0, 2, 3):
+            own_b = ((seg_f * own["closest"] if dom in ("k_extend", "k_trace", "k_stream") else 0.0) +
+                     (sh_f * own["anyhit"] if dom in ("k_shadow", "k_trace", "k_stream") else 0.0)) / launches
             own_block = {"bytes_per_ray": {k: round(v, 1) for k, v in own.items()}, "algorithmic_bytes": round(own_b),
                          "achieved": round(own_b / (kern_ms / 1e3) / 1e9, 1),
                          "frac": round(own_b / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
@@ -208,7 +210,7 @@ def main():
             "scaling": "strong",  # one fixed frame is split into pixel tiles over the N GPUs
             "vs_baseline": None,
             "dtype": "f32",
-            "pipeline": {0: "wavefront", 1: "megakernel", 2: "wavefront-merged"}[pipeline],
+            "pipeline": {0: "wavefront", 1: "megakernel", 2: "wavefront-merged", 3: "stream"}[pipeline],
             "data": "synthetic (seeded procedural heightfield, textures, sky; scenes.py)",
             "config": {"workload": f"{sd.name}: {info.triangles} tris, {W}x{H}, {args.spp} spp, depth {args.bounces}",
                        "global_batch": W * H, "seq_len": args.bounces,

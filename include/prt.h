@@ -116,10 +116,12 @@ typedef struct {
     uint64_t paths;         /* camera paths traced */
     double   ms;            /* device time of the render (HIP events) */
     double   ms_trace;      /* device time of the path-tracing kernel(s) only */
-    double   ms_closest;    /* device time of the traversal launches (pipeline 2: closest + shadow rays together) */
+    double   ms_closest;    /* device time of the traversal launches (pipeline 2: closest + shadow rays together;
+                               pipeline 3: the whole persistent launch, shading included) */
     double   ms_anyhit;     /* device time of the shadow any-hit launches (pipeline 0 only) */
     int32_t  pipeline;      /* 2 = merged-trace wavefront (default), 0 = wavefront with separate extend /
-                               shadow launches (PRT_PIPELINE=wave1), 1 = megakernel (PRT_PIPELINE=mega) */
+                               shadow launches (PRT_PIPELINE=wave1), 1 = megakernel (PRT_PIPELINE=mega),
+                               3 = streaming engine, one persistent launch (PRT_PIPELINE=stream) */
     int32_t  iterations;    /* wavefront iterations launched */
 } prt_stats;
 

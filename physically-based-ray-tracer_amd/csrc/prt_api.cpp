@@ -131,6 +131,13 @@ struct prt_ctx {
   WaveBufs wb{};
   uint32_t wave_n = 0, wave_levels = 0;
   WaveTimers wt{};
+  // streaming engine (prt_stream.hip)
+  DevBuf sq, sctl;
+  StreamBufs sb{};
+  size_t sq_rcap = 0, sq_hcap = 0;
+  uint32_t sq_n = 0;
+  uint32_t serial = 0;
+  uint32_t nparts = 0, xcc_part = 0xFFFFFFFFu;
 };
 
 namespace {
@@ -309,12 +316,82 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces) {
 }
 
 // PRT_PIPELINE: "mega" = one megakernel per pixel-frame, "wave1" = wavefront with separate extend /
-// shadow launches (prt_wave.hip), default = merged-trace wavefront (prt_wave2.hip)
+// shadow launches (prt_wave.hip), "stream" = one persistent launch per frame batch (prt_stream.hip),
+// default = merged-trace wavefront (prt_wave2.hip)
 int pipeline_from_env() {
   const char* e = std::getenv("PRT_PIPELINE");
   if (e && std::strcmp(e, "mega") == 0) return 1;
   if (e && std::strcmp(e, "wave1") == 0) return 0;
+  if (e && std::strcmp(e, "stream") == 0) return 3;
   return 2;
+}
+
+// XCC ids of the device (one census per context): part k of the streaming engine runs on the k-th id
+int ensure_parts(prt_ctx* c) {
+  if (c->nparts) return PRT_OK;
+  HIP_TRY(c->sctl.ensure(4 * kStreamCtlWords));
+  HIP_TRY(hipMemsetAsync(c->sctl.p, 0, 4, c->stream));
+  HIP_TRY(launch_xcc_census(c->stream, c->sctl.as<uint32_t>()));
+  uint32_t mask = 0;
+  HIP_TRY(hipMemcpyAsync(&mask, c->sctl.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  uint32_t map = 0xFFFFFFFFu, np = 0;
+  for (uint32_t k = 0; k < 8; k++)
+    if (mask & (1u << k)) {
+      map = (map & ~(0xFu << (4 * k))) | (np << (4 * k));
+      np++;
+    }
+  if (np == 0) return fail(PRT_ERR_HIP, "XCC census saw no workgroup");
+  c->nparts = np;
+  c->xcc_part = map;
+  return PRT_OK;
+}
+
+// streaming queues for n items over `iters` bounces: every shading task queues at most 5 rays (1 closest
+// + 4 shadow) and an item has at most iters + 1 shading tasks; sub-queues are fed round-robin per wave,
+// so one sub-queue holds at most 1/kSSub of its part's entries plus one 64-lane push per wave
+int ensure_stream(prt_ctx* c, uint32_t n, uint32_t iters, uint32_t grid) {
+  int rc = ensure_parts(c);
+  if (rc) return rc;
+  const uint64_t per_part = ((uint64_t)(n + 63) / 64 + c->nparts - 1) / c->nparts * 64;
+  const uint64_t slack = 320ull * (grid + 64);
+  const uint64_t rcap = (per_part * (1 + 5ull * (iters + 1)) + kSSub - 1) / kSSub + slack + 4096;
+  const uint64_t hcap = (per_part * (iters + 2ull) + kSSub - 1) / kSSub + slack / 5 + 4096;
+  const uint64_t total = (uint64_t)c->nparts * kSSub;
+  if (total * rcap >= (1ull << 32)) return fail(PRT_ERR_UNSUPPORTED, "streaming queues exceed 32-bit slots");
+  if (!(c->sq.p && c->sq_rcap >= rcap && c->sq_hcap >= hcap && c->sq_n >= n)) {
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+    const size_t o_rq = take(8 * total * rcap), o_hq = take(8 * total * hcap), o_pend = take(4ull * n),
+                 o_ctr = take(4 * kStreamCtrWords);
+    c->sq.release();
+    HIP_TRY(c->sq.ensure(off));
+    HIP_TRY(hipMemsetAsync(c->sq.p, 0, off, c->stream));  // granule tags 0: never a launch serial
+    char* b = c->sq.as<char>();
+    c->sb.rq = (unsigned long long*)(b + o_rq);
+    c->sb.hq = (unsigned long long*)(b + o_hq);
+    c->sb.pend = (uint32_t*)(b + o_pend);
+    c->sb.ctr = (uint32_t*)(b + o_ctr);
+    c->sq_rcap = rcap;
+    c->sq_hcap = hcap;
+    c->sq_n = n;
+  }
+  HIP_TRY(c->sctl.ensure(4 * kStreamCtlWords + 64));
+  c->sb.ctl = c->sctl.as<uint32_t>();
+  c->sb.stat = reinterpret_cast<unsigned long long*>(c->sctl.as<char>() + 4 * kStreamCtlWords);
+  c->sb.rcap = (uint32_t)c->sq_rcap;
+  c->sb.hcap = (uint32_t)c->sq_hcap;
+  c->sb.nparts = c->nparts;
+  c->sb.xcc_part = c->xcc_part;
+  const char* e = std::getenv("PRT_STREAM_BUDGET_MS");
+  c->sb.budget_ms = e ? (uint32_t)std::atoi(e) : 20000u;
+  const char* w = std::getenv("PRT_STREAM_WAVES");
+  c->sb.waves = (w && std::atoi(w) == 4) ? 4u : 5u;
+  if (++c->serial == 0) c->serial = 1;
+  c->sb.serial = c->serial;
+  HIP_TRY(hipMemsetAsync(c->sb.ctr, 0, 4 * kStreamCtrWords, c->stream));
+  HIP_TRY(hipMemsetAsync(c->sctl.p, 0, 4 * kStreamCtlWords + 64, c->stream));
+  return PRT_OK;
 }
 
 // the shared trace + accumulate sequence for prt_render / prt_render_tiles
@@ -339,7 +416,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   LaunchCfg L{c->stream, layout, trav_from_env(), occ_for(c)};
   // the merged pipeline runs the persistent 8-wide traversal only: Node4 and the lock-step kernels use wave1
   int pipe = pipeline_from_env();
-  if (pipe == 2 && (layout == 4 || L.trav == 1)) pipe = 0;
+  if ((pipe == 2 || pipe == 3) && (layout == 4 || L.trav == 1)) pipe = 0;
   const bool mega = pipe == 1;
   const uint32_t iters = (uint32_t)p->bounces * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
   if (!mega && iters > (uint32_t)kMaxIters) return fail(PRT_ERR_UNSUPPORTED, "too many wavefront iterations");
@@ -352,7 +429,26 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     rc = ensure_wave(c, (uint32_t)n, p->bounces);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * kCtrWords, c->stream));
-    if (pipe == 2) HIP_TRY(launch_wavefront2(L, S, A, M, c->wb, c->frames.as<float4>(), stats ? &c->wt : nullptr));
+    if (pipe == 3) {
+      // byte offsets of the sc1 buffer loads are 32-bit: R/T levels x n and the 4 x n shadow slots
+      if ((uint64_t)c->wave_levels * n * 16 >= (1ull << 32) || 64ull * n >= (1ull << 32))
+        return fail(PRT_ERR_UNSUPPORTED, "streaming engine: too many work items in one call (split spp)");
+      int dev = 0, cus = 256;
+      HIP_TRY(hipGetDevice(&dev));
+      HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      rc = ensure_stream(c, (uint32_t)n, iters, (uint32_t)cus * 4u * 5u);
+      if (rc) return rc;
+      if (stats) HIP_TRY(hipEventRecord(c->wt.ev[0], c->stream));
+      HIP_TRY(launch_stream(L, S, A, M, c->wb, c->sb, c->frames.as<float4>()));
+      if (stats) HIP_TRY(hipEventRecord(c->wt.ev[1], c->stream));
+      uint32_t ctl[2] = {0, 0};
+      HIP_TRY(hipMemcpyAsync(ctl, c->sb.ctl, 8, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (ctl[0] != 0) {
+        static const char* what[] = {"?", "watchdog expired (PRT_STREAM_BUDGET_MS)", "queue overflow", "item state"};
+        return fail(PRT_ERR_HIP, std::string("streaming engine aborted: ") + what[ctl[1] < 4 ? ctl[1] : 0]);
+      }
+    } else if (pipe == 2) HIP_TRY(launch_wavefront2(L, S, A, M, c->wb, c->frames.as<float4>(), stats ? &c->wt : nullptr));
     else HIP_TRY(launch_wavefront(L, S, A, M, c->wb, c->frames.as<float4>(), stats ? &c->wt : nullptr));
   }
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
@@ -368,6 +464,21 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
       stats->segments = h.segments;
       stats->shadow_rays = h.shadow;
       stats->pipeline = 1;
+    } else if (pipe == 3) {
+      unsigned long long h[8] = {};
+      HIP_TRY(hipMemcpyAsync(h, c->sb.stat, 7 * sizeof(h[0]), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (std::getenv("PRT_DEBUG_QUEUES") && h[4])  // wave-time shares of the two roles (s_memrealtime ticks)
+        std::fprintf(stderr, "prt: stream: shade %.1f%% trace %.1f%% other %.1f%% of wave time; %llu batches, %.1f items/batch\n",
+                     100.0 * h[2] / h[4], 100.0 * h[3] / h[4], 100.0 * (h[4] - h[2] - h[3]) / h[4], h[5],
+                     h[5] ? (double)h[6] / h[5] : 0.0);
+      stats->segments = h[0];
+      stats->shadow_rays = h[1];
+      float a = 0;
+      HIP_TRY(hipEventElapsedTime(&a, c->wt.ev[0], c->wt.ev[1]));
+      stats->ms_closest = a;
+      stats->pipeline = 3;
+      stats->iterations = 1;
     } else {
       std::vector<uint32_t> ctr(kCtrWords);
       HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
@@ -480,6 +591,8 @@ int prt_destroy(prt_ctx* c) {
   for (auto e : c->wt.ev)
     if (e) (void)hipEventDestroy(e);
   c->wave.release();
+  c->sq.release();
+  c->sctl.release();
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return PRT_OK;

@@ -49,6 +49,26 @@ struct WaveBufs {
   float4* shd;      // shadow queue: D, bits(4 * item + slot)
   uint32_t* ctr;    // [iteration][path|shadow][sub-queue] counters, kCtrStride apart
 };
+// streaming engine (prt_stream.hip): per-XCD ray / shade queues of tagged 8-byte granules
+constexpr uint32_t kSSub = 8;        // sub-queues per XCD part and queue
+constexpr uint32_t kMaxParts = 8;
+struct StreamBufs {
+  uint32_t* pend;               // n: rays of the item still in flight (agent atomics only)
+  unsigned long long* rq;       // ray queue   [part][sub][rcap]: serial << 32 | ray id
+  unsigned long long* hq;       // shade queue [part][sub][hcap]: serial << 32 | item
+  uint32_t* ctr;                // [part][rq tail, rq head, hq tail, hq head][sub], kCtrStride apart
+  uint32_t* ctl;                // [0] abort, [1] error code, kCtrStride * (2 + part): live items of the part
+  unsigned long long* stat;     // closest segments, shadow rays traced
+  uint32_t rcap, hcap;          // per sub-queue capacities
+  uint32_t serial;              // granule tag of this launch (never 0)
+  uint32_t nparts;              // XCD parts present
+  uint32_t xcc_part;            // 4 bits per HW_REG_XCC_ID: its part (0xF = none)
+  uint32_t budget_ms;           // in-kernel watchdog
+  uint32_t waves;               // waves per SIMD of the persistent launch (4 or 5)
+};
+constexpr size_t kStreamCtlWords = (size_t)(2 + kMaxParts) * kCtrStride;
+constexpr size_t kStreamCtrWords = (size_t)kMaxParts * 4 * kSSub * kCtrStride;
+
 constexpr int kMaxIters = 32;
 struct WaveTimers {
   hipEvent_t ev[4 * kMaxIters];
@@ -62,6 +82,11 @@ hipError_t launch_wave_init(const LaunchCfg& c, const SceneDev& S, const TraceAr
 // merged pipeline (prt_wave2.hip): one traversal launch per iteration for P(i) closest + S(i-1) any-hit
 hipError_t launch_wavefront2(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                              const WaveBufs& B, float4* out, WaveTimers* tm);
+// streaming engine (prt_stream.hip): one persistent launch per frame batch, no per-bounce boundaries
+hipError_t launch_stream(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
+                         const WaveBufs& B, const StreamBufs& Q, float4* out);
+// XCC ids the device schedules on (bit k = HW_REG_XCC_ID k seen); writes one word to dev_mask
+hipError_t launch_xcc_census(hipStream_t s, uint32_t* dev_mask);
 hipError_t launch_trace_frames(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                                float4* out, Counters* cnt);
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,

@@ -27,11 +27,14 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 //                                                                       and (MODE 2) its query kind
 //   reload(uint32_t handle, bool any, V3& O, V3& D)        world ray again (next instance of the TLAS loop)
 //   finish(uint32_t handle, const Hit& h, bool any, bool hit)  closest: h; any-hit: hit = occluded
+//   tick(idle, drained)                                     wave-uniform, once at the top of every iteration:
+//                                                           idle lanes, no refill coming (the streaming
+//                                                           engine publishes finished rays there)
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
-template <int MODE, bool HALF, int STACK, int REFILL, class Fetch, class Load, class Reload, class Finish>
-__device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
-                                                 Load load, Reload reload, Finish finish) {
+template <int MODE, bool HALF, int STACK, int REFILL, class Fetch, class Load, class Reload, class Finish, class Tick>
+__device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
+                                                   Load load, Reload reload, Finish finish, Tick tick) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   bool active = false, drained = false;
@@ -66,6 +69,7 @@ __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __
   while (true) {
     // ---- refill idle lanes from the queue
     const uint64_t idle = __ballot(!active);
+    tick((uint32_t)__popcll(idle), drained);
     if (!drained && __popcll(idle) >= (uint32_t)REFILL) {
       uint32_t base = 0;
       const uint32_t want = (uint32_t)__popcll(idle);
@@ -175,6 +179,12 @@ __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __
       }
     }
   }
+}
+
+template <int MODE, bool HALF, int STACK, int REFILL, class Fetch, class Load, class Reload, class Finish>
+__device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
+                                                 Load load, Reload reload, Finish finish) {
+  trav8_persistent_t<MODE, HALF, STACK, REFILL>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {});
 }
 
 }  // namespace prt

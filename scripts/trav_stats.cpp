@@ -230,6 +230,18 @@ int main(int argc, char** argv) {
                 tr.size(), visits / tr.size(), tris / tr.size(), pushes / tr.size());
     std::fprintf(stderr, "{\"kind\": \"%s\", \"rays\": %zu, \"node_visits\": %.4f, \"tri_tests\": %.4f}\n",
                  kind ? "anyhit" : "closest", tr.size(), visits / tr.size(), tris / tr.size());
+    if (argc > 3 && std::strcmp(argv[3], "--dist") == 0) {  // per-ray sequential steps: the launch tail
+      std::vector<int> st;
+      for (const Trace& t : tr) {
+        int k = (int)t.tris_per_visit.size();
+        for (uint8_t c : t.tris_per_visit) k += c;
+        st.push_back(k);
+      }
+      std::sort(st.begin(), st.end());
+      auto q = [&](double p) { return st[std::min(st.size() - 1, (size_t)(p * st.size()))]; };
+      std::printf("    steps (visits + tri tests) per ray: p50 %d  p90 %d  p99 %d  p99.9 %d  p99.99 %d  max %d\n",
+                  q(0.5), q(0.9), q(0.99), q(0.999), q(0.9999), st.back());
+    }
     if (argc > 3 && std::strcmp(argv[3], "--models") == 0) {
       for (int ra : {64, 32, 16, 8}) wave_model(tr, ra, 130.0, 35.0, 40.0);
       for (int ra : {64, 32, 16})

@@ -97,23 +97,57 @@ def test_render_c3_reduced(gpu_ctx):
 
 @pytest.mark.parametrize("flags", [oracle.DEFAULT_FLAGS, oracle.DEFAULT_FLAGS & ~oracle.AA])
 def test_pipelines_identical(gpu_ctx, monkeypatch, flags):
-    """The three pipelines -- merged-trace wavefront (default), wavefront with separate extend / shadow
-    launches (PRT_PIPELINE=wave1) and the megakernel (PRT_PIPELINE=mega) -- render bit-identical frames."""
+    """The four pipelines -- merged-trace wavefront (default), wavefront with separate extend / shadow
+    launches (PRT_PIPELINE=wave1), the megakernel (PRT_PIPELINE=mega) and the streaming engine
+    (PRT_PIPELINE=stream) -- render bit-identical frames."""
     sd = scenes.multi_instance(scenes.config_small(60, 50))
     W, H = 128, 96
     gpu_scene(gpu_ctx, sd, W, H)
     out = {}
     for pipe, code, iters in (("", 2, 9 if flags & oracle.AA else 5), ("wave1", 0, 8 if flags & oracle.AA else 4),
-                              ("mega", 1, 0)):
+                              ("mega", 1, 0), ("stream", 3, 1)):
         if pipe:
             monkeypatch.setenv("PRT_PIPELINE", pipe)
         gpu_ctx.reset_accumulation(full=True)
         a, r, st = gpu_ctx.render(W, H, 4, 4, flags)
         assert st.pipeline == code and st.iterations == iters
         out[code] = (a, r, st)
-    for code in (0, 1):
+    for code in (0, 1, 3):
         assert np.array_equal(out[2][0], out[code][0]) and np.array_equal(out[2][1], out[code][1])
         assert out[2][2].segments == out[code][2].segments and out[2][2].shadow_rays == out[code][2].shadow_rays
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3, 6])
+def test_stream_debug_modes(gpu_ctx, monkeypatch, mode):
+    """Debug render modes (Core/Renderer.cpp:170-194) through the streaming engine match the merged pipeline."""
+    sd = scenes.multi_instance(scenes.config_small(40, 30))
+    W, H = 96, 64
+    gpu_scene(gpu_ctx, sd, W, H)
+    out = []
+    for pipe in ("", "stream"):
+        monkeypatch.setenv("PRT_PIPELINE", pipe)
+        gpu_ctx.reset_accumulation(full=True)
+        out.append(gpu_ctx.render(W, H, 2, 3, mode=mode))
+    assert np.array_equal(out[0][0], out[1][0], equal_nan=True) and np.array_equal(out[0][1], out[1][1])
+
+
+def test_stream_large_identical(gpu_ctx, monkeypatch):
+    """The streaming engine under full-chip load (C3, 960x540, 4 spp, depth 4: about 4M rays through the
+    per-XCD queues) renders the merged pipeline's frame bit for bit, also on the second call (new serial)."""
+    sd = scenes.config_c3()
+    W, H = 960, 540
+    gpu_scene(gpu_ctx, sd, W, H)
+    out = {}
+    for pipe in ("", "stream", "stream"):
+        monkeypatch.setenv("PRT_PIPELINE", pipe)
+        gpu_ctx.reset_accumulation(full=True)
+        a, r, st = gpu_ctx.render(W, H, 4, 4)
+        if pipe in out:
+            assert np.array_equal(out[pipe][0], a)
+        out[pipe] = (a, r, st)
+    assert np.array_equal(out[""][0], out["stream"][0]) and np.array_equal(out[""][1], out["stream"][1])
+    assert out[""][2].segments == out["stream"][2].segments
+    assert out[""][2].shadow_rays == out["stream"][2].shadow_rays
 
 
 def test_bvh_layouts_render_identical(gpu_ctx, monkeypatch):
