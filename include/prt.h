@@ -11,7 +11,8 @@
  *                         Core/tiny_bvh.h:1243-1256)
  *   prt_set_lights     <- Renderer point-light SoA (Core/Renderer.h:80-88), directionalLights[0], spotlights[0]
  *   prt_set_sky        <- Camera::skyPixels (Core/Camera.cpp:9)
- *   prt_set_camera     <- Camera::camPos/topLeft/topRight/bottomLeft (Core/Camera.cpp:29-36)
+ *   prt_set_camera     <- Camera::camPos/topLeft/topRight/bottomLeft/right/up/ahead (Core/Camera.cpp:29-36)
+ *   prt_set_postfx     <- Renderer::isPostProcessed + Camera post-process members (Core/Camera.h:11-31)
  *   prt_render         <- the OpenMP pixel loop + Renderer::Trace (Core/Renderer.cpp:43-141,150-406)
  *
  * Conventions: plain pointers and sizes, no C++ types; every call returns PRT_OK (0) or a negative
@@ -28,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PRT_ABI_VERSION 1
+#define PRT_ABI_VERSION 2
 
 typedef enum {
     PRT_OK = 0,
@@ -94,10 +95,12 @@ typedef struct {
     float spot_pos[3], spot_color[3], spot_rot[3];   /* spotlights[0]->transform        */
 } prt_lights;
 
-/* Camera screen plane (Core/Camera.cpp:29-36, 113-139) */
+/* Camera screen plane and basis (Core/Camera.cpp:29-36, 113-139; Core/Camera.h:15-17).  right / up /
+ * ahead are only read by the Panini projection (post-processing on); prt_camera_look_at fills all. */
 typedef struct {
     float pos[3];
     float top_left[3], top_right[3], bottom_left[3];
+    float right[3], up[3], ahead[3];
 } prt_camera;
 
 typedef struct {
@@ -152,6 +155,25 @@ int prt_set_camera(prt_ctx* ctx, const prt_camera* cam);
 /* Camera::Camera basis from position/target and aspect (Core/Camera.cpp:29-36) */
 int prt_camera_look_at(const float pos[3], const float target[3], float aspect, prt_camera* out);
 
+/* Post-processing (Renderer::isPostProcessed, Core/Renderer.h:48): Panini primary rays
+ * (Camera::GetPrimaryRay/Panini, Core/Camera.cpp:81-139) and the screen pass of Core/Renderer.cpp:107-133
+ * (chromatic aberration from the accumulator, vignette, colour grading).  avg_rgba stays the plain
+ * average; rgb8 gets the post-processed pixel. */
+typedef struct {
+    int32_t enabled;            /* Renderer::isPostProcessed (default false) */
+    int32_t aberration;         /* Camera::abberationIntensity, pixels */
+    float fov;                  /* Camera::fov (Camera::Panini uses it as radians, :86) */
+    float distortion;           /* Camera::distortion */
+    float vignette_intensity;   /* Camera::vignetteIntensity */
+    float vignette_radius;      /* Camera::vignetteRadius (the pow exponent) */
+    float color_grading[4];     /* Camera::colorGrading */
+} prt_postfx;
+/* preset 0: the Camera member defaults (Core/Camera.h:12,23,27; DEBUGMODE build), 1: the GAME preset P1
+ * (Core/Camera.cpp:18-23, vignetteRadius keeps its default: the constructor self-assigns it).
+ * enabled is set to 1. */
+int prt_postfx_preset(int32_t preset, prt_postfx* out);
+int prt_set_postfx(prt_ctx* ctx, const prt_postfx* pfx);
+
 /* ---- rendering (Renderer::Tick) ----
  * Traces params.spp camera paths per pixel as spp/2 (AA) or spp reference frames and folds each
  * frame into the persistent accumulation state exactly as Core/Renderer.cpp:81-104 does.
@@ -176,7 +198,9 @@ int prt_tile_pixel_map(int32_t width, int32_t height, int32_t tile_size, int32_t
                        int32_t* pixel_of_slot);
 int prt_render_tiles(prt_ctx* ctx, const prt_render_params* params, int32_t tile_size, int32_t rank,
                      int32_t world, float* tiles_rgba_device, prt_stats* stats);
-/* rank-0 side: gathered [world][tile_buffer_pixels] float4 device buffer -> W*H avg_rgba + rgb8 (device) */
+/* rank-0 side: gathered [world][tile_buffer_pixels] float4 device buffer -> W*H avg_rgba + rgb8 (device).
+ * With post-processing the vignette / grading apply to rgb8; chromatic aberration needs the neighbours'
+ * accumulators, which stay on their ranks: PRT_ERR_UNSUPPORTED there. */
 int prt_untile(prt_ctx* ctx, const float* gathered_device, int32_t width, int32_t height, int32_t tile_size,
                int32_t world, float* avg_rgba_device, uint32_t* rgb8_device);
 

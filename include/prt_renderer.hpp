@@ -101,12 +101,17 @@ class Scene {
   }
 };
 
-// Camera (Core/Camera.h:15-17): position, target and the screen plane GetPrimaryRay interpolates
+// Camera (Core/Camera.h:11-31): position, target, the screen plane GetPrimaryRay interpolates, its basis
+// and the post-process members (defaults of Camera.h; read when Renderer::isPostProcessed is set)
 class Camera {
  public:
   float camPos[3] = {0, 0, -1}, camTarget[3] = {0, 0, 0};
   float aspect = 1.0f;
   float topLeft[3] = {}, topRight[3] = {}, bottomLeft[3] = {};
+  float right[3] = {}, up[3] = {}, ahead[3] = {};
+  float colorGrading[4] = {1.f, 1.f, 1.f, 1.f};
+  float fov = 40.f, distortion = 40.f, vignetteIntensity = 20.f, vignetteRadius = 0.3f;
+  int32_t abberationIntensity = 0;
 
   Camera() = default;
   Camera(const float pos[3], const float target[3], float aspect_) : aspect(aspect_) {
@@ -117,14 +122,27 @@ class Camera {
   void Update() {
     prt_camera c{};
     check(prt_camera_look_at(camPos, camTarget, aspect, &c));
-    for (int k = 0; k < 3; k++) { topLeft[k] = c.top_left[k]; topRight[k] = c.top_right[k]; bottomLeft[k] = c.bottom_left[k]; }
+    for (int k = 0; k < 3; k++) {
+      topLeft[k] = c.top_left[k]; topRight[k] = c.top_right[k]; bottomLeft[k] = c.bottom_left[k];
+      right[k] = c.right[k]; up[k] = c.up[k]; ahead[k] = c.ahead[k];
+    }
   }
   prt_camera Plane() const {
     prt_camera c{};
     for (int k = 0; k < 3; k++) {
       c.pos[k] = camPos[k]; c.top_left[k] = topLeft[k]; c.top_right[k] = topRight[k]; c.bottom_left[k] = bottomLeft[k];
+      c.right[k] = right[k]; c.up[k] = up[k]; c.ahead[k] = ahead[k];
     }
     return c;
+  }
+  prt_postfx PostFx(bool enabled) const {
+    prt_postfx p{};
+    p.enabled = enabled ? 1 : 0;
+    p.aberration = abberationIntensity;
+    p.fov = fov; p.distortion = distortion;
+    p.vignette_intensity = vignetteIntensity; p.vignette_radius = vignetteRadius;
+    for (int k = 0; k < 4; k++) p.color_grading[k] = colorGrading[k];
+    return p;
   }
 };
 
@@ -137,6 +155,7 @@ class Renderer {
   int bounces = 2;
   RENDER_STATES renderingMode = RENDER_STATES::BRDF;
   bool LIGHTED = true, GAMMACORRECTED = true, NORMALMAPPED = true, SKYBOX = true, AA = true, isStochastic = true;
+  bool isPostProcessed = false;
 
   Scene scene;
   Camera camera;
@@ -175,6 +194,8 @@ class Renderer {
     p.render_mode = (int32_t)renderingMode;
     p.frame_index = frame_;
     p.seed = 0;
+    const prt_postfx pf = camera.PostFx(isPostProcessed);
+    check(prt_set_postfx(ctx_, &pf));
     check(prt_render(ctx_, &p, accumulator.data(), screen.data(), 0u, &stats_));
     frame_ += (uint32_t)frames;
   }

@@ -63,6 +63,8 @@ def lib():
         L.orc_build.argtypes = [C.c_void_p]
         L.orc_set_backend.argtypes = [C.c_void_p, C.c_void_p]
         L.orc_camera_lookat.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_camera_basis.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_set_postfx.argtypes = [C.c_void_p, C.c_int32, C.c_int32] + [C.c_float] * 4 + [C.c_void_p] * 2
         L.orc_render.argtypes = [C.c_void_p, C.POINTER(Params), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_int32, C.POINTER(Stats)]
         L.orc_render_frames.argtypes = [C.c_void_p, C.POINTER(Params), C.c_void_p, C.c_void_p, C.c_int32,
@@ -160,6 +162,16 @@ class OracleScene:
         pos, tl, tr, bl = self.camera_basis(width, height)
         self.L.orc_set_camera(self.h, pos.ctypes.data, tl.ctypes.data, tr.ctypes.data, bl.ctypes.data)
         self.width, self.height = width, height
+
+    def set_postfx(self, enabled=True, aberration=0, fov=40.0, distortion=40.0, vignette_intensity=20.0,
+                   vignette_radius=0.3, color_grading=(1, 1, 1, 1)):
+        """Renderer::isPostProcessed + the Camera post-process members (defaults: Core/Camera.h:12,23,27)."""
+        basis = np.zeros(9, np.float32)
+        pos, tgt = f32(self.sd.cam_pos), f32(self.sd.cam_target)
+        self.L.orc_camera_basis(pos.ctypes.data, tgt.ctypes.data, basis.ctypes.data)
+        g = f32(color_grading)
+        self.L.orc_set_postfx(self.h, int(enabled), int(aberration), fov, distortion, vignette_intensity,
+                              vignette_radius, g.ctypes.data, basis.ctypes.data)
 
     def use_reference_traversal(self):
         """Route closest/any-hit through the reference's tinybvh BVH8_CPU + TLAS (oracle/_ref)."""

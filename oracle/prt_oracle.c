@@ -170,6 +170,9 @@ struct orc_scene {
     float ppos[12], pcol[12], dpos[3], dcol[3], spos[3], scol[3], srot[3];
     float* sky; int32_t skyw, skyh;
     float cam[12];
+    /* post-processing (Renderer::isPostProcessed + Camera members, Core/Camera.h:11-31) */
+    int32_t post_on, post_aberration;
+    float post_fov, post_distortion, post_vig_int, post_vig_rad, post_grade[4], basis[9];
     orc_backend backend; int has_backend;
     int built;
 };
@@ -233,6 +236,12 @@ void orc_set_sky(orc_scene* s, int32_t w, int32_t h, const float* rgb) {
 void orc_set_camera(orc_scene* s, const float* p, const float* tl, const float* tr, const float* bl) {
     memcpy(s->cam, p, 12); memcpy(s->cam + 3, tl, 12); memcpy(s->cam + 6, tr, 12); memcpy(s->cam + 9, bl, 12);
 }
+void orc_set_postfx(orc_scene* s, int32_t enabled, int32_t aberration, float fov, float distortion, float vig_int,
+                    float vig_rad, const float* grade4, const float* basis9) {
+    s->post_on = enabled; s->post_aberration = aberration;
+    s->post_fov = fov; s->post_distortion = distortion; s->post_vig_int = vig_int; s->post_vig_rad = vig_rad;
+    memcpy(s->post_grade, grade4, 16); memcpy(s->basis, basis9, 36);
+}
 void orc_set_backend(orc_scene* s, const orc_backend* b) {
     if (b) { s->backend = *b; s->has_backend = 1; } else s->has_backend = 0;
 }
@@ -250,6 +259,16 @@ void orc_camera_lookat(const float* p3, const float* t3, float aspect, float* tl
     tl[0] = TL.x; tl[1] = TL.y; tl[2] = TL.z;
     tr[0] = TR.x; tr[1] = TR.y; tr[2] = TR.z;
     bl[0] = BL.x; bl[1] = BL.y; bl[2] = BL.z;
+}
+/* the same basis as right | up | ahead (Core/Camera.h:17) */
+void orc_camera_basis(const float* p3, const float* t3, float* basis9) {
+    f3 camPos = v3(p3[0], p3[1], p3[2]), camTarget = v3(t3[0], t3[1], t3[2]);
+    f3 ahead = norm_t8(sub3(camTarget, camPos));
+    f3 right = norm_t8(cross3(ahead, v3(0, 1, 0)));
+    f3 up = norm_t8(cross3(right, ahead));
+    basis9[0] = right.x; basis9[1] = right.y; basis9[2] = right.z;
+    basis9[3] = up.x; basis9[4] = up.y; basis9[5] = up.z;
+    basis9[6] = ahead.x; basis9[7] = ahead.y; basis9[8] = ahead.z;
 }
 
 /* ------------------------------------------------------------------ built-in BVH (binary, binned SAH)
@@ -882,13 +901,47 @@ static f3 trace(const orc_scene* s, const orc_params* P, ray_t r, uint32_t* seed
     return L;
 }
 
-/* Camera::GetPrimaryRay, Core/Camera.cpp:113-139 (non-Panini branch) */
+/* Camera::Panini, Core/Camera.cpp:81-110 (std::max -> smax; cos / sin in double rounded once) */
+static float panini_b(float fov, float distortion) {
+    const float fo = PI_F / 2 - fov * 0.5f;
+    const float f = cr_cos(fo) / cr_sin(fo) * 2.0f;
+    const float f2 = f * f;
+    const float d2 = distortion * distortion;
+    return (sqrtf(smax(0.0f, (distortion + d2) * (distortion + d2) * (f2 + f2 * f2))) - (distortion * f + f)) /
+           (d2 + d2 * f2 - 1.0f);
+}
+static f3 panini(float ndcx, float ndcy, float b, float distortion) {
+    ndcx *= b; ndcy *= b;
+    const float h = ndcx, v = ndcy;
+    const float h2 = h * h;
+    const float k = h2 / ((distortion + 1.0f) * (distortion + 1.0f));
+    const float k2 = k * k;
+    const float d2 = distortion * distortion;
+    const float discr = smax(0.0f, k2 * d2 - (k + 1.0f) * (k * d2 - 1.0f));
+    const float cosPhi = (-k * distortion + sqrtf(discr)) / (k + 1.0f);
+    const float S = (distortion + 1.0f) / (distortion + cosPhi);
+    const float tanTheta = v / S;
+    float sinPhi = sqrtf(smax(0.0f, 1.0f - cosPhi * cosPhi));
+    if (ndcx < 0.0f) sinPhi *= -1.0f;
+    const float sc = 1.0f / sqrtf(1.0f + tanTheta * tanTheta);
+    return muls(v3(sinPhi, tanTheta, cosPhi), sc);
+}
+
+/* Camera::GetPrimaryRay, Core/Camera.cpp:113-139 (Panini branch when post-processing is on) */
 static ray_t primary_ray(const orc_scene* s, float x, float y, int W, int H) {
     const float u = x * (1.0f / (float)W);
     const float v = y * (1.0f / (float)H);
     f3 camPos = v3(s->cam[0], s->cam[1], s->cam[2]);
     f3 TL = v3(s->cam[3], s->cam[4], s->cam[5]), TR = v3(s->cam[6], s->cam[7], s->cam[8]), BL = v3(s->cam[9], s->cam[10], s->cam[11]);
     f3 P = add3(add3(TL, smul(u, sub3(TR, TL))), smul(v, sub3(BL, TL)));
+    if (s->post_on) {
+        const f3 pd = panini((2.0f * u) - 1.0f, 1.0f - (2.0f * v), panini_b(s->post_fov, s->post_distortion),
+                             s->post_distortion);
+        const f3 c = muls(pd, length3(sub3(P, camPos)));
+        const f3 right = v3(s->basis[0], s->basis[1], s->basis[2]), up = v3(s->basis[3], s->basis[4], s->basis[5]),
+                 ahead = v3(s->basis[6], s->basis[7], s->basis[8]);
+        return make_ray(camPos, norm_t8(add3(add3(muls(right, c.x), muls(up, c.y)), muls(ahead, c.z))));
+    }
     f3 dir = norm_t8(sub3(P, camPos));
     return make_ray(camPos, dir);
 }
@@ -953,42 +1006,67 @@ static inline uint32_t pack1(float x) {
 }
 uint32_t orc_pack_rgb8(const float* v) { return (pack1(v[0]) << 16) + (pack1(v[1]) << 8) + pack1(v[2]); }
 
-/* Core/Renderer.cpp:81-104,137 */
+/* Core/Renderer.cpp:81-104,107-137,147, frame after frame: the distance-keyed progressive mean, the
+ * end-of-frame accumulator memset when !accumulates, and -- with post-processing -- the screen pass of
+ * the last frame walked as the reference walks it: each row left to right, so the chromatic aberration
+ * reads this frame's accumulator left of x and the previous one right of x. */
+static inline int clampi(int x, int a, int b) { return x < a ? a : (x > b ? b : x); }
 int orc_render(orc_scene* s, const orc_params* P, float* acc, int32_t* nsamp, float* dist, float* avg, uint32_t* rgb8,
                int32_t nthreads, orc_stats* st) {
     const int W = P->width, H = P->height, F = nframes_of(P);
     size_t np = (size_t)W * H;
     float* fr = (float*)malloc(sizeof(float) * 4 * np * (F ? F : 1));
     float* tp = (float*)malloc(sizeof(float) * np * (F ? F : 1));
+    float* av = (float*)calloc(4 * np, sizeof(float));
     int rc = orc_render_frames(s, P, fr, tp, nthreads, st);
-    if (rc) { free(fr); free(tp); return rc; }
-    for (size_t p = 0; p < np; p++) {
-        float a[4] = {0, 0, 0, 0};
-        for (int f = 0; f < F; f++) {
-            const float* v = fr + 4 * ((size_t)f * np + p);
-            float t1 = tp[(size_t)f * np + p];
-            float* A = acc + 4 * p;
-            if (P->flags & ORC_ACCUMULATE) {
-                if (fabsf(dist[p] - t1) < EPSILON) {
-                    nsamp[p]++;
-                    A[0] += v[0]; A[1] += v[1]; A[2] += v[2];
-                    float inv = 1.f / (float)nsamp[p];
-                    a[0] = A[0] * inv; a[1] = A[1] * inv; a[2] = A[2] * inv; a[3] = A[3] * inv;
+    if (rc) { free(fr); free(tp); free(av); return rc; }
+    for (int f = 0; f < F; f++) {
+        const int last = f == F - 1;
+        for (int y = 0; y < H; y++) {
+            for (int x = 0; x < W; x++) {
+                const size_t p = (size_t)y * W + x;
+                const float* v = fr + 4 * ((size_t)f * np + p);
+                float t1 = tp[(size_t)f * np + p];
+                float* A = acc + 4 * p;
+                float* a = av + 4 * p;
+                if (P->flags & ORC_ACCUMULATE) {
+                    if (fabsf(dist[p] - t1) < EPSILON) {
+                        nsamp[p]++;
+                        A[0] += v[0]; A[1] += v[1]; A[2] += v[2];
+                        float inv = 1.f / (float)nsamp[p];
+                        a[0] = A[0] * inv; a[1] = A[1] * inv; a[2] = A[2] * inv; a[3] = A[3] * inv;
+                    } else {
+                        nsamp[p] = 1;
+                        A[0] = v[0]; A[1] = v[1]; A[2] = v[2]; A[3] = 0.0f;
+                        a[0] = A[0]; a[1] = A[1]; a[2] = A[2]; a[3] = A[3];
+                    }
+                    dist[p] = t1;
                 } else {
-                    nsamp[p] = 1;
                     A[0] = v[0]; A[1] = v[1]; A[2] = v[2]; A[3] = 0.0f;
                     a[0] = A[0]; a[1] = A[1]; a[2] = A[2]; a[3] = A[3];
                 }
-                dist[p] = t1;
-            } else {
-                A[0] = v[0]; A[1] = v[1]; A[2] = v[2]; A[3] = 0.0f;
-                a[0] = A[0]; a[1] = A[1]; a[2] = A[2]; a[3] = A[3];
+                if (!last) continue;
+                if (!(s->post_on)) { if (rgb8) rgb8[p] = orc_pack_rgb8(a); continue; }
+                float c[4] = {a[0], a[1], a[2], a[3]};
+                if (s->post_aberration != 0) {                                    /* :111-120 */
+                    const int xr = clampi(x + s->post_aberration, 0, W - 1), xb = clampi(x - s->post_aberration, 0, W - 1);
+                    const float inv = 1.f / (float)nsamp[p];
+                    const float* R = acc + 4 * ((size_t)y * W + xr);
+                    const float* B = acc + 4 * ((size_t)y * W + xb);
+                    c[0] = 0.75f * a[0] + 0.25f * (R[0] * inv);
+                    c[2] = 0.75f * a[2] + 0.25f * (B[2] * inv);
+                }
+                float ux = (float)x / (float)W, uy = (float)y / (float)H;  /* :121-125 */
+                ux *= 1.0f - ux; uy *= 1.0f - uy;
+                const float vig = cr_pow(ux * uy * s->post_vig_int, s->post_vig_rad);
+                for (int k = 0; k < 4; k++) c[k] = (c[k] * s->post_grade[k]) * vig;   /* :128-130 */
+                if (rgb8) rgb8[p] = orc_pack_rgb8(c);
             }
         }
-        if (avg) { avg[4 * p] = a[0]; avg[4 * p + 1] = a[1]; avg[4 * p + 2] = a[2]; avg[4 * p + 3] = a[3]; }
-        if (rgb8) rgb8[p] = orc_pack_rgb8(a);
+        if (!(P->flags & ORC_ACCUMULATE)) memset(acc, 0, sizeof(float) * 4 * np);  /* :147 */
     }
-    free(fr); free(tp);
+    if (avg) memcpy(avg, av, sizeof(float) * 4 * np);
+    free(fr); free(tp); free(av);
     return 0;
 }
 

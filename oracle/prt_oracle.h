@@ -48,6 +48,12 @@ enum { ORC_MODE_BRDF = 0, ORC_MODE_BASECOLOR, ORC_MODE_GEOMETRYNORMAL, ORC_MODE_
 
 typedef struct orc_scene orc_scene;
 
+/* post-processing: Renderer::isPostProcessed + Camera::{abberationIntensity, fov, distortion,
+ * vignetteIntensity, vignetteRadius, colorGrading} and the camera basis right|up|ahead (9 floats) */
+void orc_set_postfx(orc_scene* s, int32_t enabled, int32_t aberration, float fov, float distortion, float vig_int,
+                    float vig_rad, const float* grade4, const float* basis9);
+void orc_camera_basis(const float* pos3, const float* target3, float* basis9);
+
 typedef struct {
     int32_t width, height;
     int32_t spp;          /* camera paths per pixel in this call (AA: 2 per reference frame) */

@@ -121,6 +121,8 @@ struct prt_ctx {
   bool have_lights = false;
   prt_camera cam{};
   bool have_camera = false;
+  prt_postfx pfx{};  // post-processing off until prt_set_postfx
+  DevBuf accprev;    // accumulator before the last frame of a call (screen-pass aberration)
   // accumulation state (Core/Renderer.h:61-63) and scratch
   DevBuf acc, nsamp, dist;
   int32_t accW = 0, accH = 0;
@@ -242,7 +244,24 @@ int scene_ready(prt_ctx* c, SceneDev& S) {
   std::memcpy(S.cam + 3, c->cam.top_left, 12);
   std::memcpy(S.cam + 6, c->cam.top_right, 12);
   std::memcpy(S.cam + 9, c->cam.bottom_left, 12);
+  std::memcpy(S.basis, c->cam.right, 12);
+  std::memcpy(S.basis + 3, c->cam.up, 12);
+  std::memcpy(S.basis + 6, c->cam.ahead, 12);
+  S.panini = c->pfx.enabled ? 1 : 0;
+  S.pan_d = c->pfx.distortion;
+  S.pan_b = panini_scale(c->pfx.fov, c->pfx.distortion);
   return PRT_OK;
+}
+
+PostDev post_params(const prt_ctx* c, int32_t W, int32_t H) {
+  PostDev P{};
+  for (int k = 0; k < 4; k++) P.grade[k] = c->pfx.color_grading[k];
+  P.vig_int = c->pfx.vignette_intensity;
+  P.vig_rad = c->pfx.vignette_radius;
+  P.aberration = c->pfx.aberration;
+  P.W = W;
+  P.H = H;
+  return P;
 }
 
 int check_params(const prt_render_params* p) {
@@ -452,8 +471,23 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     else HIP_TRY(launch_wavefront(L, S, A, M, c->wb, c->frames.as<float4>(), stats ? &c->wt : nullptr));
   }
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  // post-processing (single-GPU image): the screen pass needs the average and, for the aberration, the
+  // accumulator before the last frame
+  const bool post = c->pfx.enabled && !tiles_dev && rgb8_dev && F > 0;
+  float4* acc_prev = nullptr;
+  if (post) {
+    const size_t np = (size_t)p->width * p->height;
+    if (!avg_dev) { HIP_TRY(c->avg.ensure(np * 16)); avg_dev = c->avg.as<float4>(); }
+    if (c->pfx.aberration != 0) { HIP_TRY(c->accprev.ensure(np * 16)); acc_prev = c->accprev.as<float4>(); }
+  }
   HIP_TRY(launch_accumulate(L, M, F, p->flags, c->frames.as<float4>(), c->acc.as<float4>(), c->nsamp.as<int32_t>(),
-                            c->dist.as<float>(), avg_dev, rgb8_dev, tiles_dev));
+                            c->dist.as<float>(), avg_dev, post ? nullptr : rgb8_dev, tiles_dev, acc_prev));
+  if (post) {
+    // with !accumulates the accumulator held this frame's value until the end-of-frame memset
+    const float4* acc_new = (p->flags & PRT_FLAG_ACCUMULATE) ? c->acc.as<float4>() : avg_dev;
+    HIP_TRY(launch_postfx(L, post_params(c, p->width, p->height), acc_new, acc_prev, c->nsamp.as<int32_t>(), avg_dev,
+                          rgb8_dev));
+  }
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   if (stats) {
     std::memset(stats, 0, sizeof(*stats));
@@ -593,6 +627,7 @@ int prt_destroy(prt_ctx* c) {
   c->wave.release();
   c->sq.release();
   c->sctl.release();
+  c->accprev.release();
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return PRT_OK;
@@ -796,6 +831,29 @@ int prt_camera_look_at(const float pos[3], const float target[3], float aspect, 
   o->top_left[0] = TL.x; o->top_left[1] = TL.y; o->top_left[2] = TL.z;
   o->top_right[0] = TR.x; o->top_right[1] = TR.y; o->top_right[2] = TR.z;
   o->bottom_left[0] = BL.x; o->bottom_left[1] = BL.y; o->bottom_left[2] = BL.z;
+  o->right[0] = right.x; o->right[1] = right.y; o->right[2] = right.z;
+  o->up[0] = up.x; o->up[1] = up.y; o->up[2] = up.z;
+  o->ahead[0] = ahead.x; o->ahead[1] = ahead.y; o->ahead[2] = ahead.z;
+  return PRT_OK;
+}
+
+int prt_postfx_preset(int32_t preset, prt_postfx* o) {
+  if (!o || preset < 0 || preset > 1) return fail(PRT_ERR_INVALID_ARGUMENT, "bad post-process preset");
+  std::memset(o, 0, sizeof(*o));
+  o->enabled = 1;
+  if (preset == 0) {  // Camera member defaults (Core/Camera.h:12,23,27): float4{1.f} is all ones
+    o->fov = 40.f; o->distortion = 40.f; o->vignette_intensity = 20.f; o->vignette_radius = 0.3f; o->aberration = 0;
+    for (int k = 0; k < 4; k++) o->color_grading[k] = 1.f;
+  } else {            // P1 (Core/Camera.cpp:18-23, Camera.h:11,20,28); vignetteRadius = vignetteRadius keeps 0.3
+    o->fov = 90.f; o->distortion = 2.f; o->vignette_intensity = 5.5f; o->vignette_radius = 0.3f; o->aberration = -1;
+    o->color_grading[0] = 1.f; o->color_grading[1] = 1.f; o->color_grading[2] = 1.2f; o->color_grading[3] = 0.f;
+  }
+  return PRT_OK;
+}
+
+int prt_set_postfx(prt_ctx* c, const prt_postfx* pfx) {
+  if (!c || !pfx) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/postfx is NULL");
+  c->pfx = *pfx;
   return PRT_OK;
 }
 
@@ -887,9 +945,12 @@ int prt_untile(prt_ctx* c, const float* gathered, int32_t W, int32_t H, int32_t 
   int rc = prt_tile_buffer_pixels(W, H, ts, world, &per);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
+  if (c->pfx.enabled && c->pfx.aberration != 0 && rgb8_dev)
+    return fail(PRT_ERR_UNSUPPORTED, "chromatic aberration needs the accumulators of neighbouring tiles");
   LaunchCfg L{c->stream, c->layout, trav_from_env(), occ_for(c)};
+  const PostDev P = post_params(c, W, H);
   HIP_TRY(launch_untile(L, W, H, ts, world, (uint32_t)per, reinterpret_cast<const float4*>(gathered),
-                        reinterpret_cast<float4*>(avg_dev), rgb8_dev));
+                        reinterpret_cast<float4*>(avg_dev), rgb8_dev, c->pfx.enabled ? &P : nullptr));
   return PRT_OK;
 }
 

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "prt_kernels.h"
+#include "prt_post.h"
 #include "prt_traverse8.h"
 
 namespace prt {
@@ -89,10 +90,15 @@ hipError_t launch_stream(const LaunchCfg& c, const SceneDev& S, const TraceArgs&
 hipError_t launch_xcc_census(hipStream_t s, uint32_t* dev_mask);
 hipError_t launch_trace_frames(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                                float4* out, Counters* cnt);
+// acc_prev (nullable): the accumulator state before the last frame of the call (screen-pass input)
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,
-                             float4* acc, int32_t* nsamp, float* dist, float4* avg, uint32_t* rgb8, float4* tiles);
+                             float4* acc, int32_t* nsamp, float* dist, float4* avg, uint32_t* rgb8, float4* tiles,
+                             float4* acc_prev);
+// post-processed RGB8 of the whole image (Core/Renderer.cpp:107-133)
+hipError_t launch_postfx(const LaunchCfg& c, const PostDev& P, const float4* acc_new, const float4* acc_old,
+                         const int32_t* nsamp, const float4* avg, uint32_t* rgb8);
 hipError_t launch_untile(const LaunchCfg& c, int32_t W, int32_t H, int32_t ts, int32_t world, uint32_t per_rank,
-                         const float4* gathered, float4* avg, uint32_t* rgb8);
+                         const float4* gathered, float4* avg, uint32_t* rgb8, const PostDev* post);
 hipError_t launch_primary_hits(const LaunchCfg& c, const SceneDev& S, const TileMap& M, HitOut* out, Counters* cnt);
 hipError_t launch_intersect(const LaunchCfg& c, const SceneDev& S, int32_t n, const float* O, const float* D,
                             const float* tmax, HitOut* out);

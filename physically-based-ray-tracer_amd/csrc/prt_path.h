@@ -1,6 +1,7 @@
 // prt_path.h -- device pieces of Renderer::Trace shared by the megakernel and the wavefront pipeline.
 #pragma once
 #include "prt_kernels.h"
+#include "prt_post.h"
 
 namespace prt {
 
@@ -10,7 +11,8 @@ enum : uint32_t {
 };
 constexpr int kMaxBounces = 16;
 
-// Camera::GetPrimaryRay (Core/Camera.cpp:113-139, non-Panini branch)
+// Camera::GetPrimaryRay (Core/Camera.cpp:113-139): screen plane, or the Panini projection when
+// post-processing is on
 __device__ __forceinline__ Ray primary_ray(const SceneDev& S, float x, float y, int W, int H) {
   const float u = x * (1.0f / (float)W);
   const float v = y * (1.0f / (float)H);
@@ -18,6 +20,13 @@ __device__ __forceinline__ Ray primary_ray(const SceneDev& S, float x, float y, 
   const V3 TL = v3(S.cam[3], S.cam[4], S.cam[5]), TR = v3(S.cam[6], S.cam[7], S.cam[8]),
            BL = v3(S.cam[9], S.cam[10], S.cam[11]);
   const V3 P = TL + u * (TR - TL) + v * (BL - TL);
+  if (S.panini) {                                                                           // :125-134
+    const V3 pd = panini_dir((2.0f * u) - 1.0f, 1.0f - (2.0f * v), S.pan_b, S.pan_d);
+    const V3 c = pd * length(P - camPos);
+    const V3 right = v3(S.basis[0], S.basis[1], S.basis[2]), up = v3(S.basis[3], S.basis[4], S.basis[5]),
+             ahead = v3(S.basis[6], S.basis[7], S.basis[8]);
+    return make_ray(camPos, normalize(right * c.x + up * c.y + ahead * c.z));
+  }
   const V3 dir = normalize(P - camPos);
   return make_ray(camPos, dir);
 }

@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(TileMap M, int32_t frames
                                                        const float4* __restrict__ fr, float4* __restrict__ acc,
                                                        int32_t* __restrict__ nsamp, float* __restrict__ dist,
                                                        float4* __restrict__ avg_out, uint32_t* __restrict__ rgb8_out,
-                                                       float4* __restrict__ tiles_out) {
+                                                       float4* __restrict__ tiles_out, float4* __restrict__ acc_prev) {
   const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
   if (r >= M.items) return;
   int32_t x, y;
@@ -124,6 +124,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(TileMap M, int32_t frames
   for (int32_t f = 0; f < frames; f++) {
     const float4 v = fr[(size_t)f * M.items + r];
     const float t1 = v.w;
+    if (acc_prev && f == frames - 1) acc_prev[p] = A;  // what the screen pass sees right of the pixel
     if (flags & kAccumulate) {
       if (fabsf(d - t1) < kEpsilon) {
         n++;
@@ -137,8 +138,8 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(TileMap M, int32_t frames
       }
       d = t1;
     } else {
-      A = make_float4(v.x, v.y, v.z, 0.0f);
-      a = A;
+      a = make_float4(v.x, v.y, v.z, 0.0f);
+      A = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // !accumulates: memset after the frame (:147)
     }
   }
   acc[p] = A;
@@ -152,7 +153,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(TileMap M, int32_t frames
 // rank-0 untile of the gathered tile buffers (one item = one gathered element)
 __global__ void __launch_bounds__(kBlock) k_untile(int32_t W, int32_t H, int32_t ts, int32_t world, uint32_t per_rank,
                                                    const float4* __restrict__ gathered, float4* __restrict__ avg_out,
-                                                   uint32_t* __restrict__ rgb8_out) {
+                                                   uint32_t* __restrict__ rgb8_out, PostDev post, int32_t use_post) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= (uint64_t)per_rank * (uint64_t)world) return;
   const int32_t rank = (int32_t)(i / per_rank);
@@ -164,7 +165,42 @@ __global__ void __launch_bounds__(kBlock) k_untile(int32_t W, int32_t H, int32_t
   const float4 a = gathered[i];
   const uint32_t p = (uint32_t)(y * W + x);
   if (avg_out) avg_out[p] = a;
-  if (rgb8_out) rgb8_out[p] = (pack1(a.x) << 16) + (pack1(a.y) << 8) + pack1(a.z);
+  if (rgb8_out) {
+    float4 c = a;
+    if (use_post) {  // Core/Renderer.cpp:121-133 without aberration
+      const float vig = vignette(post, x, y);
+      c = make_float4(c.x * post.grade[0] * vig, c.y * post.grade[1] * vig, c.z * post.grade[2] * vig, 0.0f);
+    }
+    rgb8_out[p] = (pack1(c.x) << 16) + (pack1(c.y) << 8) + pack1(c.z);
+  }
+}
+
+// Renderer::Tick's screen pass (Core/Renderer.cpp:107-133) over the whole image: chromatic aberration from
+// the accumulator -- the reference walks each row left to right, so a neighbour left of x already holds
+// this frame's accumulator (acc_new) and one right of x the state before it (acc_old) -- divided by this
+// pixel's sample count, then colour grading and the vignette, RGBF32_to_RGB8
+__global__ void __launch_bounds__(kBlock) k_postfx(PostDev P, const float4* __restrict__ acc_new,
+                                                   const float4* __restrict__ acc_old, const int32_t* __restrict__ nsamp,
+                                                   const float4* __restrict__ avg, uint32_t* __restrict__ rgb8_out) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= (uint32_t)P.W * (uint32_t)P.H) return;
+  const int32_t x = (int32_t)(p % (uint32_t)P.W), y = (int32_t)(p / (uint32_t)P.W);
+  const float4 a = avg[p];
+  float4 c = a;
+  if (P.aberration != 0) {
+    const int32_t xr = max(0, min(x + P.aberration, P.W - 1)), xb = max(0, min(x - P.aberration, P.W - 1));
+    const float inv = 1.f / (float)nsamp[p];
+    const uint32_t row = (uint32_t)y * (uint32_t)P.W;
+    const float4 R = xr <= x ? acc_new[row + xr] : acc_old[row + xr];
+    const float4 B = xb <= x ? acc_new[row + xb] : acc_old[row + xb];
+    const float red = 0.75f * a.x + 0.25f * (R.x * inv);
+    const float blue = 0.75f * a.z + 0.25f * (B.z * inv);
+    c = make_float4(red, a.y, blue, a.w);
+  }
+  const float vig = vignette(P, x, y);
+  c = make_float4(c.x * P.grade[0], c.y * P.grade[1], c.z * P.grade[2], c.w * P.grade[3]);
+  c = make_float4(c.x * vig, c.y * vig, c.z * vig, c.w * vig);
+  rgb8_out[p] = (pack1(c.x) << 16) + (pack1(c.y) << 8) + pack1(c.z);
 }
 
 // ---- geometry-only kernels
@@ -237,19 +273,29 @@ hipError_t launch_trace_frames(const LaunchCfg& c, const SceneDev& S, const Trac
 }
 
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,
-                             float4* acc, int32_t* nsamp, float* dist, float4* avg, uint32_t* rgb8, float4* tiles) {
+                             float4* acc, int32_t* nsamp, float* dist, float4* avg, uint32_t* rgb8, float4* tiles,
+                             float4* acc_prev) {
   if (M.items == 0) return hipSuccess;
   hipLaunchKernelGGL(k_accumulate, dim3(grid_of(M.items)), dim3(kBlock), 0, c.stream, M, frames, flags, fr, acc, nsamp,
-                     dist, avg, rgb8, tiles);
+                     dist, avg, rgb8, tiles, acc_prev);
+  return hipGetLastError();
+}
+
+hipError_t launch_postfx(const LaunchCfg& c, const PostDev& P, const float4* acc_new, const float4* acc_old,
+                         const int32_t* nsamp, const float4* avg, uint32_t* rgb8) {
+  const uint64_t n = (uint64_t)P.W * (uint64_t)P.H;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_postfx, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, P, acc_new, acc_old, nsamp, avg, rgb8);
   return hipGetLastError();
 }
 
 hipError_t launch_untile(const LaunchCfg& c, int32_t W, int32_t H, int32_t ts, int32_t world, uint32_t per_rank,
-                         const float4* gathered, float4* avg, uint32_t* rgb8) {
+                         const float4* gathered, float4* avg, uint32_t* rgb8, const PostDev* post) {
   const uint64_t n = (uint64_t)per_rank * (uint64_t)world;
   if (n == 0) return hipSuccess;
+  const PostDev none{};
   hipLaunchKernelGGL(k_untile, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, W, H, ts, world, per_rank, gathered, avg,
-                     rgb8);
+                     rgb8, post ? *post : none, post ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -69,6 +69,11 @@ struct SceneDev {
   float ppos[12], pcol[12];
   float dpos[3], dcol[3], spos[3], scol[3], srot[3];
   float cam[12];  // pos, top_left, top_right, bottom_left
+  // post-processing (Core/Camera.cpp:113-139): Panini primary rays when panini != 0
+  float basis[9];  // right, up, ahead (Core/Camera.h:17)
+  float pan_b, pan_d;
+  int32_t panini;
+  int32_t pad1;
 };
 
 }  // namespace prt

@@ -9,6 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIBPATH = os.path.join(HERE, "libprt.so")
 
 PRT_OK = 0
+ABI_VERSION = 2  # PRT_ABI_VERSION of the include/prt.h these structs mirror
 FLAG_AA, FLAG_ACCUMULATE, FLAG_GAMMA, FLAG_NORMALMAP, FLAG_SKYBOX, FLAG_LIGHTED, FLAG_STOCHASTIC = (1 << i for i in range(7))
 FLAGS_DEFAULT = 0x7F
 OUT_DEVICE = 1
@@ -20,7 +21,7 @@ MODE_BRDF, MODE_BASECOLOR, MODE_GEOMETRYNORMAL, MODE_SHADINGNORMAL, MODE_METAL, 
 EXPORTS = [
     "prt_abi_version", "prt_last_error", "prt_device_count", "prt_create", "prt_destroy", "prt_set_stream",
     "prt_set_textures", "prt_set_meshes", "prt_set_instances", "prt_set_lights", "prt_set_sky", "prt_set_camera",
-    "prt_camera_look_at", "prt_render", "prt_reset_accumulation", "prt_tile_buffer_pixels", "prt_tile_pixel_map",
+    "prt_camera_look_at", "prt_postfx_preset", "prt_set_postfx", "prt_render", "prt_reset_accumulation", "prt_tile_buffer_pixels", "prt_tile_pixel_map",
     "prt_render_tiles",
     "prt_untile", "prt_trace_primary", "prt_intersect", "prt_occluded", "prt_get_scene_info",
 ]
@@ -53,7 +54,14 @@ class Lights(C.Structure):
 
 class CameraDesc(C.Structure):
     _fields_ = [("pos", C.c_float * 3), ("top_left", C.c_float * 3), ("top_right", C.c_float * 3),
-                ("bottom_left", C.c_float * 3)]
+                ("bottom_left", C.c_float * 3), ("right", C.c_float * 3), ("up", C.c_float * 3),
+                ("ahead", C.c_float * 3)]
+
+
+class PostFx(C.Structure):
+    """prt_postfx: Renderer::isPostProcessed + the Camera post-process members (Core/Camera.h:11-31)."""
+    _fields_ = [("enabled", C.c_int32), ("aberration", C.c_int32), ("fov", C.c_float), ("distortion", C.c_float),
+                ("vignette_intensity", C.c_float), ("vignette_radius", C.c_float), ("color_grading", C.c_float * 4)]
 
 
 class RenderParams(C.Structure):
@@ -108,6 +116,8 @@ def load():
         "prt_set_sky": ([vp, vp, i32, i32], C.c_int),
         "prt_set_camera": ([vp, C.POINTER(CameraDesc)], C.c_int),
         "prt_camera_look_at": ([vp, vp, C.c_float, C.POINTER(CameraDesc)], C.c_int),
+        "prt_postfx_preset": ([i32, C.POINTER(PostFx)], C.c_int),
+        "prt_set_postfx": ([vp, C.POINTER(PostFx)], C.c_int),
         "prt_render": ([vp, C.POINTER(RenderParams), vp, vp, u32, C.POINTER(Stats)], C.c_int),
         "prt_reset_accumulation": ([vp, i32], C.c_int),
         "prt_tile_buffer_pixels": ([i32, i32, i32, i32, C.POINTER(C.c_int64)], C.c_int),
@@ -123,6 +133,8 @@ def load():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
+    if L.prt_abi_version() != ABI_VERSION:
+        raise PrtError(f"{LIBPATH}: ABI {L.prt_abi_version()} != {ABI_VERSION} (stale build: rerun __graft_entry__.build())")
     _lib = L
     return L
 

@@ -37,7 +37,21 @@ class Camera:
         self.camPos = _f32(camPos)
         self.camTarget = _f32(camTarget)
         self.aspect = np.float32(aspect)
+        # post-process members (Core/Camera.h:12,23,27), read when Renderer.isPostProcessed is set
+        self.colorGrading = np.ones(4, F32)
+        self.fov, self.distortion, self.vignetteIntensity, self.vignetteRadius = 40.0, 40.0, 20.0, 0.3
+        self.abberationIntensity = 0
         self.update()
+
+    def postfx(self, enabled=True):
+        pf = _lib.PostFx()
+        pf.enabled = 1 if enabled else 0
+        pf.aberration = int(self.abberationIntensity)
+        pf.fov, pf.distortion = float(self.fov), float(self.distortion)
+        pf.vignette_intensity, pf.vignette_radius = float(self.vignetteIntensity), float(self.vignetteRadius)
+        for i in range(4):
+            pf.color_grading[i] = float(self.colorGrading[i])
+        return pf
 
     def update(self):
         L = _lib.load()
@@ -48,6 +62,23 @@ class Camera:
         self.topLeft = np.array(cd.top_left[:], F32)
         self.topRight = np.array(cd.top_right[:], F32)
         self.bottomLeft = np.array(cd.bottom_left[:], F32)
+        self.right = np.array(cd.right[:], F32)
+        self.up = np.array(cd.up[:], F32)
+        self.ahead = np.array(cd.ahead[:], F32)
+
+
+def postfx_preset(preset=0, **overrides):
+    """prt_postfx with Renderer::isPostProcessed on: preset 0 = the Camera member defaults, 1 = the GAME
+    preset P1 (Core/Camera.cpp:18-23); keyword overrides set single fields (color_grading: 4 floats)."""
+    pf = _lib.PostFx()
+    check(_lib.load().prt_postfx_preset(preset, C.byref(pf)))
+    for k, v in overrides.items():
+        if k == "color_grading":
+            for i in range(4):
+                pf.color_grading[i] = float(v[i])
+        else:
+            setattr(pf, k, v)
+    return pf
 
 
 class Scene:
@@ -147,6 +178,12 @@ class Context:
     def set_camera(self, cam: Camera):
         check(self.L.prt_set_camera(self.h, C.byref(cam.desc)))
 
+    def set_postfx(self, pf=None):
+        """Post-processing on (a prt_postfx, see postfx_preset) or off (None)."""
+        if pf is None:
+            pf = _lib.PostFx()
+        check(self.L.prt_set_postfx(self.h, C.byref(pf)))
+
     def scene_info(self):
         si = _lib.SceneInfo()
         check(self.L.prt_get_scene_info(self.h, C.byref(si)))
@@ -226,6 +263,7 @@ class Renderer:
         self.bounces = 2
         self.renderingMode = 0
         self.LIGHTED = self.GAMMACORRECTED = self.NORMALMAPPED = self.SKYBOX = self.AA = self.isStochastic = True
+        self.isPostProcessed = False
         self.width, self.height = width, height
         self.scene, self.camera = scene, camera
         self.ctx = Context(device)
@@ -252,6 +290,7 @@ class Renderer:
 
     def Tick(self, deltaTime: float = 0.0, frames: int = 1):
         spp = frames * (2 if self.AA else 1)
+        self.ctx.set_postfx(self.camera.postfx(self.isPostProcessed))
         _, _, st = self.ctx.render(self.width, self.height, spp, self.bounces, self.flags(), self.renderingMode,
                                    self.frame, self.seed, avg=self.average, rgb8=self.screen)
         self.frame += frames

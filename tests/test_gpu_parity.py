@@ -178,20 +178,25 @@ def test_progressive_accumulation(gpu_ctx):
     assert np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)) > 0.999
 
 
-def test_tiles_match_full_frame(gpu_ctx):
+@pytest.mark.parametrize("post", [False, True])
+def test_tiles_match_full_frame(gpu_ctx, post):
     """Pixel-tile sharding (config C4's decomposition) on one GPU: world ranks rendered by separate
-    contexts, gathered and untiled, equal the single-context image bit for bit."""
+    contexts, gathered and untiled, equal the single-context image bit for bit (also with post-processing
+    without aberration: Panini rays per rank, vignette / grading in the untile)."""
     import torch
     import prt
     sd = scenes.config_small(60, 40)
     W, H, ts, world = 100, 70, 32, 3
+    pf = prt.postfx_preset(0, color_grading=(1.0, 0.9, 1.2, 1.0)) if post else None
     gpu_scene(gpu_ctx, sd, W, H)
+    gpu_ctx.set_postfx(pf)
     a_full, r_full, _ = gpu_ctx.render(W, H, 4, 3)
     per = gpu_ctx.tile_buffer_pixels(W, H, ts, world)
     gathered = torch.zeros((world, per, 4), dtype=torch.float32, device="cuda")
     for r in range(world):
         c = prt.Context(0)
         gpu_scene(c, sd, W, H)
+        c.set_postfx(pf)
         c.render_tiles(W, H, 4, 3, ts, r, world, gathered[r].data_ptr())
         torch.cuda.synchronize()
         c.close()
@@ -199,6 +204,7 @@ def test_tiles_match_full_frame(gpu_ctx):
     rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     gpu_ctx.untile(gathered.data_ptr(), W, H, ts, world, avg.data_ptr(), rgb.data_ptr())
     torch.cuda.synchronize()
+    gpu_ctx.set_postfx(None)
     assert np.array_equal(avg.cpu().numpy(), a_full)
     assert np.array_equal(rgb.cpu().numpy().view(np.uint32), r_full)
 
@@ -217,3 +223,33 @@ def test_determinism_c4_full_size(gpu_ctx):
     assert W * H * 4 <= s1.segments <= W * H * 4 * 4
     assert s1.shadow_rays <= 4 * s1.segments
     assert np.isfinite(a1).all()
+
+
+@pytest.mark.parametrize("preset,over,flags", [
+    (0, {}, oracle.DEFAULT_FLAGS),
+    (1, {}, oracle.DEFAULT_FLAGS),                                   # GAME preset P1: aberration -1, Panini d=2
+    (1, {"aberration": 2}, oracle.DEFAULT_FLAGS & ~oracle.ACCUMULATE),
+])
+def test_postfx_matches_oracle(gpu_ctx, preset, over, flags):
+    """Post-processing (Core/Camera.cpp:81-139, Core/Renderer.cpp:107-133): Panini primary rays and the
+    screen pass, over two accumulating calls (the aberration reads the accumulator before the last frame)."""
+    import prt
+    sd = scenes.multi_instance(scenes.config_small(50, 40))
+    W, H = 96, 64
+    gpu_scene(gpu_ctx, sd, W, H)
+    pf = prt.postfx_preset(preset, **over)
+    gpu_ctx.set_postfx(pf)
+    osc = oracle.OracleScene(sd, W, H)
+    osc.set_postfx(True, aberration=pf.aberration, fov=pf.fov, distortion=pf.distortion,
+                   vignette_intensity=pf.vignette_intensity, vignette_radius=pf.vignette_radius,
+                   color_grading=tuple(pf.color_grading))
+    try:
+        state = oracle.new_state(W, H)
+        for call in range(2):
+            a_o, r_o, state, _ = osc.render(W, H, spp=4, bounces=3, flags=flags, frame_index=2 * call, state=state)
+            a_g, r_g, _ = gpu_ctx.render(W, H, 4, 3, flags, frame_index=2 * call)
+            assert rmse(a_o, a_g) <= RMSE_TOL
+            assert np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)) >= 0.999
+            assert np.mean(r_o == r_g) >= 0.999
+    finally:
+        gpu_ctx.set_postfx(None)
