@@ -15,6 +15,10 @@ extern "C" {
  * bytes, out = height x width*bpp.  Returns 0, -1 on bad arguments / short input, -2 on a bad filter. */
 int prt_png_unfilter(const uint8_t* raw, int64_t raw_len, int32_t width, int32_t height, int32_t bpp, uint8_t* out);
 
+/* Renderer::Capture (Core/Renderer.cpp:437-465): the 0x00RRGGBB screen (width x height) as an 8-bit RGB
+ * PNG at path.  Returns 0, -1 on bad arguments, -2 on a file error, -3 on out of memory / zlib. */
+int prt_capture_png(const char* path, const uint32_t* rgb8, int32_t width, int32_t height);
+
 #ifdef __cplusplus
 }
 #endif

@@ -297,6 +297,11 @@ class Renderer:
         self.last_stats = st
         return st
 
+    def Capture(self, path):
+        """Renderer::Capture (Core/Renderer.cpp:437-465): the screen as a PNG (the reference names it by time)."""
+        from .ingest import capture_png
+        capture_png(path, self.screen, self.width, self.height)
+
     def CameraMoved(self):
         """Camera::HandleInput returned true: memset of the accumulator only (Core/Renderer.cpp:147)."""
         self.ctx.set_camera(self.camera)

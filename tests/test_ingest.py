@@ -159,3 +159,12 @@ def test_scene1_c1_ingest(oracle_mod):
     base, _, _, _ = osc.render(W, H, spp=1, bounces=1, flags=scenes.C1_FLAGS, mode=1)
     t = osc.primary_hits(W, H)[0]
     assert (t < 1e30).sum() > 1000 and np.all(base[t < 1e30, :3] > 0)
+
+
+def test_capture_png_round_trip(tmp_path):
+    """Renderer::Capture's PNG (prt_capture_png) decodes back to the screen's 0x00RRGGBB pixels."""
+    rng = np.random.default_rng(5)
+    scr = rng.integers(0, 1 << 24, (37, 53), dtype=np.uint32)
+    f = str(tmp_path / "capture.png")
+    ingest.capture_png(f, scr, 53, 37)
+    assert np.array_equal(ingest.load_png(f), scr)
