@@ -126,7 +126,7 @@ struct prt_ctx {
   // accumulation state (Core/Renderer.h:61-63) and scratch
   DevBuf acc, nsamp, dist;
   int32_t accW = 0, accH = 0;
-  DevBuf frames, avg, rgb8, counters, hits;
+  DevBuf frames, avg, rgb8, counters, hits, tl;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   // wavefront pipeline
   DevBuf wave;
@@ -448,6 +448,17 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     rc = ensure_wave(c, (uint32_t)n, p->bounces);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * kCtrWords, c->stream));
+    c->wb.tl = nullptr;
+    {
+      const char* e = std::getenv("PRT_TAIL");
+      c->wb.coop_tail = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
+    }
+    if (stats && std::getenv("PRT_DEBUG_QUEUES")) {
+      const size_t tlb = 32ull * kTlWaves * (kMaxIters + 2);
+      HIP_TRY(c->tl.ensure(tlb));
+      HIP_TRY(hipMemsetAsync(c->tl.p, 0, tlb, c->stream));
+      c->wb.tl = c->tl.as<unsigned long long>();
+    }
     if (pipe == 3) {
       // byte offsets of the sc1 buffer loads are 32-bit: R/T levels x n and the 4 x n shadow slots
       if ((uint64_t)c->wave_levels * n * 16 >= (1ull << 32) || 64ull * n >= (1ull << 32))
@@ -535,6 +546,30 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
           std::fprintf(stderr, "prt: iteration %u: %llu closest rays %.3f ms, %llu shadow rays %.3f ms\n", k,
                        (unsigned long long)qs, a, (unsigned long long)qa, b);
       }
+      if (dump && c->wb.tl && pipe == 2) {  // launch timeline: start -> queue drained -> last wave out (us)
+        std::vector<unsigned long long> t(4ull * kTlWaves * (kMaxIters + 2));
+        HIP_TRY(hipMemcpy(t.data(), c->tl.p, 8 * t.size(), hipMemcpyDeviceToHost));
+        for (uint32_t k = 0; k <= iters; k++) {
+          unsigned long long s0 = ~0ull, d0 = ~0ull;
+          std::vector<double> ex;
+          for (int w = 0; w < kTlWaves; w++) {
+            const unsigned long long* r = t.data() + 4 * ((size_t)k * kTlWaves + w);
+            if (!r[0]) continue;
+            s0 = std::min(s0, r[0]);
+            if (r[1]) d0 = std::min(d0, r[1]);
+          }
+          if (s0 == ~0ull || d0 == ~0ull) continue;
+          for (int w = 0; w < kTlWaves; w++) {
+            const unsigned long long* r = t.data() + 4 * ((size_t)k * kTlWaves + w);
+            if (r[0] && r[2]) ex.push_back(((double)r[2] - (double)d0) / 100.0);
+          }
+          std::sort(ex.begin(), ex.end());
+          auto q = [&](double p) { return ex.empty() ? 0.0 : ex[std::min(ex.size() - 1, (size_t)(p * ex.size()))]; };
+          std::fprintf(stderr, "prt: trace %u: %zu waves, queue empty after %.1f us; waves out at +%.1f / +%.1f / "
+                       "+%.1f / +%.1f us (50/90/99/100 %%)\n", k, ex.size(), (d0 - s0) / 100.0, q(0.5), q(0.9),
+                       q(0.99), ex.empty() ? 0.0 : ex.back());
+        }
+      }
       if (pipe == 2) {  // one merged trace launch per iteration plus the final shadow-only one
         float a = 0;
         HIP_TRY(hipEventElapsedTime(&a, c->wt.ev[4 * iters + 0], c->wt.ev[4 * iters + 1]));
@@ -618,7 +653,7 @@ int prt_destroy(prt_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->texels, &c->tex, &c->nodes, &c->nodes8, &c->nodes8h, &c->tris, &c->stri,
                     &c->mesh, &c->inst, &c->sky, &c->srgb, &c->acc, &c->nsamp, &c->dist, &c->frames, &c->avg, &c->rgb8,
-                    &c->counters, &c->hits})
+                    &c->counters, &c->hits, &c->tl})
     b->release();
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);
@@ -753,6 +788,9 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
       }
       stri.push_back(st);
     }
+    // ShadeTri.pad[0]: the primitive's TriMT record (the cooperative traversal tail re-tests a helper's
+    // winning triangle from its primitive id, prt_persist.h)
+    for (size_t g = tri_base; g < tris.size(); g++) stri[mh[i].prim_base + tris[g].prim].pad[0] = (uint32_t)g;
 
     for (int k = 0; k < 3; k++) { info[i].bmin[k] = bmin[k]; info[i].bmax[k] = bmax[k]; }
     info[i].depth = depth;

@@ -49,6 +49,8 @@ struct WaveBufs {
   float4* sho;      // shadow queue: O, tmax
   float4* shd;      // shadow queue: D, bits(4 * item + slot)
   uint32_t* ctr;    // [iteration][path|shadow][sub-queue] counters, kCtrStride apart
+  unsigned long long* tl;  // PRT_DEBUG_QUEUES: [launch][wave] {start, first empty fetch, exit, -}
+  int32_t coop_tail;       // cooperative traversal tail (prt_persist.h); PRT_TAIL=0 turns it off
 };
 // streaming engine (prt_stream.hip): per-XCD ray / shade queues of tagged 8-byte granules
 constexpr uint32_t kSSub = 8;        // sub-queues per XCD part and queue
@@ -71,6 +73,7 @@ constexpr size_t kStreamCtlWords = (size_t)(2 + kMaxParts) * kCtrStride;
 constexpr size_t kStreamCtrWords = (size_t)kMaxParts * 4 * kSSub * kCtrStride;
 
 constexpr int kMaxIters = 32;
+constexpr int kTlWaves = 256 * 4 * 8;  // timeline records per traversal launch (max persistent grid)
 struct WaveTimers {
   hipEvent_t ev[4 * kMaxIters];
   uint32_t iters;

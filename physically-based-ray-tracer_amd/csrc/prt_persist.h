@@ -13,12 +13,37 @@
 // so node visits and triangle tests of different lanes share iterations instead of serialising.
 // Results are those of blas_traverse8: the hit rule is order-independent (closest t, then smaller
 // (instance, prim)) and the box tests are conservative, so visiting order cannot change a hit.
+//
+// Cooperative tail (tail != nullptr).  Once the queue is drained a launch lasts as long as its slowest
+// rays: a lone wave still spends ~0.5-1 us per iteration (a wave64 node visit is ~220 VALU), and the
+// slowest rays take 100-200 iterations (scripts/trav_stats.cpp --dist), so the last waves leave
+// 100-270 us after the queue emptied (PRT_DEBUG_QUEUES timeline).  When a drained wave holds
+// <= kTailRays rays, its idle lanes become helpers: each takes a pending node group (the top of a
+// walking lane's stack, or its remaining sibling group) and walks that subtree with the ray copied from
+// the donor.  A team (owner + helpers) shares one LDS slot: helper count, best (t, prim) key, any-hit
+// flag.  When the owner's own walk and all its helpers are done it merges the team's best hit --
+// re-testing the winning triangle (ShadeTri.pad[0]) for its (u, v) -- and continues with the next
+// instance or finishes.  The hit rule makes the split exact: the result does not depend on which lane
+// visits which subtree.
 #pragma once
 #include "prt_traverse8.h"
 
 namespace prt {
 
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
+constexpr uint32_t kTailRays = 32;       // a drained wave with at most this many rays turns cooperative
+constexpr uint32_t kTailLdsWords = 96;   // per wave: kTailRays x {count | found << 16, key lo, key hi}
+
+// index of the n-th (0-based) set bit of m; n < popcount(m)
+__device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint32_t c = (uint32_t)__popcll(m & ((1ull << w) - 1ull));
+    if (n >= c) { n -= c; m >>= w; pos += (uint32_t)w; }
+  }
+  return pos;
+}
 
 // Persistent traversal of one wave (blockDim.x == 64).  MODE 0: closest hit, 1: any hit, 2: each ray says
 // (mixed queues).  Ray source and sink are callbacks:
@@ -30,11 +55,13 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 //   tick(idle, drained)                                     wave-uniform, once at the top of every iteration:
 //                                                           idle lanes, no refill coming (the streaming
 //                                                           engine publishes finished rays there)
+// tail: kTailLdsWords of LDS for the cooperative tail, or nullptr (no tail mode).
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
 template <int MODE, bool HALF, int STACK, int REFILL, class Fetch, class Load, class Reload, class Finish, class Tick>
 __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
-                                                   Load load, Reload reload, Finish finish, Tick tick) {
+                                                   Load load, Reload reload, Finish finish, Tick tick,
+                                                   uint32_t* __restrict__ tail = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   bool active = false, drained = false;
@@ -48,6 +75,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   uint32_t node = kNoNode, gbase = 0, gmask = 0, gimask = 0;
   int sp = 0;
   uint32_t lhit = 0, ltri = 0, lmeta0 = 0, lmeta1 = 0, tcur = 0, tcnt = 0;  // pending leaf triangles
+  bool found = false;  // tail: this lane improved its closest hit
   // enter the first instance >= i0 whose world box the ray hits before h.t (tiny_bvh.h:2500-2565 TLAS
   // walk as a linear loop over <= 64 instance boxes); false when there is none
   auto enter = [&](int i0, const V3& Ow, const V3& Dw) -> bool {
@@ -65,6 +93,82 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     gmask = 0;
     sp = 0;
     return true;
+  };
+  // next child of the current group, or the next stacked group, or done with this BLAS
+  auto next_node = [&]() {
+    if (!gmask && sp > 0) {
+      sp--;
+      gbase = stk[(2 * sp) * 64];
+      const uint32_t m = stk[(2 * sp + 1) * 64];
+      gmask = m & 0xFFu;
+      gimask = m >> 8;
+    }
+    if (gmask) {
+      const uint32_t bit = __builtin_ctz(gmask);
+      gmask &= gmask - 1u;
+      const uint32_t k = bit ^ oct;
+      node = gbase + __builtin_popcount(gimask & ((1u << k) - 1u));
+    } else {
+      node = kNoNode;
+    }
+  };
+  // one node visit (lanes without pending triangles)
+  auto node_step = [&]() {
+    uint4 a, b;
+    uint32_t hits;
+    if (HALF) {  // Node8H: one 128-B line
+      const uint4* np = reinterpret_cast<const uint4*>(S.nodes8h + node);
+      a = np[0];
+      b = np[1];
+      hits = node8h_hits(np, a, O, rD, h.t);
+    } else {     // Node8: 80 B
+      const uint4* np = reinterpret_cast<const uint4*>(S.nodes8 + node);
+      a = np[0];
+      b = np[1];
+      const uint4 c = np[2], d = np[3], e = np[4];
+      hits = node8_hits(a, c, d, e, O, rD, h.t);
+    }
+    const uint32_t imask = a.w >> 24;
+    lhit = hits & ~imask;
+    ltri = b.y; lmeta0 = b.z; lmeta1 = b.w;
+    const uint32_t ihit = hits & imask;
+    if (ihit) {
+      if (gmask && sp < STACK) {
+        stk[(2 * sp) * 64] = gbase;
+        stk[(2 * sp + 1) * 64] = gmask | (gimask << 8);
+        sp++;
+      }
+      gbase = b.x;
+      gmask = order_mask(ihit, oct);
+      gimask = imask;
+    }
+    next_node();
+  };
+  // one triangle test (lanes with pending leaf triangles); returns true when an any-hit query hit
+  auto tri_step = [&]() -> bool {
+    if (tcnt == 0) {
+      const uint32_t k = __builtin_ctz(lhit);
+      lhit &= lhit - 1u;
+      const uint32_t meta = ((k < 4 ? lmeta0 : lmeta1) >> (8 * (k & 3))) & 0xFFu;
+      tcur = ltri + (meta >> 3);
+      tcnt = meta & 7u;
+    }
+    float t, u, v;
+    uint32_t prim;
+    const bool hit = mt_test(S.tris + tcur, O, D, t, u, v, prim);
+    tcur++;
+    tcnt--;
+    if (MODE == 1 || (MODE == 2 && any)) {
+      if (hit && t < h.t) {  // tiny_bvh.h:6594 (h.t holds tmax)
+        node = kNoNode; lhit = 0; tcnt = 0;
+        return true;
+      }
+    } else if (hit && (t < h.t || (t == h.t && ((uint32_t)inst < h.inst ||
+                                                ((uint32_t)inst == h.inst && prim < h.prim))))) {
+      h.t = t; h.u = u; h.v = v; h.prim = prim; h.inst = (uint32_t)inst;
+      found = true;
+    }
+    return false;
   };
   while (true) {
     // ---- refill idle lanes from the queue
@@ -90,10 +194,12 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
         }
       }
     }
-    if (__ballot(active) == 0) {
+    const uint64_t act = __ballot(active);
+    if (act == 0) {
       if (drained) break;
       continue;
     }
+    if (tail && drained && __popcll(act) <= kTailRays) break;  // cooperative tail below
     // ---- BLAS done: next instance, or the ray is finished
     if (active && node == kNoNode && lhit == 0 && tcnt == 0) {
       bool more = false;
@@ -108,83 +214,139 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       }
     }
     // ---- one node visit for lanes without pending triangles
-    if (active && node != kNoNode && lhit == 0 && tcnt == 0) {
-      uint4 a, b;
-      uint32_t hits;
-      if (HALF) {  // Node8H: one 128-B line
-        const uint4* np = reinterpret_cast<const uint4*>(S.nodes8h + node);
-        a = np[0];
-        b = np[1];
-        hits = node8h_hits(np, a, O, rD, h.t);
-      } else {     // Node8: 80 B
-        const uint4* np = reinterpret_cast<const uint4*>(S.nodes8 + node);
-        a = np[0];
-        b = np[1];
-        const uint4 c = np[2], d = np[3], e = np[4];
-        hits = node8_hits(a, c, d, e, O, rD, h.t);
-      }
-      const uint32_t imask = a.w >> 24;
-      lhit = hits & ~imask;
-      ltri = b.y; lmeta0 = b.z; lmeta1 = b.w;
-      const uint32_t ihit = hits & imask;
-      if (ihit) {
-        if (gmask && sp < STACK) {
-          stk[(2 * sp) * 64] = gbase;
-          stk[(2 * sp + 1) * 64] = gmask | (gimask << 8);
-          sp++;
-        }
-        gbase = b.x;
-        gmask = order_mask(ihit, oct);
-        gimask = imask;
-      }
-      if (!gmask && sp > 0) {
-        sp--;
-        gbase = stk[(2 * sp) * 64];
-        const uint32_t m = stk[(2 * sp + 1) * 64];
-        gmask = m & 0xFFu;
-        gimask = m >> 8;
-      }
-      if (gmask) {
-        const uint32_t bit = __builtin_ctz(gmask);
-        gmask &= gmask - 1u;
-        const uint32_t k = bit ^ oct;
-        node = gbase + __builtin_popcount(gimask & ((1u << k) - 1u));
-      } else {
-        node = kNoNode;
-      }
-    }
+    if (active && node != kNoNode && lhit == 0 && tcnt == 0) node_step();
     // ---- one triangle test for lanes with pending leaf triangles
     if (active && (lhit | tcnt)) {
-      if (tcnt == 0) {
-        const uint32_t k = __builtin_ctz(lhit);
-        lhit &= lhit - 1u;
-        const uint32_t meta = ((k < 4 ? lmeta0 : lmeta1) >> (8 * (k & 3))) & 0xFFu;
-        tcur = ltri + (meta >> 3);
-        tcnt = meta & 7u;
+      if (tri_step()) {
+        finish(handle, h, true, true);
+        active = false;
       }
-      float t, u, v;
-      uint32_t prim;
-      const bool hit = mt_test(S.tris + tcur, O, D, t, u, v, prim);
-      tcur++;
-      tcnt--;
-      if (MODE == 1 || (MODE == 2 && any)) {
-        if (hit && t < h.t) {  // tiny_bvh.h:6594 (h.t holds tmax)
-          finish(handle, h, true, true);
-          active = false;
-          node = kNoNode; lhit = 0; tcnt = 0;
+    }
+  }
+  if (!tail || __ballot(active) == 0) return;
+
+  // ---------------------------------------------------------------- cooperative tail
+  // role: owner (active: holds the ray's handle) / helper (walks one subtree of an owner's ray) / free;
+  // team slot of an owner = its rank among the owners at tail entry (< kTailRays)
+  // tstate: helpers still walking (low 16 bits) | any-hit: some team lane hit (kFoundBit)
+  constexpr uint32_t kFoundBit = 1u << 16;
+  uint32_t* tstate = tail;
+  unsigned long long* tkey = reinterpret_cast<unsigned long long*>(tail + kTailRays);  // best (t, prim)
+  bool helper = false;
+  uint32_t slot = (uint32_t)__popcll(__ballot(active) & lanes_below);
+  if (active) {
+    tstate[slot] = 0u;
+    tkey[slot] = ~0ull;
+  }
+  found = false;
+  while (true) {
+    const bool member = active || helper;
+    // an any-hit team that hit stops walking
+    if (member && any && (tstate[slot] & kFoundBit)) { node = kNoNode; lhit = 0; tcnt = 0; }
+    bool busy = member && (node != kNoNode || lhit != 0 || tcnt != 0);
+    // ---- helpers done with their subtree: publish, leave the team
+    if (helper && !busy) {
+      if (!any && found) atomicMin(&tkey[slot], ((unsigned long long)__float_as_uint(h.t) << 32) | h.prim);
+      atomicSub(&tstate[slot], 1u);
+      helper = false;
+    }
+    // ---- owners whose walk and helpers are done: merge, next instance or finish
+    if (active && !busy) {
+      const uint32_t ts = tstate[slot];
+      const bool occl = any && (ts & kFoundBit);
+      if (occl || (ts & 0xFFFFu) == 0u) {
+        if (!any) {
+          const unsigned long long k = tkey[slot];
+          tkey[slot] = ~0ull;
+          const float kt = __uint_as_float((uint32_t)(k >> 32));
+          const uint32_t kp = (uint32_t)k;
+          if (k != ~0ull && (kt < h.t || (kt == h.t && ((uint32_t)inst < h.inst ||
+                                                       ((uint32_t)inst == h.inst && kp < h.prim))))) {
+            // a helper's hit wins: its (u, v) from the same triangle test on the same instance-space ray
+            const uint32_t g = S.stri[S.mesh[S.inst[inst].mesh].prim_base + kp].pad[0];
+            float t, u, v;
+            uint32_t prim;
+            (void)mt_test(S.tris + g, O, D, t, u, v, prim);
+            h.t = t; h.u = u; h.v = v; h.prim = prim; h.inst = (uint32_t)inst;
+          }
         }
-      } else if (hit && (t < h.t || (t == h.t && ((uint32_t)inst < h.inst ||
-                                                  ((uint32_t)inst == h.inst && prim < h.prim))))) {
-        h.t = t; h.u = u; h.v = v; h.prim = prim; h.inst = (uint32_t)inst;
+        bool more = false;
+        if (!occl && inst + 1 < S.ninst) {
+          V3 Ow, Dw;
+          reload(handle, any, Ow, Dw);
+          more = enter(inst + 1, Ow, Dw);
+        }
+        if (more) {
+          busy = true;  // a closest query; no helper of this team is left
+        } else {
+          finish(handle, h, any, occl);
+          active = false;
+        }
       }
+    }
+    if (__ballot(active) == 0) break;  // helpers always belong to a live owner
+    // ---- free lanes take a pending group from a walking lane: its top stack entry or its sibling group
+    const uint64_t freem = __ballot(!active && !helper);
+    const uint64_t donm = __ballot((active || helper) && busy && (sp > 0 || gmask != 0) &&
+                                   !(any && (tstate[slot] & kFoundBit)));
+    if (freem && donm) {
+      const uint32_t npair = min((uint32_t)__popcll(freem), (uint32_t)__popcll(donm));
+      uint32_t ub = 0, um = 0, ui = 0;
+      if (((donm >> lane) & 1ull) && (uint32_t)__popcll(donm & lanes_below) < npair) {
+        if (sp > 0) {
+          sp--;
+          ub = stk[(2 * sp) * 64];
+          const uint32_t m = stk[(2 * sp + 1) * 64];
+          um = m & 0xFFu;
+          ui = m >> 8;
+        } else {
+          ub = gbase; um = gmask; ui = gimask;
+          gmask = 0;
+        }
+      }
+      const uint32_t frank = (uint32_t)__popcll(freem & lanes_below);
+      const bool take = ((freem >> lane) & 1ull) && frank < npair;
+      const int src = (int)nth_set(donm, take ? frank : 0u);
+      // every lane joins the shuffles (ds_bpermute); only the takers keep the values
+      const float ox = __shfl(O.x, src), oy = __shfl(O.y, src), oz = __shfl(O.z, src);
+      const float dx = __shfl(D.x, src), dy = __shfl(D.y, src), dz = __shfl(D.z, src);
+      const float tt = __shfl(h.t, src);
+      const int sinst = __shfl(inst, src), sany = __shfl((int)any, src);
+      const uint32_t sslot = (uint32_t)__shfl((int)slot, src), shp = (uint32_t)__shfl((int)h.prim, src);
+      const uint32_t shi = (uint32_t)__shfl((int)h.inst, src);
+      const uint32_t sb = (uint32_t)__shfl((int)ub, src), sm = (uint32_t)__shfl((int)um, src);
+      const uint32_t si = (uint32_t)__shfl((int)ui, src);
+      if (take) {
+        helper = true;
+        O = v3(ox, oy, oz);
+        D = v3(dx, dy, dz);
+        rD = v3(safercp(D.x), safercp(D.y), safercp(D.z));
+        oct = (rD.x < 0.0f ? 1u : 0u) | (rD.y < 0.0f ? 2u : 0u) | (rD.z < 0.0f ? 4u : 0u);
+        inst = sinst;
+        any = MODE == 1 || (MODE == 2 && sany != 0);
+        slot = sslot;
+        h.t = tt; h.prim = shp; h.inst = shi;
+        gbase = sb; gmask = sm; gimask = si;
+        sp = 0; lhit = 0; tcnt = 0;
+        found = false;
+        next_node();
+        atomicAdd(&tstate[slot], 1u);
+        busy = true;
+      }
+    }
+    // ---- one node visit / one triangle test per walking lane, as in the main loop
+    if (busy && node != kNoNode && lhit == 0 && tcnt == 0) node_step();
+    if (busy && (lhit | tcnt)) {
+      if (tri_step()) atomicOr(&tstate[slot], kFoundBit);
     }
   }
 }
 
 template <int MODE, bool HALF, int STACK, int REFILL, class Fetch, class Load, class Reload, class Finish>
 __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
-                                                 Load load, Reload reload, Finish finish) {
-  trav8_persistent_t<MODE, HALF, STACK, REFILL>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {});
+                                                 Load load, Reload reload, Finish finish,
+                                                 uint32_t* __restrict__ tail = nullptr) {
+  trav8_persistent_t<MODE, HALF, STACK, REFILL>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {}, tail);
 }
 
 }  // namespace prt

@@ -30,7 +30,7 @@ struct alignas(16) ShadeTri {
   float uv[6];   // fixedTextureCoords[3p..3p+2]
   float p[9];    // vertices[indices[3p+k]], k = 0..2 (normal-map tangent frame, Scene.cpp:93-103)
   float fn[3];   // faceNormals[p]
-  uint32_t pad[5];
+  uint32_t pad[5];  // pad[0]: index of the primitive's TriMT record (leaf order)
 };
 static_assert(sizeof(ShadeTri) == 128, "ShadeTri must be one 128-byte line");
 

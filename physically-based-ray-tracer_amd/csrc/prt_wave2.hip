@@ -30,6 +30,7 @@ template <bool HALF, int REFILL, int STACK, int WAVES>
 __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, uint32_t iter, uint32_t iters) {
   __shared__ uint32_t lds_stack[2 * STACK * 64];
   __shared__ uint32_t prefP[kNSub + 1], prefS[kNSub + 1];
+  __shared__ uint32_t tail_lds[kTailLdsWords];
   uint8_t* vis8 = reinterpret_cast<uint8_t*>(B.vis);
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
   const uint32_t nP = iter < iters ? load_prefix(B.ctr, iter, 0, prefP) : 0u;
@@ -38,9 +39,20 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   if (blockIdx.x * 64u >= total) return;
   uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
   uint32_t part = xcc_id();
+  // timeline diagnostic (s_memrealtime, one record per wave: start, first empty fetch, exit)
+  unsigned long long* tl = B.tl ? B.tl + ((size_t)iter * kTlWaves + blockIdx.x) * 4 : nullptr;
+  bool seen_drain = false;
+  if (tl && threadIdx.x == 0) tl[0] = __builtin_amdgcn_s_memrealtime();
   trav8_persistent<2, HALF, STACK, REFILL>(
       S, lds_stack + threadIdx.x,
-      [&](uint32_t* base, uint32_t want) { return fetch_some(fctr, total, part, base, want); },
+      [&](uint32_t* base, uint32_t want) {
+        const uint32_t got = fetch_some(fctr, total, part, base, want);
+        if (tl && got == 0 && !seen_drain) {
+          seen_drain = true;
+          if (threadIdx.x == 0) tl[1] = __builtin_amdgcn_s_memrealtime();
+        }
+        return got;
+      },
       [&](uint32_t g, V3& O, V3& D, float& tmax, bool& any) -> uint32_t {
         float4 o, d;
         uint32_t h;
@@ -72,7 +84,9 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
         } else {
           B.hit[h] = make_float4(hit.t, hit.u, hit.v, __uint_as_float(hit.prim | (hit.inst << 26)));
         }
-      });
+      },
+      B.coop_tail ? tail_lds : nullptr);
+  if (tl && threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---- misses of P(iter) (:159): sky radiance (or 0) into ne, before k_shade2 replaces the ray
