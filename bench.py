@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--scene", default="c4", choices=["c3", "c4"])
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-out", action="store_true",
+                    help="outputs (avg + rgb8) to host memory every step: the PCIe-inclusive rate (not the contract value)")
     args = ap.parse_args()
 
     import torch
@@ -126,8 +128,14 @@ def main():
     if world > 1:
         shard = prt.tiles.ShardedFrame(ctx, dist, W, H, args.tile, device=dev)
 
+    avg_h = np.zeros((H * W, 4), np.float32) if args.host_out else None
+    rgb_h = np.zeros(H * W, np.uint32) if args.host_out else None
+
     def step(i):
-        if world == 1:
+        if world == 1 and args.host_out:
+            _, _, st = ctx.render(W, H, args.spp, args.bounces, frame_index=2 * i, avg=avg_h, rgb8=rgb_h,
+                                  device_out=False, stats=True)
+        elif world == 1:
             _, _, st = ctx.render(W, H, args.spp, args.bounces, frame_index=2 * i, avg=avg.data_ptr(),
                                   rgb8=rgb.data_ptr(), device_out=True, stats=True)
         else:
@@ -215,6 +223,7 @@ def main():
             "config": {"workload": f"{sd.name}: {info.triangles} tris, {W}x{H}, {args.spp} spp, depth {args.bounces}",
                        "global_batch": W * H, "seq_len": args.bounces,
                        "parallelism": f"pixel-tile{args.tile} x{world}" if world > 1 else "single-gpu",
+                       "outputs": "host memory (PCIe-inclusive)" if args.host_out else "device (HBM-resident)",
                        "rays_per_step": int(rays / args.steps), "segments_per_step": int(seg / args.steps),
                        "shadow_per_step": int(shadow / args.steps),
                        "mpix_per_s": round(W * H / (ms_step / 1e3) / 1e6, 2)},
