@@ -31,8 +31,8 @@
 namespace prt {
 
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
-constexpr uint32_t kTailRays = 32;       // a drained wave with at most this many rays turns cooperative
-constexpr uint32_t kTailLdsWords = 96;   // per wave: kTailRays x {count | found << 16, key lo, key hi}
+// a drained wave with at most TAILN rays turns cooperative; its LDS: TAILN x {count | found << 16, key lo, key hi}
+constexpr uint32_t tail_lds_words(int tailn) { return 3u * (uint32_t)tailn; }
 
 // index of the n-th (0-based) set bit of m; n < popcount(m)
 __device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
@@ -55,10 +55,11 @@ __device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
 //   tick(idle, drained)                                     wave-uniform, once at the top of every iteration:
 //                                                           idle lanes, no refill coming (the streaming
 //                                                           engine publishes finished rays there)
-// tail: kTailLdsWords of LDS for the cooperative tail, or nullptr (no tail mode).
+// tail: tail_lds_words(TAILN) words of LDS for the cooperative tail, or nullptr (no tail mode).
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
-template <int MODE, bool HALF, int STACK, int REFILL, class Fetch, class Load, class Reload, class Finish, class Tick>
+template <int MODE, bool HALF, int STACK, int REFILL, int TAILN = 32, class Fetch, class Load, class Reload, class Finish,
+          class Tick>
 __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                    Load load, Reload reload, Finish finish, Tick tick,
                                                    uint32_t* __restrict__ tail = nullptr) {
@@ -199,7 +200,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       if (drained) break;
       continue;
     }
-    if (tail && drained && __popcll(act) <= kTailRays) break;  // cooperative tail below
+    if (tail && drained && __popcll(act) <= (uint32_t)TAILN) break;  // cooperative tail below
     // ---- BLAS done: next instance, or the ray is finished
     if (active && node == kNoNode && lhit == 0 && tcnt == 0) {
       bool more = false;
@@ -227,11 +228,11 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
 
   // ---------------------------------------------------------------- cooperative tail
   // role: owner (active: holds the ray's handle) / helper (walks one subtree of an owner's ray) / free;
-  // team slot of an owner = its rank among the owners at tail entry (< kTailRays)
+  // team slot of an owner = its rank among the owners at tail entry (< TAILN)
   // tstate: helpers still walking (low 16 bits) | any-hit: some team lane hit (kFoundBit)
   constexpr uint32_t kFoundBit = 1u << 16;
   uint32_t* tstate = tail;
-  unsigned long long* tkey = reinterpret_cast<unsigned long long*>(tail + kTailRays);  // best (t, prim)
+  unsigned long long* tkey = reinterpret_cast<unsigned long long*>(tail + TAILN);  // best (t, prim)
   bool helper = false;
   uint32_t slot = (uint32_t)__popcll(__ballot(active) & lanes_below);
   if (active) {
@@ -342,11 +343,13 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   }
 }
 
-template <int MODE, bool HALF, int STACK, int REFILL, class Fetch, class Load, class Reload, class Finish>
+template <int MODE, bool HALF, int STACK, int REFILL, int TAILN = 32, class Fetch, class Load, class Reload,
+          class Finish>
 __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                  Load load, Reload reload, Finish finish,
                                                  uint32_t* __restrict__ tail = nullptr) {
-  trav8_persistent_t<MODE, HALF, STACK, REFILL>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {}, tail);
+  trav8_persistent_t<MODE, HALF, STACK, REFILL, TAILN>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {},
+                                                       tail);
 }
 
 }  // namespace prt

@@ -386,8 +386,10 @@ void launch_persistent(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B,
     if (c.trav == 32) launch_p1<ANY, 32, 8, 8>(c, S, B, it); else launch_p1<ANY, 16, 8, 8>(c, S, B, it);
   } else if (c.occ == 6) {
     if (c.trav == 32) launch_p1<ANY, 32, 12, 6>(c, S, B, it); else launch_p1<ANY, 16, 12, 6>(c, S, B, it);
+  } else if (c.occ == 5) {
+    if (c.trav == 32) launch_p1<ANY, 32, 14, 5>(c, S, B, it); else launch_p1<ANY, 16, 14, 5>(c, S, B, it);
   } else {
-    if (c.trav == 32) launch_p1<ANY, 32, 16, 5>(c, S, B, it); else launch_p1<ANY, 16, 16, 5>(c, S, B, it);
+    if (c.trav == 32) launch_p1<ANY, 32, 18, 4>(c, S, B, it); else launch_p1<ANY, 16, 18, 4>(c, S, B, it);
   }
 }
 

@@ -26,11 +26,11 @@
 namespace prt {
 
 // ---- one traversal launch: closest hits of P(iter) (iter < iters) + any hits of S(iter - 1) (iter > 0)
-template <bool HALF, int REFILL, int STACK, int WAVES>
+template <bool HALF, int REFILL, int STACK, int WAVES, int TAILN>
 __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, uint32_t iter, uint32_t iters) {
   __shared__ uint32_t lds_stack[2 * STACK * 64];
   __shared__ uint32_t prefP[kNSub + 1], prefS[kNSub + 1];
-  __shared__ uint32_t tail_lds[kTailLdsWords];
+  __shared__ uint32_t tail_lds[tail_lds_words(TAILN)];
   uint8_t* vis8 = reinterpret_cast<uint8_t*>(B.vis);
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
   const uint32_t nP = iter < iters ? load_prefix(B.ctr, iter, 0, prefP) : 0u;
@@ -43,7 +43,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   unsigned long long* tl = B.tl ? B.tl + ((size_t)iter * kTlWaves + blockIdx.x) * 4 : nullptr;
   bool seen_drain = false;
   if (tl && threadIdx.x == 0) tl[0] = __builtin_amdgcn_s_memrealtime();
-  trav8_persistent<2, HALF, STACK, REFILL>(
+  trav8_persistent<2, HALF, STACK, REFILL, TAILN>(
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) {
         const uint32_t got = fetch_some(fctr, total, part, base, want);
@@ -283,21 +283,26 @@ __global__ void __launch_bounds__(kBlock) k_resolve2(SceneDev S, TraceArgs A, Wa
   }
 }
 
-template <int REFILL, int STACK, int WAVES>
+// LDS per wave (one block): 2 x STACK x 256 B of stack + 264 B of prefix tables + the tail slots, within
+// 160 KB / (4 x WAVES) blocks per CU
+template <int REFILL, int STACK, int WAVES, int TAILN>
 void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
+  static_assert(2 * STACK * 256 + 264 + 4 * 3 * TAILN <= 163840 / (4 * WAVES), "LDS over the occupancy budget");
   const dim3 grid(256u * 4u * WAVES);
   if (c.layout == 9)
-    hipLaunchKernelGGL((k_trace2<true, REFILL, STACK, WAVES>), grid, dim3(64), 0, c.stream, S, B, it, iters);
+    hipLaunchKernelGGL((k_trace2<true, REFILL, STACK, WAVES, TAILN>), grid, dim3(64), 0, c.stream, S, B, it, iters);
   else
-    hipLaunchKernelGGL((k_trace2<false, REFILL, STACK, WAVES>), grid, dim3(64), 0, c.stream, S, B, it, iters);
+    hipLaunchKernelGGL((k_trace2<false, REFILL, STACK, WAVES, TAILN>), grid, dim3(64), 0, c.stream, S, B, it, iters);
 }
 static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
   if (c.occ == 8) {
-    if (c.trav == 16) launch_t2<16, 8, 8>(c, S, B, it, iters); else launch_t2<32, 8, 8>(c, S, B, it, iters);
+    if (c.trav == 16) launch_t2<16, 8, 8, 32>(c, S, B, it, iters); else launch_t2<32, 8, 8, 32>(c, S, B, it, iters);
   } else if (c.occ == 6) {
-    if (c.trav == 16) launch_t2<16, 12, 6>(c, S, B, it, iters); else launch_t2<32, 12, 6>(c, S, B, it, iters);
+    if (c.trav == 16) launch_t2<16, 11, 6, 64>(c, S, B, it, iters); else launch_t2<32, 11, 6, 64>(c, S, B, it, iters);
+  } else if (c.occ == 5) {
+    if (c.trav == 16) launch_t2<16, 14, 5, 32>(c, S, B, it, iters); else launch_t2<32, 14, 5, 32>(c, S, B, it, iters);
   } else {
-    if (c.trav == 16) launch_t2<16, 16, 5>(c, S, B, it, iters); else launch_t2<32, 16, 5>(c, S, B, it, iters);
+    if (c.trav == 16) launch_t2<16, 18, 4, 32>(c, S, B, it, iters); else launch_t2<32, 18, 4, 32>(c, S, B, it, iters);
   }
 }
 
