@@ -214,6 +214,14 @@ int prt_intersect(prt_ctx* ctx, int32_t n, const float* origins, const float* di
 int prt_occluded(prt_ctx* ctx, int32_t n, const float* origins, const float* dirs, const float* tmax,
                  int32_t* occluded);
 
+/* ---- BLAS builder (the reference builds on the CPU, Core/tiny_bvh.h:1968-2284,3706-3781)
+ * HOST_SAH (default): binned SAH binary tree + SAH-optimal 8-wide collapse on the host.
+ * GPU_LBVH: Morton-code LBVH (Karras 2012) + greedy 8-wide collapse on the device, Node8 layout only.
+ * Applies to the next prt_set_meshes.  Hits do not depend on the builder (order-independent hit rule). */
+#define PRT_BUILDER_HOST_SAH 0
+#define PRT_BUILDER_GPU_LBVH 1
+int prt_set_bvh_builder(prt_ctx* ctx, int32_t builder);
+
 /* ---- introspection ---- */
 typedef struct {
     int64_t blas_nodes;     /* device BVH nodes over all meshes */
@@ -221,6 +229,9 @@ typedef struct {
     int64_t device_bytes;   /* BVH + triangle + shading arrays resident in HBM */
     int32_t max_depth;
     int32_t triangles;
+    double  build_ms;       /* wall time of the last prt_set_meshes (BLAS builds + uploads) */
+    int32_t builder;        /* PRT_BUILDER_* used by the last prt_set_meshes */
+    int32_t pad;
 } prt_scene_info;
 int prt_get_scene_info(prt_ctx* ctx, prt_scene_info* info);
 

@@ -1,0 +1,428 @@
+// bvh_gpu.hip -- on-device BLAS build (the reference builds on the CPU,
+// Core/tiny_bvh.h:1968-2284 BVH::Build / 3706-3781 BuildHQ, then BVH8_CPU's collapse).
+//
+// LBVH (Karras 2012, "Maximizing Parallelism in the Construction of BVHs, Octrees, and k-d Trees"):
+//   1. centroid bounds (ordered-int atomics), 30-bit Morton code per triangle, key = code << 32 | index
+//   2. hipcub radix sort of the 64-bit keys (unique keys: no duplicate-code special case)
+//   3. binary radix tree: one thread per internal node finds its range and split from common prefixes
+//   4. boxes bottom-up: one thread per leaf walks towards the root; the second child to arrive at a node
+//      (agent atomic) unions both boxes.  Boxes are stored write-through (sc1) and read with sc1 loads
+//      after the atomic, the in-launch hand-off of MI355X_MICROARCH.md (per-XCD L2s are not coherent)
+//   5. greedy 8-wide collapse, one launch per level: a wide node opens its largest-area child with more
+//      than max_leaf triangles until it has 8 children; subtrees of <= max_leaf triangles become leaf
+//      children.  Nodes are quantised and laid out exactly as the host builder's Node8 (bvh_build.h):
+//      interior children contiguous (one atomic per node), leaf triangles contiguous (one atomic per node)
+// The result is a different tree from the host's SAH build, so traversal cost differs; hits do not (the
+// hit rule is BVH-independent), which is what the GPU tests check.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+
+#include "bvh_build.h"
+#include "bvh_gpu.h"
+
+namespace prt {
+
+namespace {
+
+constexpr int kB = 256;
+inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kB - 1) / kB); }
+
+__device__ __forceinline__ uint32_t ord(float f) {  // float -> order-preserving uint
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float unord(uint32_t u) { return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u); }
+
+__device__ __forceinline__ uint32_t spread10(uint32_t v) {  // 10 bits -> every third bit
+  v = (v * 0x00010001u) & 0xFF0000FFu;
+  v = (v * 0x00000101u) & 0x0F00F00Fu;
+  v = (v * 0x00000011u) & 0xC30C30C3u;
+  v = (v * 0x00000005u) & 0x49249249u;
+  return v;
+}
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<uint32_t*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// ---- 1. centroid bounds
+__global__ void __launch_bounds__(kB) k_centroid_bounds(const float4* __restrict__ tri, uint32_t n, uint32_t* cb) {
+  const uint32_t i = blockIdx.x * kB + threadIdx.x;
+  float c[3] = {0.0f, 0.0f, 0.0f};
+  const bool ok = i < n;
+  if (ok) {
+    const float4 a = tri[3 * i], b = tri[3 * i + 1], d = tri[3 * i + 2];
+    c[0] = (a.x + b.x + d.x) * (1.0f / 3.0f);
+    c[1] = (a.y + b.y + d.y) * (1.0f / 3.0f);
+    c[2] = (a.z + b.z + d.z) * (1.0f / 3.0f);
+  }
+  for (int k = 0; k < 3; k++) {
+    uint32_t lo = ok ? ord(c[k]) : 0xFFFFFFFFu, hi = ok ? ord(c[k]) : 0u;
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+      hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+    }
+    if ((threadIdx.x & 63u) == 0) {
+      atomicMin(cb + k, lo);
+      atomicMax(cb + 3 + k, hi);
+    }
+  }
+}
+
+// ---- 2. Morton keys
+__global__ void __launch_bounds__(kB) k_morton(const float4* __restrict__ tri, uint32_t n, const uint32_t* cb,
+                                               unsigned long long* keys) {
+  const uint32_t i = blockIdx.x * kB + threadIdx.x;
+  if (i >= n) return;
+  const float4 a = tri[3 * i], b = tri[3 * i + 1], d = tri[3 * i + 2];
+  const float c[3] = {(a.x + b.x + d.x) * (1.0f / 3.0f), (a.y + b.y + d.y) * (1.0f / 3.0f),
+                      (a.z + b.z + d.z) * (1.0f / 3.0f)};
+  uint32_t q[3];
+  for (int k = 0; k < 3; k++) {
+    const float lo = unord(cb[k]), hi = unord(cb[3 + k]);
+    const float ext = hi - lo;
+    const float t = ext > 0.0f ? (c[k] - lo) / ext : 0.0f;
+    q[k] = (uint32_t)fminf(fmaxf(t * 1024.0f, 0.0f), 1023.0f);
+  }
+  const uint32_t code = (spread10(q[0]) << 2) | (spread10(q[1]) << 1) | spread10(q[2]);
+  keys[i] = ((unsigned long long)code << 32) | i;
+}
+
+// ---- 3. binary radix tree.  Internal nodes 0 .. n-2, leaf i = node n-1+i.
+__device__ __forceinline__ int delta(const unsigned long long* k, int n, int i, int j) {
+  if (j < 0 || j >= n) return -1;
+  return __clzll(k[i] ^ k[j]);
+}
+__global__ void __launch_bounds__(kB) k_radix_tree(const unsigned long long* __restrict__ keys, int n, int* left,
+                                                   int* right, int* parent, uint32_t* first, uint32_t* count) {
+  const int i = (int)(blockIdx.x * kB + threadIdx.x);
+  if (i >= n - 1) return;
+  const int d = delta(keys, n, i, i + 1) - delta(keys, n, i, i - 1) >= 0 ? 1 : -1;
+  const int dmin = delta(keys, n, i, i - d);
+  int lmax = 2;
+  while (delta(keys, n, i, i + lmax * d) > dmin) lmax <<= 1;
+  int l = 0;
+  for (int t = lmax >> 1; t >= 1; t >>= 1)
+    if (delta(keys, n, i, i + (l + t) * d) > dmin) l += t;
+  const int j = i + l * d;
+  const int dnode = delta(keys, n, i, j);
+  int s = 0;
+  for (int t = (l + 1) >> 1;; t = (t + 1) >> 1) {
+    if (delta(keys, n, i, i + (s + t) * d) > dnode) s += t;
+    if (t == 1) break;
+  }
+  const int g = i + s * d + min(d, 0);
+  const int lo = min(i, j), hi = max(i, j);
+  const int lc = (lo == g) ? (n - 1 + g) : g;
+  const int rc = (hi == g + 1) ? (n - 1 + g + 1) : (g + 1);
+  left[i] = lc;
+  right[i] = rc;
+  parent[lc] = i;
+  parent[rc] = i;
+  first[i] = (uint32_t)lo;
+  count[i] = (uint32_t)(hi - lo + 1);
+}
+
+// ---- 4. boxes bottom-up (flag[] zeroed before the launch)
+__global__ void __launch_bounds__(kB) k_boxes(const float4* __restrict__ tri, const unsigned long long* __restrict__ keys,
+                                              int n, const int* __restrict__ left, const int* __restrict__ right,
+                                              const int* __restrict__ parent, float* box, uint32_t* flag,
+                                              uint32_t* first, uint32_t* count) {
+  const int i = (int)(blockIdx.x * kB + threadIdx.x);
+  if (i >= n) return;
+  const uint32_t prim = (uint32_t)keys[i];
+  const float4 a = tri[3 * prim], b = tri[3 * prim + 1], c = tri[3 * prim + 2];
+  int node = n - 1 + i;
+  float* bx = box + 6 * (size_t)node;
+  st_sc1(bx + 0, fminf(fminf(a.x, b.x), c.x));
+  st_sc1(bx + 1, fminf(fminf(a.y, b.y), c.y));
+  st_sc1(bx + 2, fminf(fminf(a.z, b.z), c.z));
+  st_sc1(bx + 3, fmaxf(fmaxf(a.x, b.x), c.x));
+  st_sc1(bx + 4, fmaxf(fmaxf(a.y, b.y), c.y));
+  st_sc1(bx + 5, fmaxf(fmaxf(a.z, b.z), c.z));
+  first[node] = (uint32_t)i;
+  count[node] = 1u;
+  if (n == 1) return;
+  while (node != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this node's box is out before the arrival
+    const int p = parent[node];
+    if (p < 0 || p >= n - 1) return;                    // malformed tree: the host checks the node count
+    if (atomicAdd(flag + p, 1u) == 0u) return;          // the sibling's thread finishes the parent
+    const float* l = box + 6 * (size_t)left[p];
+    const float* r = box + 6 * (size_t)right[p];
+    float* o = box + 6 * (size_t)p;
+    for (int k = 0; k < 3; k++) st_sc1(o + k, fminf(ld_sc1(l + k), ld_sc1(r + k)));
+    for (int k = 3; k < 6; k++) st_sc1(o + k, fmaxf(ld_sc1(l + k), ld_sc1(r + k)));
+    node = p;
+  }
+}
+
+// ---- 5. greedy 8-wide collapse, one level per launch
+__device__ __forceinline__ float area6(const float* b) {
+  const float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+__device__ __forceinline__ void inflate(float* lo, float* hi) {  // inflate_box (bvh_build.cpp)
+  for (int k = 0; k < 3; k++) {
+    const float ext = fmaxf(fabsf(lo[k]), fabsf(hi[k]));
+    const float pad = ext * 1e-6f + 1e-7f;
+    lo[k] -= pad;
+    hi[k] += pad;
+  }
+}
+__device__ __forceinline__ uint8_t grid_exp(double ext, double qmax) {  // grid_exponent (bvh_build.cpp)
+  if (!(ext > 0)) return 1;
+  int e = (int)ceil(log2(ext / qmax));
+  while (ldexp(qmax, e) < ext) e++;
+  while (e > -126 && ldexp(qmax, e - 1) >= ext) e--;
+  return (uint8_t)min(254, max(1, e + 127));
+}
+
+struct Task {
+  int n2;       // binary node
+  uint32_t n8;  // wide node slot
+};
+
+__global__ void __launch_bounds__(kB) k_collapse(const float4* __restrict__ tri, const unsigned long long* __restrict__ keys,
+                                                 int n, const int* __restrict__ left, const int* __restrict__ right,
+                                                 const float* __restrict__ box, const uint32_t* __restrict__ first,
+                                                 const uint32_t* __restrict__ count, int max_leaf,
+                                                 const Task* __restrict__ tasks, uint32_t ntasks, Task* next,
+                                                 uint32_t* ctr, Node8* nodes, TriMT* tris) {
+  const uint32_t t = blockIdx.x * kB + threadIdx.x;
+  if (t >= ntasks) return;
+  const Task tk = tasks[t];
+  const int nn = 2 * n - 1;
+  if (tk.n2 < 0 || tk.n2 >= nn || tk.n8 >= (uint32_t)n) { atomicOr(ctr + 3, 0x80000000u); return; }
+  auto is_leaf = [&](int v) { return v >= n - 1 || (int)count[v] <= max_leaf; };
+  int ch[8];
+  int nc = 0;
+  if (is_leaf(tk.n2)) {
+    ch[nc++] = tk.n2;
+  } else {
+    ch[nc++] = left[tk.n2];
+    ch[nc++] = right[tk.n2];
+    while (nc < 8) {
+      int bi = -1;
+      float ba = -1.0f;
+      for (int i = 0; i < nc; i++)
+        if (!is_leaf(ch[i])) {
+          const float a = area6(box + 6 * (size_t)ch[i]);
+          if (a > ba) { ba = a; bi = i; }
+        }
+      if (bi < 0) break;
+      const int c = ch[bi];
+      ch[bi] = left[c];
+      ch[nc++] = right[c];
+    }
+  }
+  for (int i = 0; i < nc; i++)
+    if (ch[i] < 0 || ch[i] >= nn) { atomicOr(ctr + 3, 0x80000000u); return; }
+  float clo[8][3], chi[8][3];
+  double nlo[3] = {1e300, 1e300, 1e300}, nhi[3] = {-1e300, -1e300, -1e300};
+  for (int i = 0; i < nc; i++) {
+    const float* b = box + 6 * (size_t)ch[i];
+    for (int k = 0; k < 3; k++) { clo[i][k] = b[k]; chi[i][k] = b[3 + k]; }
+    inflate(clo[i], chi[i]);
+    for (int k = 0; k < 3; k++) {
+      nlo[k] = fmin(nlo[k], (double)clo[i][k]);
+      nhi[k] = fmax(nhi[k], (double)chi[i][k]);
+    }
+  }
+  // octant slots: slot s holds the child that comes first for rays of octant s (greedy assignment)
+  int child_in[8];
+  for (int s = 0; s < 8; s++) child_in[s] = -1;
+  {
+    double pc[3];
+    for (int k = 0; k < 3; k++) pc[k] = 0.5 * (nlo[k] + nhi[k]);
+    uint32_t used_c = 0, used_s = 0;
+    for (int m = 0; m < nc; m++) {
+      double best = 1e300;
+      int bi = -1, bs = -1;
+      for (int i = 0; i < nc; i++) {
+        if (used_c & (1u << i)) continue;
+        for (int s = 0; s < 8; s++) {
+          if (used_s & (1u << s)) continue;
+          double d = 0;
+          for (int k = 0; k < 3; k++) {
+            const double cc = 0.5 * ((double)clo[i][k] + (double)chi[i][k]) - pc[k];
+            d += ((s >> k) & 1) ? -cc : cc;
+          }
+          if (d < best) { best = d; bi = i; bs = s; }
+        }
+      }
+      used_c |= 1u << bi;
+      used_s |= 1u << bs;
+      child_in[bs] = bi;
+    }
+  }
+  Node8 nd;
+  uint8_t* raw = reinterpret_cast<uint8_t*>(&nd);
+  for (int b = 0; b < (int)sizeof(Node8); b++) raw[b] = 0;
+  nd.px = (float)nlo[0]; nd.py = (float)nlo[1]; nd.pz = (float)nlo[2];
+  const double p[3] = {(double)nd.px, (double)nd.py, (double)nd.pz};
+  uint8_t e[3];
+  for (int k = 0; k < 3; k++) e[k] = grid_exp(nhi[k] - p[k], 255.0);
+  nd.ex = e[0]; nd.ey = e[1]; nd.ez = e[2];
+  const double sc[3] = {ldexp(1.0, (int)e[0] - 127), ldexp(1.0, (int)e[1] - 127), ldexp(1.0, (int)e[2] - 127)};
+  uint32_t ninterior = 0, ntri = 0;
+  for (int i = 0; i < nc; i++) {
+    if (is_leaf(ch[i])) ntri += count[ch[i]];
+    else ninterior++;
+  }
+  if ((uint32_t)nc > ninterior) atomicAdd(ctr + 3, (uint32_t)nc - ninterior);  // leaf children
+  nd.child_base = ninterior ? atomicAdd(ctr + 0, ninterior) : 0u;
+  nd.tri_base = ntri ? atomicAdd(ctr + 1, ntri) : 0u;
+  const uint32_t tbase = ninterior ? atomicAdd(ctr + 2, ninterior) : 0u;  // next-level task slots
+  if (nd.child_base + ninterior > (uint32_t)n || nd.tri_base + ntri > (uint32_t)n || tbase + ninterior > (uint32_t)n) {
+    atomicOr(ctr + 3, 0x80000000u);  // capacity exceeded: cannot happen for a well-formed radix tree
+    return;
+  }
+  uint32_t nextchild = nd.child_base, tri_off = 0, tslot = tbase;
+  for (int s = 0; s < 8; s++) {
+    const int i = child_in[s];
+    if (i < 0) {
+      nd.qlox[s] = nd.qloy[s] = nd.qloz[s] = 255;
+      nd.qhix[s] = nd.qhiy[s] = nd.qhiz[s] = 0;
+      continue;
+    }
+    uint8_t* ql[3] = {&nd.qlox[s], &nd.qloy[s], &nd.qloz[s]};
+    uint8_t* qh[3] = {&nd.qhix[s], &nd.qhiy[s], &nd.qhiz[s]};
+    for (int k = 0; k < 3; k++) {
+      *ql[k] = (uint8_t)fmin(255.0, fmax(0.0, floor(((double)clo[i][k] - p[k]) / sc[k])));
+      *qh[k] = (uint8_t)fmin(255.0, fmax(0.0, ceil(((double)chi[i][k] - p[k]) / sc[k])));
+    }
+    const int c = ch[i];
+    if (is_leaf(c)) {
+      const uint32_t f = c >= n - 1 ? (uint32_t)(c - (n - 1)) : first[c], cnt = count[c];
+      for (uint32_t j = 0; j < cnt; j++) {
+        const uint32_t pr = (uint32_t)keys[f + j];
+        const float4 a = tri[3 * pr], b = tri[3 * pr + 1], d = tri[3 * pr + 2];
+        TriMT m;
+        m.v0[0] = a.x; m.v0[1] = a.y; m.v0[2] = a.z;
+        m.e1[0] = b.x - a.x; m.e1[1] = b.y - a.y; m.e1[2] = b.z - a.z;  // e1 = v1 - v0 (tiny_bvh.h:4614-4616)
+        m.e2[0] = d.x - a.x; m.e2[1] = d.y - a.y; m.e2[2] = d.z - a.z;
+        m.prim = pr; m.pad1 = 0.0f; m.pad2 = 0.0f;
+        tris[nd.tri_base + tri_off + j] = m;
+      }
+      nd.meta[s] = (uint8_t)((tri_off << 3) | cnt);
+      tri_off += cnt;
+    } else {
+      nd.imask |= (uint8_t)(1u << s);
+      next[tslot++] = Task{c, nextchild++};
+    }
+  }
+  nodes[tk.n8] = nd;
+}
+
+// ShadeTri.pad[0] = the primitive's TriMT record (the cooperative traversal tail, prt_persist.h)
+__global__ void __launch_bounds__(kB) k_prim_records(const TriMT* __restrict__ tris, uint32_t n, uint32_t tri_base,
+                                                     ShadeTri* stri, uint32_t prim_base) {
+  const uint32_t g = blockIdx.x * kB + threadIdx.x;
+  if (g >= n) return;
+  stri[prim_base + tris[g].prim].pad[0] = tri_base + g;
+}
+
+// rebase one mesh's nodes into the concatenated arrays
+__global__ void __launch_bounds__(kB) k_rebase(Node8* nodes, uint32_t n, uint32_t node_base, uint32_t tri_base) {
+  const uint32_t i = blockIdx.x * kB + threadIdx.x;
+  if (i >= n) return;
+  nodes[i].child_base += node_base;
+  nodes[i].tri_base += tri_base;
+}
+
+}  // namespace
+
+#define GB_TRY(x)                          \
+  do {                                     \
+    const hipError_t e_ = (x);             \
+    if (e_ != hipSuccess) return e_;       \
+  } while (0)
+
+hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, int max_leaf, Node8* nodes_out,
+                           TriMT* tris_out, GpuBlasInfo* info) {
+  const int n = n_tris;
+  if (n <= 0) return hipErrorInvalidValue;
+  const size_t nn = 2 * (size_t)n - 1;
+  // scratch: keys x2, left/right/parent/first/count/flag, boxes, two task arrays, counters
+  unsigned long long *keys = nullptr, *keys2 = nullptr;
+  int *left = nullptr, *right = nullptr, *parent = nullptr;
+  uint32_t *first = nullptr, *count = nullptr, *flag = nullptr, *ctr = nullptr, *cb = nullptr;
+  float* box = nullptr;
+  Task *ta = nullptr, *tb = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  hipError_t err = hipSuccess;
+  auto fail = [&](hipError_t e) {
+    (void)hipFree(keys); (void)hipFree(keys2); (void)hipFree(left); (void)hipFree(right); (void)hipFree(parent);
+    (void)hipFree(first); (void)hipFree(count); (void)hipFree(flag); (void)hipFree(ctr); (void)hipFree(cb);
+    (void)hipFree(box); (void)hipFree(ta); (void)hipFree(tb); (void)hipFree(tmp);
+    return e;
+  };
+  const float4* tri = reinterpret_cast<const float4*>(tri_dev);
+  if ((err = hipMalloc(&keys, 8 * (size_t)n)) || (err = hipMalloc(&keys2, 8 * (size_t)n)) ||
+      (err = hipMalloc(&left, 4 * nn)) || (err = hipMalloc(&right, 4 * nn)) || (err = hipMalloc(&parent, 4 * nn)) ||
+      (err = hipMalloc(&first, 4 * nn)) || (err = hipMalloc(&count, 4 * nn)) || (err = hipMalloc(&flag, 4 * nn)) ||
+      (err = hipMalloc(&box, 24 * nn)) || (err = hipMalloc(&ta, sizeof(Task) * (size_t)n)) ||
+      (err = hipMalloc(&tb, sizeof(Task) * (size_t)n)) || (err = hipMalloc(&ctr, 16)) || (err = hipMalloc(&cb, 24)))
+    return fail(err);
+  const uint32_t init_cb[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+  if ((err = hipMemcpyAsync(cb, init_cb, 24, hipMemcpyHostToDevice, s))) return fail(err);
+  hipLaunchKernelGGL(k_centroid_bounds, dim3(grid_of(n)), dim3(kB), 0, s, tri, (uint32_t)n, cb);
+  hipLaunchKernelGGL(k_morton, dim3(grid_of(n)), dim3(kB), 0, s, tri, (uint32_t)n, cb, keys);
+  if ((err = hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, keys2, n, 0, 64, s))) return fail(err);
+  if ((err = hipMalloc(&tmp, tmp_bytes))) return fail(err);
+  if ((err = hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, keys2, n, 0, 64, s))) return fail(err);
+  if ((err = hipMemsetAsync(parent, 0xFF, 4 * nn, s))) return fail(err);
+  if (n > 1)
+    hipLaunchKernelGGL(k_radix_tree, dim3(grid_of(n - 1)), dim3(kB), 0, s, keys2, n, left, right, parent, first, count);
+  if ((err = hipMemsetAsync(flag, 0, 4 * nn, s))) return fail(err);
+  hipLaunchKernelGGL(k_boxes, dim3(grid_of(n)), dim3(kB), 0, s, tri, keys2, n, left, right, parent, box, flag, first,
+                     count);
+  // collapse, level by level from the binary root (node 0; the single leaf when n == 1)
+  const Task t0{0, 0u};  // binary root: internal node 0, or the single leaf (node n - 1 = 0) when n == 1
+  const uint32_t c0[4] = {1u, 0u, 0u, 0u};  // wide nodes used (the root), triangles used, next tasks
+  if ((err = hipMemcpyAsync(ta, &t0, sizeof(Task), hipMemcpyHostToDevice, s)) ||
+      (err = hipMemcpyAsync(ctr, c0, 16, hipMemcpyHostToDevice, s)))
+    return fail(err);
+  uint32_t ntasks = 1, depth = 0;
+  while (ntasks) {
+    depth++;
+    const uint32_t zero = 0;
+    if ((err = hipMemcpyAsync(ctr + 2, &zero, 4, hipMemcpyHostToDevice, s))) return fail(err);
+    hipLaunchKernelGGL(k_collapse, dim3(grid_of(ntasks)), dim3(kB), 0, s, tri, keys2, n, left, right, box, first,
+                       count, max_leaf, ta, ntasks, tb, ctr, nodes_out, tris_out);
+    if ((err = hipGetLastError())) return fail(err);
+    uint32_t c[4];
+    if ((err = hipMemcpyAsync(c, ctr, 16, hipMemcpyDeviceToHost, s)) || (err = hipStreamSynchronize(s)))
+      return fail(err);
+    if (c[3] & 0x80000000u) return fail(hipErrorInvalidValue);  // malformed tree (bounds checks above)
+    ntasks = c[2];
+    std::swap(ta, tb);
+    info->nodes = c[0];
+    info->tris = c[1];
+    info->leaves = c[3];
+  }
+  info->depth = (int32_t)depth;
+  if (info->tris != (uint32_t)n) return fail(hipErrorInvalidValue);
+  float rb[6];
+  if ((err = hipMemcpyAsync(rb, box, 24, hipMemcpyDeviceToHost, s)) || (err = hipStreamSynchronize(s))) return fail(err);
+  for (int k = 0; k < 3; k++) { info->bmin[k] = rb[k]; info->bmax[k] = rb[3 + k]; }
+  return fail(hipSuccess);
+}
+
+hipError_t gpu_blas_finish(hipStream_t s, Node8* nodes, uint32_t n_nodes, uint32_t node_base, const TriMT* tris,
+                           uint32_t n_tris, uint32_t tri_base, ShadeTri* stri, uint32_t prim_base) {
+  if (n_nodes) hipLaunchKernelGGL(k_rebase, dim3(grid_of(n_nodes)), dim3(kB), 0, s, nodes, n_nodes, node_base, tri_base);
+  if (n_tris)
+    hipLaunchKernelGGL(k_prim_records, dim3(grid_of(n_tris)), dim3(kB), 0, s, tris, n_tris, tri_base, stri, prim_base);
+  return hipGetLastError();
+}
+
+}  // namespace prt

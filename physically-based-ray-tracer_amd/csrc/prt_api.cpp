@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -12,6 +13,7 @@
 
 #include "../../include/prt.h"
 #include "bvh_build.h"
+#include "bvh_gpu.h"
 #include "prt_launch.h"
 
 using namespace prt;
@@ -108,6 +110,9 @@ struct prt_ctx {
   DevBuf nodes, nodes8, nodes8h, tris, stri, mesh;
   int max_depth = 0;
   int layout = 8;  // BLAS node layout of the uploaded meshes: 8 = Node8, 9 = Node8H, 4 = Node4 (PRT_BVH)
+  int builder = -1;  // BLAS builder: PRT_BUILDER_HOST_SAH / PRT_BUILDER_GPU_LBVH (-1: PRT_BUILDER env, else host)
+  double build_ms = 0;  // wall time of the last prt_set_meshes BLAS builds
+  int built_with = PRT_BUILDER_HOST_SAH;
   // instances
   std::vector<float> inst_xf;
   std::vector<uint32_t> inst_mesh;
@@ -698,6 +703,18 @@ int prt_set_textures(prt_ctx* c, const prt_texture* t, int32_t n) {
 int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
   if (!c || !m || n <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad meshes");
   const int layout = layout_from_env();
+  int builder = c->builder;
+  if (builder < 0) {
+    const char* e = std::getenv("PRT_BUILDER");
+    builder = (e && std::strcmp(e, "gpu") == 0) ? PRT_BUILDER_GPU_LBVH : PRT_BUILDER_HOST_SAH;
+  }
+  const bool gpu = builder == PRT_BUILDER_GPU_LBVH;
+  if (gpu && layout != 8) return fail(PRT_ERR_UNSUPPORTED, "the GPU builder emits Node8 only (PRT_BVH=8)");
+  HIP_TRY(hipSetDevice(c->device));
+  const auto t_build0 = std::chrono::steady_clock::now();
+  struct GpuMesh { DevBuf nodes, tris; GpuBlasInfo gi; uint32_t node_base, tri_base, prim_base; };
+  std::vector<GpuMesh> gm(gpu ? n : 0);
+  uint32_t gpu_nodes = 0, gpu_tris = 0;
   std::vector<Node4> nodes;
   std::vector<Node8> nodes8;
   std::vector<Node8H> nodes8h;
@@ -725,11 +742,28 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
     }
     for (int64_t k = 0; k < 3 * (int64_t)M.tri_count; k++)
       if (M.indices[k] < 0 || M.indices[k] >= M.vertex_count) return fail(PRT_ERR_INVALID_ARGUMENT, "index out of range");
-    const uint32_t tri_base = (uint32_t)tris.size();
+    const uint32_t tri_base = gpu ? gpu_tris : (uint32_t)tris.size();
     float bmin[3], bmax[3];
     int depth = 0;
     int64_t nnodes = 0, nleaves = 0;
-    if (layout == 4) {
+    if (gpu) {  // LBVH + greedy 8-wide collapse on the device (bvh_gpu.hip)
+      GpuMesh& g = gm[i];
+      DevBuf fat;
+      HIP_TRY(upload(fat, M.triangles, 48ull * (size_t)M.tri_count));
+      HIP_TRY(g.nodes.ensure(sizeof(Node8) * (size_t)M.tri_count));
+      HIP_TRY(g.tris.ensure(sizeof(TriMT) * (size_t)M.tri_count));
+      HIP_TRY(gpu_build_blas8(c->stream, fat.as<float>(), M.tri_count, 3, g.nodes.as<Node8>(), g.tris.as<TriMT>(), &g.gi));
+      fat.release();
+      if ((uint64_t)gpu_nodes + g.gi.nodes >= (1ull << 32) || (uint64_t)gpu_tris + g.gi.tris >= (1ull << 32))
+        return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
+      g.node_base = gpu_nodes;
+      g.tri_base = gpu_tris;
+      gpu_nodes += g.gi.nodes;
+      gpu_tris += g.gi.tris;
+      mh[i].root = g.node_base;
+      for (int k = 0; k < 3; k++) { bmin[k] = g.gi.bmin[k]; bmax[k] = g.gi.bmax[k]; }
+      depth = g.gi.depth; nnodes = g.gi.nodes; nleaves = g.gi.leaves;
+    } else if (layout == 4) {
       BuiltBlas b = build_blas(M.triangles, M.tri_count, 4);
       const uint32_t node_base = (uint32_t)nodes.size();
       if ((uint64_t)tri_base + b.tris.size() >= (1u << 29)) return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
@@ -792,7 +826,9 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
     }
     // ShadeTri.pad[0]: the primitive's TriMT record (the cooperative traversal tail re-tests a helper's
     // winning triangle from its primitive id, prt_persist.h)
-    for (size_t g = tri_base; g < tris.size(); g++) stri[mh[i].prim_base + tris[g].prim].pad[0] = (uint32_t)g;
+    if (gpu) gm[i].prim_base = mh[i].prim_base;
+    else
+      for (size_t g = tri_base; g < tris.size(); g++) stri[mh[i].prim_base + tris[g].prim].pad[0] = (uint32_t)g;
 
     for (int k = 0; k < 3; k++) { info[i].bmin[k] = bmin[k]; info[i].bmax[k] = bmax[k]; }
     info[i].depth = depth;
@@ -801,21 +837,46 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
     info[i].tris = M.tri_count;
     maxd = std::max(maxd, depth);
   }
-  HIP_TRY(hipSetDevice(c->device));
   c->nodes.release();
   c->nodes8.release();
   c->nodes8h.release();
-  if (layout == 4) HIP_TRY(upload(c->nodes, nodes.data(), nodes.size() * sizeof(Node4)));
-  else if (layout == 9) HIP_TRY(upload(c->nodes8h, nodes8h.data(), nodes8h.size() * sizeof(Node8H)));
-  else HIP_TRY(upload(c->nodes8, nodes8.data(), nodes8.size() * sizeof(Node8)));
-  HIP_TRY(upload(c->tris, tris.data(), tris.size() * sizeof(TriMT)));
-  HIP_TRY(upload(c->stri, stri.data(), stri.size() * sizeof(ShadeTri)));
+  if (gpu) {  // concatenate the per-mesh device results, rebase offsets, primitive -> triangle records
+    HIP_TRY(c->nodes8.ensure(sizeof(Node8) * (size_t)gpu_nodes));
+    HIP_TRY(c->tris.ensure(sizeof(TriMT) * (size_t)gpu_tris));
+    HIP_TRY(upload(c->stri, stri.data(), stri.size() * sizeof(ShadeTri)));
+    for (int32_t i = 0; i < n; i++) {
+      GpuMesh& g = gm[i];
+      HIP_TRY(hipMemcpyAsync(c->nodes8.as<Node8>() + g.node_base, g.nodes.p, sizeof(Node8) * (size_t)g.gi.nodes,
+                             hipMemcpyDeviceToDevice, c->stream));
+      HIP_TRY(hipMemcpyAsync(c->tris.as<TriMT>() + g.tri_base, g.tris.p, sizeof(TriMT) * (size_t)g.gi.tris,
+                             hipMemcpyDeviceToDevice, c->stream));
+      HIP_TRY(gpu_blas_finish(c->stream, c->nodes8.as<Node8>() + g.node_base, g.gi.nodes, g.node_base,
+                              c->tris.as<TriMT>() + g.tri_base, g.gi.tris, g.tri_base, c->stri.as<ShadeTri>(),
+                              g.prim_base));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  } else {
+    if (layout == 4) HIP_TRY(upload(c->nodes, nodes.data(), nodes.size() * sizeof(Node4)));
+    else if (layout == 9) HIP_TRY(upload(c->nodes8h, nodes8h.data(), nodes8h.size() * sizeof(Node8H)));
+    else HIP_TRY(upload(c->nodes8, nodes8.data(), nodes8.size() * sizeof(Node8)));
+    HIP_TRY(upload(c->tris, tris.data(), tris.size() * sizeof(TriMT)));
+    HIP_TRY(upload(c->stri, stri.data(), stri.size() * sizeof(ShadeTri)));
+  }
+  c->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_build0).count();
+  c->built_with = builder;
   HIP_TRY(upload(c->mesh, mh.data(), mh.size() * sizeof(MeshDev)));
   c->mesh_host = mh;
   c->mesh_info = info;
   c->max_depth = maxd;
   c->layout = layout;
   c->inst_dirty = true;
+  return PRT_OK;
+}
+
+int prt_set_bvh_builder(prt_ctx* c, int32_t builder) {
+  if (!c || (builder != PRT_BUILDER_HOST_SAH && builder != PRT_BUILDER_GPU_LBVH))
+    return fail(PRT_ERR_INVALID_ARGUMENT, "bad BLAS builder");
+  c->builder = builder;
   return PRT_OK;
 }
 
@@ -1077,6 +1138,8 @@ int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
     info->triangles += m.tris;
   }
   info->max_depth = c->max_depth;
+  info->build_ms = c->build_ms;
+  info->builder = c->built_with;
   info->device_bytes = (int64_t)(c->nodes.bytes + c->nodes8.bytes + c->nodes8h.bytes + c->tris.bytes + c->stri.bytes + c->texels.bytes + c->sky.bytes + c->inst.bytes);
   return PRT_OK;
 }

@@ -13,6 +13,7 @@ ABI_VERSION = 2  # PRT_ABI_VERSION of the include/prt.h these structs mirror
 FLAG_AA, FLAG_ACCUMULATE, FLAG_GAMMA, FLAG_NORMALMAP, FLAG_SKYBOX, FLAG_LIGHTED, FLAG_STOCHASTIC = (1 << i for i in range(7))
 FLAGS_DEFAULT = 0x7F
 OUT_DEVICE = 1
+BUILDER_HOST_SAH, BUILDER_GPU_LBVH = 0, 1
 
 # Renderer::RENDER_STATES (Core/Renderer.h:37-46)
 MODE_BRDF, MODE_BASECOLOR, MODE_GEOMETRYNORMAL, MODE_SHADINGNORMAL, MODE_METAL, MODE_ROUGHNESS, MODE_EMISSIVE = range(7)
@@ -23,7 +24,7 @@ EXPORTS = [
     "prt_set_textures", "prt_set_meshes", "prt_set_instances", "prt_set_lights", "prt_set_sky", "prt_set_camera",
     "prt_camera_look_at", "prt_postfx_preset", "prt_set_postfx", "prt_render", "prt_reset_accumulation", "prt_tile_buffer_pixels", "prt_tile_pixel_map",
     "prt_render_tiles",
-    "prt_untile", "prt_trace_primary", "prt_intersect", "prt_occluded", "prt_get_scene_info",
+    "prt_untile", "prt_trace_primary", "prt_intersect", "prt_occluded", "prt_get_scene_info", "prt_set_bvh_builder",
 ]
 
 
@@ -81,7 +82,8 @@ class Hit(C.Structure):
 
 class SceneInfo(C.Structure):
     _fields_ = [("blas_nodes", C.c_int64), ("blas_leaves", C.c_int64), ("device_bytes", C.c_int64),
-                ("max_depth", C.c_int32), ("triangles", C.c_int32)]
+                ("max_depth", C.c_int32), ("triangles", C.c_int32), ("build_ms", C.c_double), ("builder", C.c_int32),
+                ("pad", C.c_int32)]
 
 
 _lib = None
@@ -128,6 +130,7 @@ def load():
         "prt_intersect": ([vp, i32, vp, vp, vp, vp], C.c_int),
         "prt_occluded": ([vp, i32, vp, vp, vp, vp], C.c_int),
         "prt_get_scene_info": ([vp, C.POINTER(SceneInfo)], C.c_int),
+        "prt_set_bvh_builder": ([vp, i32], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -184,6 +184,10 @@ class Context:
             pf = _lib.PostFx()
         check(self.L.prt_set_postfx(self.h, C.byref(pf)))
 
+    def set_bvh_builder(self, builder):
+        """BLAS builder for the next set_scene: _lib.BUILDER_HOST_SAH (default) or _lib.BUILDER_GPU_LBVH."""
+        check(self.L.prt_set_bvh_builder(self.h, builder))
+
     def scene_info(self):
         si = _lib.SceneInfo()
         check(self.L.prt_get_scene_info(self.h, C.byref(si)))
