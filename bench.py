@@ -149,7 +149,7 @@ def main():
     torch.cuda.synchronize()
     seg = shadow = 0
     ms_trace, ms_closest, ms_anyhit = [], [], []
-    pipeline = iters = 0
+    pipeline = iters = batches = 0
     t0 = time.perf_counter()
     for i in range(args.steps):
         st = step(args.warmup + i)
@@ -160,6 +160,7 @@ def main():
         ms_anyhit.append(st.ms_anyhit)
         pipeline = st.pipeline
         iters = st.iterations
+        batches = st.batches
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -219,6 +220,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "pipeline": {0: "wavefront", 1: "megakernel", 2: "wavefront-merged", 3: "stream"}[pipeline],
+            "batches": batches,
             "data": "synthetic (seeded procedural heightfield, textures, sky; scenes.py)",
             "config": {"workload": f"{sd.name}: {info.triangles} tris, {W}x{H}, {args.spp} spp, depth {args.bounces}",
                        "global_batch": W * H, "seq_len": args.bounces,

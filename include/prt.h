@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PRT_ABI_VERSION 2
+#define PRT_ABI_VERSION 3
 
 typedef enum {
     PRT_OK = 0,
@@ -125,7 +125,9 @@ typedef struct {
     int32_t  pipeline;      /* 2 = merged-trace wavefront (default), 0 = wavefront with separate extend /
                                shadow launches (PRT_PIPELINE=wave1), 1 = megakernel (PRT_PIPELINE=mega),
                                3 = streaming engine, one persistent launch (PRT_PIPELINE=stream) */
-    int32_t  iterations;    /* wavefront iterations launched */
+    int32_t  iterations;    /* traversal launches (pipelines 0 / 2: per batch, summed over the batches) */
+    int32_t  batches;       /* wavefront batches: consecutive item ranges on concurrent streams (PRT_BATCHES) */
+    int32_t  reserved;
 } prt_stats;
 
 /* closest-hit record, tinybvh::Intersection (Core/tiny_bvh.h:545-567) minus user data */

@@ -20,6 +20,10 @@ using namespace prt;
 
 namespace {
 
+// wavefront batches: independent consecutive item ranges of one call, each on its own HIP stream, so one
+// batch's launches fill the other's traversal tails and shading gaps (PRT_BATCHES)
+constexpr int kMaxBatches = 4;
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -133,11 +137,13 @@ struct prt_ctx {
   int32_t accW = 0, accH = 0;
   DevBuf frames, avg, rgb8, counters, hits, tl;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  // wavefront pipeline
-  DevBuf wave;
-  WaveBufs wb{};
-  uint32_t wave_n = 0, wave_levels = 0;
-  WaveTimers wt{};
+  // wavefront pipeline: batch 0 runs on `stream`, batch k > 0 on bstream[k] (fork / join events)
+  DevBuf wave[kMaxBatches];
+  WaveBufs wb[kMaxBatches] = {};
+  uint32_t wave_n[kMaxBatches] = {}, wave_levels[kMaxBatches] = {};
+  WaveTimers wt[kMaxBatches] = {};
+  hipStream_t bstream[kMaxBatches] = {};
+  hipEvent_t bev[kMaxBatches] = {};
   // streaming engine (prt_stream.hip)
   DevBuf sq, sctl;
   StreamBufs sb{};
@@ -306,14 +312,14 @@ int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
 // wavefront buffers sized for n items and (bounces-1) (result, throughput) stack levels
 // queue counters [iter][path|shadow][kNSub] + traversal fetch counters [iter][path|shadow][8 parts]
 constexpr size_t kCtrWords = (size_t)(kMaxIters + 2) * 2 * (kNSub + 8) * kCtrStride;
-int ensure_wave(prt_ctx* c, uint32_t n, int bounces) {
+int ensure_wave(prt_ctx* c, int k, uint32_t n, int bounces) {
   const uint32_t levels = (uint32_t)std::max(1, bounces - 1);
   // sub-queue t receives the 256-entry chunks c == t (mod kNSub): at most ceil(ceil(n/256)/kNSub) of them
   const uint32_t qcap = 256u * (((n + 255u) / 256u + kNSub - 1) / kNSub);
-  if (c->wave_n >= n && c->wave_levels >= levels && c->wave.p) {
-    c->wb.n = n;  // capacity stays; the SoA strides (R/T: depth * n + item) follow the current n
-    c->wb.qcap = qcap;
-    c->wb.scap = 4u * qcap;
+  if (c->wave_n[k] >= n && c->wave_levels[k] >= levels && c->wave[k].p) {
+    c->wb[k].n = n;  // capacity stays; the SoA strides (R/T: depth * n + item) follow the current n
+    c->wb[k].qcap = qcap;
+    c->wb[k].scap = 4u * qcap;
     return PRT_OK;
   }
   const size_t qn = (size_t)kNSub * qcap, sn = 4 * qn;
@@ -324,9 +330,9 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces) {
                o_jit = take(8ull * n), o_hit = take(16ull * n), o_ne = take(16ull * n), o_nb = take(16ull * n),
                o_nf = take(64ull * n), o_vis = take(4ull * n), o_q0 = take(4 * qn), o_q1 = take(4 * qn),
                o_sho = take(16 * sn), o_shd = take(16 * sn), o_ctr = take(4 * kCtrWords);
-  HIP_TRY(c->wave.ensure(off));
-  char* b = c->wave.as<char>();
-  WaveBufs& W = c->wb;
+  HIP_TRY(c->wave[k].ensure(off));
+  char* b = c->wave[k].as<char>();
+  WaveBufs& W = c->wb[k];
   W.n = n;
   W.qcap = qcap;
   W.scap = 4u * qcap;
@@ -336,8 +342,30 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces) {
   W.ne = (float4*)(b + o_ne); W.nb = (float4*)(b + o_nb); W.nf = (float4*)(b + o_nf); W.vis = (uint32_t*)(b + o_vis);
   W.q0 = (uint32_t*)(b + o_q0); W.q1 = (uint32_t*)(b + o_q1); W.sho = (float4*)(b + o_sho);
   W.shd = (float4*)(b + o_shd); W.ctr = (uint32_t*)(b + o_ctr);
-  c->wave_n = n;
-  c->wave_levels = levels;
+  c->wave_n[k] = n;
+  c->wave_levels[k] = levels;
+  return PRT_OK;
+}
+
+// batches of the wavefront pipelines for n items: PRT_BATCHES (default 1: measured no faster),
+// at least PRT_BATCH_MIN (128k) items each
+int batches_for(uint64_t n) {
+  const char* e = std::getenv("PRT_BATCHES");
+  const char* m = std::getenv("PRT_BATCH_MIN");
+  int want = e ? std::atoi(e) : 1;
+  const uint64_t min_items = m ? (uint64_t)std::max(1, std::atoi(m)) : (128u << 10);
+  want = std::max(1, std::min(kMaxBatches, want));
+  while (want > 1 && n / (uint64_t)want < min_items) want--;
+  return want;
+}
+
+int ensure_batch_streams(prt_ctx* c, int nb) {
+  for (int k = 0; k < nb; k++) {
+    if (!c->bev[k] && hipEventCreateWithFlags(&c->bev[k], hipEventDisableTiming) != hipSuccess)
+      return fail(PRT_ERR_HIP, "hipEventCreate failed");
+    if (k > 0 && !c->bstream[k] && hipStreamCreateWithFlags(&c->bstream[k], hipStreamNonBlocking) != hipSuccess)
+      return fail(PRT_ERR_HIP, "hipStreamCreate failed");
+  }
   return PRT_OK;
 }
 
@@ -447,37 +475,47 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   const uint32_t iters = (uint32_t)p->bounces * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
   if (!mega && iters > (uint32_t)kMaxIters) return fail(PRT_ERR_UNSUPPORTED, "too many wavefront iterations");
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  int nb = 1;
   if (mega) {
     HIP_TRY(c->counters.ensure(sizeof(Counters)));
     HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
     HIP_TRY(launch_trace_frames(L, S, A, M, c->frames.as<float4>(), c->counters.as<Counters>()));
   } else {
-    rc = ensure_wave(c, (uint32_t)n, p->bounces);
+    nb = pipe == 3 ? 1 : batches_for(n);
+    rc = ensure_batch_streams(c, nb);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * kCtrWords, c->stream));
-    c->wb.tl = nullptr;
-    {
-      const char* e = std::getenv("PRT_TAIL");
-      c->wb.coop_tail = (e && std::strcmp(e, "0") == 0) ? 0 : 1;
+    const char* et = std::getenv("PRT_TAIL");
+    for (int k = 0; k < nb; k++) {  // consecutive item ranges, multiples of 256 items (the last one takes the rest)
+      const uint64_t b0 = k == 0 ? 0 : ((n * k / nb + 255) & ~255ull), b1 = k == nb - 1 ? n : ((n * (k + 1) / nb + 255) & ~255ull);
+      rc = ensure_wave(c, k, (uint32_t)(b1 - b0), p->bounces);
+      if (rc) return rc;
+      c->wb[k].base = (uint32_t)b0;
+      c->wb[k].tl = nullptr;
+      c->wb[k].coop_tail = (et && std::strcmp(et, "0") == 0) ? 0 : 1;
     }
     if (stats && std::getenv("PRT_DEBUG_QUEUES")) {
       const size_t tlb = 32ull * kTlWaves * (kMaxIters + 2);
       HIP_TRY(c->tl.ensure(tlb));
       HIP_TRY(hipMemsetAsync(c->tl.p, 0, tlb, c->stream));
-      c->wb.tl = c->tl.as<unsigned long long>();
+      c->wb[0].tl = c->tl.as<unsigned long long>();
+    }
+    if (nb > 1) {  // fork: the batch streams start after everything queued on `stream` so far
+      HIP_TRY(hipEventRecord(c->bev[0], c->stream));
+      for (int k = 1; k < nb; k++) HIP_TRY(hipStreamWaitEvent(c->bstream[k], c->bev[0], 0));
     }
     if (pipe == 3) {
+      HIP_TRY(hipMemsetAsync(c->wb[0].ctr, 0, 4 * kCtrWords, c->stream));
       // byte offsets of the sc1 buffer loads are 32-bit: R/T levels x n and the 4 x n shadow slots
-      if ((uint64_t)c->wave_levels * n * 16 >= (1ull << 32) || 64ull * n >= (1ull << 32))
+      if ((uint64_t)c->wave_levels[0] * n * 16 >= (1ull << 32) || 64ull * n >= (1ull << 32))
         return fail(PRT_ERR_UNSUPPORTED, "streaming engine: too many work items in one call (split spp)");
       int dev = 0, cus = 256;
       HIP_TRY(hipGetDevice(&dev));
       HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
       rc = ensure_stream(c, (uint32_t)n, iters, (uint32_t)cus * 4u * 5u);
       if (rc) return rc;
-      if (stats) HIP_TRY(hipEventRecord(c->wt.ev[0], c->stream));
-      HIP_TRY(launch_stream(L, S, A, M, c->wb, c->sb, c->frames.as<float4>()));
-      if (stats) HIP_TRY(hipEventRecord(c->wt.ev[1], c->stream));
+      if (stats) HIP_TRY(hipEventRecord(c->wt[0].ev[0], c->stream));
+      HIP_TRY(launch_stream(L, S, A, M, c->wb[0], c->sb, c->frames.as<float4>()));
+      if (stats) HIP_TRY(hipEventRecord(c->wt[0].ev[1], c->stream));
       uint32_t ctl[2] = {0, 0};
       HIP_TRY(hipMemcpyAsync(ctl, c->sb.ctl, 8, hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
@@ -485,8 +523,25 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
         static const char* what[] = {"?", "watchdog expired (PRT_STREAM_BUDGET_MS)", "queue overflow", "item state"};
         return fail(PRT_ERR_HIP, std::string("streaming engine aborted: ") + what[ctl[1] < 4 ? ctl[1] : 0]);
       }
-    } else if (pipe == 2) HIP_TRY(launch_wavefront2(L, S, A, M, c->wb, c->frames.as<float4>(), stats ? &c->wt : nullptr));
-    else HIP_TRY(launch_wavefront(L, S, A, M, c->wb, c->frames.as<float4>(), stats ? &c->wt : nullptr));
+    } else {
+      LaunchCfg Lk[kMaxBatches];
+      for (int k = 0; k < nb; k++) {
+        Lk[k] = L;
+        Lk[k].stream = k == 0 ? c->stream : c->bstream[k];
+        HIP_TRY(hipMemsetAsync(c->wb[k].ctr, 0, 4 * kCtrWords, Lk[k].stream));
+        float4* out = c->frames.as<float4>() + c->wb[k].base;
+        if (pipe == 2) HIP_TRY(launch_wave_init(Lk[k], S, A, M, c->wb[k], out));
+        else HIP_TRY(launch_wavefront(Lk[k], S, A, M, c->wb[k], out, stats ? &c->wt[k] : nullptr));
+      }
+      for (uint32_t it = 0; pipe == 2 && it <= iters; it++)  // merged pipeline: iterations round-robin over batches
+        for (int k = 0; k < nb; k++)
+          HIP_TRY(launch_wave2_iter(Lk[k], S, A, M, c->wb[k], c->frames.as<float4>() + c->wb[k].base,
+                                    stats ? &c->wt[k] : nullptr, it));
+      for (int k = 1; k < nb; k++) {  // join
+        HIP_TRY(hipEventRecord(c->bev[k], c->bstream[k]));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->bev[k], 0));
+      }
+    }
   }
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   // post-processing (single-GPU image): the screen pass needs the average and, for the aberration, the
@@ -527,33 +582,42 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
       stats->segments = h[0];
       stats->shadow_rays = h[1];
       float a = 0;
-      HIP_TRY(hipEventElapsedTime(&a, c->wt.ev[0], c->wt.ev[1]));
+      HIP_TRY(hipEventElapsedTime(&a, c->wt[0].ev[0], c->wt[0].ev[1]));
       stats->ms_closest = a;
       stats->pipeline = 3;
       stats->iterations = 1;
     } else {
+      // per-launch traversal times summed over every launch of every batch (batches may overlap in time)
       std::vector<uint32_t> ctr(kCtrWords);
-      HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
       const bool dump = std::getenv("PRT_DEBUG_QUEUES") != nullptr;
-      for (uint32_t k = 0; k < iters; k++) {
-        uint64_t qs = 0, qa = 0;
-        for (uint32_t s = 0; s < kNSub; s++) {
-          qs += ctr[((k * 2 + 0) * kNSub + s) * kCtrStride];
-          qa += ctr[((k * 2 + 1) * kNSub + s) * kCtrStride];
+      for (int bk = 0; bk < nb; bk++) {
+        HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb[bk].ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        const WaveTimers& wt = c->wt[bk];
+        for (uint32_t k = 0; k < iters; k++) {
+          uint64_t qs = 0, qa = 0;
+          for (uint32_t s = 0; s < kNSub; s++) {
+            qs += ctr[((k * 2 + 0) * kNSub + s) * kCtrStride];
+            qa += ctr[((k * 2 + 1) * kNSub + s) * kCtrStride];
+          }
+          stats->segments += qs;
+          stats->shadow_rays += qa;
+          float a = 0, b = 0;
+          HIP_TRY(hipEventElapsedTime(&a, wt.ev[4 * k + 0], wt.ev[4 * k + 1]));
+          if (pipe == 0) HIP_TRY(hipEventElapsedTime(&b, wt.ev[4 * k + 2], wt.ev[4 * k + 3]));
+          stats->ms_closest += a;
+          stats->ms_anyhit += b;
+          if (dump)
+            std::fprintf(stderr, "prt: batch %d iteration %u: %llu closest rays %.3f ms, %llu shadow rays %.3f ms\n", bk,
+                         k, (unsigned long long)qs, a, (unsigned long long)qa, b);
         }
-        stats->segments += qs;
-        stats->shadow_rays += qa;
-        float a = 0, b = 0;
-        HIP_TRY(hipEventElapsedTime(&a, c->wt.ev[4 * k + 0], c->wt.ev[4 * k + 1]));
-        if (pipe == 0) HIP_TRY(hipEventElapsedTime(&b, c->wt.ev[4 * k + 2], c->wt.ev[4 * k + 3]));
-        stats->ms_closest += a;
-        stats->ms_anyhit += b;
-        if (dump)
-          std::fprintf(stderr, "prt: iteration %u: %llu closest rays %.3f ms, %llu shadow rays %.3f ms\n", k,
-                       (unsigned long long)qs, a, (unsigned long long)qa, b);
+        if (pipe == 2) {  // one merged trace launch per iteration plus the final shadow-only one
+          float a = 0;
+          HIP_TRY(hipEventElapsedTime(&a, wt.ev[4 * iters + 0], wt.ev[4 * iters + 1]));
+          stats->ms_closest += a;
+        }
       }
-      if (dump && c->wb.tl && pipe == 2) {  // launch timeline: start -> queue drained -> last wave out (us)
+      if (dump && c->wb[0].tl && pipe == 2) {  // launch timeline of batch 0: start -> queue drained -> last wave out (us)
         std::vector<unsigned long long> t(4ull * kTlWaves * (kMaxIters + 2));
         HIP_TRY(hipMemcpy(t.data(), c->tl.p, 8 * t.size(), hipMemcpyDeviceToHost));
         for (uint32_t k = 0; k <= iters; k++) {
@@ -577,13 +641,9 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
                        q(0.99), ex.empty() ? 0.0 : ex.back());
         }
       }
-      if (pipe == 2) {  // one merged trace launch per iteration plus the final shadow-only one
-        float a = 0;
-        HIP_TRY(hipEventElapsedTime(&a, c->wt.ev[4 * iters + 0], c->wt.ev[4 * iters + 1]));
-        stats->ms_closest += a;
-      }
       stats->pipeline = pipe;
-      stats->iterations = (int32_t)(pipe == 2 ? iters + 1 : iters);
+      stats->iterations = (int32_t)(pipe == 2 ? iters + 1 : iters) * nb;  // traversal launches of all batches
+      stats->batches = nb;
     }
     float ms = 0, ms_trace = 0;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[2]));
@@ -644,12 +704,13 @@ int prt_create(const prt_device_desc* desc, prt_ctx** out) {
       return fail(PRT_ERR_HIP, "hipEventCreate failed");
     }
   }
-  for (auto& e : c->wt.ev) {  // per-launch timers only: no system-scope fence / cache writeback per record
-    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess && hipEventCreate(&e) != hipSuccess) {
-      delete c;
-      return fail(PRT_ERR_HIP, "hipEventCreate failed");
+  for (auto& wt : c->wt)
+    for (auto& e : wt.ev) {  // per-launch timers only: no system-scope fence / cache writeback per record
+      if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess && hipEventCreate(&e) != hipSuccess) {
+        delete c;
+        return fail(PRT_ERR_HIP, "hipEventCreate failed");
+      }
     }
-  }
   *out = c;
   return PRT_OK;
 }
@@ -664,9 +725,16 @@ int prt_destroy(prt_ctx* c) {
     b->release();
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);
-  for (auto e : c->wt.ev)
+  for (int k = 1; k < kMaxBatches; k++)
+    if (c->bstream[k]) (void)hipStreamSynchronize(c->bstream[k]);
+  for (auto& wt : c->wt)
+    for (auto e : wt.ev)
+      if (e) (void)hipEventDestroy(e);
+  for (auto e : c->bev)
     if (e) (void)hipEventDestroy(e);
-  c->wave.release();
+  for (auto& w : c->wave) w.release();
+  for (auto s : c->bstream)
+    if (s) (void)hipStreamDestroy(s);
   c->sq.release();
   c->sctl.release();
   c->accprev.release();

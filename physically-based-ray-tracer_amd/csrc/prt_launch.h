@@ -27,7 +27,8 @@ struct LaunchCfg {
 constexpr uint32_t kNSub = 32;       // sub-queues per queue (one append counter each)
 constexpr uint32_t kCtrStride = 32;  // words between counters (each on its own 128-B line)
 struct WaveBufs {
-  uint32_t n;
+  uint32_t n;       // items of this batch
+  uint32_t base;    // first item of this batch within the call (out / the state arrays are batch-local)
   uint32_t qcap;    // capacity of one path sub-queue  (multiple of 256)
   uint32_t scap;    // capacity of one shadow sub-queue (4 x qcap)
   uint32_t* seed;
@@ -86,6 +87,9 @@ hipError_t launch_wave_init(const LaunchCfg& c, const SceneDev& S, const TraceAr
 // merged pipeline (prt_wave2.hip): one traversal launch per iteration for P(i) closest + S(i-1) any-hit
 hipError_t launch_wavefront2(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                              const WaveBufs& B, float4* out, WaveTimers* tm);
+// its iteration `it` (0..iters) alone, after launch_wave_init: batches on several streams enqueue round-robin
+hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
+                             const WaveBufs& B, float4* out, WaveTimers* tm, uint32_t it);
 // streaming engine (prt_stream.hip): one persistent launch per frame batch, no per-bounce boundaries
 hipError_t launch_stream(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                          const WaveBufs& B, const StreamBufs& Q, float4* out);

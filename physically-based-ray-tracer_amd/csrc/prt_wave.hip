@@ -35,7 +35,8 @@ __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, T
     const uint32_t i = c * kBlock + threadIdx.x;
     bool enq = false;
     if (i < B.n) {
-      const uint32_t f = i / M.items, r = i % M.items;
+      const uint32_t gi = B.base + i;  // item index within the call (batches cover consecutive ranges)
+      const uint32_t f = gi / M.items, r = gi % M.items;
       int32_t x, y;
       const bool valid = item_pixel(M, r, x, y);
       if (valid && A.bounces > 0) {
@@ -346,7 +347,7 @@ __global__ void __launch_bounds__(kBlock) k_resolve(SceneDev S, TraceArgs A, Til
         const float4 s1 = B.s1[item];
         if (path == 0 && (fl & kAA)) {                                                       // start Trace(r2)
           B.s1[item] = make_float4(L.x, L.y, L.z, s1.w);
-          const uint32_t r = item % M.items;
+          const uint32_t r = (B.base + item) % M.items;
           int32_t x, y;
           item_pixel(M, r, x, y);
           const float2 j = B.jit[item];

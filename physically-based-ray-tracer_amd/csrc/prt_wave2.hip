@@ -113,7 +113,7 @@ __global__ void __launch_bounds__(kBlock) k_miss2(SceneDev S, TraceArgs A, WaveB
 __device__ __forceinline__ bool start_path2(const SceneDev& S, const TraceArgs& A, const TileMap& M,
                                             const WaveBufs& B, uint32_t item, uint32_t path) {
   if (path != 0 || !(A.flags & kAA)) return false;
-  const uint32_t r = item % M.items;
+  const uint32_t r = (B.base + item) % M.items;
   int32_t x, y;
   item_pixel(M, r, x, y);
   const float2 j = B.jit[item];
@@ -306,25 +306,34 @@ static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs&
   }
 }
 
-hipError_t launch_wavefront2(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
-                             const WaveBufs& B, float4* out, WaveTimers* tm) {
+// one iteration of the merged pipeline: trace P(it) + S(it - 1), resolve P(it - 1), miss + shade P(it)
+hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
+                             const WaveBufs& B, float4* out, WaveTimers* tm, uint32_t it) {
   if (B.n == 0) return hipSuccess;
   const unsigned gprod = 256u * 4u;  // producer blocks (multiple of kNSub)
-  hipError_t e = launch_wave_init(c, S, A, M, B, out);
-  if (e != hipSuccess) return e;
   const uint32_t iters = (uint32_t)A.bounces * ((A.flags & kAA) ? 2u : 1u);
-  for (uint32_t it = 0; it <= iters; it++) {
-    if (tm) (void)hipEventRecord(tm->ev[4 * it + 0], c.stream);
-    launch_trace2(c, S, B, it, iters);
-    if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
-    if (it > 0) hipLaunchKernelGGL(k_resolve2, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it - 1, out);
-    if (it == iters) break;
+  if (tm) (void)hipEventRecord(tm->ev[4 * it + 0], c.stream);
+  launch_trace2(c, S, B, it, iters);
+  if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
+  if (it > 0) hipLaunchKernelGGL(k_resolve2, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it - 1, out);
+  if (it < iters) {
     hipLaunchKernelGGL(k_miss2, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
     if (A.mode != 0) hipLaunchKernelGGL(k_shade2_debug, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
     else hipLaunchKernelGGL(k_shade2, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
   }
   if (tm) tm->iters = iters + 1;
   return hipGetLastError();
+}
+
+hipError_t launch_wavefront2(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
+                             const WaveBufs& B, float4* out, WaveTimers* tm) {
+  if (B.n == 0) return hipSuccess;
+  hipError_t e = launch_wave_init(c, S, A, M, B, out);
+  if (e != hipSuccess) return e;
+  const uint32_t iters = (uint32_t)A.bounces * ((A.flags & kAA) ? 2u : 1u);
+  for (uint32_t it = 0; it <= iters; it++)
+    if ((e = launch_wave2_iter(c, S, A, M, B, out, tm, it)) != hipSuccess) return e;
+  return hipSuccess;
 }
 
 }  // namespace prt

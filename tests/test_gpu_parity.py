@@ -117,6 +117,42 @@ def test_pipelines_identical(gpu_ctx, monkeypatch, flags):
         assert out[2][2].segments == out[code][2].segments and out[2][2].shadow_rays == out[code][2].shadow_rays
 
 
+@pytest.mark.parametrize("pipe", ["", "wave1"])
+def test_batches_identical(gpu_ctx, monkeypatch, pipe):
+    """Wavefront batches (consecutive item ranges on concurrent streams, PRT_BATCHES) render bit-identical
+    frames and ray counts for every batch count, including splits that end mid-frame and mid-tile."""
+    sd = scenes.multi_instance(scenes.config_small(60, 50))
+    W, H = 100, 75
+    gpu_scene(gpu_ctx, sd, W, H)
+    monkeypatch.setenv("PRT_BATCH_MIN", "1000")
+    if pipe:
+        monkeypatch.setenv("PRT_PIPELINE", pipe)
+    out = {}
+    for nb in (1, 2, 3, 4):
+        monkeypatch.setenv("PRT_BATCHES", str(nb))
+        gpu_ctx.reset_accumulation(full=True)
+        a, r, st = gpu_ctx.render(W, H, 4, 4, stats=True)
+        assert st.batches == nb
+        out[nb] = (a, r, st)
+        if nb > 1:
+            assert np.array_equal(out[1][0], a) and np.array_equal(out[1][1], r)
+            assert out[1][2].segments == st.segments and out[1][2].shadow_rays == st.shadow_rays
+    # one rank's tiles (world 3) rendered in 3 batches equal those pixels of the full frame
+    import torch
+    import prt
+    monkeypatch.setenv("PRT_BATCHES", "3")
+    per = gpu_ctx.tile_buffer_pixels(W, H, 16, 3)
+    pix = prt.tiles.tile_pixel_map(W, H, 16, 1, 3)
+    tiles = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
+    gpu_ctx.reset_accumulation(full=True)
+    st = gpu_ctx.render_tiles(W, H, 4, 4, 16, 1, 3, tiles.data_ptr(), stats=True)
+    torch.cuda.synchronize()
+    assert st.batches == 3
+    t = tiles.cpu().numpy()
+    ok = pix >= 0
+    assert np.array_equal(t[ok], out[1][0][pix[ok]])
+
+
 @pytest.mark.parametrize("mode", [1, 2, 3, 6])
 def test_stream_debug_modes(gpu_ctx, monkeypatch, mode):
     """Debug render modes (Core/Renderer.cpp:170-194) through the streaming engine match the merged pipeline."""
