@@ -68,18 +68,24 @@ def measured_traffic(kernel):
     return None
 
 
-def cpu_baseline(sd, threads):
-    """The oracle (C restatement, OpenMP over rows) on a bounded sample of the same workload."""
+def cpu_baseline(sd, threads, W, H, spp, bounces):
+    """The oracle (C restatement, OpenMP over rows) on a bounded sample of the same workload: the full frame
+    when it is <= ~40M rays (C4: ~29M rays, 10-30 s of CPU-core work), else a centred crop of the camera's
+    pixel grid with the same spp / depth (every pixel-frame is independent, so Mrays/s carries over)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    W, H = 1920, 1080  # the full C4 frame (4 spp, depth 4): ~29M rays, 10-30 s of CPU-core work
-    osc = oracle.OracleScene(sd, W, H)
+    scale = 1
+    while W * H * spp * bounces * 3 // (scale * scale) > 120_000_000:
+        scale *= 2
+    w, h = W // scale, H // scale
+    osc = oracle.OracleScene(sd, w, h)
     t0 = time.perf_counter()
-    _, _, _, st = osc.render(W, H, spp=4, bounces=4, nthreads=threads)
+    _, _, _, st = osc.render(w, h, spp=spp, bounces=bounces, nthreads=threads)
     dt = time.perf_counter() - t0
     rays = st.segments + st.shadow_rays
+    what = "the full frame" if scale == 1 else f"the same camera at {w}x{h} (1/{scale * scale} of the pixels)"
     return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"C4 scene at {W}x{H}, 4 spp, depth 4 ({rays} rays, {dt:.2f} s)"}
+            "sample": f"{sd.name}: {what}, {spp} spp, depth {bounces} ({rays} rays, {dt:.2f} s)"}
 
 
 def main():
@@ -87,11 +93,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=4)
-    ap.add_argument("--bounces", type=int, default=4)
-    ap.add_argument("--scene", default="c4", choices=["c3", "c4"])
+    ap.add_argument("--width", type=int, default=None, help="default 1920 (c3/c4), 3840 (c5)")
+    ap.add_argument("--height", type=int, default=None, help="default 1080 (c3/c4), 2160 (c5)")
+    ap.add_argument("--spp", type=int, default=None, help="default 4 (c3/c4), 16 (c5)")
+    ap.add_argument("--bounces", type=int, default=None, help="default 4 (c3/c4), 8 (c5)")
+    ap.add_argument("--scene", default="c4", choices=["c3", "c4", "c5"],
+                    help="c4 = the metric's workload (default); c5 = C4 + a quad area light with MIS at 4K, 16 spp, depth 8")
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-out", action="store_true",
@@ -113,7 +120,12 @@ def main():
     else:
         torch.cuda.set_device(0)
 
-    sd = scenes.config_c4() if args.scene == "c4" else scenes.config_c3()
+    sd = {"c3": scenes.config_c3, "c4": scenes.config_c4, "c5": scenes.config_c5}[args.scene]()
+    big = args.scene == "c5"
+    args.width = args.width or (3840 if big else 1920)
+    args.height = args.height or (2160 if big else 1080)
+    args.spp = args.spp or (16 if big else 4)
+    args.bounces = args.bounces if args.bounces is not None else (8 if big else 4)
     W, H = args.width, args.height
     ctx = prt.Context(local)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -131,15 +143,17 @@ def main():
     avg_h = np.zeros((H * W, 4), np.float32) if args.host_out else None
     rgb_h = np.zeros(H * W, np.uint32) if args.host_out else None
 
+    fpc = max(1, args.spp // 2)  # reference frames per call (AA: 2 paths each): distinct RNG streams per step
+
     def step(i):
         if world == 1 and args.host_out:
-            _, _, st = ctx.render(W, H, args.spp, args.bounces, frame_index=2 * i, avg=avg_h, rgb8=rgb_h,
+            _, _, st = ctx.render(W, H, args.spp, args.bounces, frame_index=fpc * i, avg=avg_h, rgb8=rgb_h,
                                   device_out=False, stats=True)
         elif world == 1:
-            _, _, st = ctx.render(W, H, args.spp, args.bounces, frame_index=2 * i, avg=avg.data_ptr(),
+            _, _, st = ctx.render(W, H, args.spp, args.bounces, frame_index=fpc * i, avg=avg.data_ptr(),
                                   rgb8=rgb.data_ptr(), device_out=True, stats=True)
         else:
-            st = shard.render(args.spp, args.bounces, avg.data_ptr(), rgb.data_ptr(), frame_index=2 * i)
+            st = shard.render(args.spp, args.bounces, avg.data_ptr(), rgb.data_ptr(), frame_index=fpc * i)
         return st
 
     for i in range(args.warmup):
@@ -208,7 +222,7 @@ def main():
                          "achieved": round(own_b / (kern_ms / 1e3) / 1e9, 1),
                          "frac": round(own_b / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
         out = {
-            "metric": "Mrays/s (closest-hit segments + shadow any-hit rays) at 1920x1080, 4 spp, depth 4",
+            "metric": f"Mrays/s (closest-hit segments + shadow any-hit rays) at {W}x{H}, {args.spp} spp, depth {args.bounces}",
             "value": round(value, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -241,7 +255,7 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(sd, threads)
+            out["cpu_baseline"] = cpu_baseline(sd, threads, W, H, args.spp, args.bounces)
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:

@@ -95,6 +95,25 @@ typedef struct {
     float spot_pos[3], spot_color[3], spot_rot[3];   /* spotlights[0]->transform        */
 } prt_lights;
 
+/* Instance material kinds (prt_set_instance_materials).  The reference's Scene::GetMaterialBRDF has a
+ * dielectric and a perfect-mirror branch gated on `modelIndex == -1`, which never holds (Core/Scene.cpp:
+ * 193-205, "Instead of -1 place model index"); here the caller names the instances that take them.
+ * DIELECTRIC takes Renderer::Trace's glass branch (Core/Renderer.cpp:331-372: reflection + refraction
+ * rays, Schlick-weighted, depth first); MIRROR forces metalness 1 / roughness 0 (the :376 fast path). */
+#define PRT_MAT_TEXTURED   0
+#define PRT_MAT_DIELECTRIC 1
+#define PRT_MAT_MIRROR     2
+
+/* One emitting parallelogram corner + a*edge_u + b*edge_v (a, b in [0,1]) -- an extension: the reference's
+ * AreaLight (Core/AreaLight.h) is never sampled by Trace.  Radiance on the side of cross(edge_u, edge_v)
+ * (both sides when two_sided); sampled by next-event estimation at every lit hit and reached by BRDF rays,
+ * combined with the power heuristic. */
+typedef struct {
+    float corner[3], edge_u[3], edge_v[3];
+    float radiance[3];
+    int32_t two_sided;
+} prt_area_light;
+
 /* Camera screen plane and basis (Core/Camera.cpp:29-36, 113-139; Core/Camera.h:15-17).  right / up /
  * ahead are only read by the Panini projection (post-processing on); prt_camera_look_at fills all. */
 typedef struct {
@@ -151,6 +170,12 @@ int prt_set_meshes(prt_ctx* ctx, const prt_mesh* meshes, int32_t count);
 /* transforms: 16*count floats, row-major BLASInstance::transform; mesh_index: count */
 int prt_set_instances(prt_ctx* ctx, const float* transforms, const uint32_t* mesh_index, int32_t count);
 int prt_set_lights(prt_ctx* ctx, const prt_lights* lights);
+/* kinds: one PRT_MAT_* per instance (count = the instance count), or count 0 = all textured.  Reset by
+ * prt_set_instances with a different instance count.  Dielectric instances need bounces <= 4 with AA (5 without): the depth-first path tree
+ * has up to 2^bounces - 1 segments per path. */
+int prt_set_instance_materials(prt_ctx* ctx, const int32_t* kinds, int32_t count);
+/* count 0 (none) or 1 */
+int prt_set_area_lights(prt_ctx* ctx, const prt_area_light* lights, int32_t count);
 /* float RGB equirect, w*h*3; NULL/0 = no sky (misses shade 0 even with PRT_FLAG_SKYBOX) */
 int prt_set_sky(prt_ctx* ctx, const float* rgb, int32_t width, int32_t height);
 int prt_set_camera(prt_ctx* ctx, const prt_camera* cam);

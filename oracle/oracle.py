@@ -58,6 +58,8 @@ def lib():
         L.orc_add_mesh.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 5 + [C.c_int32, C.c_void_p] + [C.c_int32] * 4
         L.orc_add_instance.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
         L.orc_set_lights.argtypes = [C.c_void_p] + [C.c_void_p] * 7
+        L.orc_set_instance_material.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+        L.orc_set_area_light.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 4 + [C.c_int32]
         L.orc_set_sky.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
         L.orc_set_camera.argtypes = [C.c_void_p] + [C.c_void_p] * 4
         L.orc_build.argtypes = [C.c_void_p]
@@ -140,6 +142,13 @@ class OracleScene:
         la = [f32(lt.point_pos), f32(lt.point_col), f32(lt.dir_pos), f32(lt.dir_col), f32(lt.spot_pos),
               f32(lt.spot_col), f32(lt.spot_rot)]
         L.orc_set_lights(self.h, *[a.ctypes.data for a in la])
+        for i, k in enumerate(getattr(sd, "materials", None) or []):
+            assert L.orc_set_instance_material(self.h, i, int(k)) == 0
+        al = getattr(sd, "area_light", None)
+        if al is not None:
+            arr = [f32(al[k]) for k in ("corner", "edge_u", "edge_v", "radiance")]
+            self._keep.extend(arr)
+            L.orc_set_area_light(self.h, 1, *[a.ctypes.data for a in arr], 1 if al.get("two_sided", False) else 0)
         if sd.sky is not None:
             sky = f32(sd.sky)
             L.orc_set_sky(self.h, sky.shape[1], sky.shape[0], sky.ctypes.data)

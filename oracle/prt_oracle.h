@@ -79,6 +79,15 @@ typedef struct {
     int (*anyhit)(void* user, const float* O, const float* D, const float* rD, float tmax);
 } orc_backend;
 
+/* extensions: instance material kinds (the reference's dead Scene.cpp:193-205 branches)
+ * and one area light (never sampled by the reference's Trace) */
+#define ORC_MAT_TEXTURED   0
+#define ORC_MAT_DIELECTRIC 1
+#define ORC_MAT_MIRROR     2
+int orc_set_instance_material(orc_scene* s, int32_t inst, int32_t kind);
+void orc_set_area_light(orc_scene* s, int32_t enabled, const float* corner3, const float* edge_u3, const float* edge_v3,
+                        const float* radiance3, int32_t two_sided);
+
 orc_scene* orc_scene_create(void);
 void orc_scene_destroy(orc_scene* s);
 int orc_add_texture(orc_scene* s, int32_t w, int32_t h, const uint32_t* pixels);

@@ -120,7 +120,11 @@ struct prt_ctx {
   // instances
   std::vector<float> inst_xf;
   std::vector<uint32_t> inst_mesh;
+  std::vector<uint32_t> inst_kind;  // prt_set_instance_materials (PRT_MAT_*), textured by default
   DevBuf inst;
+  // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
+  float al[16] = {};
+  int32_t area = 0, area_two_sided = 0;
   bool inst_dirty = true;
   // sky, lights, camera
   DevBuf sky;
@@ -141,6 +145,7 @@ struct prt_ctx {
   DevBuf wave[kMaxBatches];
   WaveBufs wb[kMaxBatches] = {};
   uint32_t wave_n[kMaxBatches] = {}, wave_levels[kMaxBatches] = {};
+  bool wave_ext[kMaxBatches] = {};
   WaveTimers wt[kMaxBatches] = {};
   hipStream_t bstream[kMaxBatches] = {};
   hipEvent_t bev[kMaxBatches] = {};
@@ -200,6 +205,7 @@ int ensure_instances(prt_ctx* c) {
     for (int r = 0; r < 4; r++)
       for (int k = 0; k < 4; k++) I.nrm[4 * r + k] = I.inv[4 * k + r];  // Inverted().Transposed()
     I.mesh = m;
+    I.kind = i < (int32_t)c->inst_kind.size() ? c->inst_kind[i] : 0u;
     const MeshHost& mh = c->mesh_info[m];
     float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
     for (int j = 0; j < 8; j++) {  // BLASInstance::Update: world AABB of the 8 root corners
@@ -263,6 +269,12 @@ int scene_ready(prt_ctx* c, SceneDev& S) {
   S.panini = c->pfx.enabled ? 1 : 0;
   S.pan_d = c->pfx.distortion;
   S.pan_b = panini_scale(c->pfx.fov, c->pfx.distortion);
+  std::memcpy(S.al, c->al, sizeof(S.al));
+  S.area = c->area;
+  S.area_two_sided = c->area_two_sided;
+  S.has_diel = 0;
+  for (size_t i = 0; i < c->inst_mesh.size() && i < c->inst_kind.size(); i++)
+    if (c->inst_kind[i] == kMatDielectric) S.has_diel = 1;
   return PRT_OK;
 }
 
@@ -312,38 +324,43 @@ int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
 // wavefront buffers sized for n items and (bounces-1) (result, throughput) stack levels
 // queue counters [iter][path|shadow][kNSub] + traversal fetch counters [iter][path|shadow][8 parts]
 constexpr size_t kCtrWords = (size_t)(kMaxIters + 2) * 2 * (kNSub + 8) * kCtrStride;
-int ensure_wave(prt_ctx* c, int k, uint32_t n, int bounces) {
+int ensure_wave(prt_ctx* c, int k, uint32_t n, int bounces, bool ext) {
   const uint32_t levels = (uint32_t)std::max(1, bounces - 1);
   // sub-queue t receives the 256-entry chunks c == t (mod kNSub): at most ceil(ceil(n/256)/kNSub) of them
   const uint32_t qcap = 256u * (((n + 255u) / 256u + kNSub - 1) / kNSub);
-  if (c->wave_n[k] >= n && c->wave_levels[k] >= levels && c->wave[k].p) {
+  if (c->wave_n[k] >= n && c->wave_levels[k] >= levels && (c->wave_ext[k] || !ext) && c->wave[k].p) {
     c->wb[k].n = n;  // capacity stays; the SoA strides (R/T: depth * n + item) follow the current n
     c->wb[k].qcap = qcap;
-    c->wb[k].scap = 4u * qcap;
+    c->wb[k].scap = 5u * qcap;
     return PRT_OK;
   }
-  const size_t qn = (size_t)kNSub * qcap, sn = 4 * qn;
+  const size_t qn = (size_t)kNSub * qcap, sn = 5 * qn;  // <= 4 light-class + 1 area-light shadow rays per item
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
   const size_t o_seed = take(4ull * n), o_info = take(4ull * n), o_rinfo = take(4ull * n), o_ro = take(16ull * n), o_rd = take(16ull * n),
                o_R = take(16ull * n * levels), o_T = take(16ull * n * levels), o_s1 = take(16ull * n),
                o_jit = take(8ull * n), o_hit = take(16ull * n), o_ne = take(16ull * n), o_nb = take(16ull * n),
-               o_nf = take(64ull * n), o_vis = take(4ull * n), o_q0 = take(4 * qn), o_q1 = take(4 * qn),
+               o_nf = take(64ull * n), o_vis = take(5ull * n), o_q0 = take(4 * qn), o_q1 = take(4 * qn),
                o_sho = take(16 * sn), o_shd = take(16 * sn), o_ctr = take(4 * kCtrWords);
+  const size_t o_na = ext ? take(16ull * n) : 0, o_dst = ext ? take(4ull * n) : 0,
+               o_dro = ext ? take(16ull * n * levels) : 0, o_drd = ext ? take(16ull * n * levels) : 0;
   HIP_TRY(c->wave[k].ensure(off));
   char* b = c->wave[k].as<char>();
   WaveBufs& W = c->wb[k];
   W.n = n;
   W.qcap = qcap;
-  W.scap = 4u * qcap;
+  W.scap = 5u * qcap;
   W.seed = (uint32_t*)(b + o_seed); W.info = (uint32_t*)(b + o_info); W.rinfo = (uint32_t*)(b + o_rinfo);
   W.ro = (float4*)(b + o_ro); W.rd = (float4*)(b + o_rd); W.R = (float4*)(b + o_R); W.T = (float4*)(b + o_T);
   W.s1 = (float4*)(b + o_s1); W.jit = (float2*)(b + o_jit); W.hit = (float4*)(b + o_hit);
   W.ne = (float4*)(b + o_ne); W.nb = (float4*)(b + o_nb); W.nf = (float4*)(b + o_nf); W.vis = (uint32_t*)(b + o_vis);
   W.q0 = (uint32_t*)(b + o_q0); W.q1 = (uint32_t*)(b + o_q1); W.sho = (float4*)(b + o_sho);
   W.shd = (float4*)(b + o_shd); W.ctr = (uint32_t*)(b + o_ctr);
+  W.na = ext ? (float4*)(b + o_na) : nullptr; W.dst = ext ? (uint32_t*)(b + o_dst) : nullptr;
+  W.dro = ext ? (float4*)(b + o_dro) : nullptr; W.drd = ext ? (float4*)(b + o_drd) : nullptr;
   c->wave_n[k] = n;
   c->wave_levels[k] = levels;
+  c->wave_ext[k] = ext;
   return PRT_OK;
 }
 
@@ -472,8 +489,14 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   int pipe = pipeline_from_env();
   if ((pipe == 2 || pipe == 3) && (layout == 4 || L.trav == 1)) pipe = 0;
   const bool mega = pipe == 1;
-  const uint32_t iters = (uint32_t)p->bounces * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
-  if (!mega && iters > (uint32_t)kMaxIters) return fail(PRT_ERR_UNSUPPORTED, "too many wavefront iterations");
+  // extensions (area light, dielectric instances) run on the merged pipeline only
+  const bool ext = (S.area || S.has_diel) && p->render_mode == 0;
+  if (ext && pipe != 2)
+    return fail(PRT_ERR_UNSUPPORTED, "area lights / dielectric instances need the merged pipeline (PRT_PIPELINE unset)");
+  const uint32_t iters = wave_iters(S.has_diel != 0, p->bounces, p->flags);
+  if (!mega && iters > (uint32_t)kMaxIters)
+    return fail(PRT_ERR_UNSUPPORTED, S.has_diel ? "dielectric path trees exceed the wavefront iteration limit (lower bounces)"
+                                                : "too many wavefront iterations");
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   int nb = 1;
   if (mega) {
@@ -487,7 +510,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     const char* et = std::getenv("PRT_TAIL");
     for (int k = 0; k < nb; k++) {  // consecutive item ranges, multiples of 256 items (the last one takes the rest)
       const uint64_t b0 = k == 0 ? 0 : ((n * k / nb + 255) & ~255ull), b1 = k == nb - 1 ? n : ((n * (k + 1) / nb + 255) & ~255ull);
-      rc = ensure_wave(c, k, (uint32_t)(b1 - b0), p->bounces);
+      rc = ensure_wave(c, k, (uint32_t)(b1 - b0), p->bounces, ext);
       if (rc) return rc;
       c->wb[k].base = (uint32_t)b0;
       c->wb[k].tl = nullptr;
@@ -529,6 +552,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
         Lk[k] = L;
         Lk[k].stream = k == 0 ? c->stream : c->bstream[k];
         HIP_TRY(hipMemsetAsync(c->wb[k].ctr, 0, 4 * kCtrWords, Lk[k].stream));
+        if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(c->wb[k].dst, 0, 4ull * c->wb[k].n, Lk[k].stream));
         float4* out = c->frames.as<float4>() + c->wb[k].base;
         if (pipe == 2) HIP_TRY(launch_wave_init(Lk[k], S, A, M, c->wb[k], out));
         else HIP_TRY(launch_wavefront(Lk[k], S, A, M, c->wb[k], out, stats ? &c->wt[k] : nullptr));
@@ -952,10 +976,48 @@ int prt_set_instances(prt_ctx* c, const float* xf, const uint32_t* mi, int32_t n
   if (!c || !xf || !mi || n <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad instances");
   if (n > kMaxInstances) return fail(PRT_ERR_UNSUPPORTED, "more than 64 instances");
   c->inst_xf.assign(xf, xf + 16 * (size_t)n);
+  if ((size_t)n != c->inst_mesh.size()) c->inst_kind.clear();  // materials survive transform updates only
   c->inst_mesh.assign(mi, mi + n);
   c->inst_dirty = true;
   HIP_TRY(hipSetDevice(c->device));
   if (!c->mesh_host.empty()) return ensure_instances(c);
+  return PRT_OK;
+}
+
+int prt_set_instance_materials(prt_ctx* c, const int32_t* kinds, int32_t n) {
+  if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  if (n == 0 || !kinds) {
+    c->inst_kind.clear();
+  } else {
+    if (n != (int32_t)c->inst_mesh.size()) return fail(PRT_ERR_INVALID_ARGUMENT, "one material kind per instance");
+    for (int32_t i = 0; i < n; i++)
+      if (kinds[i] < PRT_MAT_TEXTURED || kinds[i] > PRT_MAT_MIRROR) return fail(PRT_ERR_INVALID_ARGUMENT, "bad material kind");
+    c->inst_kind.assign(kinds, kinds + n);
+  }
+  c->inst_dirty = true;
+  HIP_TRY(hipSetDevice(c->device));
+  if (!c->mesh_host.empty() && !c->inst_mesh.empty()) return ensure_instances(c);
+  return PRT_OK;
+}
+
+int prt_set_area_lights(prt_ctx* c, const prt_area_light* a, int32_t n) {
+  if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  if (n < 0 || n > 1 || (n == 1 && !a)) return fail(PRT_ERR_UNSUPPORTED, "at most one area light");
+  if (n == 0) {
+    c->area = 0;
+    return PRT_OK;
+  }
+  const float* u = a->edge_u;
+  const float* v = a->edge_v;
+  const float cx = u[1] * v[2] - u[2] * v[1], cy = u[2] * v[0] - u[0] * v[2], cz = u[0] * v[1] - u[1] * v[0];
+  const float area = sqrtf(cx * cx + cy * cy + cz * cz);
+  if (!(area > 0.0f)) return fail(PRT_ERR_INVALID_ARGUMENT, "degenerate area light");
+  const float inv = 1.0f / sqrtf(cx * cx + cy * cy + cz * cz);  // normalize(): v * (1 / sqrtf(dot(v, v)))
+  const float al[16] = {a->corner[0], a->corner[1], a->corner[2], u[0], u[1], u[2], v[0], v[1], v[2],
+                        cx * inv, cy * inv, cz * inv, a->radiance[0], a->radiance[1], a->radiance[2], area};
+  std::memcpy(c->al, al, sizeof(al));
+  c->area = 1;
+  c->area_two_sided = a->two_sided ? 1 : 0;
   return PRT_OK;
 }
 

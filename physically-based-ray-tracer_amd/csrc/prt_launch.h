@@ -50,6 +50,13 @@ struct WaveBufs {
   float4* sho;      // shadow queue: O, tmax
   float4* shd;      // shadow queue: D, bits(4 * item + slot)
   uint32_t* ctr;    // [iteration][path|shadow][sub-queue] counters, kCtrStride apart
+  // extensions (area light / dielectric instances; merged pipeline only): vis holds 5 x n bytes, the area
+  // light's shadow ray writes byte 4 * n + item
+  float4* na;       // area-light NEE contribution before visibility
+  uint32_t* dst;    // dielectric DFS state: bits 0-7 dielectric level, 8-15 refraction started,
+                    // 16-23 reflected radiance stored (in T[level]), 24-31 no refraction (k <= 0)
+  float4* dro;      // per level: refraction ray origin, fresnel
+  float4* drd;      // per level: refraction ray direction
   unsigned long long* tl;  // PRT_DEBUG_QUEUES: [launch][wave] {start, first empty fetch, exit, -}
   int32_t coop_tail;       // cooperative traversal tail (prt_persist.h); PRT_TAIL=0 turns it off
 };
@@ -74,9 +81,16 @@ constexpr size_t kStreamCtlWords = (size_t)(2 + kMaxParts) * kCtrStride;
 constexpr size_t kStreamCtrWords = (size_t)kMaxParts * 4 * kSSub * kCtrStride;
 
 constexpr int kMaxIters = 32;
+// wavefront iterations of one call: one per path segment, paths x bounces; with dielectric instances a path
+// is a binary tree walked depth first (one segment per iteration), at most 2^bounces - 1 segments per path
+inline uint32_t wave_iters(bool dielectric, int bounces, uint32_t flags) {
+  const uint32_t paths = (flags & 1u) ? 2u : 1u;  // PRT_FLAG_AA: two camera paths per reference frame
+  if (!dielectric) return paths * (uint32_t)bounces;
+  return bounces >= 6 ? 0xFFFFFFFFu : paths * ((1u << bounces) - 1u);
+}
 constexpr int kTlWaves = 256 * 4 * 8;  // timeline records per traversal launch (max persistent grid)
 struct WaveTimers {
-  hipEvent_t ev[4 * kMaxIters];
+  hipEvent_t ev[4 * (kMaxIters + 1)];
   uint32_t iters;
 };
 

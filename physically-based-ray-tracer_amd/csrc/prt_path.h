@@ -123,12 +123,15 @@ __device__ __forceinline__ V3 nee_resolve(int kind, uint32_t vis, V3 e, V3 brdf,
 }
 
 // lobe pick + BRDF sampling (Core/Renderer.cpp:376-404).  Returns false when the path ends here.
-__device__ __forceinline__ bool sample_bounce(const Material& m, V3 V, V3 N, uint32_t& seed, V3& dir, V3& thr) {
+// bp_out (optional) receives the lobe probability; it is left alone on the perfect-mirror fast path.
+__device__ __forceinline__ bool sample_bounce(const Material& m, V3 V, V3 N, uint32_t& seed, V3& dir, V3& thr,
+                                             float* bp_out = nullptr) {
   int type = 1;
   thr = v3(1.0f, 1.0f, 1.0f);
   if (m.metal == 1.0f && m.rough == 0.0f) type = 2;                                         // :376
   else {
     const float bp = brdf_probability(m, V, N);                                             // :380
+    if (bp_out) *bp_out = bp;
     if (random_float(seed) < bp) { type = 2; thr = thr / bp; }
     else { type = 1; thr = thr / (1.0f - bp); }
   }
@@ -139,6 +142,141 @@ __device__ __forceinline__ bool sample_bounce(const Material& m, V3 V, V3 N, uin
   if (!eval_indirect_brdf(u, N, V, m, type, dir, wgt)) return false;                       // :398
   thr = thr * wgt;
   return true;
+}
+
+
+// ---- dielectrics (Core/Renderer.cpp:331-372, refract :522-550).  The reference gates this branch on a
+// material flag its Scene never sets (Core/Scene.cpp:193-197 tests modelIndex == -1); here an instance
+// flagged PRT_MAT_DIELECTRIC takes it, restated literally (the refract() helper receives eta = n1/n2 as the
+// material index, so entering rays bend by 1.46 and a negative k returns a zero direction).
+struct Dielectric {
+  Ray refl, refr;   // reflection ray, refraction ray (direction 0 when refract() reports total reflection)
+  float fresnel;    // weight of the reflected radiance; 1 - fresnel weighs the refracted one
+  bool has_refr;    // k > 0 (:349-357): the refracted ray is traced
+};
+PRT_HD V3 refract_ref(V3 D, V3 N, float eta) {                                             // :522-550
+  const float cosi = clampf(dot(D, N), -1.0f, 1.0f);
+  float etai = 1.0f, etat = eta;
+  if (cosi > 0.0f) { const float t = etai; etai = etat; etat = t; }
+  const float etaRatio = etai / etat;
+  const float cosTheta = fabsf(cosi);
+  const float k = 1.0f - etaRatio * etaRatio * (1.0f - cosTheta * cosTheta);
+  if (k < 0.0f) return v3(0.0f, 0.0f, 0.0f);
+  return etaRatio * (D - N * cosTheta) - N * sqrtf(k);
+}
+__device__ __forceinline__ Dielectric dielectric_split(V3 I, V3 D, V3 N) {
+  Dielectric o;
+  const float n1 = 1.0f, n2 = 1.46f;                                                        // :336-337
+  const float cosTheta = clampf(-dot(D, N), 0.0f, 1.0f);                                   // :340
+  o.refl = make_ray(I + N * kEpsilon, reflect(D, N));                                       // :343-346
+  const float eta = n1 / n2;                                                                // :349
+  const float k = 1.0f - eta * eta * (1.0f - cosTheta * cosTheta);                          // :350
+  o.has_refr = k > 0.0f;
+  o.refr = make_ray(I - N * kEpsilon, refract_ref(D, N, eta));                              // :353-358
+  const float R0 = ((n1 - n2) / (n1 + n2)) * ((n1 - n2) / (n1 + n2));                      // :362
+  o.fresnel = R0 + (1.0f - R0) * cr_pow(1.0f - cosTheta, 5.0f);                            // :363
+  if (k <= 0.0f) o.fresnel = 1.0f;                                                          // :366
+  return o;
+}
+// albedo * (fresnel * reflected + (1 - fresnel) * refracted), albedo = float3(1) (:369)
+PRT_HD V3 dielectric_combine(float fresnel, V3 reflected, V3 refracted) {
+  return v3(1.0f, 1.0f, 1.0f) * (fresnel * reflected + (1.0f - fresnel) * refracted);
+}
+
+// ---- area light (extension beyond the reference: Core/AreaLight.cpp defines the light but Trace never
+// samples it).  One emitting parallelogram p0 + a*eu + b*ev, a, b in [0,1], radiance Le on the side of
+// n = normalize(cross(eu, ev)) (both sides when two-sided).  Every shaded hit of a lit render samples it
+// once (next-event estimation, 2 extra draws) and BRDF-sampled rays that reach it first see Le; the two
+// strategies are combined with the power heuristic.  Paths end at the light; it casts no shadow for the
+// reference's lights.  Same arithmetic in oracle/prt_oracle.c.
+struct AreaLight {
+  V3 p0, eu, ev, n, le;
+  float area;
+  int two_sided;
+};
+__device__ __forceinline__ AreaLight area_light(const SceneDev& S) {
+  AreaLight A;
+  A.p0 = v3(S.al[0], S.al[1], S.al[2]);
+  A.eu = v3(S.al[3], S.al[4], S.al[5]);
+  A.ev = v3(S.al[6], S.al[7], S.al[8]);
+  A.n = v3(S.al[9], S.al[10], S.al[11]);
+  A.le = v3(S.al[12], S.al[13], S.al[14]);
+  A.area = S.al[15];
+  A.two_sided = S.area_two_sided;
+  return A;
+}
+// ray vs parallelogram (Moller-Trumbore on the triangle p0, p0+eu, p0+ev with a, b each in [0, 1]):
+// t in (0, tmax) -> true, with cos_l = the emitting-side cosine (<= 0 means the back of a one-sided light)
+PRT_HD bool area_hit(const AreaLight& A, V3 O, V3 D, float tmax, float& t, float& cos_l) {
+  const V3 h = cross(D, A.ev);
+  const float det = dot(A.eu, h);
+  if (fabsf(det) < 1e-12f) return false;
+  const float f = 1.0f / det;
+  const V3 s = O - A.p0;
+  const float a = f * dot(s, h);
+  if (a < 0.0f || a > 1.0f) return false;
+  const V3 q = cross(s, A.eu);
+  const float b = f * dot(D, q);
+  if (b < 0.0f || b > 1.0f) return false;
+  t = f * dot(A.ev, q);
+  if (!(t > 0.0f && t < tmax)) return false;
+  cos_l = -dot(A.n, D);
+  if (A.two_sided) cos_l = fabsf(cos_l);
+  return true;
+}
+PRT_HD float mis_power(float a, float b) {  // a^2 / (a^2 + b^2); an infinite b (delta strategy) gives 0
+  const float a2 = a * a, b2 = b * b;
+  return a2 / (a2 + b2);
+}
+// solid-angle density of the BRDF sampling at this vertex (Core/Renderer.cpp:376-399): lobe pick p_spec,
+// cosine hemisphere (BRDF.cpp:62-82), GGX VNDF (BRDF.cpp:224-269, alpha = roughness^2)
+PRT_HD float brdf_pdf(const Material& m, V3 N, V3 V, V3 L, float p_spec) {
+  const V3 Nn = normalize(N);
+  const float NdotL = dot(Nn, L);
+  if (NdotL <= 0.0f) return 0.0f;
+  const float pd = NdotL * (1.0f / kPi);
+  const V3 H = normalize(L + V);
+  const float NdotV = smin(smax(0.00001f, dot(Nn, V)), 1.0f);
+  const float NdotH = saturate(dot(Nn, H));
+  const float alpha = m.rough * m.rough;
+  const float a2 = smax(0.00001f, alpha * alpha);
+  const float b = ((a2 - 1.0f) * NdotH * NdotH + 1.0f);
+  const float D = a2 / (kPi * b * b);
+  const float G1 = 2.0f * NdotV / (NdotV + sqrtf(a2 + (1.0f - a2) * (NdotV * NdotV)));
+  const float ps = D * G1 / (4.0f * NdotV);
+  return p_spec * ps + (1.0f - p_spec) * pd;
+}
+// the BRDF lobe probability used above: 1 for the perfect-mirror fast path (:376), else getBrdfProbability
+PRT_HD bool delta_lobe(const Material& m) { return m.metal == 1.0f && m.rough == 0.0f; }
+
+
+// next-event estimation of the area light at a shaded hit: false when the sample faces away (no ray);
+// else the shadow ray, its tmax and the unoccluded contribution BRDF * Le * w_light / p_light
+__device__ __forceinline__ bool area_nee(const AreaLight& A, V3 I, V3 N, V3 V, const Material& m, float xi1, float xi2,
+                                         Ray& sr, float& tmax, V3& f) {
+  const V3 y = A.p0 + xi1 * A.eu + xi2 * A.ev;
+  V3 L = y - I;
+  const float dsq = dot(L, L);
+  const float dist = sqrtf(dsq);
+  L = L / dist;
+  float cos_l = -dot(A.n, L);
+  if (A.two_sided) cos_l = fabsf(cos_l);
+  if (!(cos_l > 0.0f) || !(dot(N, L) > 0.0f)) return false;
+  const float pl = dsq / (A.area * cos_l);
+  const float pb = brdf_pdf(m, N, V, L, brdf_probability(m, V, N));
+  const float w = mis_power(pl, pb);
+  f = eval_combined_brdf(N, L, V, m) * (A.le * (w / pl));
+  sr = make_ray(I + L * kEpsilon, L);
+  tmax = dist - kEpsilon;
+  return true;
+}
+// radiance a ray sees when it reaches the light first: Le weighted against light sampling at the vertex
+// that sampled it (pdf_prev = its brdf_pdf; kFar for camera rays, delta lobes, dielectric rays, unlit)
+__device__ __forceinline__ V3 area_seen(const AreaLight& A, float t, float cos_l, float pdf_prev) {
+  if (!(cos_l > 0.0f)) return v3(0.0f, 0.0f, 0.0f);
+  if (pdf_prev >= kFar) return A.le;
+  const float pl = (t * t) / (A.area * cos_l);
+  return A.le * mis_power(pdf_prev, pl);
 }
 
 // RGBF32_to_RGB8 (template/precomp.h:310-315, scalar path)

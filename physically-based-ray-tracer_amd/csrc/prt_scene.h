@@ -21,8 +21,9 @@ struct InstDev {
   float bmin[3];   // world AABB of the BLAS root (BLASInstance::Update), inflated
   uint32_t mesh;
   float bmax[3];
-  uint32_t pad;
+  uint32_t kind;   // instance material: kMatTextured / kMatDielectric / kMatMirror (Core/Scene.cpp:193-205)
 };
+enum : uint32_t { kMatTextured = 0, kMatDielectric = 1, kMatMirror = 2 };
 
 // one primitive's shading inputs (Core/Scene.cpp:47-218 reads them from five arrays; here one line)
 struct alignas(16) ShadeTri {
@@ -74,6 +75,12 @@ struct SceneDev {
   float pan_b, pan_d;
   int32_t panini;
   int32_t pad1;
+  // extensions beyond the reference's Trace: one area light, dielectric instances
+  float al[16];     // p0, eu, ev, n = normalize(cross(eu, ev)), Le, area
+  int32_t area;     // 1 = the area light is set
+  int32_t area_two_sided;
+  int32_t has_diel; // some instance is kMatDielectric
+  int32_t pad2;
 };
 
 }  // namespace prt

@@ -156,6 +156,7 @@ __device__ __forceinline__ float srgb1(float c) {  // :256-263
 struct HitAttr {
   V3 N;        // shading normal
   Material m;
+  uint32_t kind;  // instance material kind (kMatDielectric takes Trace's dielectric branch)
 };
 
 // uv = v*uv2 + u*uv1 + w*uv0 (Scene.cpp:75-77,156-158); texel index with ALBEDO dims (:79-85,160-165)
@@ -221,6 +222,12 @@ __device__ __forceinline__ HitAttr hit_attributes(const SceneDev& S, uint32_t in
     out.m.metal = (float)(rma & 255) * sc;
   }
   if (M.tex[3] >= 0) out.m.emis = texel_color(S.texels[S.tex[M.tex[3]].offset + px]);
+  out.kind = I.kind;
+  if (I.kind == kMatMirror) {  // perfect mirror (:199-204): base colour kept, emission never set
+    out.m.metal = 1.0f;
+    out.m.rough = 0.0f;
+    out.m.emis = v3(0.0f, 0.0f, 0.0f);
+  }
   return out;
 }
 

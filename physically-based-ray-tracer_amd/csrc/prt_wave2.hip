@@ -89,7 +89,9 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   if (tl && threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
 
-// ---- misses of P(iter) (:159): sky radiance (or 0) into ne, before k_shade2 replaces the ray
+// ---- misses of P(iter) (:159): sky radiance (or 0) into ne, before k_shade2 replaces the ray.  EXT: a ray
+// that reaches the area light before any geometry ends there (ne = its MIS-weighted radiance, hit = miss).
+template <bool EXT>
 __global__ void __launch_bounds__(kBlock) k_miss2(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter) {
   __shared__ uint32_t pref[kNSub + 1];
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
@@ -98,7 +100,23 @@ __global__ void __launch_bounds__(kBlock) k_miss2(SceneDev S, TraceArgs A, WaveB
     const uint32_t g = c * kBlock + threadIdx.x;
     if (g >= total) continue;
     const uint32_t item = q[map_slot(pref, g, B.qcap)];
-    if (B.hit[item].x < kFar) continue;
+    float4 hh = B.hit[item];
+    if constexpr (EXT) {
+      if (S.area) {
+        const float4 o = B.ro[item], d = B.rd[item];
+        const AreaLight AL = area_light(S);
+        float tq, cl;
+        if (area_hit(AL, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), hh.x, tq, cl)) {
+          const uint32_t depth = B.info[item] & 0xFFu;
+          const float pdf = depth == 0 ? kFar : B.T[(size_t)(depth - 1) * B.n + item].w;
+          const V3 L = area_seen(AL, tq, cl, pdf);
+          B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
+          B.hit[item] = make_float4(kFar, 0.0f, 0.0f, 0.0f);
+          continue;
+        }
+      }
+    }
+    if (hh.x < kFar) continue;
     V3 L = v3(0.0f, 0.0f, 0.0f);
     if (A.flags & kSkybox) {
       const float4 d = B.rd[item];
@@ -124,7 +142,24 @@ __device__ __forceinline__ bool start_path2(const SceneDev& S, const TraceArgs& 
   return true;
 }
 
+// the sub-path of `item` ends at this iteration (EXT): continue with the refraction ray of the deepest
+// dielectric node whose reflection subtree this was (the reference's depth-first recursion order,
+// Core/Renderer.cpp:346 before :358) -- returns true when a ray was set up for P(iter + 1)
+__device__ __forceinline__ bool diel_next(const WaveBufs& B, uint32_t item, uint32_t depth, uint32_t path) {
+  uint32_t ds = B.dst[item];
+  const uint32_t pend = ds & ~(ds >> 8) & ~(ds >> 24) & 0xFFu & ((1u << depth) - 1u);
+  if (!pend) return false;
+  const uint32_t k = 31u - (uint32_t)__builtin_clz(pend);
+  const float4 o = B.dro[(size_t)k * B.n + item], d = B.drd[(size_t)k * B.n + item];
+  B.ro[item] = make_float4(o.x, o.y, o.z, 0.0f);
+  B.rd[item] = make_float4(d.x, d.y, d.z, 0.0f);
+  B.info[item] = (k + 1u) | (path << 8);
+  B.dst[item] = ds | (1u << (8 + k));
+  return true;
+}
+
 // ---- shading of P(iter): NEE set-up -> S(iter), BRDF sample or path-2 start -> P(iter + 1)
+template <bool EXT>
 __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, TileMap M, WaveBufs B, uint32_t iter) {
   __shared__ uint32_t pref[kNSub + 1];
   __shared__ uint32_t sm[8];
@@ -158,6 +193,8 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
     const uint32_t depth = info & 0xFFu, path = (info >> 8) & 1u;
     uint32_t status = kStMiss;
     bool next = false;
+    bool area_ray = false;
+    float4 ar_o, ar_d;
     if (nr) {
       const float4 o = B.ro[item], d = B.rd[item];
       const V3 D = v3(d.x, d.y, d.z);
@@ -175,23 +212,68 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
       B.nb[item] = make_float4(brdf.x, brdf.y, brdf.z, 0.0f);
       B.vis[item] = 0u;
       status = kStNeeEnd;
+      if constexpr (EXT) {
+        // area-light sample (2 draws after the light-class NEE draws) at lit, non-delta, non-dielectric hits
+        reinterpret_cast<uint8_t*>(B.vis)[4 * (size_t)B.n + item] = 0;
+        if (S.area && (fl & kLighted) && ha.kind != kMatDielectric && !delta_lobe(ha.m)) {
+          const float xi1 = random_float(seed), xi2 = random_float(seed);
+          Ray sr;
+          float tmax;
+          V3 fa;
+          if (area_nee(area_light(S), I, ha.N, V, ha.m, xi1, xi2, sr, tmax, fa)) {
+            area_ray = true;
+            ar_o = make_float4(sr.O.x, sr.O.y, sr.O.z, tmax);
+            ar_d = make_float4(sr.D.x, sr.D.y, sr.D.z, __uint_as_float(4u * B.n + item));
+            B.na[item] = make_float4(fa.x, fa.y, fa.z, 0.0f);
+          }
+        }
+      }
       if ((int)depth != A.bounces - 1) {                                                     // :329
-        V3 dir, thr;
-        if (sample_bounce(ha.m, V, ha.N, seed, dir, thr)) {                                  // :376-399
+        if (EXT && ha.kind == kMatDielectric) {                                              // :331-372
+          const Dielectric dl = dielectric_split(I, D, ha.N);
+          const size_t e = (size_t)depth * B.n + item;
+          B.dro[e] = make_float4(dl.refr.O.x, dl.refr.O.y, dl.refr.O.z, dl.fresnel);
+          B.drd[e] = make_float4(dl.refr.D.x, dl.refr.D.y, dl.refr.D.z, 0.0f);
+          B.T[e] = make_float4(0.0f, 0.0f, 0.0f, kFar);  // w: the continuation is not BRDF-sampled
+          const uint32_t bit = 1u << depth, keep = ~(0x01010101u << depth);
+          B.dst[item] = (B.dst[item] & keep) | bit | (dl.has_refr ? 0u : (bit << 24));
           status = kStNeeCont;
-          B.T[(size_t)depth * B.n + item] = make_float4(thr.x, thr.y, thr.z, 0.0f);
-          const Ray nr2 = make_ray(I + dir * kEpsilon, dir);                                 // :404
-          B.ro[item] = make_float4(nr2.O.x, nr2.O.y, nr2.O.z, 0.0f);
-          B.rd[item] = make_float4(nr2.D.x, nr2.D.y, nr2.D.z, 0.0f);
+          B.ro[item] = make_float4(dl.refl.O.x, dl.refl.O.y, dl.refl.O.z, 0.0f);
+          B.rd[item] = make_float4(dl.refl.D.x, dl.refl.D.y, dl.refl.D.z, 0.0f);
           B.info[item] = (depth + 1u) | (path << 8);
           next = true;
+        } else {
+          V3 dir, thr;
+          float bp = 2.0f;
+          if (sample_bounce(ha.m, V, ha.N, seed, dir, thr, EXT ? &bp : nullptr)) {           // :376-399
+            status = kStNeeCont;
+            float pdf = 0.0f;
+            if constexpr (EXT)  // MIS density of the sampled direction (kFar: delta lobe or no light sampling)
+              pdf = (bp > 1.0f || !S.area || !(fl & kLighted)) ? kFar : brdf_pdf(ha.m, ha.N, V, dir, bp);
+            B.T[(size_t)depth * B.n + item] = make_float4(thr.x, thr.y, thr.z, pdf);
+            const Ray nr2 = make_ray(I + dir * kEpsilon, dir);                               // :404
+            B.ro[item] = make_float4(nr2.O.x, nr2.O.y, nr2.O.z, 0.0f);
+            B.rd[item] = make_float4(nr2.D.x, nr2.D.y, nr2.D.z, 0.0f);
+            B.info[item] = (depth + 1u) | (path << 8);
+            next = true;
+          }
         }
       }
       B.seed[item] = seed;
     }
+    if constexpr (EXT) {  // the area-light shadow rays of the block, one more append
+      const uint32_t a0 = block_append(shcnt, area_ray ? 1u : 0u, sm);
+      if (area_ray) {
+        sho[a0] = ar_o;
+        shd[a0] = ar_d;
+      }
+    }
     if (active) {
       B.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20);
-      if (status != kStNeeCont) next = start_path2(S, A, M, B, item, path);
+      if (status != kStNeeCont) {
+        if (EXT && S.has_diel) next = diel_next(B, item, depth, path);
+        if (!next) next = start_path2(S, A, M, B, item, path);
+      }
     }
     const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
     if (next) qn[sub * B.qcap + slot] = item;
@@ -232,6 +314,7 @@ __global__ void __launch_bounds__(kBlock) k_shade2_debug(SceneDev S, TraceArgs A
 }
 
 // ---- NEE resolve of P(iter) (after k_trace2(iter + 1) traced S(iter)), stack, path end, frame write
+template <bool EXT>
 __global__ void __launch_bounds__(kBlock) k_resolve2(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter,
                                                      float4* __restrict__ out) {
   __shared__ uint32_t pref[kNSub + 1];
@@ -261,16 +344,53 @@ __global__ void __launch_bounds__(kBlock) k_resolve2(SceneDev S, TraceArgs A, Wa
           f[k] = v3(0.0f, 0.0f, 0.0f);
         }
       }
-      const V3 result = nee_resolve((int)kind, vis, L, v3(nb.x, nb.y, nb.z), f, fl);
+      V3 result = nee_resolve((int)kind, vis, L, v3(nb.x, nb.y, nb.z), f, fl);
+      if constexpr (EXT) {
+        if (reinterpret_cast<const uint8_t*>(B.vis)[4 * (size_t)B.n + item]) {  // area light unoccluded
+          const float4 a = B.na[item];
+          result = result + v3(a.x, a.y, a.z);
+        }
+      }
       if (status == kStNeeCont) {  // the path goes on: result joins the stack
         B.R[(size_t)depth * B.n + item] = make_float4(result.x, result.y, result.z, 0.0f);
         continue;
       }
       L = result;
     }
-    for (int k = (int)depth - 1; k >= 0; k--) {                                              // result + Trace(..) * throughput
-      const float4 Rk = B.R[(size_t)k * B.n + item], Tk = B.T[(size_t)k * B.n + item];
-      L = v3(Rk.x, Rk.y, Rk.z) + L * v3(Tk.x, Tk.y, Tk.z);
+    if constexpr (EXT) {
+      // unwind through dielectric nodes: the end of a reflection subtree parks its radiance in T[level] and
+      // stops (the refraction subtree is already queued); the end of a refraction subtree combines (:369)
+      uint32_t ds = S.has_diel ? B.dst[item] : 0u;
+      bool parked = false;
+      for (int k = (int)depth - 1; k >= 0; k--) {
+        const size_t e = (size_t)k * B.n + item;
+        const uint32_t bit = 1u << k;
+        if (ds & bit) {
+          const float F = B.dro[e].w;
+          if (ds & (bit << 24)) {
+            L = dielectric_combine(F, L, v3(0.0f, 0.0f, 0.0f));
+          } else if (!(ds & (bit << 16))) {
+            B.T[e] = make_float4(L.x, L.y, L.z, kFar);
+            ds |= bit << 16;
+            parked = true;
+            break;
+          } else {
+            const float4 Lr = B.T[e];
+            L = dielectric_combine(F, v3(Lr.x, Lr.y, Lr.z), L);
+          }
+          ds &= ~(0x01010101u << k);
+          continue;
+        }
+        const float4 Rk = B.R[e], Tk = B.T[e];
+        L = v3(Rk.x, Rk.y, Rk.z) + L * v3(Tk.x, Tk.y, Tk.z);
+      }
+      if (S.has_diel) B.dst[item] = ds;
+      if (parked) continue;
+    } else {
+      for (int k = (int)depth - 1; k >= 0; k--) {                                            // result + Trace(..) * throughput
+        const float4 Rk = B.R[(size_t)k * B.n + item], Tk = B.T[(size_t)k * B.n + item];
+        L = v3(Rk.x, Rk.y, Rk.z) + L * v3(Tk.x, Tk.y, Tk.z);
+      }
     }
     const float4 s1 = B.s1[item];
     if (path == 0 && (fl & kAA)) {  // path 2 was queued by k_shade2; keep path 1's radiance
@@ -311,15 +431,21 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
                              const WaveBufs& B, float4* out, WaveTimers* tm, uint32_t it) {
   if (B.n == 0) return hipSuccess;
   const unsigned gprod = 256u * 4u;  // producer blocks (multiple of kNSub)
-  const uint32_t iters = (uint32_t)A.bounces * ((A.flags & kAA) ? 2u : 1u);
+  const uint32_t iters = wave_iters(S.has_diel != 0, A.bounces, A.flags);
   if (tm) (void)hipEventRecord(tm->ev[4 * it + 0], c.stream);
   launch_trace2(c, S, B, it, iters);
   if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
-  if (it > 0) hipLaunchKernelGGL(k_resolve2, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it - 1, out);
+  const bool ext = (S.area || S.has_diel) && A.mode == 0;
+  if (it > 0) {
+    if (ext) hipLaunchKernelGGL(k_resolve2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it - 1, out);
+    else hipLaunchKernelGGL(k_resolve2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it - 1, out);
+  }
   if (it < iters) {
-    hipLaunchKernelGGL(k_miss2, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
+    if (ext) hipLaunchKernelGGL(k_miss2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
+    else hipLaunchKernelGGL(k_miss2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
     if (A.mode != 0) hipLaunchKernelGGL(k_shade2_debug, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
-    else hipLaunchKernelGGL(k_shade2, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
+    else if (ext) hipLaunchKernelGGL(k_shade2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
+    else hipLaunchKernelGGL(k_shade2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
   }
   if (tm) tm->iters = iters + 1;
   return hipGetLastError();
@@ -330,7 +456,7 @@ hipError_t launch_wavefront2(const LaunchCfg& c, const SceneDev& S, const TraceA
   if (B.n == 0) return hipSuccess;
   hipError_t e = launch_wave_init(c, S, A, M, B, out);
   if (e != hipSuccess) return e;
-  const uint32_t iters = (uint32_t)A.bounces * ((A.flags & kAA) ? 2u : 1u);
+  const uint32_t iters = wave_iters(S.has_diel != 0, A.bounces, A.flags);
   for (uint32_t it = 0; it <= iters; it++)
     if ((e = launch_wave2_iter(c, S, A, M, B, out, tm, it)) != hipSuccess) return e;
   return hipSuccess;

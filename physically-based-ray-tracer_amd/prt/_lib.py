@@ -25,7 +25,11 @@ EXPORTS = [
     "prt_camera_look_at", "prt_postfx_preset", "prt_set_postfx", "prt_render", "prt_reset_accumulation", "prt_tile_buffer_pixels", "prt_tile_pixel_map",
     "prt_render_tiles",
     "prt_untile", "prt_trace_primary", "prt_intersect", "prt_occluded", "prt_get_scene_info", "prt_set_bvh_builder",
+    "prt_set_instance_materials", "prt_set_area_lights",
 ]
+
+# instance material kinds (prt_set_instance_materials; the reference's dead Scene.cpp:193-205 branches)
+MAT_TEXTURED, MAT_DIELECTRIC, MAT_MIRROR = 0, 1, 2
 
 
 class PrtError(RuntimeError):
@@ -51,6 +55,11 @@ class Lights(C.Structure):
     _fields_ = [("point_pos", (C.c_float * 3) * 4), ("point_color", (C.c_float * 3) * 4),
                 ("dir_pos", C.c_float * 3), ("dir_color", C.c_float * 3),
                 ("spot_pos", C.c_float * 3), ("spot_color", C.c_float * 3), ("spot_rot", C.c_float * 3)]
+
+
+class AreaLight(C.Structure):
+    _fields_ = [("corner", C.c_float * 3), ("edge_u", C.c_float * 3), ("edge_v", C.c_float * 3),
+                ("radiance", C.c_float * 3), ("two_sided", C.c_int32)]
 
 
 class CameraDesc(C.Structure):
@@ -132,6 +141,8 @@ def load():
         "prt_occluded": ([vp, i32, vp, vp, vp, vp], C.c_int),
         "prt_get_scene_info": ([vp, C.POINTER(SceneInfo)], C.c_int),
         "prt_set_bvh_builder": ([vp, i32], C.c_int),
+        "prt_set_instance_materials": ([vp, vp, i32], C.c_int),
+        "prt_set_area_lights": ([vp, C.POINTER(AreaLight), i32], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -92,6 +92,8 @@ class Scene:
         self.directionalLights = []
         self.spotlights = []
         self.sky = None           # (h, w, 3) float32
+        self.materials = None     # per-blas material kind (_lib.MAT_*), None = all textured (Scene.cpp:193-205)
+        self.areaLights = []      # at most one dict(corner, edge_u, edge_v, radiance, two_sided) (AreaLight.h)
 
     @classmethod
     def from_data(cls, sd):
@@ -104,6 +106,8 @@ class Scene:
         s.directionalLights = [LightTransform(_f32(lt.dir_pos), _f32(lt.dir_col))]
         s.spotlights = [LightTransform(_f32(lt.spot_pos), _f32(lt.spot_col), _f32(lt.spot_rot))]
         s.sky = sd.sky
+        s.materials = list(sd.materials) if sd.materials is not None else None
+        s.areaLights = [dict(sd.area_light)] if sd.area_light is not None else []
         return s
 
     @property
@@ -158,6 +162,8 @@ class Context:
         xf = _f32(np.stack([T for _, T in scene.blases]).reshape(-1))
         mi = np.ascontiguousarray([m for m, _ in scene.blases], np.uint32)
         check(L.prt_set_instances(self.h, xf.ctypes.data, mi.ctypes.data, len(scene.blases)))
+        self.set_materials(scene.materials)
+        self.set_area_light(scene.areaLights[0] if scene.areaLights else None)
         lt = _lib.Lights()
         for i in range(4):
             lt.point_pos[i][:] = [float(v) for v in scene.pointLights[i].position]
@@ -174,6 +180,27 @@ class Context:
             check(L.prt_set_sky(self.h, sky.ctypes.data, sky.shape[1], sky.shape[0]))
         else:
             check(L.prt_set_sky(self.h, None, 0, 0))
+
+    def set_materials(self, kinds=None):
+        """Per-instance material kinds (_lib.MAT_TEXTURED / MAT_DIELECTRIC / MAT_MIRROR), None = all textured."""
+        if kinds is None:
+            check(self.L.prt_set_instance_materials(self.h, None, 0))
+            return
+        k = np.ascontiguousarray(kinds, np.int32)
+        check(self.L.prt_set_instance_materials(self.h, k.ctypes.data, len(k)))
+
+    def set_area_light(self, al=None):
+        """One area light (dict: corner, edge_u, edge_v, radiance, two_sided) or None."""
+        if al is None:
+            check(self.L.prt_set_area_lights(self.h, None, 0))
+            return
+        a = _lib.AreaLight()
+        a.corner[:] = [float(v) for v in al["corner"]]
+        a.edge_u[:] = [float(v) for v in al["edge_u"]]
+        a.edge_v[:] = [float(v) for v in al["edge_v"]]
+        a.radiance[:] = [float(v) for v in al["radiance"]]
+        a.two_sided = 1 if al.get("two_sided", False) else 0
+        check(self.L.prt_set_area_lights(self.h, C.byref(a), 1))
 
     def set_camera(self, cam: Camera):
         check(self.L.prt_set_camera(self.h, C.byref(cam.desc)))

@@ -64,6 +64,10 @@ class SceneData:
     cam_pos: np.ndarray
     cam_target: np.ndarray
     name: str = ""
+    # extensions: per-instance material kinds (_lib.MAT_*; None = all textured) and one
+    # area light {"corner", "edge_u", "edge_v", "radiance": (3,) float32, "two_sided": bool} (None = none)
+    materials: list | None = None
+    area_light: dict | None = None
 
     @property
     def tri_count(self) -> int:
@@ -231,6 +235,25 @@ def multi_instance(base: SceneData) -> SceneData:
         return M.astype(F32)
     inst = list(base.instances) + [(0, trs((1.5, 0.6, 2.0), 0.7, 0.35)), (0, trs((-1.8, 0.9, 1.0), -0.4, 0.25))]
     return dataclasses.replace(base, instances=inst, name=base.name + "+inst")
+
+
+def ceiling_light(corner=(-1.5, 4.0, -1.0), edge_u=(3.0, 0.0, 0.0), edge_v=(0.0, 0.0, 2.0), radiance=(8.0, 7.0, 6.0),
+                  two_sided=False) -> dict:
+    """One quad area light (extension; the reference's AreaLight is never sampled): by default a 3 x 2 panel
+    4 units above the heightfield, emitting downwards (cross(edge_u, edge_v) points to -y)."""
+    return {"corner": np.asarray(corner, F32), "edge_u": np.asarray(edge_u, F32), "edge_v": np.asarray(edge_v, F32),
+            "radiance": np.asarray(radiance, F32), "two_sided": bool(two_sided)}
+
+
+def with_extensions(base: SceneData, materials=None, area_light=None) -> SceneData:
+    """base with per-instance material kinds (_lib.MAT_*) and/or an area light."""
+    return dataclasses.replace(base, materials=list(materials) if materials is not None else None,
+                               area_light=area_light, name=base.name + "+ext")
+
+
+def config_c5() -> SceneData:
+    """C5 (BASELINE configs[4]): the C4 scene plus one quad area light (3840x2160, 16 spp, depth 8)."""
+    return dataclasses.replace(config_c4(), area_light=ceiling_light(), name="c5-heightfield1m-arealight")
 
 
 REFERENCE_ROOT = os.environ.get("PRT_REFERENCE_ROOT", "/root/reference")

@@ -1,0 +1,163 @@
+"""dielectric / perfect-mirror instances and the area light with MIS.
+
+The reference gates its dielectric and mirror branches on a condition that never holds
+(Core/Scene.cpp:193-205) and never samples its AreaLight, so no reference output pins these paths
+("parity unpinned" against reference binaries).  The oracle restates them (oracle/prt_oracle.c
+trace_ext: the reference's own recursion, reflection before refraction); the CPU tests below pin the
+restatement by properties the reference code implies, and the GPU tests check the HIP path against it
+(bar: per-channel RMSE <= 1e-4, in practice bit-exact)."""
+import numpy as np
+import pytest
+
+import oracle
+from helpers import RMSE_TOL, gpu_scene, rmse
+from prt import _lib, scenes
+
+F32 = np.float32
+NO_AA = oracle.DEFAULT_FLAGS & ~oracle.AA
+
+
+def _base():
+    return scenes.multi_instance(scenes.config_small(40, 30))
+
+
+def _facing_light():
+    """A two-sided 1 x 1 panel between the camera (0.3, 3, -7) and the origin: the centre pixel sees it."""
+    return scenes.ceiling_light(corner=(-0.5, 1.0, -3.5), edge_u=(1.0, 0.0, 0.0), edge_v=(0.0, 1.0, 0.0),
+                                radiance=(3.0, 2.0, 1.0), two_sided=True)
+
+
+def test_extensions_off_is_the_reference_path():
+    """All-textured materials and no area light render bit-identically to the plain scene."""
+    W, H = 48, 32
+    a0, r0, _, s0 = oracle.OracleScene(_base(), W, H).render(W, H, spp=2, bounces=3)
+    sd = scenes.with_extensions(_base(), materials=[0, 0, 0])
+    a1, r1, _, s1 = oracle.OracleScene(sd, W, H).render(W, H, spp=2, bounces=3)
+    assert np.array_equal(a0, a1) and np.array_equal(r0, r1)
+    assert (s0.segments, s0.shadow_rays) == (s1.segments, s1.shadow_rays)
+
+
+def test_area_light_seen_directly():
+    """A camera ray that reaches the light first returns its radiance with weight 1 (no NEE at the camera):
+    with AA off, 1 spp and gamma on, the centre pixel is exactly sqrt(Le)."""
+    W, H = 48, 32
+    sd = scenes.with_extensions(_base(), area_light=_facing_light())
+    avg, _, _, st = oracle.OracleScene(sd, W, H).render(W, H, spp=1, bounces=3, flags=NO_AA)
+    c = (H // 2) * W + W // 2
+    assert np.array_equal(avg[c, :3], np.sqrt(np.asarray([3.0, 2.0, 1.0], F32)))
+    assert st.segments >= W * H
+
+
+def test_area_light_adds_energy_and_rays():
+    """The light only adds radiance (both strategies are non-negative) and one shadow ray per lit,
+    light-facing hit.  One path per pixel and one segment, so its two draws shift no later draw."""
+    W, H = 48, 32
+    base = _base()
+    sd = scenes.with_extensions(base, area_light=scenes.ceiling_light())
+    a0, _, _, s0 = oracle.OracleScene(base, W, H).render(W, H, spp=1, bounces=1, flags=NO_AA)
+    a1, _, _, s1 = oracle.OracleScene(sd, W, H).render(W, H, spp=1, bounces=1, flags=NO_AA)
+    assert s1.segments == s0.segments
+    assert s0.shadow_rays < s1.shadow_rays <= s0.shadow_rays + s0.segments
+    assert np.all(a1[:, :3] >= a0[:, :3]) and float(np.mean(a1[:, :3] - a0[:, :3])) > 1e-3
+
+
+def test_mirror_material_debug_views():
+    """A MIRROR instance reads metalness 1, roughness 0, no emission (Scene.cpp:199-204); the others keep
+    their texture values."""
+    W, H = 48, 32
+    base = _base()
+    sd = scenes.with_extensions(base, materials=[0, 2, 0])
+    _, _, _, _, inst = oracle.OracleScene(base, W, H).primary_hits(W, H)
+    hit1 = inst == 1
+    assert hit1.sum() > 20
+    for mode, val in ((4, 1.0), (5, 0.0), (6, 0.0)):
+        plain, _, _, _ = oracle.OracleScene(base, W, H).render(W, H, spp=1, bounces=1, flags=NO_AA & ~oracle.GAMMA,
+                                                              mode=mode)
+        mir, _, _, _ = oracle.OracleScene(sd, W, H).render(W, H, spp=1, bounces=1, flags=NO_AA & ~oracle.GAMMA,
+                                                            mode=mode)
+        assert np.all(mir[hit1, :3] == F32(val))
+        assert np.array_equal(mir[~hit1], plain[~hit1])
+
+
+def test_dielectric_path_tree():
+    """A dielectric heightfield turns every non-terminal hit into two sub-paths (Renderer.cpp:331-372):
+    more segments than the plain estimator can fire, never more than the full binary tree, finite output."""
+    W, H, B = 32, 24, 3
+    base = _base()
+    sd = scenes.with_extensions(base, materials=[1, 0, 0])
+    a0, _, _, s0 = oracle.OracleScene(base, W, H).render(W, H, spp=1, bounces=B, flags=NO_AA)
+    a1, _, _, s1 = oracle.OracleScene(sd, W, H).render(W, H, spp=1, bounces=B, flags=NO_AA)
+    assert s1.segments > s0.segments
+    assert s1.segments <= W * H * (2 ** B - 1)
+    assert np.all(np.isfinite(a1)) and not np.array_equal(a0, a1)
+
+
+# ---------------------------------------------------------------- GPU vs oracle
+CASES = {
+    "dielectric": dict(materials=[0, 1, 0]),
+    "mirror": dict(materials=[0, 2, 0]),
+    "area": dict(area_light="ceiling"),
+    "area_facing": dict(area_light="facing"),
+    "all": dict(materials=[1, 2, 0], area_light="ceiling"),
+}
+
+
+def _ext_scene(case):
+    kw = dict(CASES[case])
+    al = kw.pop("area_light", None)
+    if al is not None:
+        kw["area_light"] = scenes.ceiling_light() if al == "ceiling" else _facing_light()
+    return scenes.with_extensions(_base(), **kw)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(CASES))
+@pytest.mark.parametrize("flags", [oracle.DEFAULT_FLAGS, NO_AA & ~oracle.STOCHASTIC])
+def test_extensions_match_oracle(gpu_ctx, case, flags):
+    sd = _ext_scene(case)
+    W, H = 64, 48
+    spp = 4 if flags & oracle.AA else 2
+    gpu_scene(gpu_ctx, sd, W, H)
+    a_o, r_o, _, s_o = oracle.OracleScene(sd, W, H).render(W, H, spp=spp, bounces=4, flags=flags)
+    a_g, r_g, s_g = gpu_ctx.render(W, H, spp, 4, flags)
+    err = rmse(a_o, a_g)
+    exact = float(np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)))
+    assert err <= RMSE_TOL, (case, err, exact)
+    assert exact >= 0.999, (case, exact)
+    assert (s_o.segments, s_o.shadow_rays) == (s_g.segments, s_g.shadow_rays)
+
+
+@pytest.mark.gpu
+def test_extensions_tiles_match_full_frame(gpu_ctx):
+    """Pixel-tile sharding with dielectric + mirror + area light: one rank's tiles equal the full frame."""
+    import torch
+    import prt
+    sd = _ext_scene("all")
+    W, H = 70, 50
+    gpu_scene(gpu_ctx, sd, W, H)
+    a_full, _, _ = gpu_ctx.render(W, H, 4, 4)
+    per = gpu_ctx.tile_buffer_pixels(W, H, 16, 2)
+    pix = prt.tiles.tile_pixel_map(W, H, 16, 1, 2)
+    tiles = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
+    gpu_ctx.reset_accumulation(full=True)
+    gpu_ctx.render_tiles(W, H, 4, 4, 16, 1, 2, tiles.data_ptr())
+    torch.cuda.synchronize()
+    ok = pix >= 0
+    assert np.array_equal(tiles.cpu().numpy()[ok], a_full[pix[ok]])
+
+
+@pytest.mark.gpu
+def test_extensions_refusals(gpu_ctx, monkeypatch):
+    """The extensions run on the merged pipeline only; dielectric path trees beyond the iteration limit
+    are refused, not truncated."""
+    sd = _ext_scene("all")
+    W, H = 32, 24
+    gpu_scene(gpu_ctx, sd, W, H)
+    with pytest.raises(_lib.PrtError):
+        gpu_ctx.render(W, H, 2, 6)  # 2 paths x 63 segments > 32 iterations
+    for pipe in ("mega", "wave1", "stream"):
+        monkeypatch.setenv("PRT_PIPELINE", pipe)
+        with pytest.raises(_lib.PrtError):
+            gpu_ctx.render(W, H, 2, 3)
+    monkeypatch.delenv("PRT_PIPELINE")
+    gpu_ctx.render(W, H, 2, 3)
