@@ -75,7 +75,7 @@ def cpu_baseline(sd, threads, W, H, spp, bounces):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     scale = 1
-    while W * H * spp * bounces * 3 // (scale * scale) > 120_000_000:
+    while W * H * spp * bounces // (scale * scale) > 300_000_000:
         scale *= 2
     w, h = W // scale, H // scale
     osc = oracle.OracleScene(sd, w, h)
@@ -212,7 +212,7 @@ def main():
         dom = max(kern, key=lambda k: kern[k][1])
         alg_bytes, kern_ms = kern[dom]
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-        traffic = measured_traffic(dom)
+        traffic = measured_traffic(dom) if args.scene == "c4" else None  # the committed PMC passes are of C4
         own = own_layout_bytes_per_ray()
         own_block = None
         if own is not None and pipeline in (0, 2, 3):
