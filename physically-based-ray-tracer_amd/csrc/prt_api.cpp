@@ -15,6 +15,7 @@
 #include "bvh_build.h"
 #include "bvh_gpu.h"
 #include "prt_launch.h"
+#include "prt_refit.h"
 
 using namespace prt;
 
@@ -64,33 +65,6 @@ hipError_t upload(DevBuf& b, const void* src, size_t n) {
   return hipSuccess;
 }
 
-// MESA 4x4 inverse (template/tmpl8math.h:701-746 == BLASInstance::InvertTransform, tiny_bvh.h:7883-7905)
-void mesa_inverse(const float* c, float* out) {
-  float inv[16];
-  inv[0] = c[5] * c[10] * c[15] - c[5] * c[11] * c[14] - c[9] * c[6] * c[15] + c[9] * c[7] * c[14] + c[13] * c[6] * c[11] - c[13] * c[7] * c[10];
-  inv[1] = -c[1] * c[10] * c[15] + c[1] * c[11] * c[14] + c[9] * c[2] * c[15] - c[9] * c[3] * c[14] - c[13] * c[2] * c[11] + c[13] * c[3] * c[10];
-  inv[2] = c[1] * c[6] * c[15] - c[1] * c[7] * c[14] - c[5] * c[2] * c[15] + c[5] * c[3] * c[14] + c[13] * c[2] * c[7] - c[13] * c[3] * c[6];
-  inv[3] = -c[1] * c[6] * c[11] + c[1] * c[7] * c[10] + c[5] * c[2] * c[11] - c[5] * c[3] * c[10] - c[9] * c[2] * c[7] + c[9] * c[3] * c[6];
-  inv[4] = -c[4] * c[10] * c[15] + c[4] * c[11] * c[14] + c[8] * c[6] * c[15] - c[8] * c[7] * c[14] - c[12] * c[6] * c[11] + c[12] * c[7] * c[10];
-  inv[5] = c[0] * c[10] * c[15] - c[0] * c[11] * c[14] - c[8] * c[2] * c[15] + c[8] * c[3] * c[14] + c[12] * c[2] * c[11] - c[12] * c[3] * c[10];
-  inv[6] = -c[0] * c[6] * c[15] + c[0] * c[7] * c[14] + c[4] * c[2] * c[15] - c[4] * c[3] * c[14] - c[12] * c[2] * c[7] + c[12] * c[3] * c[6];
-  inv[7] = c[0] * c[6] * c[11] - c[0] * c[7] * c[10] - c[4] * c[2] * c[11] + c[4] * c[3] * c[10] + c[8] * c[2] * c[7] - c[8] * c[3] * c[6];
-  inv[8] = c[4] * c[9] * c[15] - c[4] * c[11] * c[13] - c[8] * c[5] * c[15] + c[8] * c[7] * c[13] + c[12] * c[5] * c[11] - c[12] * c[7] * c[9];
-  inv[9] = -c[0] * c[9] * c[15] + c[0] * c[11] * c[13] + c[8] * c[1] * c[15] - c[8] * c[3] * c[13] - c[12] * c[1] * c[11] + c[12] * c[3] * c[9];
-  inv[10] = c[0] * c[5] * c[15] - c[0] * c[7] * c[13] - c[4] * c[1] * c[15] + c[4] * c[3] * c[13] + c[12] * c[1] * c[7] - c[12] * c[3] * c[5];
-  inv[11] = -c[0] * c[5] * c[11] + c[0] * c[7] * c[9] + c[4] * c[1] * c[11] - c[4] * c[3] * c[9] - c[8] * c[1] * c[7] + c[8] * c[3] * c[5];
-  inv[12] = -c[4] * c[9] * c[14] + c[4] * c[10] * c[13] + c[8] * c[5] * c[14] - c[8] * c[6] * c[13] - c[12] * c[5] * c[10] + c[12] * c[6] * c[9];
-  inv[13] = c[0] * c[9] * c[14] - c[0] * c[10] * c[13] - c[8] * c[1] * c[14] + c[8] * c[2] * c[13] + c[12] * c[1] * c[10] - c[12] * c[2] * c[9];
-  inv[14] = -c[0] * c[5] * c[14] + c[0] * c[6] * c[13] + c[4] * c[1] * c[14] - c[4] * c[2] * c[13] - c[12] * c[1] * c[6] + c[12] * c[2] * c[5];
-  inv[15] = c[0] * c[5] * c[10] - c[0] * c[6] * c[9] - c[4] * c[1] * c[10] + c[4] * c[2] * c[9] + c[8] * c[1] * c[6] - c[8] * c[2] * c[5];
-  const float det = c[0] * inv[0] + c[1] * inv[4] + c[2] * inv[8] + c[3] * inv[12];
-  if (det != 0) {
-    const float invdet = 1.0f / det;
-    for (int i = 0; i < 16; i++) out[i] = inv[i] * invdet;
-  } else {
-    for (int i = 0; i < 16; i++) out[i] = (i % 5 == 0) ? 1.0f : 0.0f;
-  }
-}
 
 struct MeshHost {
   float bmin[3], bmax[3];
@@ -121,7 +95,8 @@ struct prt_ctx {
   std::vector<float> inst_xf;
   std::vector<uint32_t> inst_mesh;
   std::vector<uint32_t> inst_kind;  // prt_set_instance_materials (PRT_MAT_*), textured by default
-  DevBuf inst;
+  std::vector<InstSrc> inst_stage;  // host side of the refit input (prt_refit.h)
+  DevBuf inst, inst_src;
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
   float al[16] = {};
   int32_t area = 0, area_two_sided = 0;
@@ -191,41 +166,28 @@ int layout_from_env() {
   return 8;
 }
 
+// instance refit on the device (prt_refit.h): one async copy of the transforms + k_refit, both on the
+// render stream, so frames already queued keep reading the previous instances
 int ensure_instances(prt_ctx* c) {
   if (!c->inst_dirty) return PRT_OK;
   const int32_t n = (int32_t)c->inst_mesh.size();
-  std::vector<InstDev> host(n);
+  std::vector<InstSrc>& src = c->inst_stage;
+  src.assign(n, InstSrc{});
   for (int32_t i = 0; i < n; i++) {
-    InstDev& I = host[i];
-    std::memset(&I, 0, sizeof(I));
-    const float* T = &c->inst_xf[16 * (size_t)i];
+    InstSrc& s = src[i];
     const uint32_t m = c->inst_mesh[i];
     if (m >= c->mesh_host.size()) return fail(PRT_ERR_INVALID_ARGUMENT, "instance references a missing mesh");
-    mesa_inverse(T, I.inv);
-    for (int r = 0; r < 4; r++)
-      for (int k = 0; k < 4; k++) I.nrm[4 * r + k] = I.inv[4 * k + r];  // Inverted().Transposed()
-    I.mesh = m;
-    I.kind = i < (int32_t)c->inst_kind.size() ? c->inst_kind[i] : 0u;
+    std::memcpy(s.T, &c->inst_xf[16 * (size_t)i], sizeof(s.T));
     const MeshHost& mh = c->mesh_info[m];
-    float lo[3] = {1e30f, 1e30f, 1e30f}, hi[3] = {-1e30f, -1e30f, -1e30f};
-    for (int j = 0; j < 8; j++) {  // BLASInstance::Update: world AABB of the 8 root corners
-      const float p[3] = {j & 1 ? mh.bmax[0] : mh.bmin[0], j & 2 ? mh.bmax[1] : mh.bmin[1],
-                          j & 4 ? mh.bmax[2] : mh.bmin[2]};
-      float t[3];
-      for (int r = 0; r < 3; r++) t[r] = T[4 * r] * p[0] + T[4 * r + 1] * p[1] + T[4 * r + 2] * p[2] + T[4 * r + 3];
-      const float w = T[12] * p[0] + T[13] * p[1] + T[14] * p[2] + T[15];
-      if (w != 1)
-        for (int r = 0; r < 3; r++) t[r] = t[r] * (1.f / w);
-      for (int r = 0; r < 3; r++) { lo[r] = std::min(lo[r], t[r]); hi[r] = std::max(hi[r], t[r]); }
-    }
-    for (int r = 0; r < 3; r++) {  // generous inflation: the TLAS test must be conservative
-      const float ext = std::max(std::fabs(lo[r]), std::fabs(hi[r]));
-      const float pad = ext * 1e-5f + 1e-6f;
-      I.bmin[r] = lo[r] - pad;
-      I.bmax[r] = hi[r] + pad;
-    }
+    std::memcpy(s.bmin, mh.bmin, sizeof(s.bmin));
+    std::memcpy(s.bmax, mh.bmax, sizeof(s.bmax));
+    s.mesh = m;
+    s.kind = i < (int32_t)c->inst_kind.size() ? c->inst_kind[i] : 0u;
   }
-  HIP_TRY(upload(c->inst, host.data(), sizeof(InstDev) * host.size()));
+  HIP_TRY(c->inst.ensure(sizeof(InstDev) * kMaxInstances));
+  HIP_TRY(c->inst_src.ensure(sizeof(InstSrc) * kMaxInstances));
+  HIP_TRY(hipMemcpyAsync(c->inst_src.p, src.data(), sizeof(InstSrc) * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(launch_refit(c->stream, c->inst_src.as<InstSrc>(), n, c->inst.as<InstDev>()));
   c->inst_dirty = false;
   return PRT_OK;
 }
@@ -743,7 +705,7 @@ int prt_destroy(prt_ctx* c) {
   if (!c) return PRT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->texels, &c->tex, &c->nodes, &c->nodes8, &c->nodes8h, &c->tris, &c->stri,
+  for (DevBuf* b : {&c->texels, &c->tex, &c->inst_src, &c->nodes, &c->nodes8, &c->nodes8h, &c->tris, &c->stri,
                     &c->mesh, &c->inst, &c->sky, &c->srgb, &c->acc, &c->nsamp, &c->dist, &c->frames, &c->avg, &c->rgb8,
                     &c->counters, &c->hits, &c->tl})
     b->release();

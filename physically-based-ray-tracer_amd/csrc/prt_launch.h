@@ -120,6 +120,9 @@ hipError_t launch_postfx(const LaunchCfg& c, const PostDev& P, const float4* acc
                          const int32_t* nsamp, const float4* avg, uint32_t* rgb8);
 hipError_t launch_untile(const LaunchCfg& c, int32_t W, int32_t H, int32_t ts, int32_t world, uint32_t per_rank,
                          const float4* gathered, float4* avg, uint32_t* rgb8, const PostDev* post);
+struct InstSrc;
+// device refit of n <= kMaxInstances instances (prt_refit.h)
+hipError_t launch_refit(hipStream_t s, const InstSrc* src, int32_t n, InstDev* out);
 hipError_t launch_primary_hits(const LaunchCfg& c, const SceneDev& S, const TileMap& M, HitOut* out, Counters* cnt);
 hipError_t launch_intersect(const LaunchCfg& c, const SceneDev& S, int32_t n, const float* O, const float* D,
                             const float* tmax, HitOut* out);

@@ -10,6 +10,7 @@
 // k_accumulate: per pixel, folds the frames into the persistent accumulator with the reference's
 //   distance-keyed progressive mean (Core/Renderer.cpp:81-104) and packs RGB8 (precomp.h:310-315).
 #include "prt_launch.h"
+#include "prt_refit.h"
 #include "prt_path.h"
 
 namespace prt {
@@ -316,6 +317,21 @@ hipError_t launch_occluded(const LaunchCfg& c, const SceneDev& S, int32_t n, con
                            const float* tmax, int32_t* out) {
   if (n <= 0) return hipSuccess;
   PRT_BY_LAYOUT(c.layout, k_occluded, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
+  return hipGetLastError();
+}
+
+// ---- instance refit (BLASInstance::Update on the device): one thread per instance
+__global__ void k_refit(const InstSrc* __restrict__ src, int32_t n, InstDev* __restrict__ out) {
+  const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  InstDev I;
+  refit_instance(src[i], I);
+  out[i] = I;
+}
+
+hipError_t launch_refit(hipStream_t s, const InstSrc* src, int32_t n, InstDev* out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_refit, dim3((n + 63) / 64), dim3(64), 0, s, src, n, out);
   return hipGetLastError();
 }
 

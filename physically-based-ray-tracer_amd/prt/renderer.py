@@ -181,6 +181,13 @@ class Context:
         else:
             check(L.prt_set_sky(self.h, None, 0, 0))
 
+    def set_instances(self, blases):
+        """Per-frame instance update (physics moved the game objects, Core/Renderer.cpp:33-41): the transforms
+        go to the device and are refit there in stream order, so frames already queued keep the old ones."""
+        xf = _f32(np.stack([T for _, T in blases]).reshape(-1))
+        mi = np.ascontiguousarray([m for m, _ in blases], np.uint32)
+        check(self.L.prt_set_instances(self.h, xf.ctypes.data, mi.ctypes.data, len(blases)))
+
     def set_materials(self, kinds=None):
         """Per-instance material kinds (_lib.MAT_TEXTURED / MAT_DIELECTRIC / MAT_MIRROR), None = all textured."""
         if kinds is None:

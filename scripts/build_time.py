@@ -19,6 +19,7 @@ ctx.set_stream(torch.cuda.current_stream().cuda_stream)
 scene = prt.Scene.from_data(sd)
 avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
 rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+print("BLAS builders (C4):", flush=True)
 for name, b in (("host SAH", _lib.BUILDER_HOST_SAH), ("GPU LBVH", _lib.BUILDER_GPU_LBVH)):
     ctx.set_bvh_builder(b)
     ctx.set_scene(scene)
