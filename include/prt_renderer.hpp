@@ -51,6 +51,7 @@ struct Texture {
 struct GameObject {
   std::array<float, 16> transform{1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
   uint32_t modelIndex = 0;
+  int32_t material = PRT_MAT_TEXTURED;  // the model index Scene.cpp:193-205 should have tested: DIELECTRIC / MIRROR
 };
 
 class Scene {
@@ -61,6 +62,7 @@ class Scene {
   prt_lights lights{};              // Renderer point-light SoA + directionalLights[0] + spotlights[0]
   std::vector<float> skyPixels;     // Camera::skyPixels, float RGB equirect (empty = no sky)
   int32_t skyWidth = 0, skyHeight = 0;
+  std::vector<prt_area_light> areaLights;  // Scene::areaLights (Core/AreaLight.h): at most one, sampled with MIS
 
   // everything the hot path reads, copied to HBM (Scene::Init + BuildTLAS, Core/Scene.cpp:10-28,220-223)
   void Upload(prt_ctx* ctx) const {
@@ -87,17 +89,23 @@ class Scene {
     check(prt_set_meshes(ctx, ms.data(), (int32_t)ms.size()));
     UploadInstances(ctx);
     check(prt_set_lights(ctx, &lights));
+    check(prt_set_area_lights(ctx, areaLights.empty() ? nullptr : areaLights.data(), (int32_t)areaLights.size()));
     check(prt_set_sky(ctx, skyPixels.empty() ? nullptr : skyPixels.data(), skyWidth, skyHeight));
   }
   // GameObject::Synchronise moved an instance: new transforms, TLAS rebuilt (Core/Renderer.cpp:33-41)
   void UploadInstances(prt_ctx* ctx) const {
     std::vector<float> xf;
     std::vector<uint32_t> mi;
+    std::vector<int32_t> mat;
+    bool any = false;
     for (const GameObject& g : gameobjects) {
       xf.insert(xf.end(), g.transform.begin(), g.transform.end());
       mi.push_back(g.modelIndex);
+      mat.push_back(g.material);
+      any = any || g.material != PRT_MAT_TEXTURED;
     }
     check(prt_set_instances(ctx, xf.data(), mi.data(), (int32_t)mi.size()));
+    check(prt_set_instance_materials(ctx, any ? mat.data() : nullptr, any ? (int32_t)mat.size() : 0));
   }
 };
 

@@ -81,6 +81,14 @@ int main(int argc, char** argv) {
       for (float& v : g.transform) v = r.get<float>();
       g.modelIndex = r.get<uint32_t>();
     }
+    for (prt::GameObject& g : S.gameobjects) g.material = r.get<int32_t>();
+    if (r.get<int32_t>()) {
+      prt_area_light a{};
+      float* aw = a.corner;  // corner, edge_u, edge_v, radiance: 12 consecutive floats
+      for (int k = 0; k < 12; k++) aw[k] = r.get<float>();
+      a.two_sided = r.get<int32_t>();
+      S.areaLights.push_back(a);
+    }
     std::fclose(fp);
 
     R.camera = prt::Camera(pos, tgt, aspect);

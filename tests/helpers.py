@@ -48,7 +48,8 @@ def dump_scene(sd, W, H, path):
     Little-endian: b"PRTS", int32 W, H; camera pos[3], target[3], aspect (f32); lights: 39 f32 in prt_lights
     order; sky: int32 w, h + w*h*3 f32; textures: int32 n + per texture int32 w, h + w*h u32; meshes:
     int32 n + per mesh int32 T, V, 4 texture ids + triangles 12T f32, normals 12T f32, uvs 6T f32,
-    indices 3T i32, vertices 3V f32, face normals 3T f32; instances: int32 n + per instance 16 f32, u32 mesh."""
+    indices 3T i32, vertices 3V f32, face normals 3T f32; instances: int32 n + per instance 16 f32, u32 mesh;
+    then the extensions (materials, area light) as written below."""
     import struct
     F = np.float32
     with open(path, "wb") as f:
@@ -76,3 +77,11 @@ def dump_scene(sd, W, H, path):
         f.write(struct.pack("<i", len(sd.instances)))
         for mi, xf in sd.instances:
             f.write(np.ascontiguousarray(xf, F).tobytes() + struct.pack("<I", mi))
+        # extensions: int32 material per instance (all 0 when None); int32 area flag + 12 f32 + int32 two_sided
+        mats = sd.materials if sd.materials is not None else [0] * len(sd.instances)
+        f.write(np.asarray(mats, np.int32).tobytes())
+        al = sd.area_light
+        f.write(struct.pack("<i", 0 if al is None else 1))
+        if al is not None:
+            f.write(np.concatenate([np.asarray(al[k], F) for k in ("corner", "edge_u", "edge_v", "radiance")]).tobytes())
+            f.write(struct.pack("<i", 1 if al.get("two_sided", False) else 0))

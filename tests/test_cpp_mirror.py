@@ -27,11 +27,14 @@ def test_cpp_mirror_compiles_and_links(tmp_path):
 
 
 @pytest.mark.gpu
-def test_cpp_mirror_matches_python_mirror(tmp_path):
+@pytest.mark.parametrize("ext", [False, True])
+def test_cpp_mirror_matches_python_mirror(tmp_path, ext):
     import prt
     from prt import scenes
     exe = _build(tmp_path)
     sd = scenes.multi_instance(scenes.config_small(50, 40))
+    if ext:  # dielectric + mirror instances and the area light through GameObject::material / Scene::areaLights
+        sd = scenes.with_extensions(sd, materials=[0, 1, 2], area_light=scenes.ceiling_light())
     W, H, ticks, bounces = 80, 56, 3, 3
     dump_scene(sd, W, H, str(tmp_path / "scene.bin"))
     r = subprocess.run([exe, str(tmp_path / "scene.bin"), str(tmp_path / "out.bin"), str(ticks), str(bounces)],
