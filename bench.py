@@ -211,6 +211,7 @@ def main():
             kern["k_trace_frames"] = (seg_f * bpr["closest"] + sh_f * bpr["anyhit"], float(np.mean(ms_trace)))
         dom = max(kern, key=lambda k: kern[k][1])
         alg_bytes, kern_ms = kern[dom]
+        kern_ms = max(kern_ms, 1e-9)  # PRT_LAUNCH_TIMERS=0 (A/B runs): no per-launch times
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
         traffic = measured_traffic(dom) if args.scene == "c4" else None  # the committed PMC passes are of C4
         own = own_layout_bytes_per_ray()

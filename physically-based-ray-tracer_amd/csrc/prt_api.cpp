@@ -461,6 +461,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
                                                 : "too many wavefront iterations");
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   int nb = 1;
+  bool timers = false;
   if (mega) {
     HIP_TRY(c->counters.ensure(sizeof(Counters)));
     HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
@@ -478,6 +479,10 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
       c->wb[k].tl = nullptr;
       c->wb[k].coop_tail = (et && std::strcmp(et, "0") == 0) ? 0 : 1;
     }
+    // per-launch traversal timers (HIP events around every k_trace launch) with stats, unless
+    // PRT_LAUNCH_TIMERS=0: each event record costs a few us between kernels
+    const char* elt = std::getenv("PRT_LAUNCH_TIMERS");
+    timers = stats && !(elt && std::strcmp(elt, "0") == 0);
     if (stats && std::getenv("PRT_DEBUG_QUEUES")) {
       const size_t tlb = 32ull * kTlWaves * (kMaxIters + 2);
       HIP_TRY(c->tl.ensure(tlb));
@@ -517,12 +522,12 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
         if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(c->wb[k].dst, 0, 4ull * c->wb[k].n, Lk[k].stream));
         float4* out = c->frames.as<float4>() + c->wb[k].base;
         if (pipe == 2) HIP_TRY(launch_wave_init(Lk[k], S, A, M, c->wb[k], out));
-        else HIP_TRY(launch_wavefront(Lk[k], S, A, M, c->wb[k], out, stats ? &c->wt[k] : nullptr));
+        else HIP_TRY(launch_wavefront(Lk[k], S, A, M, c->wb[k], out, timers ? &c->wt[k] : nullptr));
       }
       for (uint32_t it = 0; pipe == 2 && it <= iters; it++)  // merged pipeline: iterations round-robin over batches
         for (int k = 0; k < nb; k++)
           HIP_TRY(launch_wave2_iter(Lk[k], S, A, M, c->wb[k], c->frames.as<float4>() + c->wb[k].base,
-                                    stats ? &c->wt[k] : nullptr, it));
+                                    timers ? &c->wt[k] : nullptr, it));
       for (int k = 1; k < nb; k++) {  // join
         HIP_TRY(hipEventRecord(c->bev[k], c->bstream[k]));
         HIP_TRY(hipStreamWaitEvent(c->stream, c->bev[k], 0));
@@ -589,15 +594,15 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
           stats->segments += qs;
           stats->shadow_rays += qa;
           float a = 0, b = 0;
-          HIP_TRY(hipEventElapsedTime(&a, wt.ev[4 * k + 0], wt.ev[4 * k + 1]));
-          if (pipe == 0) HIP_TRY(hipEventElapsedTime(&b, wt.ev[4 * k + 2], wt.ev[4 * k + 3]));
+          if (timers) HIP_TRY(hipEventElapsedTime(&a, wt.ev[4 * k + 0], wt.ev[4 * k + 1]));
+          if (timers && pipe == 0) HIP_TRY(hipEventElapsedTime(&b, wt.ev[4 * k + 2], wt.ev[4 * k + 3]));
           stats->ms_closest += a;
           stats->ms_anyhit += b;
           if (dump)
             std::fprintf(stderr, "prt: batch %d iteration %u: %llu closest rays %.3f ms, %llu shadow rays %.3f ms\n", bk,
                          k, (unsigned long long)qs, a, (unsigned long long)qa, b);
         }
-        if (pipe == 2) {  // one merged trace launch per iteration plus the final shadow-only one
+        if (pipe == 2 && timers) {  // one merged trace launch per iteration plus the final shadow-only one
           float a = 0;
           HIP_TRY(hipEventElapsedTime(&a, wt.ev[4 * iters + 0], wt.ev[4 * iters + 1]));
           stats->ms_closest += a;
