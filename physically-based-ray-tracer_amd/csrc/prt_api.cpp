@@ -470,14 +470,20 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     nb = pipe == 3 ? 1 : batches_for(n);
     rc = ensure_batch_streams(c, nb);
     if (rc) return rc;
+    // traversal tails (prt_persist.h), PRT_TAIL: 0 none, 1 cooperative, 2 group, 3 cooperative then group;
+    // PRT_GTAIL: rays per wave at which the group tail takes over (1-8, default 8)
     const char* et = std::getenv("PRT_TAIL");
+    const char* eg = std::getenv("PRT_GTAIL");
+    const int tmode = et ? std::atoi(et) : 1;
+    const int gthr = eg ? std::min(8, std::max(1, std::atoi(eg))) : 8;
     for (int k = 0; k < nb; k++) {  // consecutive item ranges, multiples of 256 items (the last one takes the rest)
       const uint64_t b0 = k == 0 ? 0 : ((n * k / nb + 255) & ~255ull), b1 = k == nb - 1 ? n : ((n * (k + 1) / nb + 255) & ~255ull);
       rc = ensure_wave(c, k, (uint32_t)(b1 - b0), p->bounces, ext);
       if (rc) return rc;
       c->wb[k].base = (uint32_t)b0;
       c->wb[k].tl = nullptr;
-      c->wb[k].coop_tail = (et && std::strcmp(et, "0") == 0) ? 0 : 1;
+      c->wb[k].coop_tail = (tmode == 1 || tmode == 3) ? 1 : 0;
+      c->wb[k].group_tail = (tmode == 2 || tmode == 3) && L.layout == 8 ? gthr : 0;
     }
     // per-launch traversal timers (HIP events around every k_trace launch) with stats, unless
     // PRT_LAUNCH_TIMERS=0: each event record costs a few us between kernels

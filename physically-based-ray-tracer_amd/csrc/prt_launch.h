@@ -58,7 +58,8 @@ struct WaveBufs {
   float4* dro;      // per level: refraction ray origin, fresnel
   float4* drd;      // per level: refraction ray direction
   unsigned long long* tl;  // PRT_DEBUG_QUEUES: [launch][wave] {start, first empty fetch, exit, -}
-  int32_t coop_tail;       // cooperative traversal tail (prt_persist.h); PRT_TAIL=0 turns it off
+  int32_t coop_tail;       // cooperative traversal tail (prt_persist.h)
+  int32_t group_tail;      // group traversal tail threshold (prt_persist.h), 0 = off
 };
 // streaming engine (prt_stream.hip): per-XCD ray / shade queues of tagged 8-byte granules
 constexpr uint32_t kSSub = 8;        // sub-queues per XCD part and queue

@@ -25,6 +25,16 @@
 // re-testing the winning triangle (ShadeTri.pad[0]) for its (u, v) -- and continues with the next
 // instance or finishes.  The hit rule makes the split exact: the result does not depend on which lane
 // visits which subtree.
+//
+// Group tail (gtail != 0, Node8).  A drained wave with at most gtail (<= 8) rays gives every ray a group of
+// 8 lanes.  Lane k of a group tests child k of the ray's node, the group's ballot is the node's hit mask,
+// and the triangles of the hit leaf children are tested in the same iteration, one leaf per lane.  A
+// straggler's step is then one child slab plus one leaf instead of eight slabs, and its node visits and
+// triangle tests no longer take separate iterations.  The traversal state is replicated in the group's 8
+// lanes (each computes the same uniform update) and the stack stays in the owner lane's LDS column.  The
+// group's closest candidate is a min-reduction of (t, prim) over its lanes, which is the hit rule again.
+// With both tails on, the cooperative tail stops handing out subtrees once <= gtail owners are left, merges
+// its teams when the last helper is done and hands the owners to the group tail.
 #pragma once
 #include "prt_traverse8.h"
 
@@ -56,13 +66,14 @@ __device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
 //                                                           idle lanes, no refill coming (the streaming
 //                                                           engine publishes finished rays there)
 // tail: tail_lds_words(TAILN) words of LDS for the cooperative tail, or nullptr (no tail mode).
+// gtail: group tail threshold (<= 8 rays, Node8 only), 0 = off.
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
 template <int MODE, bool HALF, int STACK, int REFILL, int TAILN = 32, class Fetch, class Load, class Reload, class Finish,
           class Tick>
 __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                    Load load, Reload reload, Finish finish, Tick tick,
-                                                   uint32_t* __restrict__ tail = nullptr) {
+                                                   uint32_t* __restrict__ tail = nullptr, uint32_t gtail = 0) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   bool active = false, drained = false;
@@ -75,8 +86,10 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   int inst = -1;
   uint32_t node = kNoNode, gbase = 0, gmask = 0, gimask = 0;
   int sp = 0;
+  uint32_t* st = stk;  // the LDS stack column this lane walks with (group tail: the owner's)
   uint32_t lhit = 0, ltri = 0, lmeta0 = 0, lmeta1 = 0, tcur = 0, tcnt = 0;  // pending leaf triangles
   bool found = false;  // tail: this lane improved its closest hit
+  if (HALF) gtail = 0;
   // enter the first instance >= i0 whose world box the ray hits before h.t (tiny_bvh.h:2500-2565 TLAS
   // walk as a linear loop over <= 64 instance boxes); false when there is none
   auto enter = [&](int i0, const V3& Ow, const V3& Dw) -> bool {
@@ -99,8 +112,8 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   auto next_node = [&]() {
     if (!gmask && sp > 0) {
       sp--;
-      gbase = stk[(2 * sp) * 64];
-      const uint32_t m = stk[(2 * sp + 1) * 64];
+      gbase = st[(2 * sp) * 64];
+      const uint32_t m = st[(2 * sp + 1) * 64];
       gmask = m & 0xFFu;
       gimask = m >> 8;
     }
@@ -112,6 +125,20 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     } else {
       node = kNoNode;
     }
+  };
+  // interior children hit at a visited node: stack the rest of the current group, descend into the new one
+  auto push_group = [&](uint32_t ihit, uint32_t imask, uint32_t child_base) {
+    if (ihit) {
+      if (gmask && sp < STACK) {
+        st[(2 * sp) * 64] = gbase;
+        st[(2 * sp + 1) * 64] = gmask | (gimask << 8);
+        sp++;
+      }
+      gbase = child_base;
+      gmask = order_mask(ihit, oct);
+      gimask = imask;
+    }
+    next_node();
   };
   // one node visit (lanes without pending triangles)
   auto node_step = [&]() {
@@ -132,18 +159,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     const uint32_t imask = a.w >> 24;
     lhit = hits & ~imask;
     ltri = b.y; lmeta0 = b.z; lmeta1 = b.w;
-    const uint32_t ihit = hits & imask;
-    if (ihit) {
-      if (gmask && sp < STACK) {
-        stk[(2 * sp) * 64] = gbase;
-        stk[(2 * sp + 1) * 64] = gmask | (gimask << 8);
-        sp++;
-      }
-      gbase = b.x;
-      gmask = order_mask(ihit, oct);
-      gimask = imask;
-    }
-    next_node();
+    push_group(hits & imask, imask, b.x);
   };
   // one triangle test (lanes with pending leaf triangles); returns true when an any-hit query hit
   auto tri_step = [&]() -> bool {
@@ -200,6 +216,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       if (drained) break;
       continue;
     }
+    if (gtail && drained && __popcll(act) <= gtail) break;           // group tail below
     if (tail && drained && __popcll(act) <= (uint32_t)TAILN) break;  // cooperative tail below
     // ---- BLAS done: next instance, or the ray is finished
     if (active && node == kNoNode && lhit == 0 && tcnt == 0) {
@@ -224,121 +241,260 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       }
     }
   }
-  if (!tail || __ballot(active) == 0) return;
+  if (__ballot(active) == 0) return;
 
-  // ---------------------------------------------------------------- cooperative tail
-  // role: owner (active: holds the ray's handle) / helper (walks one subtree of an owner's ray) / free;
-  // team slot of an owner = its rank among the owners at tail entry (< TAILN)
-  // tstate: helpers still walking (low 16 bits) | any-hit: some team lane hit (kFoundBit)
-  constexpr uint32_t kFoundBit = 1u << 16;
-  uint32_t* tstate = tail;
-  unsigned long long* tkey = reinterpret_cast<unsigned long long*>(tail + TAILN);  // best (t, prim)
-  bool helper = false;
-  uint32_t slot = (uint32_t)__popcll(__ballot(active) & lanes_below);
-  if (active) {
-    tstate[slot] = 0u;
-    tkey[slot] = ~0ull;
-  }
-  found = false;
-  while (true) {
-    const bool member = active || helper;
-    // an any-hit team that hit stops walking
-    if (member && any && (tstate[slot] & kFoundBit)) { node = kNoNode; lhit = 0; tcnt = 0; }
-    bool busy = member && (node != kNoNode || lhit != 0 || tcnt != 0);
-    // ---- helpers done with their subtree: publish, leave the team
-    if (helper && !busy) {
-      if (!any && found) atomicMin(&tkey[slot], ((unsigned long long)__float_as_uint(h.t) << 32) | h.prim);
-      atomicSub(&tstate[slot], 1u);
-      helper = false;
+  if (tail && !(gtail && (uint32_t)__popcll(__ballot(active)) <= gtail)) {
+    // ---------------------------------------------------------------- cooperative tail
+    // role: owner (active: holds the ray's handle) / helper (walks one subtree of an owner's ray) / free;
+    // team slot of an owner = its rank among the owners at tail entry (< TAILN)
+    // tstate: helpers still walking (low 16 bits) | any-hit: some team lane hit (kFoundBit)
+    constexpr uint32_t kFoundBit = 1u << 16;
+    uint32_t* tstate = tail;
+    unsigned long long* tkey = reinterpret_cast<unsigned long long*>(tail + TAILN);  // best (t, prim)
+    bool helper = false;
+    uint32_t slot = (uint32_t)__popcll(__ballot(active) & lanes_below);
+    if (active) {
+      tstate[slot] = 0u;
+      tkey[slot] = ~0ull;
     }
-    // ---- owners whose walk and helpers are done: merge, next instance or finish
-    if (active && !busy) {
-      const uint32_t ts = tstate[slot];
-      const bool occl = any && (ts & kFoundBit);
-      if (occl || (ts & 0xFFFFu) == 0u) {
-        if (!any) {
-          const unsigned long long k = tkey[slot];
-          tkey[slot] = ~0ull;
-          const float kt = __uint_as_float((uint32_t)(k >> 32));
-          const uint32_t kp = (uint32_t)k;
-          if (k != ~0ull && (kt < h.t || (kt == h.t && ((uint32_t)inst < h.inst ||
-                                                       ((uint32_t)inst == h.inst && kp < h.prim))))) {
-            // a helper's hit wins: its (u, v) from the same triangle test on the same instance-space ray
-            const uint32_t g = S.stri[S.mesh[S.inst[inst].mesh].prim_base + kp].pad[0];
-            float t, u, v;
-            uint32_t prim;
-            (void)mt_test(S.tris + g, O, D, t, u, v, prim);
-            h.t = t; h.u = u; h.v = v; h.prim = prim; h.inst = (uint32_t)inst;
+    found = false;
+    // an owner takes its helpers' best hit: (u, v) from the same triangle test on the same instance-space ray
+    auto merge_team = [&]() {
+      const unsigned long long k = tkey[slot];
+      tkey[slot] = ~0ull;
+      const float kt = __uint_as_float((uint32_t)(k >> 32));
+      const uint32_t kp = (uint32_t)k;
+      if (k != ~0ull && (kt < h.t || (kt == h.t && ((uint32_t)inst < h.inst ||
+                                                   ((uint32_t)inst == h.inst && kp < h.prim))))) {
+        const uint32_t g = S.stri[S.mesh[S.inst[inst].mesh].prim_base + kp].pad[0];
+        float t, u, v;
+        uint32_t prim;
+        (void)mt_test(S.tris + g, O, D, t, u, v, prim);
+        h.t = t; h.u = u; h.v = v; h.prim = prim; h.inst = (uint32_t)inst;
+      }
+    };
+    bool to_group = false;
+    while (true) {
+      // ---- few owners left and no helper walking: the group tail takes over
+      const uint32_t nown = (uint32_t)__popcll(__ballot(active));
+      const bool few = gtail && nown <= gtail;
+      if (few && __ballot(helper) == 0) {
+        to_group = true;
+        break;
+      }
+      const bool member = active || helper;
+      // an any-hit team that hit stops walking
+      if (member && any && (tstate[slot] & kFoundBit)) { node = kNoNode; lhit = 0; tcnt = 0; }
+      bool busy = member && (node != kNoNode || lhit != 0 || tcnt != 0);
+      // ---- helpers done with their subtree: publish, leave the team
+      if (helper && !busy) {
+        if (!any && found) atomicMin(&tkey[slot], ((unsigned long long)__float_as_uint(h.t) << 32) | h.prim);
+        atomicSub(&tstate[slot], 1u);
+        helper = false;
+      }
+      // ---- owners whose walk and helpers are done: merge, next instance or finish
+      if (active && !busy) {
+        const uint32_t ts = tstate[slot];
+        const bool occl = any && (ts & kFoundBit);
+        if (occl || (ts & 0xFFFFu) == 0u) {
+          if (!any) merge_team();
+          bool more = false;
+          if (!occl && inst + 1 < S.ninst) {
+            V3 Ow, Dw;
+            reload(handle, any, Ow, Dw);
+            more = enter(inst + 1, Ow, Dw);
+          }
+          if (more) {
+            busy = true;  // a closest query; no helper of this team is left
+          } else {
+            finish(handle, h, any, occl);
+            active = false;
           }
         }
-        bool more = false;
-        if (!occl && inst + 1 < S.ninst) {
-          V3 Ow, Dw;
-          reload(handle, any, Ow, Dw);
-          more = enter(inst + 1, Ow, Dw);
+      }
+      if (__ballot(active) == 0) break;  // helpers always belong to a live owner
+      // ---- free lanes take a pending group from a walking lane: its top stack entry or its sibling group
+      // (none once the group tail is waiting for the last helpers)
+      const uint64_t freem = __ballot(!active && !helper && !few);
+      const uint64_t donm = __ballot((active || helper) && busy && (sp > 0 || gmask != 0) &&
+                                     !(any && (tstate[slot] & kFoundBit)));
+      if (freem && donm) {
+        const uint32_t npair = min((uint32_t)__popcll(freem), (uint32_t)__popcll(donm));
+        uint32_t ub = 0, um = 0, ui = 0;
+        if (((donm >> lane) & 1ull) && (uint32_t)__popcll(donm & lanes_below) < npair) {
+          if (sp > 0) {
+            sp--;
+            ub = stk[(2 * sp) * 64];
+            const uint32_t m = stk[(2 * sp + 1) * 64];
+            um = m & 0xFFu;
+            ui = m >> 8;
+          } else {
+            ub = gbase; um = gmask; ui = gimask;
+            gmask = 0;
+          }
         }
-        if (more) {
-          busy = true;  // a closest query; no helper of this team is left
-        } else {
-          finish(handle, h, any, occl);
-          active = false;
+        const uint32_t frank = (uint32_t)__popcll(freem & lanes_below);
+        const bool take = ((freem >> lane) & 1ull) && frank < npair;
+        const int src = (int)nth_set(donm, take ? frank : 0u);
+        // every lane joins the shuffles (ds_bpermute); only the takers keep the values
+        const float ox = __shfl(O.x, src), oy = __shfl(O.y, src), oz = __shfl(O.z, src);
+        const float dx = __shfl(D.x, src), dy = __shfl(D.y, src), dz = __shfl(D.z, src);
+        const float tt = __shfl(h.t, src);
+        const int sinst = __shfl(inst, src), sany = __shfl((int)any, src);
+        const uint32_t sslot = (uint32_t)__shfl((int)slot, src), shp = (uint32_t)__shfl((int)h.prim, src);
+        const uint32_t shi = (uint32_t)__shfl((int)h.inst, src);
+        const uint32_t sb = (uint32_t)__shfl((int)ub, src), sm = (uint32_t)__shfl((int)um, src);
+        const uint32_t si = (uint32_t)__shfl((int)ui, src);
+        if (take) {
+          helper = true;
+          O = v3(ox, oy, oz);
+          D = v3(dx, dy, dz);
+          rD = v3(safercp(D.x), safercp(D.y), safercp(D.z));
+          oct = (rD.x < 0.0f ? 1u : 0u) | (rD.y < 0.0f ? 2u : 0u) | (rD.z < 0.0f ? 4u : 0u);
+          inst = sinst;
+          any = MODE == 1 || (MODE == 2 && sany != 0);
+          slot = sslot;
+          h.t = tt; h.prim = shp; h.inst = shi;
+          gbase = sb; gmask = sm; gimask = si;
+          sp = 0; lhit = 0; tcnt = 0;
+          found = false;
+          next_node();
+          atomicAdd(&tstate[slot], 1u);
+          busy = true;
         }
+      }
+      // ---- one node visit / one triangle test per walking lane, as in the main loop
+      if (busy && node != kNoNode && lhit == 0 && tcnt == 0) node_step();
+      if (busy && (lhit | tcnt)) {
+        if (tri_step()) atomicOr(&tstate[slot], kFoundBit);
       }
     }
-    if (__ballot(active) == 0) break;  // helpers always belong to a live owner
-    // ---- free lanes take a pending group from a walking lane: its top stack entry or its sibling group
-    const uint64_t freem = __ballot(!active && !helper);
-    const uint64_t donm = __ballot((active || helper) && busy && (sp > 0 || gmask != 0) &&
-                                   !(any && (tstate[slot] & kFoundBit)));
-    if (freem && donm) {
-      const uint32_t npair = min((uint32_t)__popcll(freem), (uint32_t)__popcll(donm));
-      uint32_t ub = 0, um = 0, ui = 0;
-      if (((donm >> lane) & 1ull) && (uint32_t)__popcll(donm & lanes_below) < npair) {
-        if (sp > 0) {
-          sp--;
-          ub = stk[(2 * sp) * 64];
-          const uint32_t m = stk[(2 * sp + 1) * 64];
-          um = m & 0xFFu;
-          ui = m >> 8;
-        } else {
-          ub = gbase; um = gmask; ui = gimask;
-          gmask = 0;
-        }
-      }
-      const uint32_t frank = (uint32_t)__popcll(freem & lanes_below);
-      const bool take = ((freem >> lane) & 1ull) && frank < npair;
-      const int src = (int)nth_set(donm, take ? frank : 0u);
-      // every lane joins the shuffles (ds_bpermute); only the takers keep the values
-      const float ox = __shfl(O.x, src), oy = __shfl(O.y, src), oz = __shfl(O.z, src);
-      const float dx = __shfl(D.x, src), dy = __shfl(D.y, src), dz = __shfl(D.z, src);
-      const float tt = __shfl(h.t, src);
-      const int sinst = __shfl(inst, src), sany = __shfl((int)any, src);
-      const uint32_t sslot = (uint32_t)__shfl((int)slot, src), shp = (uint32_t)__shfl((int)h.prim, src);
-      const uint32_t shi = (uint32_t)__shfl((int)h.inst, src);
-      const uint32_t sb = (uint32_t)__shfl((int)ub, src), sm = (uint32_t)__shfl((int)um, src);
-      const uint32_t si = (uint32_t)__shfl((int)ui, src);
-      if (take) {
-        helper = true;
-        O = v3(ox, oy, oz);
-        D = v3(dx, dy, dz);
-        rD = v3(safercp(D.x), safercp(D.y), safercp(D.z));
-        oct = (rD.x < 0.0f ? 1u : 0u) | (rD.y < 0.0f ? 2u : 0u) | (rD.z < 0.0f ? 4u : 0u);
-        inst = sinst;
-        any = MODE == 1 || (MODE == 2 && sany != 0);
-        slot = sslot;
-        h.t = tt; h.prim = shp; h.inst = shi;
-        gbase = sb; gmask = sm; gimask = si;
-        sp = 0; lhit = 0; tcnt = 0;
-        found = false;
-        next_node();
-        atomicAdd(&tstate[slot], 1u);
-        busy = true;
+    if (!to_group) return;
+    // hand-over: every team is down to its owner; take what the helpers published
+    if (active) {
+      if (any && (tstate[slot] & kFoundBit)) {
+        finish(handle, h, true, true);
+        active = false;
+      } else if (!any) {
+        merge_team();
       }
     }
-    // ---- one node visit / one triangle test per walking lane, as in the main loop
-    if (busy && node != kNoNode && lhit == 0 && tcnt == 0) node_step();
-    if (busy && (lhit | tcnt)) {
-      if (tri_step()) atomicOr(&tstate[slot], kFoundBit);
+  }
+  if (!gtail) return;
+
+  // ---------------------------------------------------------------- group tail
+  const uint64_t own = __ballot(active);
+  if (own == 0) return;
+  const uint32_t k = lane & 7u, gsh = lane & ~7u;  // child slot of this lane, first lane of its group
+  bool live = (lane >> 3) < (uint32_t)__popcll(own);
+  const int src = (int)nth_set(own, live ? (lane >> 3) : 0u);  // the group's owner lane
+  O = v3(__shfl(O.x, src), __shfl(O.y, src), __shfl(O.z, src));
+  D = v3(__shfl(D.x, src), __shfl(D.y, src), __shfl(D.z, src));
+  rD = v3(__shfl(rD.x, src), __shfl(rD.y, src), __shfl(rD.z, src));
+  oct = (uint32_t)__shfl((int)oct, src);
+  h.t = __shfl(h.t, src); h.u = __shfl(h.u, src); h.v = __shfl(h.v, src);
+  h.prim = (uint32_t)__shfl((int)h.prim, src); h.inst = (uint32_t)__shfl((int)h.inst, src);
+  inst = __shfl(inst, src);
+  handle = (uint32_t)__shfl((int)handle, src);
+  if (MODE == 2) any = __shfl((int)any, src) != 0;
+  node = (uint32_t)__shfl((int)node, src);
+  gbase = (uint32_t)__shfl((int)gbase, src); gmask = (uint32_t)__shfl((int)gmask, src);
+  gimask = (uint32_t)__shfl((int)gimask, src);
+  sp = __shfl(sp, src);
+  lhit = (uint32_t)__shfl((int)lhit, src); ltri = (uint32_t)__shfl((int)ltri, src);
+  lmeta0 = (uint32_t)__shfl((int)lmeta0, src); lmeta1 = (uint32_t)__shfl((int)lmeta1, src);
+  tcur = (uint32_t)__shfl((int)tcur, src); tcnt = (uint32_t)__shfl((int)tcnt, src);
+  st = stk - lane + src;
+  while (true) {
+    // ---- BLAS done: next instance, or the ray is finished
+    if (live && node == kNoNode && lhit == 0 && tcnt == 0) {
+      bool more = false;
+      if (inst + 1 < S.ninst) {
+        V3 Ow, Dw;
+        reload(handle, any, Ow, Dw);
+        more = enter(inst + 1, Ow, Dw);
+      }
+      if (!more) {
+        if (k == 0) finish(handle, h, any, false);
+        live = false;
+      }
+    }
+    if (__ballot(live) == 0) break;
+    // ---- node visit: lane k tests child k, the group's ballot is the hit mask
+    const bool visit = live && node != kNoNode && lhit == 0 && tcnt == 0;
+    bool hk = false;
+    uint4 a = make_uint4(0u, 0u, 0u, 0u), b = a;
+    if (visit) {
+      const uint4* np = reinterpret_cast<const uint4*>(S.nodes8 + node);
+      a = np[0];
+      b = np[1];
+      hk = node8_child_hit(a, np[2], np[3], np[4], k, O, rD, h.t);
+    }
+    const uint32_t m = (uint32_t)(__ballot(hk) >> gsh) & 0xFFu;
+    if (visit) {
+      const uint32_t imask = a.w >> 24;
+      lhit = m & ~imask;
+      ltri = b.y; lmeta0 = b.z; lmeta1 = b.w;
+      push_group(m & imask, imask, b.x);
+    }
+    // ---- leaf triangles, same iteration: lane k takes leaf child k; a partly tested leaf (tcur, tcnt,
+    // pending at entry) goes to the first lane whose child is not pending
+    bool occ = false, got = false;
+    float bt = 0.0f, bu = 0.0f, bv = 0.0f;
+    uint32_t bp = 0;
+    if (live && (lhit | tcnt)) {
+      uint32_t first = 0, cnt = 0;
+      if ((lhit >> k) & 1u) {
+        const uint32_t meta = ((k < 4 ? lmeta0 : lmeta1) >> (8 * (k & 3))) & 0xFFu;
+        first = ltri + (meta >> 3);
+        cnt = meta & 7u;
+      } else if (tcnt && k == (uint32_t)__builtin_ctz(~lhit & 0xFFu)) {
+        first = tcur;
+        cnt = tcnt;
+      }
+      for (uint32_t i = 0; i < cnt; i++) {
+        float t, u, v;
+        uint32_t prim;
+        if (mt_test(S.tris + first + i, O, D, t, u, v, prim)) {
+          if (MODE == 1 || (MODE == 2 && any)) {
+            if (t < h.t) occ = true;  // tiny_bvh.h:6594 (h.t holds tmax)
+          } else if (!got || t < bt || (t == bt && prim < bp)) {
+            bt = t; bu = u; bv = v; bp = prim;
+            got = true;
+          }
+        }
+      }
+      lhit = 0;
+      tcnt = 0;
+    }
+    // ---- any-hit: the group's ray is occluded
+    if (live && ((__ballot(occ) >> gsh) & 0xFFull)) {
+      if (k == 0) finish(handle, h, true, true);
+      live = false;
+      node = kNoNode;
+    }
+    // ---- closest: min (t, prim) over the group (t > 0, so the float bits order like the floats), then the
+    // hit rule against the ray's best
+    if (__ballot(got) != 0) {
+      const uint64_t mine = got ? (((uint64_t)__float_as_uint(bt) << 32) | bp) : ~0ull;
+      uint64_t key = mine;
+#pragma unroll
+      for (int s = 1; s < 8; s <<= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)key, s);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), s);
+        const uint64_t o = ((uint64_t)hi << 32) | lo;
+        key = o < key ? o : key;
+      }
+      const uint64_t wm = (__ballot(got && mine == key) >> gsh) & 0xFFull;
+      const int wl = (int)gsh + (wm ? __builtin_ctzll(wm) : 0);
+      const float wu = __shfl(bu, wl), wv = __shfl(bv, wl);
+      if (live && key != ~0ull) {
+        const float kt = __uint_as_float((uint32_t)(key >> 32));
+        const uint32_t kp = (uint32_t)key;
+        if (kt < h.t || (kt == h.t && ((uint32_t)inst < h.inst || ((uint32_t)inst == h.inst && kp < h.prim)))) {
+          h.t = kt; h.u = wu; h.v = wv; h.prim = kp; h.inst = (uint32_t)inst;
+        }
+      }
     }
   }
 }
@@ -347,9 +503,9 @@ template <int MODE, bool HALF, int STACK, int REFILL, int TAILN = 32, class Fetc
           class Finish>
 __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                  Load load, Reload reload, Finish finish,
-                                                 uint32_t* __restrict__ tail = nullptr) {
+                                                 uint32_t* __restrict__ tail = nullptr, uint32_t gtail = 0) {
   trav8_persistent_t<MODE, HALF, STACK, REFILL, TAILN>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {},
-                                                       tail);
+                                                       tail, gtail);
 }
 
 }  // namespace prt

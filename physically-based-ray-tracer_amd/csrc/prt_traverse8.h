@@ -48,6 +48,30 @@ __device__ __forceinline__ uint32_t node8_hits(const uint4& a, const uint4& c, c
   return hits;
 }
 
+// child k alone (k lane-varying): the same arithmetic as bit k of node8_hits
+__device__ __forceinline__ bool node8_child_hit(const uint4& a, const uint4& c, const uint4& d, const uint4& e,
+                                                uint32_t k, const V3& O, const V3& rD, float tlimit) {
+  const float sx = __uint_as_float((a.w & 0xFFu) << 23), sy = __uint_as_float(((a.w >> 8) & 0xFFu) << 23),
+              sz = __uint_as_float(((a.w >> 16) & 0xFFu) << 23);
+  const float ax = (__uint_as_float(a.x) - O.x) * rD.x, ay = (__uint_as_float(a.y) - O.y) * rD.y,
+              az = (__uint_as_float(a.z) - O.z) * rD.z;
+  const float bx = sx * rD.x, by = sy * rD.y, bz = sz * rD.z;
+  const bool px = rD.x >= 0.0f, py = rD.y >= 0.0f, pz = rD.z >= 0.0f, lo = k < 4;
+  const uint32_t sh = 8u * (k & 3u);
+  const uint32_t wx0 = lo ? c.x : c.y, wx1 = lo ? d.z : d.w;  // lo / hi plane words of child k
+  const uint32_t wy0 = lo ? c.z : c.w, wy1 = lo ? e.x : e.y;
+  const uint32_t wz0 = lo ? d.x : d.y, wz1 = lo ? e.z : e.w;
+  const float qnx = (float)(((px ? wx0 : wx1) >> sh) & 0xFFu), qfx = (float)(((px ? wx1 : wx0) >> sh) & 0xFFu);
+  const float qny = (float)(((py ? wy0 : wy1) >> sh) & 0xFFu), qfy = (float)(((py ? wy1 : wy0) >> sh) & 0xFFu);
+  const float qnz = (float)(((pz ? wz0 : wz1) >> sh) & 0xFFu), qfz = (float)(((pz ? wz1 : wz0) >> sh) & 0xFFu);
+  const float tnx = __builtin_fmaf(qnx, bx, ax), tfx = __builtin_fmaf(qfx, bx, ax);
+  const float tny = __builtin_fmaf(qny, by, ay), tfy = __builtin_fmaf(qfy, by, ay);
+  const float tnz = __builtin_fmaf(qnz, bz, az), tfz = __builtin_fmaf(qfz, bz, az);
+  const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f)) * kNearPad;
+  const float tf = fminf(fminf(tfx, tfy), tfz) * kFarPad;
+  return tn <= tf && tn <= tlimit;
+}
+
 // Node8H: fp16 integer child bounds; the near/far block of each axis is picked by the direction sign at
 // load time and every half goes straight into v_fma_mix_f32 (no byte / half conversions)
 __device__ __forceinline__ float half_lo(uint32_t w) {

@@ -36,7 +36,10 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   const uint32_t nP = iter < iters ? load_prefix(B.ctr, iter, 0, prefP) : 0u;
   const uint32_t nS = iter > 0 ? load_prefix(B.ctr, iter - 1, 1, prefS) : 0u;
   const uint32_t total = nP + nS;
-  if (blockIdx.x * 64u >= total) return;
+  // a launch with fewer rays than lanes spreads them: at most `cap` (>= 8) per fetch, so a small queue gives
+  // many waves a few rays each (at <= 8 they go straight to the group tail) instead of few waves 64 each
+  const uint32_t cap = B.group_tail ? max(8u, (total + gridDim.x - 1u) / gridDim.x) : 64u;
+  if (blockIdx.x * min(cap, 64u) >= total) return;
   uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
   uint32_t part = xcc_id();
   // timeline diagnostic (s_memrealtime, one record per wave: start, first empty fetch, exit)
@@ -46,7 +49,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   trav8_persistent<2, HALF, STACK, REFILL, TAILN>(
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) {
-        const uint32_t got = fetch_some(fctr, total, part, base, want);
+        const uint32_t got = fetch_some(fctr, total, part, base, min(want, cap));
         if (tl && got == 0 && !seen_drain) {
           seen_drain = true;
           if (threadIdx.x == 0) tl[1] = __builtin_amdgcn_s_memrealtime();
@@ -85,7 +88,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
           B.hit[h] = make_float4(hit.t, hit.u, hit.v, __uint_as_float(hit.prim | (hit.inst << 26)));
         }
       },
-      B.coop_tail ? tail_lds : nullptr);
+      B.coop_tail ? tail_lds : nullptr, (uint32_t)B.group_tail);
   if (tl && threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
 

@@ -117,6 +117,31 @@ def test_pipelines_identical(gpu_ctx, monkeypatch, flags):
         assert out[2][2].segments == out[code][2].segments and out[2][2].shadow_rays == out[code][2].shadow_rays
 
 
+@pytest.mark.parametrize("scene", ["c3", "multi", "ext"])
+def test_traversal_tails_identical(gpu_ctx, monkeypatch, scene):
+    """The traversal tails (PRT_TAIL: 0 none, 1 cooperative, 2 group, 3 cooperative then group; prt_persist.h)
+    only change which lanes walk which part of a straggler ray's tree: frames and ray counts are bit-identical,
+    on one big BLAS, on a multi-instance TLAS and with the extension scene's mixed any-hit queues."""
+    if scene == "c3":
+        sd, W, H = scenes.config_c3(), 480, 270
+    elif scene == "multi":
+        sd, W, H = scenes.multi_instance(scenes.config_small(60, 50)), 128, 96
+    else:
+        sd = scenes.with_extensions(scenes.multi_instance(scenes.config_small(60, 50)), materials=[1, 2, 0],
+                                    area_light=scenes.ceiling_light())
+        W, H = 96, 72
+    gpu_scene(gpu_ctx, sd, W, H)
+    out = {}
+    for mode in ("0", "1", "2", "3"):
+        monkeypatch.setenv("PRT_TAIL", mode)
+        gpu_ctx.reset_accumulation(full=True)
+        out[mode] = gpu_ctx.render(W, H, 4, 4, stats=True)
+    for mode in ("1", "2", "3"):
+        assert np.array_equal(out["0"][0], out[mode][0]) and np.array_equal(out["0"][1], out[mode][1]), mode
+        assert out["0"][2].segments == out[mode][2].segments, mode
+        assert out["0"][2].shadow_rays == out[mode][2].shadow_rays, mode
+
+
 @pytest.mark.parametrize("pipe", ["", "wave1"])
 def test_batches_identical(gpu_ctx, monkeypatch, pipe):
     """Wavefront batches (consecutive item ranges on concurrent streams, PRT_BATCHES) render bit-identical
