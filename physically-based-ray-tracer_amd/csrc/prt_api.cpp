@@ -148,12 +148,13 @@ int trav_from_env() {
   return 32;
 }
 
-// waves/SIMD of the persistent traversal kernels: the LDS stack (8 / 11 / 14 / 18 groups at 8 / 6 / 5 / 4
+// waves/SIMD of the persistent traversal kernels: the LDS stack (8 / 9 / 11 / 14 / 18 groups at 8 / 7 / 6 / 5 / 4
 // waves) must hold max_depth - 1 groups; layout_for caps the depth at 16
 int occ_for(const prt_ctx* c) {
   const char* e = std::getenv("PRT_OCC");
-  int want = e ? std::atoi(e) : 6;
+  int want = e ? std::atoi(e) : 7;
   if (want >= 8 && c->max_depth <= 9) return 8;
+  if (want >= 7 && c->max_depth <= 10) return 7;
   if (want >= 6 && c->max_depth <= 12) return 6;
   if (want >= 5 && c->max_depth <= 15) return 5;
   return 4;

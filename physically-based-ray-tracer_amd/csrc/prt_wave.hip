@@ -385,7 +385,7 @@ template <bool ANY>
 void launch_persistent(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it) {
   if (c.occ == 8) {
     if (c.trav == 32) launch_p1<ANY, 32, 8, 8>(c, S, B, it); else launch_p1<ANY, 16, 8, 8>(c, S, B, it);
-  } else if (c.occ == 6) {
+  } else if (c.occ == 6 || c.occ == 7) {  // 7 (the merged pipeline's default): this launcher's 6-wave form
     if (c.trav == 32) launch_p1<ANY, 32, 12, 6>(c, S, B, it); else launch_p1<ANY, 16, 12, 6>(c, S, B, it);
   } else if (c.occ == 5) {
     if (c.trav == 32) launch_p1<ANY, 32, 14, 5>(c, S, B, it); else launch_p1<ANY, 16, 14, 5>(c, S, B, it);

@@ -420,6 +420,8 @@ void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_
 static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
   if (c.occ == 8) {
     if (c.trav == 16) launch_t2<16, 8, 8, 32>(c, S, B, it, iters); else launch_t2<32, 8, 8, 32>(c, S, B, it, iters);
+  } else if (c.occ == 7) {
+    if (c.trav == 16) launch_t2<16, 9, 7, 64>(c, S, B, it, iters); else launch_t2<32, 9, 7, 64>(c, S, B, it, iters);
   } else if (c.occ == 6) {
     if (c.trav == 16) launch_t2<16, 11, 6, 64>(c, S, B, it, iters); else launch_t2<32, 11, 6, 64>(c, S, B, it, iters);
   } else if (c.occ == 5) {
