@@ -26,7 +26,9 @@
 namespace prt {
 
 // ---- one traversal launch: closest hits of P(iter) (iter < iters) + any hits of S(iter - 1) (iter > 0)
-template <bool HALF, int REFILL, int STACK, int WAVES, int TAILN>
+// GTAIL: the opt-in group tail (PRT_TAIL=2/3, measured slower) is compiled into the default 7-wave form only: in
+// the others its registers would cost scratch spills
+template <bool HALF, int REFILL, int STACK, int WAVES, int TAILN, bool GTAIL = false>
 __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, uint32_t iter, uint32_t iters) {
   __shared__ uint32_t lds_stack[2 * STACK * 64];
   __shared__ uint32_t prefP[kNSub + 1], prefS[kNSub + 1];
@@ -38,7 +40,8 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   const uint32_t total = nP + nS;
   // a launch with fewer rays than lanes spreads them: at most `cap` (>= 8) per fetch, so a small queue gives
   // many waves a few rays each (at <= 8 they go straight to the group tail) instead of few waves 64 each
-  const uint32_t cap = B.group_tail ? max(8u, (total + gridDim.x - 1u) / gridDim.x) : 64u;
+  const uint32_t gtail = GTAIL ? (uint32_t)B.group_tail : 0u;
+  const uint32_t cap = gtail ? max(8u, (total + gridDim.x - 1u) / gridDim.x) : 64u;
   if (blockIdx.x * min(cap, 64u) >= total) return;
   uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
   uint32_t part = xcc_id();
@@ -88,7 +91,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
           B.hit[h] = make_float4(hit.t, hit.u, hit.v, __uint_as_float(hit.prim | (hit.inst << 26)));
         }
       },
-      B.coop_tail ? tail_lds : nullptr, (uint32_t)B.group_tail);
+      B.coop_tail ? tail_lds : nullptr, gtail);
   if (tl && threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -410,6 +413,13 @@ __global__ void __launch_bounds__(kBlock) k_resolve2(SceneDev S, TraceArgs A, Wa
 // 160 KB / (4 x WAVES) blocks per CU
 template <int REFILL, int STACK, int WAVES, int TAILN>
 void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
+  if constexpr (WAVES == 7 && REFILL == 32) {
+    if (c.layout != 9 && B.group_tail) {
+      hipLaunchKernelGGL((k_trace2<false, REFILL, STACK, WAVES, TAILN, true>), dim3(256u * 4u * WAVES), dim3(64), 0,
+                         c.stream, S, B, it, iters);
+      return;
+    }
+  }
   static_assert(2 * STACK * 256 + 264 + 4 * 3 * TAILN <= 163840 / (4 * WAVES), "LDS over the occupancy budget");
   const dim3 grid(256u * 4u * WAVES);
   if (c.layout == 9)
