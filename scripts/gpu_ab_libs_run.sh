@@ -1,3 +1,3 @@
 # library A/B (scripts/ab_libs.sh) of the variants in prt/ab/, interleaved
 set -o pipefail
-bash scripts/ab_libs.sh A D A D A D || exit $?
+bash scripts/ab_libs.sh S4 S5 S6 S4 S5 S6 || exit $?
