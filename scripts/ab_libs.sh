@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # A/B of library builds on the GPU box: scripts/ab_libs.sh NAME...  (prt/ab/libprt_NAME.so, built beforehand)
-# Each variant is copied over prt/libprt.so (the box's copy is scratch) and benched (C4, 5 steps) under its own
+# BENCH_ARGS overrides the bench arguments (default: C4, --steps 5 --warmup 1).  Each variant is copied over prt/libprt.so (the box's copy is scratch) and benched (C4, 5 steps) under its own
 # time limit; the original library is restored at the end.  Variants run in the order given (repeat names to
 # interleave).
 set -u
@@ -12,7 +12,7 @@ i=0
 for v in "$@"; do
   i=$((i+1))
   cp "$L/ab/libprt_$v.so" "$L/libprt.so"
-  timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > "gpurun_out/abl_$i.log" 2>&1
+  timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 5 --warmup 1} --no-cpu-baseline > "gpurun_out/abl_$i.log" 2>&1
   rc=$?
   line=$(grep '"metric"' "gpurun_out/abl_$i.log" | tail -1)
   python3 -c "import json,sys; d=json.loads(sys.argv[2]); r=d['roofline']['kernels']; print(sys.argv[1].ljust(12), d['value'], d['ms_per_step'], {k: v['launch_ms'] for k, v in r.items()})" "$v" "$line" 2>/dev/null || echo "$v: rc=$rc"

@@ -1,3 +1,3 @@
-# library A/B (scripts/ab_libs.sh) of the variants in prt/ab/, interleaved
+# library A/B (scripts/ab_libs.sh) of the variants in prt/ab/, interleaved, on C5 at reduced steps
 set -o pipefail
-bash scripts/ab_libs.sh S4 S5 S6 S4 S5 S6 || exit $?
+BENCH_ARGS="--scene c5 --steps 3 --warmup 1" bash scripts/ab_libs.sh E2 E3 E2 E3 || exit $?
