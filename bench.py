@@ -243,7 +243,11 @@ def main():
                        "outputs": "host memory (PCIe-inclusive)" if args.host_out else "device (HBM-resident)",
                        "rays_per_step": int(rays / args.steps), "segments_per_step": int(seg / args.steps),
                        "shadow_per_step": int(shadow / args.steps),
-                       "mpix_per_s": round(W * H / (ms_step / 1e3) / 1e6, 2)},
+                       "mpix_per_s": round(W * H / (ms_step / 1e3) / 1e6, 2),
+                       # camera paths (one Trace chain per camera ray: W*H*spp per frame) and the
+                       # reference's own "Mrays/s" label, pixels per second (Core/Renderer.cpp:473)
+                       "mpaths_per_s": round(W * H * args.spp / (ms_step / 1e3) / 1e6, 2),
+                       "reference_style_mrays_per_s": round(W * H / (ms_step / 1e3) / 1e6, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": dom, "per": f"launch (avg of {launches} launches per frame)",
