@@ -1,3 +1,3 @@
-# library A/B (scripts/ab_libs.sh) of the variants in prt/ab/, interleaved, on C5 at reduced steps
+# library A/B (scripts/ab_libs.sh) of the variants in prt/ab/, interleaved
 set -o pipefail
-BENCH_ARGS="--scene c5 --steps 3 --warmup 1" bash scripts/ab_libs.sh E2 E3 E2 E3 || exit $?
+bash scripts/ab_libs.sh D0 L4 B64 D0 L4 B64 || exit $?
