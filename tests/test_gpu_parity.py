@@ -286,6 +286,44 @@ def test_determinism_c4_full_size(gpu_ctx):
     assert np.isfinite(a1).all()
 
 
+def test_c4_full_size_matches_oracle(gpu_ctx):
+    """BASELINE's headline workload itself against the oracle: C4 (1M triangles), 1920x1080, 4 spp, depth 4, all
+    reference features on.  The oracle renders the full frame on the host cores (OpenMP, ~1-2 s at 16 threads), so
+    the bench frame is compared directly, not only through size-independent properties: per-channel RMSE
+    <= 1e-4 (BASELINE.json), >= 99.9 % bit-identical pixels, identical ray counts."""
+    import os
+    sd = scenes.config_c4()
+    W, H = 1920, 1080
+    gpu_scene(gpu_ctx, sd, W, H)
+    a_g, r_g, s_g = gpu_ctx.render(W, H, 4, 4)
+    osc = oracle.OracleScene(sd, W, H)
+    a_o, r_o, _, s_o = osc.render(W, H, spp=4, bounces=4, nthreads=min(16, os.cpu_count() or 1))
+    err = rmse(a_o, a_g)
+    exact = float(np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)))
+    assert err <= RMSE_TOL, (err, exact)
+    assert exact >= 0.999, (err, exact)
+    assert np.mean(r_o == r_g) >= 0.999
+    assert (s_g.segments, s_g.shadow_rays) == (s_o.segments, s_o.shadow_rays)
+
+
+def test_c5_quarter_matches_oracle(gpu_ctx):
+    """Config C5 (C4 + the quad area light with MIS, 16 spp, depth 8) at a quarter of its pixels (1920x1080, the
+    bench's CPU-baseline sample) against the oracle's extension restatement: RMSE <= 1e-4, >= 99.9 % identical
+    pixels, identical ray counts."""
+    import os
+    sd = scenes.config_c5()
+    W, H = 1920, 1080
+    gpu_scene(gpu_ctx, sd, W, H)
+    a_g, r_g, s_g = gpu_ctx.render(W, H, 16, 8)
+    osc = oracle.OracleScene(sd, W, H)
+    a_o, r_o, _, s_o = osc.render(W, H, spp=16, bounces=8, nthreads=min(16, os.cpu_count() or 1))
+    err = rmse(a_o, a_g)
+    exact = float(np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)))
+    assert err <= RMSE_TOL, (err, exact)
+    assert exact >= 0.999, (err, exact)
+    assert (s_g.segments, s_g.shadow_rays) == (s_o.segments, s_o.shadow_rays)
+
+
 @pytest.mark.parametrize("preset,over,flags", [
     (0, {}, oracle.DEFAULT_FLAGS),
     (1, {}, oracle.DEFAULT_FLAGS),                                   # GAME preset P1: aberration -1, Panini d=2
