@@ -270,6 +270,37 @@ def test_tiles_match_full_frame(gpu_ctx, post):
     assert np.array_equal(rgb.cpu().numpy().view(np.uint32), r_full)
 
 
+def test_tiles_full_size_world8(gpu_ctx):
+    """The bench's N = 8 decomposition at full size: C4 at 1920x1080, 4 spp, depth 4 cut into 32x32 tiles dealt to 8
+    ranks (each rendered by its own context on this GPU), gathered and untiled, equals the single-GPU frame bit
+    for bit, with the same total ray counts."""
+    import torch
+    import prt
+    sd = scenes.config_c4()
+    W, H, ts, world = 1920, 1080, 32, 8
+    gpu_scene(gpu_ctx, sd, W, H)
+    gpu_ctx.reset_accumulation(full=True)
+    a_full, r_full, s_full = gpu_ctx.render(W, H, 4, 4, stats=True)
+    per = gpu_ctx.tile_buffer_pixels(W, H, ts, world)
+    gathered = torch.zeros((world, per, 4), dtype=torch.float32, device="cuda")
+    seg = shadow = 0
+    for r in range(world):
+        c = prt.Context(0)
+        gpu_scene(c, sd, W, H)
+        st = c.render_tiles(W, H, 4, 4, ts, r, world, gathered[r].data_ptr(), stats=True)
+        torch.cuda.synchronize()
+        seg += st.segments
+        shadow += st.shadow_rays
+        c.close()
+    avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+    rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    gpu_ctx.untile(gathered.data_ptr(), W, H, ts, world, avg.data_ptr(), rgb.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(avg.cpu().numpy(), a_full)
+    assert np.array_equal(rgb.cpu().numpy().view(np.uint32), r_full)
+    assert (seg, shadow) == (s_full.segments, s_full.shadow_rays)
+
+
 def test_determinism_c4_full_size(gpu_ctx):
     """At the bench size (C4, 1920x1080, 4 spp, depth 4): two renders are bit-identical and the ray counts
     match the counting rule (segments <= W*H*spp*depth, shadow rays <= 4 per shaded hit)."""
