@@ -251,6 +251,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": dom, "per": f"launch (avg of {launches} launches per frame)",
+                         "basis": "SURVEY 8d algorithmic bytes in the reference's BVH8_CPU layout (256-B nodes, "
+                                  "192-B leaves) -- frac > 1 means the same traversal in this build's 80-B Node8 / "
+                                  "48-B triangle layout, served largely from L2 / Infinity Cache; own_layout prices "
+                                  "this build's bytes, traffic is PMC-measured HBM",
                          "launch_ms": round(kern_ms, 4), "algorithmic_bytes": round(alg_bytes),
                          "kernels": {k: {"launch_ms": round(v[1], 4), "alg_GBps": round(v[0] / (v[1] / 1e3) / 1e9, 1)
                                          if v[1] > 0 else None} for k, v in kern.items()},
