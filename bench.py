@@ -8,12 +8,17 @@ normal map, skybox, lighted, stochastic NEE).  A step = one prt_render of the fu
 (2 reference frames x 2 AA paths per pixel), inputs resident in HBM.
 
 Mrays/s = (closest-hit segments + any-hit shadow rays) / time, counted on the device.
-N > 1: one process per GPU (torchrun), pixel tiles 32x32 round-robin over ranks, RCCL gather of the
-per-rank tile buffers to rank 0, untile there; value = all ranks' rays / max-over-ranks time.
+--gpus N > 1: one process per GPU.  Run without WORLD_SIZE in the environment, bench.py starts the N ranks
+itself (torch.distributed.run as a child process, before anything touches a GPU) and exits with their
+status.  Every rank's context joins one RCCL communicator inside the C ABI (prt_shard_init_rccl): each renders
+its 32x32 pixel tiles (round-robin) and prt_render gathers the tile buffers on rank 0 with one ncclGather per
+frame; value = all ranks' rays / max-over-ranks time.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -22,8 +27,12 @@ sys.path.insert(0, os.path.join(ROOT, "physically-based-ray-tracer_amd"))
 
 import numpy as np  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 VALU instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md, Execution model) = 1228.8 G wave-instructions/s
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2 * 1000.0
 VISITS_JSON = os.path.join(ROOT, "profiles", "reference_visits_c4.json")
+TRACE_KERNEL = "k_trace2"
 
 
 def algorithmic_bytes_per_ray():
@@ -35,9 +44,7 @@ def algorithmic_bytes_per_ray():
     for kind in ("closest", "anyhit"):
         n = v[kind]
         out[kind] = 256.0 * n["n_int"] + 192.0 * n["n_leaf"] + 64.0 * n["n_tlas"] + 192.0 * n["n_inst"] + 48 + 16
-    out["per_shaded_hit"] = 12.0   # 3 texels
-    out["per_pixel_frame"] = 36.0  # accumulator read+write + rgb8
-    return out, v
+    return out
 
 
 def own_layout_bytes_per_ray():
@@ -53,39 +60,109 @@ def own_layout_bytes_per_ray():
             "anyhit": v["node_bytes"] * a["node_visits"] + v["tri_bytes"] * a["tri_tests"] + 32 + 1}
 
 
-def measured_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/traffic_current.json,
-    written by scripts/summarize_prof.py; FETCH_SIZE x2 gfx950 correction, MI355X_MICROARCH.md HBM)."""
-    f = os.path.join(ROOT, "profiles", "traffic_current.json")
-    if not os.path.exists(f):
-        return None
-    with open(f) as fh:
+def _pmc_kernel(path, kernel):
+    """Per-launch record of `kernel` in a committed profile summary (scripts/summarize_prof.py)."""
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as fh:
         t = json.load(fh)
     for name, d in t.get("kernels", {}).items():
-        base = name.split("::")[-1].split("<")[0]
-        if base in (kernel, kernel + "_p", kernel + "2") and "hbm_bytes_per_launch" in d:
-            return int(d["hbm_bytes_per_launch"])
-    return None
+        if name.split("::")[-1].split("<")[0] == kernel:
+            return d, t.get("name")
+    return None, None
 
 
-def cpu_baseline(sd, threads, W, H, spp, bounces):
-    """The oracle (C restatement, OpenMP over rows) on a bounded sample of the same workload: the full frame
-    when it is <= ~40M rays (C4: ~29M rays, 10-30 s of CPU-core work), else a centred crop of the camera's
-    pixel grid with the same spp / depth (every pixel-frame is independent, so Mrays/s carries over)."""
+def measured_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/traffic_current.json;
+    FETCH_SIZE x2 gfx950 correction of MI355X_MICROARCH.md, checked for this kernel's gathers by
+    profiles/fetch_calibration.json)."""
+    d, name = _pmc_kernel(os.path.join(ROOT, "profiles", "traffic_current.json"), kernel)
+    if d and "hbm_bytes_per_launch" in d:
+        return int(d["hbm_bytes_per_launch"]), name
+    return None, name
+
+
+def measured_valu(kernel):
+    """VALU wave-instructions per launch of `kernel` (SQ_INSTS_VALU, profiles/valu_current.json)."""
+    d, name = _pmc_kernel(os.path.join(ROOT, "profiles", "valu_current.json"), kernel)
+    if d and "SQ_INSTS_VALU" in d:
+        return d, name
+    return None, name
+
+
+def host_cpu():
+    """CPU model, logical CPUs of the host, and the CPUs this process may use (affinity / cgroup quota)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+            if q != "max":
+                usable = min(usable, max(1, int(int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        usable = min(usable, int(omp))
+    return model, os.cpu_count() or 1, usable
+
+
+def cpu_baseline(sd, W, H, spp, bounces):
+    """Two CPU legs on a bounded sample of the same workload, timed on this host's cores (rank 0, N=1):
+    'port'       -- the oracle: the C restatement of Renderer::Trace + its own traversal (OpenMP over rows);
+    'reference'  -- the same restated Trace running on the reference's own tinybvh BVH8_CPU + TLAS traversal
+                    (oracle/_ref, compiled from /root/reference/Core/tiny_bvh.h), the reference renderer's
+                    hot path minus the shading code that cannot be compiled here.
+    Sample: the full frame when it is <= ~300M rays-bounces, else a centred camera crop with the same spp /
+    depth (pixels are independent, so Mrays/s carries over).  The reference leg's BVH8_CPU build is outside
+    the timed region, like the GPU's BLAS build."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
+    model, nproc, threads = host_cpu()
     scale = 1
     while W * H * spp * bounces // (scale * scale) > 300_000_000:
         scale *= 2
     w, h = W // scale, H // scale
-    osc = oracle.OracleScene(sd, w, h)
-    t0 = time.perf_counter()
-    _, _, _, st = osc.render(w, h, spp=spp, bounces=bounces, nthreads=threads)
-    dt = time.perf_counter() - t0
-    rays = st.segments + st.shadow_rays
     what = "the full frame" if scale == 1 else f"the same camera at {w}x{h} (1/{scale * scale} of the pixels)"
-    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{sd.name}: {what}, {spp} spp, depth {bounces} ({rays} rays, {dt:.2f} s)"}
+    legs = []
+    osc = oracle.OracleScene(sd, w, h)
+    for kind in ("port", "reference"):
+        if kind == "reference":
+            if oracle.reflib() is None:
+                legs.append({"kind": kind, "value": None, "why": "oracle/_ref/libref_tinybvh.so not built"})
+                continue
+            osc.use_reference_traversal()
+        t0 = time.perf_counter()
+        _, _, _, st = osc.render(w, h, spp=spp, bounces=bounces, nthreads=threads)
+        dt = time.perf_counter() - t0
+        rays = st.segments + st.shadow_rays
+        legs.append({"kind": kind, "value": round(rays / dt / 1e6, 2), "unit": "Mrays/s", "seconds": round(dt, 2),
+                     "rays": int(rays)})
+    ref = legs[1] if legs[1].get("value") else legs[0]
+    return {"value": ref["value"], "unit": "Mrays/s", "cores": threads, "kind": ref["kind"],
+            "model": model, "host_logical_cpus": nproc,
+            "sample": f"{sd.name}: {what}, {spp} spp, depth {bounces}, {threads} threads "
+                      f"(this GPU's CPU share of a {nproc}-CPU host)",
+            "legs": legs}
+
+
+def spawn_ranks(n):
+    """--gpus N without WORLD_SIZE: start N ranks of this script under torch.distributed.run (a child process;
+    nothing here has touched a GPU) and return their exit status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def main():
@@ -105,6 +182,9 @@ def main():
                     help="outputs (avg + rgb8) to host memory every step: the PCIe-inclusive rate (not the contract value)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+
     import torch
     import prt
     from prt import scenes
@@ -112,13 +192,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     dist = None
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", device_id=dev)
 
     sd = {"c3": scenes.config_c3, "c4": scenes.config_c4, "c5": scenes.config_c5}[args.scene]()
     big = args.scene == "c5"
@@ -133,27 +215,28 @@ def main():
     ctx.set_scene(scene)
     ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
     info = ctx.scene_info()
+    ranks_seen = 1
+    if world > 1:
+        si = prt.tiles.join_rccl(ctx, dist, args.tile)
+        one = torch.ones(1, dtype=torch.float32, device=dev)
+        dist.all_reduce(one)  # the rank count over the torch RCCL group ...
+        ranks_seen = int(one.item())
+        if ranks_seen != world or si.world != world:  # ... and the context's own communicator
+            raise SystemExit(f"rank {rank}: {ranks_seen} ranks in the torch group, {si.world} in the context")
 
-    dev = torch.device("cuda", local)
     avg = torch.zeros((H * W, 4), dtype=torch.float32, device=dev)
     rgb = torch.zeros(H * W, dtype=torch.int32, device=dev)
-    if world > 1:
-        shard = prt.tiles.ShardedFrame(ctx, dist, W, H, args.tile, device=dev)
-
     avg_h = np.zeros((H * W, 4), np.float32) if args.host_out else None
     rgb_h = np.zeros(H * W, np.uint32) if args.host_out else None
-
     fpc = max(1, args.spp // 2)  # reference frames per call (AA: 2 paths each): distinct RNG streams per step
 
     def step(i):
-        if world == 1 and args.host_out:
+        if args.host_out:
             _, _, st = ctx.render(W, H, args.spp, args.bounces, frame_index=fpc * i, avg=avg_h, rgb8=rgb_h,
                                   device_out=False, stats=True)
-        elif world == 1:
+        else:
             _, _, st = ctx.render(W, H, args.spp, args.bounces, frame_index=fpc * i, avg=avg.data_ptr(),
                                   rgb8=rgb.data_ptr(), device_out=True, stats=True)
-        else:
-            st = shard.render(args.spp, args.bounces, avg.data_ptr(), rgb.data_ptr(), frame_index=fpc * i)
         return st
 
     for i in range(args.warmup):
@@ -162,24 +245,20 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     seg = shadow = 0
-    ms_trace, ms_closest, ms_anyhit = [], [], []
-    pipeline = iters = batches = 0
+    ms_closest = []
+    iters = 0
     t0 = time.perf_counter()
     for i in range(args.steps):
         st = step(args.warmup + i)
         seg += st.segments
         shadow += st.shadow_rays
-        ms_trace.append(st.ms_trace)
         ms_closest.append(st.ms_closest)
-        ms_anyhit.append(st.ms_anyhit)
-        pipeline = st.pipeline
         iters = st.iterations
-        batches = st.batches
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    rays = seg + shadow
+    seg_local, shadow_local = seg, shadow
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -187,41 +266,50 @@ def main():
         r = torch.tensor([seg, shadow], dtype=torch.float64, device=dev)
         dist.all_reduce(r)
         seg, shadow = int(r[0].item()), int(r[1].item())
-        rays = seg + shadow
+    rays = seg + shadow
 
     if rank == 0:
         ms_step = elapsed * 1000.0 / args.steps
         value = rays / elapsed / 1e6
-        bpr, visits = algorithmic_bytes_per_ray()
-        # roofline of the dominant kernel, per launch: algorithmic bytes (reference BVH8_CPU visit counts x
-        # SURVEY 8d bytes) of the rays one launch processes over the kernel's average launch duration (HIP events
-        # recorded on the render stream around every launch; ms_closest / ms_anyhit sum them per frame)
-        seg_f, sh_f = seg / args.steps, shadow / args.steps
-        launches = max(1, iters) if pipeline in (0, 2) else 1
-        kern = {}
-        if pipeline == 2:  # merged pipeline: one traversal launch per iteration (closest + shadow rays)
-            kern["k_trace"] = ((seg_f * bpr["closest"] + sh_f * bpr["anyhit"]) / launches,
-                               float(np.mean(ms_closest)) / launches)
-        elif pipeline == 3:  # streaming engine: one persistent launch per frame (traversal + shading)
-            kern["k_stream"] = (seg_f * bpr["closest"] + sh_f * bpr["anyhit"], float(np.mean(ms_closest)))
-        elif pipeline == 0:
-            kern["k_extend"] = (seg_f * bpr["closest"] / launches, float(np.mean(ms_closest)) / launches)
-            kern["k_shadow"] = (sh_f * bpr["anyhit"] / launches, float(np.mean(ms_anyhit)) / launches)
-        else:
-            kern["k_trace_frames"] = (seg_f * bpr["closest"] + sh_f * bpr["anyhit"], float(np.mean(ms_trace)))
-        dom = max(kern, key=lambda k: kern[k][1])
-        alg_bytes, kern_ms = kern[dom]
-        kern_ms = max(kern_ms, 1e-9)  # PRT_LAUNCH_TIMERS=0 (A/B runs): no per-launch times
-        achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-        traffic = measured_traffic(dom) if args.scene == "c4" else None  # the committed PMC passes are of C4
+        # Roofline of the dominant kernel (k_trace2: the merged closest + shadow traversal, one launch per
+        # wavefront iteration), per launch.  Launch time: HIP events recorded on the render stream around every
+        # launch (stats.ms_closest sums them per frame).  Counts per launch: rocprofv3 PMC passes of this same
+        # command, committed under profiles/ (SQ_INSTS_VALU; FETCH_SIZE + WRITE_SIZE).
+        launches = max(1, iters)
+        kern_ms = max(float(np.mean(ms_closest)) / launches, 1e-9)  # PRT_LAUNCH_TIMERS=0: no per-launch times
+        seg_f, sh_f = seg_local / args.steps, shadow_local / args.steps  # rank 0's rays: its launches
+        c4 = args.scene == "c4" and W == 1920 and H == 1080 and world == 1  # the PMC passes are of this config
+        valu, valu_src = measured_valu(TRACE_KERNEL) if c4 else (None, None)
+        traffic, traffic_src = measured_traffic(TRACE_KERNEL) if c4 else (None, None)
+        valu_rate = valu["SQ_INSTS_VALU"] / (kern_ms / 1e3) / 1e9 if valu else None
+        hbm_rate = traffic / (kern_ms / 1e3) / 1e9 if traffic else None
+        bpr = algorithmic_bytes_per_ray()
+        ref_bytes = (seg_f * bpr["closest"] + sh_f * bpr["anyhit"]) / launches
         own = own_layout_bytes_per_ray()
-        own_block = None
-        if own is not None and pipeline in (0, 2, 3):
-            own_b = ((seg_f * own["closest"] if dom in ("k_extend", "k_trace", "k_stream") else 0.0) +
-                     (sh_f * own["anyhit"] if dom in ("k_shadow", "k_trace", "k_stream") else 0.0)) / launches
-            own_block = {"bytes_per_ray": {k: round(v, 1) for k, v in own.items()}, "algorithmic_bytes": round(own_b),
-                         "achieved": round(own_b / (kern_ms / 1e3) / 1e9, 1),
-                         "frac": round(own_b / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+        own_bytes = (seg_f * own["closest"] + sh_f * own["anyhit"]) / launches if own else None
+        hbm = {"achieved": round(hbm_rate, 1) if hbm_rate else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(hbm_rate / HBM_PEAK_GBS, 4) if hbm_rate else None, "traffic": traffic,
+               "source": traffic_src}
+        if valu_rate is not None:
+            roof = {"bound": "valu", "achieved": round(valu_rate, 1), "peak": VALU_PEAK_GINST,
+                    "unit": "G VALU wave-instructions/s", "frac": round(valu_rate / VALU_PEAK_GINST, 4),
+                    "traffic": traffic, "valu_insts_per_launch": int(valu["SQ_INSTS_VALU"]), "source": valu_src}
+            if "valu_busy" in valu:
+                roof["valu_busy_pmc"] = round(valu["valu_busy"], 4)
+        else:  # no VALU pass for this config: price the measured HBM bytes (or nothing)
+            roof = {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm["frac"], "traffic": traffic}
+        roof.update({
+            "kernel": TRACE_KERNEL, "per": f"launch (avg of {launches} launches per frame)",
+            "launch_ms": round(kern_ms, 4), "hbm": hbm,
+            "algorithmic_bytes_per_launch": round(ref_bytes),
+            "reference_layout_equiv_GBps": round(ref_bytes / (kern_ms / 1e3) / 1e9, 1),
+            "own_layout_GBps": round(own_bytes / (kern_ms / 1e3) / 1e9, 1) if own_bytes else None,
+            "basis": "frac = PMC-measured VALU issue rate over the VALU issue peak (the kernel is VALU-bound); "
+                     "hbm = PMC-measured HBM bytes over the HBM peak; reference_layout_equiv_GBps = SURVEY 8d "
+                     "bytes in the reference's BVH8_CPU layout over the launch time (not HBM traffic)",
+            "bytes_per_ray": {k: round(v, 1) for k, v in bpr.items()},
+        })
         out = {
             "metric": f"Mrays/s (closest-hit segments + shadow any-hit rays) at {W}x{H}, {args.spp} spp, depth {args.bounces}",
             "value": round(value, 2),
@@ -234,12 +322,12 @@ def main():
             "scaling": "strong",  # one fixed frame is split into pixel tiles over the N GPUs
             "vs_baseline": None,
             "dtype": "f32",
-            "pipeline": {0: "wavefront", 1: "megakernel", 2: "wavefront-merged", 3: "stream"}[pipeline],
-            "batches": batches,
+            "ranks_seen": ranks_seen,
             "data": "synthetic (seeded procedural heightfield, textures, sky; scenes.py)",
             "config": {"workload": f"{sd.name}: {info.triangles} tris, {W}x{H}, {args.spp} spp, depth {args.bounces}",
                        "global_batch": W * H, "seq_len": args.bounces,
-                       "parallelism": f"pixel-tile{args.tile} x{world}" if world > 1 else "single-gpu",
+                       "parallelism": f"pixel-tile{args.tile} x{world} (RCCL gather in prt_render)" if world > 1
+                       else "single-gpu",
                        "outputs": "host memory (PCIe-inclusive)" if args.host_out else "device (HBM-resident)",
                        "rays_per_step": int(rays / args.steps), "segments_per_step": int(seg / args.steps),
                        "shadow_per_step": int(shadow / args.steps),
@@ -248,23 +336,10 @@ def main():
                        # reference's own "Mrays/s" label, pixels per second (Core/Renderer.cpp:473)
                        "mpaths_per_s": round(W * H * args.spp / (ms_step / 1e3) / 1e6, 2),
                        "reference_style_mrays_per_s": round(W * H / (ms_step / 1e3) / 1e6, 2)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": dom, "per": f"launch (avg of {launches} launches per frame)",
-                         "basis": "SURVEY 8d algorithmic bytes in the reference's BVH8_CPU layout (256-B nodes, "
-                                  "192-B leaves) -- frac > 1 means the same traversal in this build's 80-B Node8 / "
-                                  "48-B triangle layout, served largely from L2 / Infinity Cache; own_layout prices "
-                                  "this build's bytes, traffic is PMC-measured HBM",
-                         "launch_ms": round(kern_ms, 4), "algorithmic_bytes": round(alg_bytes),
-                         "kernels": {k: {"launch_ms": round(v[1], 4), "alg_GBps": round(v[0] / (v[1] / 1e3) / 1e9, 1)
-                                         if v[1] > 0 else None} for k, v in kern.items()},
-                         "bytes_per_ray": {k: round(v, 1) for k, v in bpr.items()},
-                         "own_layout": own_block,
-                         "traffic_GBps": round(traffic / (kern_ms / 1e3) / 1e9, 1) if traffic else None},
+            "roofline": roof,
         }
         if world == 1 and not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(sd, threads, W, H, args.spp, args.bounces)
+            out["cpu_baseline"] = cpu_baseline(sd, W, H, args.spp, args.bounces)
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:

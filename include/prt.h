@@ -19,6 +19,10 @@
  * prt_status; prt_last_error() gives the message for the calling thread.  No exceptions cross the ABI.
  * One host thread per context.  All scene arrays are copied to device memory (HBM) during the call;
  * the caller may free them afterwards.  A HIP device must be present: there is no CPU fallback.
+ * Ordering: prt_set_textures / prt_set_meshes / prt_set_sky first wait for the frames queued on the
+ * context's stream (they overwrite resident buffers); prt_set_instances / prt_set_instance_materials are
+ * stream-ordered (a frame queued before the call renders the old instances); the remaining setters are
+ * read at the next prt_render.
  */
 #ifndef PRT_H
 #define PRT_H
@@ -29,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PRT_ABI_VERSION 3
+#define PRT_ABI_VERSION 4
 
 typedef enum {
     PRT_OK = 0,
@@ -140,13 +144,11 @@ typedef struct {
     double   ms_trace;      /* device time of the path-tracing kernel(s) only */
     double   ms_closest;    /* device time of the traversal launches (pipeline 2: closest + shadow rays together;
                                pipeline 3: the whole persistent launch, shading included) */
-    double   ms_anyhit;     /* device time of the shadow any-hit launches (pipeline 0 only) */
-    int32_t  pipeline;      /* 2 = merged-trace wavefront (default), 0 = wavefront with separate extend /
-                               shadow launches (PRT_PIPELINE=wave1), 1 = megakernel (PRT_PIPELINE=mega),
-                               3 = streaming engine, one persistent launch (PRT_PIPELINE=stream) */
-    int32_t  iterations;    /* traversal launches (pipelines 0 / 2: per batch, summed over the batches) */
-    int32_t  batches;       /* wavefront batches: consecutive item ranges on concurrent streams (PRT_BATCHES) */
-    int32_t  reserved;
+    double   ms_anyhit;     /* reserved (0): shadow rays are traced inside the merged traversal launches */
+    int32_t  pipeline;      /* 2 = the merged-trace wavefront (prt_wave2.hip) */
+    int32_t  iterations;    /* traversal launches per call */
+    int32_t  batches;       /* 1 */
+    int32_t  ranks;         /* shards whose rays these stats count (1 unless a local group summed its members) */
 } prt_stats;
 
 /* closest-hit record, tinybvh::Intersection (Core/tiny_bvh.h:545-567) minus user data */
@@ -213,7 +215,35 @@ int prt_render(prt_ctx* ctx, const prt_render_params* params, float* avg_rgba, u
  * full != 0, also samplesPerPixel/distances (fresh Renderer). */
 int prt_reset_accumulation(prt_ctx* ctx, int32_t full);
 
-/* ---- multi-GPU pixel-tile sharding (one process per GPU, RCCL gather done by the caller) ----
+/* ---- multi-GPU inside the boundary ----
+ * A sharded context renders only its rank's pixel tiles (tile_size x tile_size, numbered row-major, dealt
+ * round-robin: rank r owns tiles r, r + world, ...), and prt_render gathers the per-rank tile buffers on
+ * rank 0 once per frame, replacing the reference's single-process OpenMP row loop (Core/Renderer.cpp:43).
+ * Rank 0's outputs then hold the whole frame; the other ranks' outputs are not written (may be NULL).
+ * Stats count the calling rank's rays (a local group sums its members, stats.ranks = world).
+ * Post-processing shards except the chromatic aberration (neighbours' accumulators): PRT_ERR_UNSUPPORTED.
+ *
+ * One process per GPU over RCCL (xGMI): rank 0 makes an id, the caller carries its bytes to the other
+ * ranks over any host channel (torch.distributed, MPI, a file), every rank joins with its own context.
+ * The context owns the communicator; RCCL is loaded on first use (the copy the process already holds). */
+#define PRT_SHARD_ID_BYTES 128
+int prt_shard_unique_id(uint8_t id[PRT_SHARD_ID_BYTES]);
+int prt_shard_init_rccl(prt_ctx* ctx, const uint8_t id[PRT_SHARD_ID_BYTES], int32_t rank, int32_t world,
+                        int32_t tile_size);
+/* ... or an existing communicator (ncclComm_t, not owned: the caller destroys it after prt_destroy) */
+int prt_shard_attach_rccl(prt_ctx* ctx, void* nccl_comm, int32_t tile_size);
+/* One process, several devices (prt_create with a device list).  The group context is member 0;
+ * every setter applies to all members, prt_render renders all shards concurrently (one stream per member)
+ * and gathers them on member 0 with device-to-device copies.  A device may repeat (several shards on one
+ * GPU: how the decomposition is tested on a one-GPU box). */
+int prt_create_group(const prt_device_desc* devices, int32_t count, int32_t tile_size, prt_ctx** out);
+typedef struct {
+    int32_t rank, world, tile_size;
+    int32_t transport;      /* 0 = none (whole frame), 1 = RCCL, 2 = local group */
+} prt_shard_info;
+int prt_get_shard_info(prt_ctx* ctx, prt_shard_info* info);
+
+/* ---- pixel-tile sharding with a caller-side transport (the building blocks of the above) ----
  * The image is cut into tile_size x tile_size tiles numbered in row-major order; rank r renders
  * tiles r, r+world, r+2*world, ...  into a compact float4 buffer laid out
  * [local_tile][tile_size*tile_size] (pixels outside the image are written as 0).

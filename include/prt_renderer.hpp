@@ -176,6 +176,28 @@ class Renderer {
     accumulator.assign(4 * (size_t)width * height, 0.0f);
     screen.assign((size_t)width * height, 0u);
   }
+  // One process, several GPUs (prt_create_group): pixel tiles of tile x tile rendered concurrently on the
+  // devices (a device may repeat), gathered on devices[0]; accumulator / screen hold the whole frame.
+  Renderer(int32_t width, int32_t height, const std::vector<int32_t>& devices, int32_t tile = 32)
+      : width_(width), height_(height) {
+    std::vector<prt_device_desc> d;
+    for (int32_t dev : devices) d.push_back(prt_device_desc{dev, 0});
+    check(prt_create_group(d.data(), (int32_t)d.size(), tile, &ctx_));
+    accumulator.assign(4 * (size_t)width * height, 0.0f);
+    screen.assign((size_t)width * height, 0u);
+  }
+  // One process per GPU: rank 0 calls UniqueId(), the host program carries the bytes to the other ranks
+  // (MPI, a socket, a file), and every rank calls JoinRccl before Init().  Tick() then renders this rank's
+  // tiles and gathers the frame on rank 0 (accumulator / screen are filled on rank 0 only).
+  static std::vector<uint8_t> UniqueId() {
+    std::vector<uint8_t> id(PRT_SHARD_ID_BYTES);
+    check(prt_shard_unique_id(id.data()));
+    return id;
+  }
+  void JoinRccl(const std::vector<uint8_t>& id, int32_t rank, int32_t world, int32_t tile = 32) {
+    if (id.size() != PRT_SHARD_ID_BYTES) throw Error(PRT_ERR_INVALID_ARGUMENT, "RCCL id must be 128 bytes");
+    check(prt_shard_init_rccl(ctx_, id.data(), rank, world, tile));
+  }
   ~Renderer() { prt_destroy(ctx_); }
   Renderer(const Renderer&) = delete;
   Renderer& operator=(const Renderer&) = delete;

@@ -1,4 +1,4 @@
-// bvh_build.cpp -- binned-SAH BLAS builder + 4-wide collapse into the device layout (see bvh_build.h).
+// bvh_build.cpp -- binned-SAH BLAS builder + SAH-optimal 8-wide collapse into the device layout (bvh_build.h).
 #include "bvh_build.h"
 
 #include <algorithm>
@@ -155,91 +155,6 @@ void inflate_box(float* lo, float* hi) {
   }
 }
 
-BuiltBlas build_blas(const float* triangles, int32_t T, int max_leaf) {
-  BuiltBlas out;
-  Builder B;
-  B.tri = triangles;
-  B.max_leaf = std::max(1, std::min(4, max_leaf));
-  B.build(T);
-  for (int k = 0; k < 3; k++) { out.bmin[k] = B.nodes[0].box.lo[k]; out.bmax[k] = B.nodes[0].box.hi[k]; }
-  out.tris.reserve(T);
-
-  // 4-wide collapse, depth-first.  Each entry: (node2 index, Node4 slot to fill).
-  struct Item { int32_t n2; int32_t n4; int depth; };
-  std::vector<Item> stack;
-  out.nodes.push_back(Node4());
-  stack.push_back({0, 0, 1});
-  auto emit_leaf = [&](const Node2& n) -> uint32_t {
-    uint32_t first = (uint32_t)out.tris.size();
-    for (int32_t i = n.first; i < n.first + n.count; i++) {
-      uint32_t p = B.idx[i];
-      const float* a = triangles + 12 * (size_t)p;
-      TriMT t;
-      for (int k = 0; k < 3; k++) {
-        t.v0[k] = a[k];
-        t.e1[k] = a[4 + k] - a[k];   // e1 = v1 - v0, e2 = v2 - v0 (tiny_bvh.h:4614-4616)
-        t.e2[k] = a[8 + k] - a[k];
-      }
-      t.prim = p; t.pad1 = 0; t.pad2 = 0;
-      out.tris.push_back(t);
-    }
-    out.leaves++;
-    return make_leaf(first, (uint32_t)n.count);
-  };
-  while (!stack.empty()) {
-    Item it = stack.back();
-    stack.pop_back();
-    out.depth = std::max(out.depth, it.depth);
-    // gather up to 4 children by opening the largest interior child
-    int32_t ch[4];
-    int nc = 0;
-    const Node2& root = B.nodes[it.n2];
-    if (root.leaf()) {
-      ch[nc++] = it.n2;  // tiny mesh: root itself is a leaf -> single-leaf Node4
-    } else {
-      ch[nc++] = root.left;
-      ch[nc++] = root.right;
-      while (nc < 4) {
-        int bi = -1;
-        float ba = -1.0f;
-        for (int i = 0; i < nc; i++) {
-          const Node2& c = B.nodes[ch[i]];
-          if (!c.leaf() && c.box.area() > ba) { ba = c.box.area(); bi = i; }
-        }
-        if (bi < 0) break;
-        const Node2& c = B.nodes[ch[bi]];
-        ch[bi] = c.left;
-        ch[nc++] = c.right;
-      }
-    }
-    Node4 nd;
-    std::memset(&nd, 0, sizeof(nd));
-    for (int i = 0; i < 4; i++) {
-      if (i >= nc) {
-        nd.lox[i] = nd.loy[i] = nd.loz[i] = 1e30f;   // empty slot: inverted box never hits
-        nd.hix[i] = nd.hiy[i] = nd.hiz[i] = -1e30f;
-        nd.child[i] = kEmptyChild;
-        continue;
-      }
-      const Node2& c = B.nodes[ch[i]];
-      float lo[3] = {c.box.lo[0], c.box.lo[1], c.box.lo[2]}, hi[3] = {c.box.hi[0], c.box.hi[1], c.box.hi[2]};
-      inflate_box(lo, hi);
-      nd.lox[i] = lo[0]; nd.loy[i] = lo[1]; nd.loz[i] = lo[2];
-      nd.hix[i] = hi[0]; nd.hiy[i] = hi[1]; nd.hiz[i] = hi[2];
-      if (c.leaf()) {
-        nd.child[i] = emit_leaf(c);
-      } else {
-        int32_t slot = (int32_t)out.nodes.size();
-        out.nodes.push_back(Node4());
-        nd.child[i] = (uint32_t)slot;
-        stack.push_back({ch[i], slot, it.depth + 1});
-      }
-    }
-    out.nodes[it.n4] = nd;
-  }
-  return out;
-}
-
 namespace {
 
 // per-axis power-of-two scale so that ext / 2^e <= 255; returns the biased exponent (e + 127)
@@ -253,7 +168,7 @@ uint8_t grid_exponent(double ext, double qmax) {
   return (uint8_t)std::min(254, std::max(1, e + 127));
 }
 
-// per-format child-bound storage: Node8 = 8-bit grid coordinates, Node8H = fp16 integers on an 11-bit grid
+// child-bound storage: 8-bit grid coordinates
 struct Fmt8 {
   static constexpr double kQMax = 255.0;
   static void set(Node8& n, int s, const double* lo, const double* hi) {
@@ -266,26 +181,6 @@ struct Fmt8 {
     n.qhix[s] = n.qhiy[s] = n.qhiz[s] = 0;
   }
 };
-uint16_t f16_of_int(int q) {  // exact fp16 encoding of an integer 0..2047
-  if (q == 0) return 0;
-  int e = 0;
-  while ((q >> e) > 1) e++;
-  const uint32_t mant = e >= 10 ? ((uint32_t)q >> (e - 10)) & 0x3FFu : ((uint32_t)q << (10 - e)) & 0x3FFu;
-  return (uint16_t)(((uint32_t)(e + 15) << 10) | mant);
-}
-struct Fmt8H {
-  static constexpr double kQMax = 2047.0;
-  static void set(Node8H& n, int s, const double* lo, const double* hi) {
-    uint16_t* ql[3] = {&n.qlox[s], &n.qloy[s], &n.qloz[s]};
-    uint16_t* qh[3] = {&n.qhix[s], &n.qhiy[s], &n.qhiz[s]};
-    for (int k = 0; k < 3; k++) { *ql[k] = f16_of_int((int)lo[k]); *qh[k] = f16_of_int((int)hi[k]); }
-  }
-  static void empty(Node8H& n, int s) {
-    n.qlox[s] = n.qloy[s] = n.qloz[s] = f16_of_int(2047);
-    n.qhix[s] = n.qhiy[s] = n.qhiz[s] = 0;
-  }
-};
-
 // SAH-optimal collapse of the binary tree into 8-wide nodes (Ylitie, Karras, Laine 2017, sec. 3.1, restated):
 // C(n, i) = cheapest cost of representing binary subtree n by at most i slots of its parent, where one slot
 // is either a leaf (<= max_leaf triangles, cost A(n) * c_tri * count) or a wide node (A(n) * c_node + the
@@ -496,12 +391,6 @@ void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out) {
 BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf) {
   BuiltBlas8 out;
   build_wide8<Node8, Fmt8>(triangles, T, max_leaf, out);
-  return out;
-}
-
-BuiltBlas8H build_blas8h(const float* triangles, int32_t T, int max_leaf) {
-  BuiltBlas8H out;
-  build_wide8<Node8H, Fmt8H>(triangles, T, max_leaf, out);
   return out;
 }
 

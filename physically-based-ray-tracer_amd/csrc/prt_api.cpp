@@ -15,15 +15,12 @@
 #include "bvh_build.h"
 #include "bvh_gpu.h"
 #include "prt_launch.h"
+#include "prt_rccl.h"
 #include "prt_refit.h"
 
 using namespace prt;
 
 namespace {
-
-// wavefront batches: independent consecutive item ranges of one call, each on its own HIP stream, so one
-// batch's launches fill the other's traversal tails and shading gaps (PRT_BATCHES)
-constexpr int kMaxBatches = 4;
 
 thread_local std::string g_err;
 
@@ -38,9 +35,19 @@ int fail(int code, const std::string& msg) {
     if (e_ != hipSuccess) return fail(PRT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
+// device allocation owned by its holder (move-only; freed on destruction)
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) { release(); p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0; }
+    return *this;
+  }
+  ~DevBuf() { release(); }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -58,6 +65,8 @@ struct DevBuf {
   T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// blocking host -> device copy into a resident buffer.  Callers that may overwrite (or reallocate) a buffer
+// that queued frames still read first drain the context stream (drain()).
 hipError_t upload(DevBuf& b, const void* src, size_t n) {
   hipError_t e = b.ensure(n);
   if (e != hipSuccess) return e;
@@ -85,9 +94,8 @@ struct prt_ctx {
   // meshes
   std::vector<MeshDev> mesh_host;
   std::vector<MeshHost> mesh_info;
-  DevBuf nodes, nodes8, nodes8h, tris, stri, mesh;
+  DevBuf nodes8, tris, stri, mesh;
   int max_depth = 0;
-  int layout = 8;  // BLAS node layout of the uploaded meshes: 8 = Node8, 9 = Node8H, 4 = Node4 (PRT_BVH)
   int builder = -1;  // BLAS builder: PRT_BUILDER_HOST_SAH / PRT_BUILDER_GPU_LBVH (-1: PRT_BUILDER env, else host)
   double build_ms = 0;  // wall time of the last prt_set_meshes BLAS builds
   int built_with = PRT_BUILDER_HOST_SAH;
@@ -116,40 +124,42 @@ struct prt_ctx {
   int32_t accW = 0, accH = 0;
   DevBuf frames, avg, rgb8, counters, hits, tl;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  // wavefront pipeline: batch 0 runs on `stream`, batch k > 0 on bstream[k] (fork / join events)
-  DevBuf wave[kMaxBatches];
-  WaveBufs wb[kMaxBatches] = {};
-  uint32_t wave_n[kMaxBatches] = {}, wave_levels[kMaxBatches] = {};
-  bool wave_ext[kMaxBatches] = {};
-  WaveTimers wt[kMaxBatches] = {};
-  hipStream_t bstream[kMaxBatches] = {};
-  hipEvent_t bev[kMaxBatches] = {};
-  // streaming engine (prt_stream.hip)
-  DevBuf sq, sctl;
-  StreamBufs sb{};
-  size_t sq_rcap = 0, sq_hcap = 0;
-  uint32_t sq_n = 0;
-  uint32_t serial = 0;
-  uint32_t nparts = 0, xcc_part = 0xFFFFFFFFu;
+  // wavefront state of the merged pipeline
+  DevBuf wave;
+  WaveBufs wb = {};
+  uint32_t wave_n = 0, wave_levels = 0;
+  bool wave_ext = false;
+  WaveTimers wt = {};
+  // the last enqueued render, for its stats (read_stats)
+  uint32_t last_iters = 0;
+  bool last_timers = false;
+  uint64_t last_paths = 0;
+  // sharding (prt_shard_init_rccl / prt_shard_attach_rccl / prt_create_group)
+  int32_t sh_kind = 0;  // 0 none, 1 RCCL, 2 local group (this context is member 0)
+  int32_t sh_rank = 0, sh_world = 1, sh_tile = 32;
+  ncclComm_t comm = nullptr;
+  bool own_comm = false;
+  std::vector<prt_ctx*> members;  // local group: members 1..world-1, owned by member 0
+  DevBuf shtiles, gathered;       // this rank's tile buffer; rank 0: [world][tile buffer] gathered
+  hipEvent_t sh_ev = nullptr;     // member: tiles handed to member 0; member 0: untile done
 };
 
 namespace {
 
-// The LDS traversal stacks are sized for Trav<L>::kMaxDepth node levels (prt_traverse8.h).
-int layout_for(const prt_ctx* c) {
-  const int maxd = c->layout == 4 ? Trav<4>::kMaxDepth : c->layout == 9 ? Trav<9>::kMaxDepth : Trav<8>::kMaxDepth;
-  return c->max_depth <= maxd ? c->layout : -1;
-}
+// The LDS traversal stacks hold one group per tree level below the root: up to 16 levels (18 groups at
+// 4 waves/SIMD, 16 in the query kernels)
+constexpr int kMaxBvhDepth = 16;
+bool depth_ok(const prt_ctx* c) { return c->max_depth <= kMaxBvhDepth; }
 
-int trav_from_env() {
-  const char* e = std::getenv("PRT_TRAV");
-  if (e && std::strcmp(e, "lockstep") == 0) return 1;
-  if (e && std::strcmp(e, "refill16") == 0) return 16;
-  return 32;
+// finish the frames queued on the context stream before a setter overwrites (or frees) resident buffers
+int drain(prt_ctx* c) {
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return PRT_OK;
 }
 
 // waves/SIMD of the persistent traversal kernels: the LDS stack (8 / 9 / 11 / 14 / 18 groups at 8 / 7 / 6 / 5 / 4
-// waves) must hold max_depth - 1 groups; layout_for caps the depth at 16
+// waves) must hold max_depth - 1 groups; depth_ok caps the depth at 16
 int occ_for(const prt_ctx* c) {
   const char* e = std::getenv("PRT_OCC");
   int want = e ? std::atoi(e) : 7;
@@ -158,13 +168,6 @@ int occ_for(const prt_ctx* c) {
   if (want >= 6 && c->max_depth <= 12) return 6;
   if (want >= 5 && c->max_depth <= 15) return 5;
   return 4;
-}
-
-int layout_from_env() {
-  const char* e = std::getenv("PRT_BVH");
-  if (e && std::strcmp(e, "4") == 0) return 4;
-  if (e && std::strcmp(e, "8h") == 0) return 9;
-  return 8;
 }
 
 // instance refit on the device (prt_refit.h): one async copy of the transforms + k_refit, both on the
@@ -200,9 +203,7 @@ int scene_ready(prt_ctx* c, SceneDev& S) {
   int rc = ensure_instances(c);
   if (rc) return rc;
   std::memset(&S, 0, sizeof(S));
-  S.nodes = c->nodes.as<Node4>();
   S.nodes8 = c->nodes8.as<Node8>();
-  S.nodes8h = c->nodes8h.as<Node8H>();
   S.tris = c->tris.as<TriMT>();
   S.stri = c->stri.as<ShadeTri>();
   S.srgb = c->srgb.as<float>();
@@ -287,14 +288,14 @@ int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
 // wavefront buffers sized for n items and (bounces-1) (result, throughput) stack levels
 // queue counters [iter][path|shadow][kNSub] + traversal fetch counters [iter][path|shadow][8 parts]
 constexpr size_t kCtrWords = (size_t)(kMaxIters + 2) * 2 * (kNSub + 8) * kCtrStride;
-int ensure_wave(prt_ctx* c, int k, uint32_t n, int bounces, bool ext) {
+int ensure_wave(prt_ctx* c, uint32_t n, int bounces, bool ext) {
   const uint32_t levels = (uint32_t)std::max(1, bounces - 1);
   // sub-queue t receives the 256-entry chunks c == t (mod kNSub): at most ceil(ceil(n/256)/kNSub) of them
   const uint32_t qcap = 256u * (((n + 255u) / 256u + kNSub - 1) / kNSub);
-  if (c->wave_n[k] >= n && c->wave_levels[k] >= levels && (c->wave_ext[k] || !ext) && c->wave[k].p) {
-    c->wb[k].n = n;  // capacity stays; the SoA strides (R/T: depth * n + item) follow the current n
-    c->wb[k].qcap = qcap;
-    c->wb[k].scap = 5u * qcap;
+  if (c->wave_n >= n && c->wave_levels >= levels && (c->wave_ext || !ext) && c->wave.p) {
+    c->wb.n = n;  // capacity stays; the SoA strides (R/T: depth * n + item) follow the current n
+    c->wb.qcap = qcap;
+    c->wb.scap = 5u * qcap;
     return PRT_OK;
   }
   const size_t qn = (size_t)kNSub * qcap, sn = 5 * qn;  // <= 4 light-class + 1 area-light shadow rays per item
@@ -307,10 +308,11 @@ int ensure_wave(prt_ctx* c, int k, uint32_t n, int bounces, bool ext) {
                o_sho = take(16 * sn), o_shd = take(16 * sn), o_ctr = take(4 * kCtrWords);
   const size_t o_na = ext ? take(16ull * n) : 0, o_dst = ext ? take(4ull * n) : 0,
                o_dro = ext ? take(16ull * n * levels) : 0, o_drd = ext ? take(16ull * n * levels) : 0;
-  HIP_TRY(c->wave[k].ensure(off));
-  char* b = c->wave[k].as<char>();
-  WaveBufs& W = c->wb[k];
+  HIP_TRY(c->wave.ensure(off));
+  char* b = c->wave.as<char>();
+  WaveBufs& W = c->wb;
   W.n = n;
+  W.base = 0;
   W.qcap = qcap;
   W.scap = 5u * qcap;
   W.seed = (uint32_t*)(b + o_seed); W.info = (uint32_t*)(b + o_info); W.rinfo = (uint32_t*)(b + o_rinfo);
@@ -321,123 +323,22 @@ int ensure_wave(prt_ctx* c, int k, uint32_t n, int bounces, bool ext) {
   W.shd = (float4*)(b + o_shd); W.ctr = (uint32_t*)(b + o_ctr);
   W.na = ext ? (float4*)(b + o_na) : nullptr; W.dst = ext ? (uint32_t*)(b + o_dst) : nullptr;
   W.dro = ext ? (float4*)(b + o_dro) : nullptr; W.drd = ext ? (float4*)(b + o_drd) : nullptr;
-  c->wave_n[k] = n;
-  c->wave_levels[k] = levels;
-  c->wave_ext[k] = ext;
-  return PRT_OK;
-}
-
-// batches of the wavefront pipelines for n items: PRT_BATCHES (default 1: measured no faster),
-// at least PRT_BATCH_MIN (128k) items each
-int batches_for(uint64_t n) {
-  const char* e = std::getenv("PRT_BATCHES");
-  const char* m = std::getenv("PRT_BATCH_MIN");
-  int want = e ? std::atoi(e) : 1;
-  const uint64_t min_items = m ? (uint64_t)std::max(1, std::atoi(m)) : (128u << 10);
-  want = std::max(1, std::min(kMaxBatches, want));
-  while (want > 1 && n / (uint64_t)want < min_items) want--;
-  return want;
-}
-
-int ensure_batch_streams(prt_ctx* c, int nb) {
-  for (int k = 0; k < nb; k++) {
-    if (!c->bev[k] && hipEventCreateWithFlags(&c->bev[k], hipEventDisableTiming) != hipSuccess)
-      return fail(PRT_ERR_HIP, "hipEventCreate failed");
-    if (k > 0 && !c->bstream[k] && hipStreamCreateWithFlags(&c->bstream[k], hipStreamNonBlocking) != hipSuccess)
-      return fail(PRT_ERR_HIP, "hipStreamCreate failed");
-  }
-  return PRT_OK;
-}
-
-// PRT_PIPELINE: "mega" = one megakernel per pixel-frame, "wave1" = wavefront with separate extend /
-// shadow launches (prt_wave.hip), "stream" = one persistent launch per frame batch (prt_stream.hip),
-// default = merged-trace wavefront (prt_wave2.hip)
-int pipeline_from_env() {
-  const char* e = std::getenv("PRT_PIPELINE");
-  if (e && std::strcmp(e, "mega") == 0) return 1;
-  if (e && std::strcmp(e, "wave1") == 0) return 0;
-  if (e && std::strcmp(e, "stream") == 0) return 3;
-  return 2;
-}
-
-// XCC ids of the device (one census per context): part k of the streaming engine runs on the k-th id
-int ensure_parts(prt_ctx* c) {
-  if (c->nparts) return PRT_OK;
-  HIP_TRY(c->sctl.ensure(4 * kStreamCtlWords));
-  HIP_TRY(hipMemsetAsync(c->sctl.p, 0, 4, c->stream));
-  HIP_TRY(launch_xcc_census(c->stream, c->sctl.as<uint32_t>()));
-  uint32_t mask = 0;
-  HIP_TRY(hipMemcpyAsync(&mask, c->sctl.p, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  uint32_t map = 0xFFFFFFFFu, np = 0;
-  for (uint32_t k = 0; k < 8; k++)
-    if (mask & (1u << k)) {
-      map = (map & ~(0xFu << (4 * k))) | (np << (4 * k));
-      np++;
-    }
-  if (np == 0) return fail(PRT_ERR_HIP, "XCC census saw no workgroup");
-  c->nparts = np;
-  c->xcc_part = map;
-  return PRT_OK;
-}
-
-// streaming queues for n items over `iters` bounces: every shading task queues at most 5 rays (1 closest
-// + 4 shadow) and an item has at most iters + 1 shading tasks; sub-queues are fed round-robin per wave,
-// so one sub-queue holds at most 1/kSSub of its part's entries plus one 64-lane push per wave
-int ensure_stream(prt_ctx* c, uint32_t n, uint32_t iters, uint32_t grid) {
-  int rc = ensure_parts(c);
-  if (rc) return rc;
-  const uint64_t per_part = ((uint64_t)(n + 63) / 64 + c->nparts - 1) / c->nparts * 64;
-  const uint64_t slack = 320ull * (grid + 64);
-  const uint64_t rcap = (per_part * (1 + 5ull * (iters + 1)) + kSSub - 1) / kSSub + slack + 4096;
-  const uint64_t hcap = (per_part * (iters + 2ull) + kSSub - 1) / kSSub + slack / 5 + 4096;
-  const uint64_t total = (uint64_t)c->nparts * kSSub;
-  if (total * rcap >= (1ull << 32)) return fail(PRT_ERR_UNSUPPORTED, "streaming queues exceed 32-bit slots");
-  if (!(c->sq.p && c->sq_rcap >= rcap && c->sq_hcap >= hcap && c->sq_n >= n)) {
-    size_t off = 0;
-    auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
-    const size_t o_rq = take(8 * total * rcap), o_hq = take(8 * total * hcap), o_pend = take(4ull * n),
-                 o_ctr = take(4 * kStreamCtrWords);
-    c->sq.release();
-    HIP_TRY(c->sq.ensure(off));
-    HIP_TRY(hipMemsetAsync(c->sq.p, 0, off, c->stream));  // granule tags 0: never a launch serial
-    char* b = c->sq.as<char>();
-    c->sb.rq = (unsigned long long*)(b + o_rq);
-    c->sb.hq = (unsigned long long*)(b + o_hq);
-    c->sb.pend = (uint32_t*)(b + o_pend);
-    c->sb.ctr = (uint32_t*)(b + o_ctr);
-    c->sq_rcap = rcap;
-    c->sq_hcap = hcap;
-    c->sq_n = n;
-  }
-  HIP_TRY(c->sctl.ensure(4 * kStreamCtlWords + 64));
-  c->sb.ctl = c->sctl.as<uint32_t>();
-  c->sb.stat = reinterpret_cast<unsigned long long*>(c->sctl.as<char>() + 4 * kStreamCtlWords);
-  c->sb.rcap = (uint32_t)c->sq_rcap;
-  c->sb.hcap = (uint32_t)c->sq_hcap;
-  c->sb.nparts = c->nparts;
-  c->sb.xcc_part = c->xcc_part;
-  const char* e = std::getenv("PRT_STREAM_BUDGET_MS");
-  c->sb.budget_ms = e ? (uint32_t)std::atoi(e) : 20000u;
-  const char* w = std::getenv("PRT_STREAM_WAVES");
-  c->sb.waves = (w && std::atoi(w) == 4) ? 4u : 5u;
-  if (++c->serial == 0) c->serial = 1;
-  c->sb.serial = c->serial;
-  HIP_TRY(hipMemsetAsync(c->sb.ctr, 0, 4 * kStreamCtrWords, c->stream));
-  HIP_TRY(hipMemsetAsync(c->sctl.p, 0, 4 * kStreamCtlWords + 64, c->stream));
+  c->wave_n = n;
+  c->wave_levels = levels;
+  c->wave_ext = ext;
   return PRT_OK;
 }
 
 // the shared trace + accumulate sequence for prt_render / prt_render_tiles
+// enqueues the render on the context stream; want_stats: per-launch timers + read_stats() afterwards
 int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4* avg_dev, uint32_t* rgb8_dev,
-               float4* tiles_dev, prt_stats* stats) {
+               float4* tiles_dev, bool want_stats) {
   SceneDev S;
   int rc = scene_ready(c, S);
   if (rc) return rc;
   if (!c->have_camera) return fail(PRT_ERR_NOT_READY, "no camera: call prt_set_camera");
   if (!c->have_lights) return fail(PRT_ERR_NOT_READY, "no lights: call prt_set_lights");
-  const int layout = layout_for(c);
-  if (layout < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
+  if (!depth_ok(c)) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
   rc = ensure_state(c, p->width, p->height);
   if (rc) return rc;
   const int32_t F = frames_of(p);
@@ -447,100 +348,36 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   TraceArgs A;
   A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
   A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F;
-  LaunchCfg L{c->stream, layout, trav_from_env(), occ_for(c)};
-  // the merged pipeline runs the persistent 8-wide traversal only: Node4 and the lock-step kernels use wave1
-  int pipe = pipeline_from_env();
-  if ((pipe == 2 || pipe == 3) && (layout == 4 || L.trav == 1)) pipe = 0;
-  const bool mega = pipe == 1;
-  // extensions (area light, dielectric instances) run on the merged pipeline only
+  LaunchCfg L{c->stream, occ_for(c)};
+  // extensions (area light, dielectric instances) take the EXT instantiations of the shading kernels
   const bool ext = (S.area || S.has_diel) && p->render_mode == 0;
-  if (ext && pipe != 2)
-    return fail(PRT_ERR_UNSUPPORTED, "area lights / dielectric instances need the merged pipeline (PRT_PIPELINE unset)");
   const uint32_t iters = wave_iters(S.has_diel != 0, p->bounces, p->flags);
-  if (!mega && iters > (uint32_t)kMaxIters)
+  if (iters > (uint32_t)kMaxIters)
     return fail(PRT_ERR_UNSUPPORTED, S.has_diel ? "dielectric path trees exceed the wavefront iteration limit (lower bounces)"
                                                 : "too many wavefront iterations");
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  int nb = 1;
-  bool timers = false;
-  if (mega) {
-    HIP_TRY(c->counters.ensure(sizeof(Counters)));
-    HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
-    HIP_TRY(launch_trace_frames(L, S, A, M, c->frames.as<float4>(), c->counters.as<Counters>()));
-  } else {
-    nb = pipe == 3 ? 1 : batches_for(n);
-    rc = ensure_batch_streams(c, nb);
-    if (rc) return rc;
-    // traversal tails (prt_persist.h), PRT_TAIL: 0 none, 1 cooperative, 2 group, 3 cooperative then group;
-    // PRT_GTAIL: rays per wave at which the group tail takes over (1-8, default 8)
-    const char* et = std::getenv("PRT_TAIL");
-    const char* eg = std::getenv("PRT_GTAIL");
-    const int tmode = et ? std::atoi(et) : 1;
-    const int gthr = eg ? std::min(8, std::max(1, std::atoi(eg))) : 8;
-    for (int k = 0; k < nb; k++) {  // consecutive item ranges, multiples of 256 items (the last one takes the rest)
-      const uint64_t b0 = k == 0 ? 0 : ((n * k / nb + 255) & ~255ull), b1 = k == nb - 1 ? n : ((n * (k + 1) / nb + 255) & ~255ull);
-      rc = ensure_wave(c, k, (uint32_t)(b1 - b0), p->bounces, ext);
-      if (rc) return rc;
-      c->wb[k].base = (uint32_t)b0;
-      c->wb[k].tl = nullptr;
-      c->wb[k].coop_tail = (tmode == 1 || tmode == 3) ? 1 : 0;
-      c->wb[k].group_tail = (tmode == 2 || tmode == 3) && L.layout == 8 ? gthr : 0;
-    }
-    // per-launch traversal timers (HIP events around every k_trace launch) with stats, unless
-    // PRT_LAUNCH_TIMERS=0: each event record costs a few us between kernels
-    const char* elt = std::getenv("PRT_LAUNCH_TIMERS");
-    timers = stats && !(elt && std::strcmp(elt, "0") == 0);
-    if (stats && std::getenv("PRT_DEBUG_QUEUES")) {
-      const size_t tlb = 32ull * kTlWaves * (kMaxIters + 2);
-      HIP_TRY(c->tl.ensure(tlb));
-      HIP_TRY(hipMemsetAsync(c->tl.p, 0, tlb, c->stream));
-      c->wb[0].tl = c->tl.as<unsigned long long>();
-    }
-    if (nb > 1) {  // fork: the batch streams start after everything queued on `stream` so far
-      HIP_TRY(hipEventRecord(c->bev[0], c->stream));
-      for (int k = 1; k < nb; k++) HIP_TRY(hipStreamWaitEvent(c->bstream[k], c->bev[0], 0));
-    }
-    if (pipe == 3) {
-      HIP_TRY(hipMemsetAsync(c->wb[0].ctr, 0, 4 * kCtrWords, c->stream));
-      // byte offsets of the sc1 buffer loads are 32-bit: R/T levels x n and the 4 x n shadow slots
-      if ((uint64_t)c->wave_levels[0] * n * 16 >= (1ull << 32) || 64ull * n >= (1ull << 32))
-        return fail(PRT_ERR_UNSUPPORTED, "streaming engine: too many work items in one call (split spp)");
-      int dev = 0, cus = 256;
-      HIP_TRY(hipGetDevice(&dev));
-      HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-      rc = ensure_stream(c, (uint32_t)n, iters, (uint32_t)cus * 4u * 5u);
-      if (rc) return rc;
-      if (stats) HIP_TRY(hipEventRecord(c->wt[0].ev[0], c->stream));
-      HIP_TRY(launch_stream(L, S, A, M, c->wb[0], c->sb, c->frames.as<float4>()));
-      if (stats) HIP_TRY(hipEventRecord(c->wt[0].ev[1], c->stream));
-      uint32_t ctl[2] = {0, 0};
-      HIP_TRY(hipMemcpyAsync(ctl, c->sb.ctl, 8, hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      if (ctl[0] != 0) {
-        static const char* what[] = {"?", "watchdog expired (PRT_STREAM_BUDGET_MS)", "queue overflow", "item state"};
-        return fail(PRT_ERR_HIP, std::string("streaming engine aborted: ") + what[ctl[1] < 4 ? ctl[1] : 0]);
-      }
-    } else {
-      LaunchCfg Lk[kMaxBatches];
-      for (int k = 0; k < nb; k++) {
-        Lk[k] = L;
-        Lk[k].stream = k == 0 ? c->stream : c->bstream[k];
-        HIP_TRY(hipMemsetAsync(c->wb[k].ctr, 0, 4 * kCtrWords, Lk[k].stream));
-        if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(c->wb[k].dst, 0, 4ull * c->wb[k].n, Lk[k].stream));
-        float4* out = c->frames.as<float4>() + c->wb[k].base;
-        if (pipe == 2) HIP_TRY(launch_wave_init(Lk[k], S, A, M, c->wb[k], out));
-        else HIP_TRY(launch_wavefront(Lk[k], S, A, M, c->wb[k], out, timers ? &c->wt[k] : nullptr));
-      }
-      for (uint32_t it = 0; pipe == 2 && it <= iters; it++)  // merged pipeline: iterations round-robin over batches
-        for (int k = 0; k < nb; k++)
-          HIP_TRY(launch_wave2_iter(Lk[k], S, A, M, c->wb[k], c->frames.as<float4>() + c->wb[k].base,
-                                    timers ? &c->wt[k] : nullptr, it));
-      for (int k = 1; k < nb; k++) {  // join
-        HIP_TRY(hipEventRecord(c->bev[k], c->bstream[k]));
-        HIP_TRY(hipStreamWaitEvent(c->stream, c->bev[k], 0));
-      }
-    }
+  rc = ensure_wave(c, (uint32_t)n, p->bounces, ext);
+  if (rc) return rc;
+  // PRT_TAIL=0 switches the cooperative traversal tail off (prt_persist.h; A/B runs only)
+  const char* et = std::getenv("PRT_TAIL");
+  c->wb.coop_tail = (et && std::atoi(et) == 0) ? 0 : 1;
+  c->wb.tl = nullptr;
+  // per-launch traversal timers (HIP events around every k_trace launch) with stats, unless
+  // PRT_LAUNCH_TIMERS=0: each event record costs a few us between kernels
+  const char* elt = std::getenv("PRT_LAUNCH_TIMERS");
+  const bool timers = want_stats && !(elt && std::strcmp(elt, "0") == 0);
+  if (want_stats && std::getenv("PRT_DEBUG_QUEUES")) {
+    const size_t tlb = 32ull * kTlWaves * (kMaxIters + 2);
+    HIP_TRY(c->tl.ensure(tlb));
+    HIP_TRY(hipMemsetAsync(c->tl.p, 0, tlb, c->stream));
+    c->wb.tl = c->tl.as<unsigned long long>();
   }
+  HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * kCtrWords, c->stream));
+  if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(c->wb.dst, 0, 4ull * c->wb.n, c->stream));
+  float4* frames = c->frames.as<float4>();
+  HIP_TRY(launch_wave_init(L, S, A, M, c->wb, frames));
+  for (uint32_t it = 0; it <= iters; it++)
+    HIP_TRY(launch_wave2_iter(L, S, A, M, c->wb, frames, timers ? &c->wt : nullptr, it));
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   // post-processing (single-GPU image): the screen pass needs the average and, for the aberration, the
   // accumulator before the last frame
@@ -551,7 +388,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     if (!avg_dev) { HIP_TRY(c->avg.ensure(np * 16)); avg_dev = c->avg.as<float4>(); }
     if (c->pfx.aberration != 0) { HIP_TRY(c->accprev.ensure(np * 16)); acc_prev = c->accprev.as<float4>(); }
   }
-  HIP_TRY(launch_accumulate(L, M, F, p->flags, c->frames.as<float4>(), c->acc.as<float4>(), c->nsamp.as<int32_t>(),
+  HIP_TRY(launch_accumulate(L, M, F, p->flags, frames, c->acc.as<float4>(), c->nsamp.as<int32_t>(),
                             c->dist.as<float>(), avg_dev, post ? nullptr : rgb8_dev, tiles_dev, acc_prev));
   if (post) {
     // with !accumulates the accumulator held this frame's value until the end-of-frame memset
@@ -560,98 +397,172 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
                           rgb8_dev));
   }
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  if (stats) {
+  c->last_iters = iters;
+  c->last_timers = timers;
+  c->last_paths = (uint64_t)M.items * (uint64_t)F * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
+  return PRT_OK;
+}
+
+// waits for the last render of run_render(..., want_stats = true) and fills its stats
+int read_stats(prt_ctx* c, prt_stats* stats) {
+  const uint32_t iters = c->last_iters;
+  const bool timers = c->last_timers;
+  {
     std::memset(stats, 0, sizeof(*stats));
-    if (mega) {
-      Counters h{};
-      HIP_TRY(hipMemcpyAsync(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      stats->segments = h.segments;
-      stats->shadow_rays = h.shadow;
-      stats->pipeline = 1;
-    } else if (pipe == 3) {
-      unsigned long long h[8] = {};
-      HIP_TRY(hipMemcpyAsync(h, c->sb.stat, 7 * sizeof(h[0]), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      if (std::getenv("PRT_DEBUG_QUEUES") && h[4])  // wave-time shares of the two roles (s_memrealtime ticks)
-        std::fprintf(stderr, "prt: stream: shade %.1f%% trace %.1f%% other %.1f%% of wave time; %llu batches, %.1f items/batch\n",
-                     100.0 * h[2] / h[4], 100.0 * h[3] / h[4], 100.0 * (h[4] - h[2] - h[3]) / h[4], h[5],
-                     h[5] ? (double)h[6] / h[5] : 0.0);
-      stats->segments = h[0];
-      stats->shadow_rays = h[1];
+    // per-launch traversal times summed over every launch
+    std::vector<uint32_t> ctr(kCtrWords);
+    const bool dump = std::getenv("PRT_DEBUG_QUEUES") != nullptr;
+    HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const WaveTimers& wt = c->wt;
+    for (uint32_t k = 0; k <= iters; k++) {
+      uint64_t qs = 0, qa = 0;
+      for (uint32_t s = 0; s < kNSub && k < iters; s++) {
+        qs += ctr[((k * 2 + 0) * kNSub + s) * kCtrStride];
+        qa += ctr[((k * 2 + 1) * kNSub + s) * kCtrStride];
+      }
+      stats->segments += qs;
+      stats->shadow_rays += qa;
       float a = 0;
-      HIP_TRY(hipEventElapsedTime(&a, c->wt[0].ev[0], c->wt[0].ev[1]));
-      stats->ms_closest = a;
-      stats->pipeline = 3;
-      stats->iterations = 1;
-    } else {
-      // per-launch traversal times summed over every launch of every batch (batches may overlap in time)
-      std::vector<uint32_t> ctr(kCtrWords);
-      const bool dump = std::getenv("PRT_DEBUG_QUEUES") != nullptr;
-      for (int bk = 0; bk < nb; bk++) {
-        HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb[bk].ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        const WaveTimers& wt = c->wt[bk];
-        for (uint32_t k = 0; k < iters; k++) {
-          uint64_t qs = 0, qa = 0;
-          for (uint32_t s = 0; s < kNSub; s++) {
-            qs += ctr[((k * 2 + 0) * kNSub + s) * kCtrStride];
-            qa += ctr[((k * 2 + 1) * kNSub + s) * kCtrStride];
-          }
-          stats->segments += qs;
-          stats->shadow_rays += qa;
-          float a = 0, b = 0;
-          if (timers) HIP_TRY(hipEventElapsedTime(&a, wt.ev[4 * k + 0], wt.ev[4 * k + 1]));
-          if (timers && pipe == 0) HIP_TRY(hipEventElapsedTime(&b, wt.ev[4 * k + 2], wt.ev[4 * k + 3]));
-          stats->ms_closest += a;
-          stats->ms_anyhit += b;
-          if (dump)
-            std::fprintf(stderr, "prt: batch %d iteration %u: %llu closest rays %.3f ms, %llu shadow rays %.3f ms\n", bk,
-                         k, (unsigned long long)qs, a, (unsigned long long)qa, b);
-        }
-        if (pipe == 2 && timers) {  // one merged trace launch per iteration plus the final shadow-only one
-          float a = 0;
-          HIP_TRY(hipEventElapsedTime(&a, wt.ev[4 * iters + 0], wt.ev[4 * iters + 1]));
-          stats->ms_closest += a;
-        }
-      }
-      if (dump && c->wb[0].tl && pipe == 2) {  // launch timeline of batch 0: start -> queue drained -> last wave out (us)
-        std::vector<unsigned long long> t(4ull * kTlWaves * (kMaxIters + 2));
-        HIP_TRY(hipMemcpy(t.data(), c->tl.p, 8 * t.size(), hipMemcpyDeviceToHost));
-        for (uint32_t k = 0; k <= iters; k++) {
-          unsigned long long s0 = ~0ull, d0 = ~0ull;
-          std::vector<double> ex;
-          for (int w = 0; w < kTlWaves; w++) {
-            const unsigned long long* r = t.data() + 4 * ((size_t)k * kTlWaves + w);
-            if (!r[0]) continue;
-            s0 = std::min(s0, r[0]);
-            if (r[1]) d0 = std::min(d0, r[1]);
-          }
-          if (s0 == ~0ull || d0 == ~0ull) continue;
-          for (int w = 0; w < kTlWaves; w++) {
-            const unsigned long long* r = t.data() + 4 * ((size_t)k * kTlWaves + w);
-            if (r[0] && r[2]) ex.push_back(((double)r[2] - (double)d0) / 100.0);
-          }
-          std::sort(ex.begin(), ex.end());
-          auto q = [&](double p) { return ex.empty() ? 0.0 : ex[std::min(ex.size() - 1, (size_t)(p * ex.size()))]; };
-          std::fprintf(stderr, "prt: trace %u: %zu waves, queue empty after %.1f us; waves out at +%.1f / +%.1f / "
-                       "+%.1f / +%.1f us (50/90/99/100 %%)\n", k, ex.size(), (d0 - s0) / 100.0, q(0.5), q(0.9),
-                       q(0.99), ex.empty() ? 0.0 : ex.back());
-        }
-      }
-      stats->pipeline = pipe;
-      stats->iterations = (int32_t)(pipe == 2 ? iters + 1 : iters) * nb;  // traversal launches of all batches
-      stats->batches = nb;
+      if (timers) HIP_TRY(hipEventElapsedTime(&a, wt.ev[4 * k + 0], wt.ev[4 * k + 1]));
+      stats->ms_closest += a;  // one merged trace launch per iteration plus the final shadow-only one
+      if (dump && k < iters)
+        std::fprintf(stderr, "prt: iteration %u: %llu closest rays, %llu shadow rays; trace launch %.3f ms\n", k,
+                     (unsigned long long)qs, (unsigned long long)qa, a);
     }
+    if (dump && c->wb.tl) {  // launch timeline: start -> queue drained -> last wave out (us)
+      std::vector<unsigned long long> t(4ull * kTlWaves * (kMaxIters + 2));
+      HIP_TRY(hipMemcpy(t.data(), c->tl.p, 8 * t.size(), hipMemcpyDeviceToHost));
+      for (uint32_t k = 0; k <= iters; k++) {
+        unsigned long long s0 = ~0ull, d0 = ~0ull;
+        std::vector<double> ex;
+        for (int w = 0; w < kTlWaves; w++) {
+          const unsigned long long* r = t.data() + 4 * ((size_t)k * kTlWaves + w);
+          if (!r[0]) continue;
+          s0 = std::min(s0, r[0]);
+          if (r[1]) d0 = std::min(d0, r[1]);
+        }
+        if (s0 == ~0ull || d0 == ~0ull) continue;
+        for (int w = 0; w < kTlWaves; w++) {
+          const unsigned long long* r = t.data() + 4 * ((size_t)k * kTlWaves + w);
+          if (r[0] && r[2]) ex.push_back(((double)r[2] - (double)d0) / 100.0);
+        }
+        std::sort(ex.begin(), ex.end());
+        auto q = [&](double pp) { return ex.empty() ? 0.0 : ex[std::min(ex.size() - 1, (size_t)(pp * ex.size()))]; };
+        std::fprintf(stderr, "prt: trace %u: %zu waves, queue empty after %.1f us; waves out at +%.1f / +%.1f / "
+                     "+%.1f / +%.1f us (50/90/99/100 %%)\n", k, ex.size(), (d0 - s0) / 100.0, q(0.5), q(0.9),
+                     q(0.99), ex.empty() ? 0.0 : ex.back());
+      }
+    }
+    stats->pipeline = 2;
+    stats->iterations = (int32_t)(iters + 1);  // traversal launches
+    stats->batches = 1;
+    stats->ranks = 1;
     float ms = 0, ms_trace = 0;
     HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[2]));
     HIP_TRY(hipEventElapsedTime(&ms_trace, c->ev[0], c->ev[1]));
-    stats->paths = (uint64_t)M.items * (uint64_t)F * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
+    stats->paths = c->last_paths;
     stats->ms = ms;
     stats->ms_trace = ms_trace;
   }
   return PRT_OK;
 }
+
+// Sharded frame: every rank renders its tiles into shtiles, rank 0 gathers [world][per] and untiles.
+// RCCL: one ncclGather per frame on this rank's stream.  Local group: each member renders on its own stream
+// and copies its tile buffer into member 0's gathered buffer (peer copy over xGMI across devices); member 0
+// waits for those copies, and the members' next copies wait for member 0's untile.
+int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint32_t* rgb_dev, prt_stats* stats) {
+  const int32_t W = p->width, H = p->height, ts = c->sh_tile, world = c->sh_world;
+  if (c->pfx.enabled && c->pfx.aberration != 0)
+    return fail(PRT_ERR_UNSUPPORTED, "chromatic aberration needs the accumulators of neighbouring tiles");
+  const TileMap M0 = make_tilemap(W, H, ts, 0, world);
+  const size_t per = M0.items;  // tile-buffer elements per rank (rank 0 owns the most)
+  std::vector<prt_ctx*> all{c};
+  all.insert(all.end(), c->members.begin(), c->members.end());
+  const bool root = c->sh_rank == 0;
+  for (size_t k = 0; k < all.size(); k++) {
+    prt_ctx* m = all[k];
+    const int32_t rank = c->sh_kind == 2 ? (int32_t)k : c->sh_rank;
+    HIP_TRY(hipSetDevice(m->device));
+    HIP_TRY(m->shtiles.ensure(per * sizeof(float4)));
+    const TileMap M = make_tilemap(W, H, ts, rank, world);
+    if (per > M.items)  // the tail of a shorter rank's buffer
+      HIP_TRY(hipMemsetAsync(m->shtiles.as<float4>() + M.items, 0, sizeof(float4) * (per - M.items), m->stream));
+    int rc = run_render(m, p, M, nullptr, nullptr, m->shtiles.as<float4>(), stats != nullptr);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  if (root) HIP_TRY(c->gathered.ensure((size_t)world * per * sizeof(float4)));
+  float4* g = root ? c->gathered.as<float4>() : nullptr;
+  if (c->sh_kind == 1) {
+    const char* why = nullptr;
+    const Rccl* R = rccl(&why);
+    if (!R) return fail(PRT_ERR_UNSUPPORTED, why);
+    const ncclResult_t r = R->Gather(c->shtiles.p, g, per * 4, ncclFloat32, 0, c->comm, c->stream);
+    if (r != ncclSuccess) return fail(PRT_ERR_HIP, std::string("ncclGather: ") + R->GetErrorString(r));
+  } else {
+    HIP_TRY(hipMemcpyAsync(g, c->shtiles.p, per * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+    for (size_t k = 1; k < all.size(); k++) {
+      prt_ctx* m = all[k];
+      HIP_TRY(hipSetDevice(m->device));
+      HIP_TRY(hipStreamWaitEvent(m->stream, c->sh_ev, 0));  // member 0's previous untile read g
+      float4* dst = g + k * per;
+      if (m->device == c->device)
+        HIP_TRY(hipMemcpyAsync(dst, m->shtiles.p, per * sizeof(float4), hipMemcpyDeviceToDevice, m->stream));
+      else
+        HIP_TRY(hipMemcpyPeerAsync(dst, c->device, m->shtiles.p, m->device, per * sizeof(float4), m->stream));
+      HIP_TRY(hipEventRecord(m->sh_ev, m->stream));
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    for (size_t k = 1; k < all.size(); k++) HIP_TRY(hipStreamWaitEvent(c->stream, all[k]->sh_ev, 0));
+  }
+  if (root && (avg_dev || rgb_dev)) {
+    LaunchCfg L{c->stream, occ_for(c)};
+    const PostDev P = post_params(c, W, H);
+    HIP_TRY(launch_untile(L, W, H, ts, world, (uint32_t)per, g, avg_dev, rgb_dev, c->pfx.enabled ? &P : nullptr));
+  }
+  if (c->sh_ev) HIP_TRY(hipEventRecord(c->sh_ev, c->stream));
+  if (stats) {
+    prt_stats sum{};
+    for (size_t k = 0; k < all.size(); k++) {
+      prt_stats st{};
+      HIP_TRY(hipSetDevice(all[k]->device));
+      int rc = read_stats(all[k], &st);
+      if (rc) return rc;
+      if (k == 0) sum = st;
+      else {
+        sum.segments += st.segments;
+        sum.shadow_rays += st.shadow_rays;
+        sum.paths += st.paths;
+        sum.ms = std::max(sum.ms, st.ms);
+        sum.ms_trace = std::max(sum.ms_trace, st.ms_trace);
+        sum.ms_closest += st.ms_closest;
+      }
+    }
+    sum.ranks = (int32_t)all.size();
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->sh_kind == 1) HIP_TRY(hipStreamSynchronize(c->stream));  // the gather is part of the frame
+    *stats = sum;
+  }
+  return PRT_OK;
+}
+
+int shard_setup(prt_ctx* c, int32_t tile) {
+  if (tile <= 0 || (tile % 8) != 0) return fail(PRT_ERR_INVALID_ARGUMENT, "tile_size must be a positive multiple of 8");
+  c->sh_tile = tile;
+  if (!c->sh_ev) HIP_TRY(hipEventCreateWithFlags(&c->sh_ev, hipEventDisableTiming));
+  return PRT_OK;
+}
+
+// a setter of a local group applies to every member (member 0 = the group context itself)
+#define PRT_FOR_MEMBERS(call)                 \
+  do {                                         \
+    for (prt_ctx* m : c->members) {            \
+      const int rc_ = (call);                  \
+      if (rc_) return rc_;                     \
+    }                                          \
+  } while (0)
 
 }  // namespace
 
@@ -702,42 +613,34 @@ int prt_create(const prt_device_desc* desc, prt_ctx** out) {
       return fail(PRT_ERR_HIP, "hipEventCreate failed");
     }
   }
-  for (auto& wt : c->wt)
-    for (auto& e : wt.ev) {  // per-launch timers only: no system-scope fence / cache writeback per record
-      if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess && hipEventCreate(&e) != hipSuccess) {
-        delete c;
-        return fail(PRT_ERR_HIP, "hipEventCreate failed");
-      }
+  for (auto& e : c->wt.ev) {  // per-launch timers only: no system-scope fence / cache writeback per record
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess && hipEventCreate(&e) != hipSuccess) {
+      delete c;
+      return fail(PRT_ERR_HIP, "hipEventCreate failed");
     }
+  }
   *out = c;
   return PRT_OK;
 }
 
 int prt_destroy(prt_ctx* c) {
   if (!c) return PRT_OK;
+  for (prt_ctx* m : c->members) (void)prt_destroy(m);
+  c->members.clear();
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->texels, &c->tex, &c->inst_src, &c->nodes, &c->nodes8, &c->nodes8h, &c->tris, &c->stri,
-                    &c->mesh, &c->inst, &c->sky, &c->srgb, &c->acc, &c->nsamp, &c->dist, &c->frames, &c->avg, &c->rgb8,
-                    &c->counters, &c->hits, &c->tl})
-    b->release();
+  if (c->comm && c->own_comm) {
+    const Rccl* R = rccl(nullptr);
+    if (R) (void)R->CommDestroy(c->comm);
+  }
+  c->comm = nullptr;
+  if (c->sh_ev) (void)hipEventDestroy(c->sh_ev);
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);
-  for (int k = 1; k < kMaxBatches; k++)
-    if (c->bstream[k]) (void)hipStreamSynchronize(c->bstream[k]);
-  for (auto& wt : c->wt)
-    for (auto e : wt.ev)
-      if (e) (void)hipEventDestroy(e);
-  for (auto e : c->bev)
+  for (auto e : c->wt.ev)
     if (e) (void)hipEventDestroy(e);
-  for (auto& w : c->wave) w.release();
-  for (auto s : c->bstream)
-    if (s) (void)hipStreamDestroy(s);
-  c->sq.release();
-  c->sctl.release();
-  c->accprev.release();
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
-  delete c;
+  delete c;  // DevBuf members free their device memory
   return PRT_OK;
 }
 
@@ -759,31 +662,31 @@ int prt_set_textures(prt_ctx* c, const prt_texture* t, int32_t n) {
     host[i].pad = 0;
     all.insert(all.end(), t[i].pixels, t[i].pixels + (size_t)t[i].width * t[i].height);
   }
-  HIP_TRY(hipSetDevice(c->device));
+  int rc = drain(c);
+  if (rc) return rc;
   HIP_TRY(upload(c->texels, all.data(), all.size() * 4));
   HIP_TRY(upload(c->tex, host.data(), host.size() * sizeof(TexDev)));
   c->tex_host = host;
+  PRT_FOR_MEMBERS(prt_set_textures(m, t, n));
   return PRT_OK;
 }
 
-int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
+int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
+  const prt_mesh* m = m_in;
   if (!c || !m || n <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad meshes");
-  const int layout = layout_from_env();
   int builder = c->builder;
   if (builder < 0) {
     const char* e = std::getenv("PRT_BUILDER");
     builder = (e && std::strcmp(e, "gpu") == 0) ? PRT_BUILDER_GPU_LBVH : PRT_BUILDER_HOST_SAH;
   }
   const bool gpu = builder == PRT_BUILDER_GPU_LBVH;
-  if (gpu && layout != 8) return fail(PRT_ERR_UNSUPPORTED, "the GPU builder emits Node8 only (PRT_BVH=8)");
-  HIP_TRY(hipSetDevice(c->device));
+  int rc = drain(c);
+  if (rc) return rc;
   const auto t_build0 = std::chrono::steady_clock::now();
   struct GpuMesh { DevBuf nodes, tris; GpuBlasInfo gi; uint32_t node_base, tri_base, prim_base; };
   std::vector<GpuMesh> gm(gpu ? n : 0);
   uint32_t gpu_nodes = 0, gpu_tris = 0;
-  std::vector<Node4> nodes;
   std::vector<Node8> nodes8;
-  std::vector<Node8H> nodes8h;
   std::vector<TriMT> tris;
   std::vector<ShadeTri> stri;
   std::vector<MeshDev> mh(n);
@@ -829,26 +732,9 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
       mh[i].root = g.node_base;
       for (int k = 0; k < 3; k++) { bmin[k] = g.gi.bmin[k]; bmax[k] = g.gi.bmax[k]; }
       depth = g.gi.depth; nnodes = g.gi.nodes; nleaves = g.gi.leaves;
-    } else if (layout == 4) {
-      BuiltBlas b = build_blas(M.triangles, M.tri_count, 4);
-      const uint32_t node_base = (uint32_t)nodes.size();
-      if ((uint64_t)tri_base + b.tris.size() >= (1u << 29)) return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
-      for (Node4& nd : b.nodes) {
-        for (int k = 0; k < 4; k++) {
-          uint32_t& ch = nd.child[k];
-          if (ch == kEmptyChild) continue;
-          if (ch & kLeafBit) ch = make_leaf(((ch >> 2) & 0x1FFFFFFFu) + tri_base, (ch & 3u) + 1u);
-          else ch += node_base;
-        }
-      }
-      nodes.insert(nodes.end(), b.nodes.begin(), b.nodes.end());
-      tris.insert(tris.end(), b.tris.begin(), b.tris.end());
-      mh[i].root = node_base;
-      std::memcpy(bmin, b.bmin, sizeof(bmin)); std::memcpy(bmax, b.bmax, sizeof(bmax));
-      depth = b.depth; nnodes = (int64_t)b.nodes.size(); nleaves = b.leaves;
     } else {
-      // 8-wide layouts: rebase child / triangle offsets into the concatenated arrays
-      auto append = [&](auto&& built, auto& all) -> bool {
+      // rebase child / triangle offsets into the concatenated arrays
+      auto append = [&](BuiltBlas8&& built, std::vector<Node8>& all) -> bool {
         const uint32_t node_base = (uint32_t)all.size();
         if ((uint64_t)tri_base + built.tris.size() >= (1ull << 32) ||
             (uint64_t)node_base + built.nodes.size() >= (1ull << 32))
@@ -865,8 +751,7 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
         depth = built.depth; nnodes = (int64_t)built.nodes.size(); nleaves = built.leaves;
         return true;
       };
-      const bool ok = layout == 9 ? append(build_blas8h(M.triangles, M.tri_count, 3), nodes8h)
-                                  : append(build_blas8(M.triangles, M.tri_count, 3), nodes8);
+      const bool ok = append(build_blas8(M.triangles, M.tri_count, 3), nodes8);
       if (!ok) return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
     }
     mh[i].prim_base = (uint32_t)stri.size();
@@ -903,9 +788,7 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
     info[i].tris = M.tri_count;
     maxd = std::max(maxd, depth);
   }
-  c->nodes.release();
   c->nodes8.release();
-  c->nodes8h.release();
   if (gpu) {  // concatenate the per-mesh device results, rebase offsets, primitive -> triangle records
     HIP_TRY(c->nodes8.ensure(sizeof(Node8) * (size_t)gpu_nodes));
     HIP_TRY(c->tris.ensure(sizeof(TriMT) * (size_t)gpu_tris));
@@ -921,10 +804,9 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
                               g.prim_base));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
+    gm.clear();  // the per-mesh device builds were copied into the concatenated arrays
   } else {
-    if (layout == 4) HIP_TRY(upload(c->nodes, nodes.data(), nodes.size() * sizeof(Node4)));
-    else if (layout == 9) HIP_TRY(upload(c->nodes8h, nodes8h.data(), nodes8h.size() * sizeof(Node8H)));
-    else HIP_TRY(upload(c->nodes8, nodes8.data(), nodes8.size() * sizeof(Node8)));
+    HIP_TRY(upload(c->nodes8, nodes8.data(), nodes8.size() * sizeof(Node8)));
     HIP_TRY(upload(c->tris, tris.data(), tris.size() * sizeof(TriMT)));
     HIP_TRY(upload(c->stri, stri.data(), stri.size() * sizeof(ShadeTri)));
   }
@@ -934,8 +816,8 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m, int32_t n) {
   c->mesh_host = mh;
   c->mesh_info = info;
   c->max_depth = maxd;
-  c->layout = layout;
   c->inst_dirty = true;
+  PRT_FOR_MEMBERS(prt_set_meshes(m, m_in, n));
   return PRT_OK;
 }
 
@@ -943,6 +825,7 @@ int prt_set_bvh_builder(prt_ctx* c, int32_t builder) {
   if (!c || (builder != PRT_BUILDER_HOST_SAH && builder != PRT_BUILDER_GPU_LBVH))
     return fail(PRT_ERR_INVALID_ARGUMENT, "bad BLAS builder");
   c->builder = builder;
+  PRT_FOR_MEMBERS(prt_set_bvh_builder(m, builder));
   return PRT_OK;
 }
 
@@ -954,7 +837,11 @@ int prt_set_instances(prt_ctx* c, const float* xf, const uint32_t* mi, int32_t n
   c->inst_mesh.assign(mi, mi + n);
   c->inst_dirty = true;
   HIP_TRY(hipSetDevice(c->device));
-  if (!c->mesh_host.empty()) return ensure_instances(c);
+  if (!c->mesh_host.empty()) {
+    const int rc = ensure_instances(c);
+    if (rc) return rc;
+  }
+  PRT_FOR_MEMBERS(prt_set_instances(m, xf, mi, n));
   return PRT_OK;
 }
 
@@ -970,7 +857,11 @@ int prt_set_instance_materials(prt_ctx* c, const int32_t* kinds, int32_t n) {
   }
   c->inst_dirty = true;
   HIP_TRY(hipSetDevice(c->device));
-  if (!c->mesh_host.empty() && !c->inst_mesh.empty()) return ensure_instances(c);
+  if (!c->mesh_host.empty() && !c->inst_mesh.empty()) {
+    const int rc = ensure_instances(c);
+    if (rc) return rc;
+  }
+  PRT_FOR_MEMBERS(prt_set_instance_materials(m, kinds, n));
   return PRT_OK;
 }
 
@@ -979,6 +870,7 @@ int prt_set_area_lights(prt_ctx* c, const prt_area_light* a, int32_t n) {
   if (n < 0 || n > 1 || (n == 1 && !a)) return fail(PRT_ERR_UNSUPPORTED, "at most one area light");
   if (n == 0) {
     c->area = 0;
+    PRT_FOR_MEMBERS(prt_set_area_lights(m, a, n));
     return PRT_OK;
   }
   const float* u = a->edge_u;
@@ -992,6 +884,7 @@ int prt_set_area_lights(prt_ctx* c, const prt_area_light* a, int32_t n) {
   std::memcpy(c->al, al, sizeof(al));
   c->area = 1;
   c->area_two_sided = a->two_sided ? 1 : 0;
+  PRT_FOR_MEMBERS(prt_set_area_lights(m, a, n));
   return PRT_OK;
 }
 
@@ -999,19 +892,23 @@ int prt_set_lights(prt_ctx* c, const prt_lights* l) {
   if (!c || !l) return fail(PRT_ERR_INVALID_ARGUMENT, "bad lights");
   c->lights = *l;
   c->have_lights = true;
+  PRT_FOR_MEMBERS(prt_set_lights(m, l));
   return PRT_OK;
 }
 
 int prt_set_sky(prt_ctx* c, const float* rgb, int32_t w, int32_t h) {
   if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
-  HIP_TRY(hipSetDevice(c->device));
+  int rc = drain(c);
+  if (rc) return rc;
   if (!rgb || w <= 0 || h <= 0) {
     c->skyw = c->skyh = 0;
+    PRT_FOR_MEMBERS(prt_set_sky(m, rgb, w, h));
     return PRT_OK;
   }
   HIP_TRY(upload(c->sky, rgb, (size_t)w * h * 3 * 4));
   c->skyw = w;
   c->skyh = h;
+  PRT_FOR_MEMBERS(prt_set_sky(m, rgb, w, h));
   return PRT_OK;
 }
 
@@ -1019,6 +916,7 @@ int prt_set_camera(prt_ctx* c, const prt_camera* cam) {
   if (!c || !cam) return fail(PRT_ERR_INVALID_ARGUMENT, "bad camera");
   c->cam = *cam;
   c->have_camera = true;
+  PRT_FOR_MEMBERS(prt_set_camera(m, cam));
   return PRT_OK;
 }
 
@@ -1059,11 +957,13 @@ int prt_postfx_preset(int32_t preset, prt_postfx* o) {
 int prt_set_postfx(prt_ctx* c, const prt_postfx* pfx) {
   if (!c || !pfx) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/postfx is NULL");
   c->pfx = *pfx;
+  PRT_FOR_MEMBERS(prt_set_postfx(m, pfx));
   return PRT_OK;
 }
 
 int prt_reset_accumulation(prt_ctx* c, int32_t full) {
   if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  PRT_FOR_MEMBERS(prt_reset_accumulation(m, full));
   if (!c->acc.p) return PRT_OK;
   HIP_TRY(hipSetDevice(c->device));
   const size_t n = (size_t)c->accW * c->accH;
@@ -1083,22 +983,28 @@ int prt_render(prt_ctx* c, const prt_render_params* p, float* avg_rgba, uint32_t
   int rc = check_params(p);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
-  const TileMap M = make_tilemap(p->width, p->height, 8, 0, 1);
   const size_t np = (size_t)p->width * p->height;
   float4* avg_dev = nullptr;
   uint32_t* rgb_dev = nullptr;
   const bool dev_out = (out_flags & PRT_OUT_DEVICE) != 0;
-  if (avg_rgba) {
+  const bool root = c->sh_kind == 0 || c->sh_rank == 0;  // the rank whose outputs receive the frame
+  if (avg_rgba && root) {
     if (dev_out) avg_dev = reinterpret_cast<float4*>(avg_rgba);
     else { HIP_TRY(c->avg.ensure(np * 16)); avg_dev = c->avg.as<float4>(); }
   }
-  if (rgb8) {
+  if (rgb8 && root) {
     if (dev_out) rgb_dev = rgb8;
     else { HIP_TRY(c->rgb8.ensure(np * 4)); rgb_dev = c->rgb8.as<uint32_t>(); }
   }
-  rc = run_render(c, p, M, avg_dev, rgb_dev, nullptr, stats);
+  if (c->sh_kind != 0) {
+    rc = render_sharded(c, p, avg_dev, rgb_dev, stats);
+  } else {
+    const TileMap M = make_tilemap(p->width, p->height, 8, 0, 1);
+    rc = run_render(c, p, M, avg_dev, rgb_dev, nullptr, stats != nullptr);
+    if (!rc && stats) rc = read_stats(c, stats);
+  }
   if (rc) return rc;
-  if (!dev_out) {
+  if (!dev_out && root) {
     if (avg_rgba) HIP_TRY(hipMemcpyAsync(avg_rgba, avg_dev, np * 16, hipMemcpyDeviceToHost, c->stream));
     if (rgb8) HIP_TRY(hipMemcpyAsync(rgb8, rgb_dev, np * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1140,7 +1046,9 @@ int prt_render_tiles(prt_ctx* c, const prt_render_params* p, int32_t ts, int32_t
   if (M0.items > M.items)  // pad the tail of the (equal-size) per-rank buffer
     HIP_TRY(hipMemsetAsync(reinterpret_cast<float4*>(tiles_dev) + M.items, 0, sizeof(float4) * (M0.items - M.items),
                            c->stream));
-  return run_render(c, p, M, nullptr, nullptr, reinterpret_cast<float4*>(tiles_dev), stats);
+  rc = run_render(c, p, M, nullptr, nullptr, reinterpret_cast<float4*>(tiles_dev), stats != nullptr);
+  if (!rc && stats) rc = read_stats(c, stats);
+  return rc;
 }
 
 int prt_untile(prt_ctx* c, const float* gathered, int32_t W, int32_t H, int32_t ts, int32_t world, float* avg_dev,
@@ -1152,7 +1060,7 @@ int prt_untile(prt_ctx* c, const float* gathered, int32_t W, int32_t H, int32_t 
   HIP_TRY(hipSetDevice(c->device));
   if (c->pfx.enabled && c->pfx.aberration != 0 && rgb8_dev)
     return fail(PRT_ERR_UNSUPPORTED, "chromatic aberration needs the accumulators of neighbouring tiles");
-  LaunchCfg L{c->stream, c->layout, trav_from_env(), occ_for(c)};
+  LaunchCfg L{c->stream, occ_for(c)};
   const PostDev P = post_params(c, W, H);
   HIP_TRY(launch_untile(L, W, H, ts, world, (uint32_t)per, reinterpret_cast<const float4*>(gathered),
                         reinterpret_cast<float4*>(avg_dev), rgb8_dev, c->pfx.enabled ? &P : nullptr));
@@ -1166,8 +1074,7 @@ int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t 
   int rc = scene_ready(c, S);
   if (rc) return rc;
   if (!c->have_camera) return fail(PRT_ERR_NOT_READY, "no camera");
-  const int layout = layout_for(c);
-  if (layout < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
+  if (!depth_ok(c)) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
   const TileMap M = make_tilemap(W, H, 8, 0, 1);
   const size_t n = (size_t)W * H;
   HitOut* out = reinterpret_cast<HitOut*>(hits);
@@ -1175,7 +1082,7 @@ int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t 
   if (!dev_out) { HIP_TRY(c->hits.ensure(n * sizeof(HitOut))); out = c->hits.as<HitOut>(); }
   HIP_TRY(c->counters.ensure(sizeof(Counters)));
   HIP_TRY(hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
-  LaunchCfg L{c->stream, layout, trav_from_env(), occ_for(c)};
+  LaunchCfg L{c->stream, occ_for(c)};
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   HIP_TRY(launch_primary_hits(L, S, M, out, c->counters.as<Counters>()));
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
@@ -1205,8 +1112,7 @@ static int ray_query(prt_ctx* c, int32_t n, const float* O, const float* D, cons
   SceneDev S;
   int rc = scene_ready(c, S);
   if (rc) return rc;
-  const int layout = layout_for(c);
-  if (layout < 0) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
+  if (!depth_ok(c)) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
   DevBuf dO, dD, dT, dOut;
   auto cleanup = [&]() { dO.release(); dD.release(); dT.release(); dOut.release(); };
   const size_t outb = (size_t)n * (any ? 4 : sizeof(HitOut));
@@ -1215,7 +1121,7 @@ static int ray_query(prt_ctx* c, int32_t n, const float* O, const float* D, cons
     cleanup();
     return fail(PRT_ERR_OUT_OF_MEMORY, "ray buffers");
   }
-  LaunchCfg L{c->stream, layout, trav_from_env(), occ_for(c)};
+  LaunchCfg L{c->stream, occ_for(c)};
   hipError_t e = any ? launch_occluded(L, S, n, dO.as<float>(), dD.as<float>(), dT.as<float>(), dOut.as<int32_t>())
                      : launch_intersect(L, S, n, dO.as<float>(), dD.as<float>(), tmax ? dT.as<float>() : nullptr,
                                         dOut.as<HitOut>());
@@ -1233,6 +1139,107 @@ int prt_occluded(prt_ctx* c, int32_t n, const float* O, const float* D, const fl
   return ray_query(c, n, O, D, tmax, occ, true);
 }
 
+int prt_shard_unique_id(uint8_t id[PRT_SHARD_ID_BYTES]) {
+  if (!id) return fail(PRT_ERR_INVALID_ARGUMENT, "id is NULL");
+  static_assert(sizeof(ncclUniqueId) == PRT_SHARD_ID_BYTES, "ncclUniqueId size");
+  const char* why = nullptr;
+  const Rccl* R = rccl(&why);
+  if (!R) return fail(PRT_ERR_UNSUPPORTED, why);
+  ncclUniqueId u;
+  const ncclResult_t r = R->GetUniqueId(&u);
+  if (r != ncclSuccess) return fail(PRT_ERR_HIP, std::string("ncclGetUniqueId: ") + R->GetErrorString(r));
+  std::memcpy(id, &u, sizeof(u));
+  return PRT_OK;
+}
+
+int prt_shard_init_rccl(prt_ctx* c, const uint8_t id[PRT_SHARD_ID_BYTES], int32_t rank, int32_t world, int32_t tile) {
+  if (!c || !id || world <= 0 || rank < 0 || rank >= world) return fail(PRT_ERR_INVALID_ARGUMENT, "bad shard rank / world");
+  if (c->sh_kind != 0) return fail(PRT_ERR_INVALID_ARGUMENT, "context is already sharded");
+  int rc = shard_setup(c, tile);
+  if (rc) return rc;
+  const char* why = nullptr;
+  const Rccl* R = rccl(&why);
+  if (!R) return fail(PRT_ERR_UNSUPPORTED, why);
+  HIP_TRY(hipSetDevice(c->device));
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  ncclComm_t comm = nullptr;
+  const ncclResult_t r = R->CommInitRank(&comm, world, u, rank);
+  if (r != ncclSuccess) return fail(PRT_ERR_HIP, std::string("ncclCommInitRank: ") + R->GetErrorString(r));
+  c->comm = comm;
+  c->own_comm = true;
+  c->sh_kind = 1;
+  c->sh_rank = rank;
+  c->sh_world = world;
+  return PRT_OK;
+}
+
+int prt_shard_attach_rccl(prt_ctx* c, void* comm, int32_t tile) {
+  if (!c || !comm) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx / comm is NULL");
+  if (c->sh_kind != 0) return fail(PRT_ERR_INVALID_ARGUMENT, "context is already sharded");
+  int rc = shard_setup(c, tile);
+  if (rc) return rc;
+  const char* why = nullptr;
+  const Rccl* R = rccl(&why);
+  if (!R) return fail(PRT_ERR_UNSUPPORTED, why);
+  ncclComm_t cm = reinterpret_cast<ncclComm_t>(comm);
+  int n = 0, r = 0;
+  if (R->CommCount(cm, &n) != ncclSuccess || R->CommUserRank(cm, &r) != ncclSuccess)
+    return fail(PRT_ERR_INVALID_ARGUMENT, "not a usable ncclComm_t");
+  c->comm = cm;
+  c->own_comm = false;
+  c->sh_kind = 1;
+  c->sh_rank = r;
+  c->sh_world = n;
+  return PRT_OK;
+}
+
+int prt_create_group(const prt_device_desc* devs, int32_t n, int32_t tile, prt_ctx** out) {
+  if (!out) return fail(PRT_ERR_INVALID_ARGUMENT, "out is NULL");
+  *out = nullptr;
+  if (!devs || n <= 0 || n > 64) return fail(PRT_ERR_INVALID_ARGUMENT, "1..64 devices");
+  prt_ctx* g = nullptr;
+  int rc = prt_create(&devs[0], &g);
+  if (rc) return rc;
+  rc = shard_setup(g, tile);
+  for (int32_t k = 1; k < n && !rc; k++) {
+    prt_ctx* m = nullptr;
+    rc = prt_create(&devs[k], &m);
+    if (!rc) {
+      g->members.push_back(m);
+      rc = shard_setup(m, tile);
+    }
+  }
+  if (!rc) {  // peer access between distinct devices (the tile copies go device to device)
+    for (prt_ctx* m : g->members) {
+      if (m->device == g->device) continue;
+      (void)hipSetDevice(m->device);
+      const hipError_t e = hipDeviceEnablePeerAccess(g->device, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+    }
+    (void)hipSetDevice(g->device);
+  }
+  if (rc) {
+    const std::string msg = g_err;
+    (void)prt_destroy(g);
+    return fail(rc, msg);
+  }
+  g->sh_kind = 2;
+  g->sh_rank = 0;
+  g->sh_world = n;
+  *out = g;
+  return PRT_OK;
+}
+
+int prt_get_shard_info(prt_ctx* c, prt_shard_info* info) {
+  if (!c || !info) return fail(PRT_ERR_INVALID_ARGUMENT, "bad arguments");
+  info->rank = c->sh_rank;
+  info->world = c->sh_world;
+  info->tile_size = c->sh_tile;
+  info->transport = c->sh_kind;
+  return PRT_OK;
+}
+
 int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
   if (!c || !info) return fail(PRT_ERR_INVALID_ARGUMENT, "bad arguments");
   std::memset(info, 0, sizeof(*info));
@@ -1244,7 +1251,8 @@ int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
   info->max_depth = c->max_depth;
   info->build_ms = c->build_ms;
   info->builder = c->built_with;
-  info->device_bytes = (int64_t)(c->nodes.bytes + c->nodes8.bytes + c->nodes8h.bytes + c->tris.bytes + c->stri.bytes + c->texels.bytes + c->sky.bytes + c->inst.bytes);
+  info->device_bytes = (int64_t)(c->nodes8.bytes + c->tris.bytes + c->stri.bytes + c->texels.bytes + c->sky.bytes +
+                                 c->inst.bytes);
   return PRT_OK;
 }
 

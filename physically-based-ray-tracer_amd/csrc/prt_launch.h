@@ -17,18 +17,15 @@ struct HitOut {
 };
 struct LaunchCfg {
   hipStream_t stream;
-  int layout;  // BLAS layout: 4 (Node4) or 8 (Node8, default)
-  int trav;    // 8-wide wavefront traversal: 32 / 16 = persistent lanes refilled at that many idle lanes
-               // (default 32; PRT_TRAV=refill16), 1 = lock-step one-ray-per-lane kernels (PRT_TRAV=lockstep)
-  int occ;     // persistent traversal waves/SIMD: 5 (16-group LDS stack), 6 (12 groups), 8 (8 groups)
+  int occ;     // persistent traversal waves/SIMD: 8 / 7 / 6 / 5 / 4 (8 / 9 / 11 / 14 / 18 LDS stack groups)
 };
 
 // wavefront pipeline buffers (SoA over n work items; R/T hold (bounces-1) x n entries)
 constexpr uint32_t kNSub = 32;       // sub-queues per queue (one append counter each)
 constexpr uint32_t kCtrStride = 32;  // words between counters (each on its own 128-B line)
 struct WaveBufs {
-  uint32_t n;       // items of this batch
-  uint32_t base;    // first item of this batch within the call (out / the state arrays are batch-local)
+  uint32_t n;       // items of this call
+  uint32_t base;    // first item of the state arrays within the call (0)
   uint32_t qcap;    // capacity of one path sub-queue  (multiple of 256)
   uint32_t scap;    // capacity of one shadow sub-queue (4 x qcap)
   uint32_t* seed;
@@ -59,28 +56,8 @@ struct WaveBufs {
   float4* drd;      // per level: refraction ray direction
   unsigned long long* tl;  // PRT_DEBUG_QUEUES: [launch][wave] {start, first empty fetch, exit, -}
   int32_t coop_tail;       // cooperative traversal tail (prt_persist.h)
-  int32_t group_tail;      // group traversal tail threshold (prt_persist.h), 0 = off
+  int32_t pad;
 };
-// streaming engine (prt_stream.hip): per-XCD ray / shade queues of tagged 8-byte granules
-constexpr uint32_t kSSub = 8;        // sub-queues per XCD part and queue
-constexpr uint32_t kMaxParts = 8;
-struct StreamBufs {
-  uint32_t* pend;               // n: rays of the item still in flight (agent atomics only)
-  unsigned long long* rq;       // ray queue   [part][sub][rcap]: serial << 32 | ray id
-  unsigned long long* hq;       // shade queue [part][sub][hcap]: serial << 32 | item
-  uint32_t* ctr;                // [part][rq tail, rq head, hq tail, hq head][sub], kCtrStride apart
-  uint32_t* ctl;                // [0] abort, [1] error code, kCtrStride * (2 + part): live items of the part
-  unsigned long long* stat;     // closest segments, shadow rays traced
-  uint32_t rcap, hcap;          // per sub-queue capacities
-  uint32_t serial;              // granule tag of this launch (never 0)
-  uint32_t nparts;              // XCD parts present
-  uint32_t xcc_part;            // 4 bits per HW_REG_XCC_ID: its part (0xF = none)
-  uint32_t budget_ms;           // in-kernel watchdog
-  uint32_t waves;               // waves per SIMD of the persistent launch (4 or 5)
-};
-constexpr size_t kStreamCtlWords = (size_t)(2 + kMaxParts) * kCtrStride;
-constexpr size_t kStreamCtrWords = (size_t)kMaxParts * 4 * kSSub * kCtrStride;
-
 constexpr int kMaxIters = 32;
 // wavefront iterations of one call: one per path segment, paths x bounces; with dielectric instances a path
 // is a binary tree walked depth first (one segment per iteration), at most 2^bounces - 1 segments per path
@@ -95,23 +72,12 @@ struct WaveTimers {
   uint32_t iters;
 };
 
-hipError_t launch_wavefront(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
-                            const WaveBufs& B, float4* out, WaveTimers* tm);
 hipError_t launch_wave_init(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                             const WaveBufs& B, float4* out);
-// merged pipeline (prt_wave2.hip): one traversal launch per iteration for P(i) closest + S(i-1) any-hit
-hipError_t launch_wavefront2(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
-                             const WaveBufs& B, float4* out, WaveTimers* tm);
-// its iteration `it` (0..iters) alone, after launch_wave_init: batches on several streams enqueue round-robin
+// merged pipeline (prt_wave2.hip): iteration `it` (0..iters) after launch_wave_init -- one traversal launch for
+// P(it) closest + S(it-1) any-hit, then resolve / miss / shade
 hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                              const WaveBufs& B, float4* out, WaveTimers* tm, uint32_t it);
-// streaming engine (prt_stream.hip): one persistent launch per frame batch, no per-bounce boundaries
-hipError_t launch_stream(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
-                         const WaveBufs& B, const StreamBufs& Q, float4* out);
-// XCC ids the device schedules on (bit k = HW_REG_XCC_ID k seen); writes one word to dev_mask
-hipError_t launch_xcc_census(hipStream_t s, uint32_t* dev_mask);
-hipError_t launch_trace_frames(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
-                               float4* out, Counters* cnt);
 // acc_prev (nullable): the accumulator state before the last frame of the call (screen-pass input)
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,
                              float4* acc, int32_t* nsamp, float* dist, float4* avg, uint32_t* rgb8, float4* tiles,

@@ -1,4 +1,4 @@
-// prt_path.h -- device pieces of Renderer::Trace shared by the megakernel and the wavefront pipeline.
+// prt_path.h -- device pieces of Renderer::Trace used by the wavefront shading kernels.
 #pragma once
 #include "prt_kernels.h"
 #include "prt_post.h"

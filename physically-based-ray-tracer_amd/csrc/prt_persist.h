@@ -5,7 +5,7 @@
 // about a third of the lanes busy (scripts/trav_stats.cpp: lane efficiency 0.34 closest, 0.43 any-hit).
 // Here every lane is a small state machine and one loop iteration does, per lane:
 //   refill     lanes without a ray take the next queue entries (once >= kRefill lanes are idle; one
-//              atomic per wave on an XCD-partitioned fetch counter, see prt_wave.hip)
+//              atomic per wave on an XCD-partitioned fetch counter, prt_queue.h)
 //   instance   lanes done with a BLAS enter the next instance whose world box the ray hits (TLAS loop)
 //   node       lanes with no pending triangles visit one Node8 node (8 quantised child slabs), keep its
 //              hit leaf children as pending and step to the next interior child / pop the LDS stack
@@ -26,15 +26,6 @@
 // instance or finishes.  The hit rule makes the split exact: the result does not depend on which lane
 // visits which subtree.
 //
-// Group tail (gtail != 0, Node8).  A drained wave with at most gtail (<= 8) rays gives every ray a group of
-// 8 lanes.  Lane k of a group tests child k of the ray's node, the group's ballot is the node's hit mask,
-// and the triangles of the hit leaf children are tested in the same iteration, one leaf per lane.  A
-// straggler's step is then one child slab plus one leaf instead of eight slabs, and its node visits and
-// triangle tests no longer take separate iterations.  The traversal state is replicated in the group's 8
-// lanes (each computes the same uniform update) and the stack stays in the owner lane's LDS column.  The
-// group's closest candidate is a min-reduction of (t, prim) over its lanes, which is the hit rule again.
-// With both tails on, the cooperative tail stops handing out subtrees once <= gtail owners are left, merges
-// its teams when the last helper is done and hands the owners to the group tail.
 #pragma once
 #include "prt_traverse8.h"
 
@@ -66,14 +57,13 @@ __device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
 //                                                           idle lanes, no refill coming (the streaming
 //                                                           engine publishes finished rays there)
 // tail: tail_lds_words(TAILN) words of LDS for the cooperative tail, or nullptr (no tail mode).
-// gtail: group tail threshold (<= 8 rays, Node8 only), 0 = off.
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
-template <int MODE, bool HALF, int STACK, int REFILL, int TAILN = 32, class Fetch, class Load, class Reload, class Finish,
+template <int MODE, int STACK, int REFILL, int TAILN = 32, class Fetch, class Load, class Reload, class Finish,
           class Tick>
 __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                    Load load, Reload reload, Finish finish, Tick tick,
-                                                   uint32_t* __restrict__ tail = nullptr, uint32_t gtail = 0) {
+                                                   uint32_t* __restrict__ tail = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   bool active = false, drained = false;
@@ -86,10 +76,9 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   int inst = -1;
   uint32_t node = kNoNode, gbase = 0, gmask = 0, gimask = 0;
   int sp = 0;
-  uint32_t* st = stk;  // the LDS stack column this lane walks with (group tail: the owner's)
+  uint32_t* st = stk;  // the LDS stack column this lane walks with
   uint32_t lhit = 0, ltri = 0, lmeta0 = 0, lmeta1 = 0, tcur = 0, tcnt = 0;  // pending leaf triangles
   bool found = false;  // tail: this lane improved its closest hit
-  if (HALF) gtail = 0;
   // enter the first instance >= i0 whose world box the ray hits before h.t (tiny_bvh.h:2500-2565 TLAS
   // walk as a linear loop over <= 64 instance boxes); false when there is none
   auto enter = [&](int i0, const V3& Ow, const V3& Dw) -> bool {
@@ -142,20 +131,10 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   };
   // one node visit (lanes without pending triangles)
   auto node_step = [&]() {
-    uint4 a, b;
-    uint32_t hits;
-    if (HALF) {  // Node8H: one 128-B line
-      const uint4* np = reinterpret_cast<const uint4*>(S.nodes8h + node);
-      a = np[0];
-      b = np[1];
-      hits = node8h_hits(np, a, O, rD, h.t);
-    } else {     // Node8: 80 B
-      const uint4* np = reinterpret_cast<const uint4*>(S.nodes8 + node);
-      a = np[0];
-      b = np[1];
-      const uint4 c = np[2], d = np[3], e = np[4];
-      hits = node8_hits(a, c, d, e, O, rD, h.t);
-    }
+    const uint4* np = reinterpret_cast<const uint4*>(S.nodes8 + node);
+    const uint4 a = np[0], b = np[1];
+    const uint4 c = np[2], d = np[3], e = np[4];
+    const uint32_t hits = node8_hits(a, c, d, e, O, rD, h.t);
     const uint32_t imask = a.w >> 24;
     lhit = hits & ~imask;
     ltri = b.y; lmeta0 = b.z; lmeta1 = b.w;
@@ -216,7 +195,6 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       if (drained) break;
       continue;
     }
-    if (gtail && drained && __popcll(act) <= gtail) break;           // group tail below
     if (tail && drained && __popcll(act) <= (uint32_t)TAILN) break;  // cooperative tail below
     // ---- BLAS done: next instance, or the ray is finished
     if (active && node == kNoNode && lhit == 0 && tcnt == 0) {
@@ -243,7 +221,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   }
   if (__ballot(active) == 0) return;
 
-  if (tail && !(gtail && (uint32_t)__popcll(__ballot(active)) <= gtail)) {
+  if (tail) {
     // ---------------------------------------------------------------- cooperative tail
     // role: owner (active: holds the ray's handle) / helper (walks one subtree of an owner's ray) / free;
     // team slot of an owner = its rank among the owners at tail entry (< TAILN)
@@ -273,15 +251,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
         h.t = t; h.u = u; h.v = v; h.prim = prim; h.inst = (uint32_t)inst;
       }
     };
-    bool to_group = false;
     while (true) {
-      // ---- few owners left and no helper walking: the group tail takes over
-      const uint32_t nown = (uint32_t)__popcll(__ballot(active));
-      const bool few = gtail && nown <= gtail;
-      if (few && __ballot(helper) == 0) {
-        to_group = true;
-        break;
-      }
       const bool member = active || helper;
       // an any-hit team that hit stops walking
       if (member && any && (tstate[slot] & kFoundBit)) { node = kNoNode; lhit = 0; tcnt = 0; }
@@ -314,8 +284,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       }
       if (__ballot(active) == 0) break;  // helpers always belong to a live owner
       // ---- free lanes take a pending group from a walking lane: its top stack entry or its sibling group
-      // (none once the group tail is waiting for the last helpers)
-      const uint64_t freem = __ballot(!active && !helper && !few);
+      const uint64_t freem = __ballot(!active && !helper);
       const uint64_t donm = __ballot((active || helper) && busy && (sp > 0 || gmask != 0) &&
                                      !(any && (tstate[slot] & kFoundBit)));
       if (freem && donm) {
@@ -369,143 +338,14 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
         if (tri_step()) atomicOr(&tstate[slot], kFoundBit);
       }
     }
-    if (!to_group) return;
-    // hand-over: every team is down to its owner; take what the helpers published
-    if (active) {
-      if (any && (tstate[slot] & kFoundBit)) {
-        finish(handle, h, true, true);
-        active = false;
-      } else if (!any) {
-        merge_team();
-      }
-    }
-  }
-  if (!gtail) return;
-
-  // ---------------------------------------------------------------- group tail
-  const uint64_t own = __ballot(active);
-  if (own == 0) return;
-  const uint32_t k = lane & 7u, gsh = lane & ~7u;  // child slot of this lane, first lane of its group
-  bool live = (lane >> 3) < (uint32_t)__popcll(own);
-  const int src = (int)nth_set(own, live ? (lane >> 3) : 0u);  // the group's owner lane
-  O = v3(__shfl(O.x, src), __shfl(O.y, src), __shfl(O.z, src));
-  D = v3(__shfl(D.x, src), __shfl(D.y, src), __shfl(D.z, src));
-  rD = v3(__shfl(rD.x, src), __shfl(rD.y, src), __shfl(rD.z, src));
-  oct = (uint32_t)__shfl((int)oct, src);
-  h.t = __shfl(h.t, src); h.u = __shfl(h.u, src); h.v = __shfl(h.v, src);
-  h.prim = (uint32_t)__shfl((int)h.prim, src); h.inst = (uint32_t)__shfl((int)h.inst, src);
-  inst = __shfl(inst, src);
-  handle = (uint32_t)__shfl((int)handle, src);
-  if (MODE == 2) any = __shfl((int)any, src) != 0;
-  node = (uint32_t)__shfl((int)node, src);
-  gbase = (uint32_t)__shfl((int)gbase, src); gmask = (uint32_t)__shfl((int)gmask, src);
-  gimask = (uint32_t)__shfl((int)gimask, src);
-  sp = __shfl(sp, src);
-  lhit = (uint32_t)__shfl((int)lhit, src); ltri = (uint32_t)__shfl((int)ltri, src);
-  lmeta0 = (uint32_t)__shfl((int)lmeta0, src); lmeta1 = (uint32_t)__shfl((int)lmeta1, src);
-  tcur = (uint32_t)__shfl((int)tcur, src); tcnt = (uint32_t)__shfl((int)tcnt, src);
-  st = stk - lane + src;
-  while (true) {
-    // ---- BLAS done: next instance, or the ray is finished
-    if (live && node == kNoNode && lhit == 0 && tcnt == 0) {
-      bool more = false;
-      if (inst + 1 < S.ninst) {
-        V3 Ow, Dw;
-        reload(handle, any, Ow, Dw);
-        more = enter(inst + 1, Ow, Dw);
-      }
-      if (!more) {
-        if (k == 0) finish(handle, h, any, false);
-        live = false;
-      }
-    }
-    if (__ballot(live) == 0) break;
-    // ---- node visit: lane k tests child k, the group's ballot is the hit mask
-    const bool visit = live && node != kNoNode && lhit == 0 && tcnt == 0;
-    bool hk = false;
-    uint4 a = make_uint4(0u, 0u, 0u, 0u), b = a;
-    if (visit) {
-      const uint4* np = reinterpret_cast<const uint4*>(S.nodes8 + node);
-      a = np[0];
-      b = np[1];
-      hk = node8_child_hit(a, np[2], np[3], np[4], k, O, rD, h.t);
-    }
-    const uint32_t m = (uint32_t)(__ballot(hk) >> gsh) & 0xFFu;
-    if (visit) {
-      const uint32_t imask = a.w >> 24;
-      lhit = m & ~imask;
-      ltri = b.y; lmeta0 = b.z; lmeta1 = b.w;
-      push_group(m & imask, imask, b.x);
-    }
-    // ---- leaf triangles, same iteration: lane k takes leaf child k; a partly tested leaf (tcur, tcnt,
-    // pending at entry) goes to the first lane whose child is not pending
-    bool occ = false, got = false;
-    float bt = 0.0f, bu = 0.0f, bv = 0.0f;
-    uint32_t bp = 0;
-    if (live && (lhit | tcnt)) {
-      uint32_t first = 0, cnt = 0;
-      if ((lhit >> k) & 1u) {
-        const uint32_t meta = ((k < 4 ? lmeta0 : lmeta1) >> (8 * (k & 3))) & 0xFFu;
-        first = ltri + (meta >> 3);
-        cnt = meta & 7u;
-      } else if (tcnt && k == (uint32_t)__builtin_ctz(~lhit & 0xFFu)) {
-        first = tcur;
-        cnt = tcnt;
-      }
-      for (uint32_t i = 0; i < cnt; i++) {
-        float t, u, v;
-        uint32_t prim;
-        if (mt_test(S.tris + first + i, O, D, t, u, v, prim)) {
-          if (MODE == 1 || (MODE == 2 && any)) {
-            if (t < h.t) occ = true;  // tiny_bvh.h:6594 (h.t holds tmax)
-          } else if (!got || t < bt || (t == bt && prim < bp)) {
-            bt = t; bu = u; bv = v; bp = prim;
-            got = true;
-          }
-        }
-      }
-      lhit = 0;
-      tcnt = 0;
-    }
-    // ---- any-hit: the group's ray is occluded
-    if (live && ((__ballot(occ) >> gsh) & 0xFFull)) {
-      if (k == 0) finish(handle, h, true, true);
-      live = false;
-      node = kNoNode;
-    }
-    // ---- closest: min (t, prim) over the group (t > 0, so the float bits order like the floats), then the
-    // hit rule against the ray's best
-    if (__ballot(got) != 0) {
-      const uint64_t mine = got ? (((uint64_t)__float_as_uint(bt) << 32) | bp) : ~0ull;
-      uint64_t key = mine;
-#pragma unroll
-      for (int s = 1; s < 8; s <<= 1) {
-        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)key, s);
-        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(key >> 32), s);
-        const uint64_t o = ((uint64_t)hi << 32) | lo;
-        key = o < key ? o : key;
-      }
-      const uint64_t wm = (__ballot(got && mine == key) >> gsh) & 0xFFull;
-      const int wl = (int)gsh + (wm ? __builtin_ctzll(wm) : 0);
-      const float wu = __shfl(bu, wl), wv = __shfl(bv, wl);
-      if (live && key != ~0ull) {
-        const float kt = __uint_as_float((uint32_t)(key >> 32));
-        const uint32_t kp = (uint32_t)key;
-        if (kt < h.t || (kt == h.t && ((uint32_t)inst < h.inst || ((uint32_t)inst == h.inst && kp < h.prim)))) {
-          h.t = kt; h.u = wu; h.v = wv; h.prim = kp; h.inst = (uint32_t)inst;
-        }
-      }
-    }
   }
 }
 
-template <int MODE, bool HALF, int STACK, int REFILL, int TAILN = 32, class Fetch, class Load, class Reload,
-          class Finish>
+template <int MODE, int STACK, int REFILL, int TAILN = 32, class Fetch, class Load, class Reload, class Finish>
 __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                  Load load, Reload reload, Finish finish,
-                                                 uint32_t* __restrict__ tail = nullptr, uint32_t gtail = 0) {
-  trav8_persistent_t<MODE, HALF, STACK, REFILL, TAILN>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {},
-                                                       tail, gtail);
+                                                 uint32_t* __restrict__ tail = nullptr) {
+  trav8_persistent_t<MODE, STACK, REFILL, TAILN>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {}, tail);
 }
 
 }  // namespace prt

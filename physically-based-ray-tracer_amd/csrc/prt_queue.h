@@ -1,4 +1,4 @@
-// prt_queue.h -- work queues of the wavefront pipelines (prt_wave.hip, prt_wave2.hip): sub-queue counters,
+// prt_queue.h -- work queues of the wavefront pipeline (prt_wave2.hip): sub-queue counters,
 // consumer-side slot mapping, block-aggregated appends, XCD-partitioned dynamic fetch for the traversal kernels.
 #pragma once
 #include "prt_launch.h"

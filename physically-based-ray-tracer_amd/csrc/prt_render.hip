@@ -1,12 +1,5 @@
-// prt_render.hip -- megakernel path tracer + accumulation / untile / geometry-query kernels (gfx950).
+// prt_render.hip -- accumulation / untile / screen-pass / geometry-query kernels (gfx950).
 //
-// k_trace_frames: one lane = one (pixel, reference frame) work item, tracing the frame's camera
-//   path(s) in the canonical order (AA jitter, Trace(r1), Trace(r2)) through
-//   the restated Renderer::Trace (Core/Renderer.cpp:150-406) with its shadow rays inline.  It is the
-//   reference-shaped baseline (PRT_PIPELINE=mega); the default pipeline is the wavefront one
-//   (prt_wave.hip) and both must produce bit-identical frames.  The recursion
-//   `result + Trace(..) * throughput` is evaluated bottom-up from a per-lane (result, throughput) stack
-//   so float rounding matches the recursive reference exactly.
 // k_accumulate: per pixel, folds the frames into the persistent accumulator with the reference's
 //   distance-keyed progressive mean (Core/Renderer.cpp:81-104) and packs RGB8 (precomp.h:310-315).
 #include "prt_launch.h"
@@ -25,82 +18,6 @@ __device__ __forceinline__ void wave_count(Counters* c, uint32_t seg, uint32_t s
     atomicAdd(&c->segments, (unsigned long long)seg);
     atomicAdd(&c->shadow, (unsigned long long)sh);
   }
-}
-
-// Renderer::Trace, iterative.  Returns radiance; *t_primary = closest-hit t of the first segment.
-template <int BV>
-__device__ V3 trace_path(const SceneDev& S, const TraceArgs& A, Ray r, uint32_t& seed, float* t_primary,
-                         uint32_t& nseg, uint32_t& nshadow, uint32_t* stk) {
-  V3 R[kMaxBounces], T[kMaxBounces];
-  int nd = 0;
-  V3 Lend = v3(0.0f, 0.0f, 0.0f);
-  const uint32_t fl = A.flags;
-  for (int depth = 0;; depth++) {
-    if (depth >= A.bounces) { Lend = v3(0.0f, 0.0f, 0.0f); break; }                   // :152
-    const Hit h = Trav<BV>::template closest<kBlock>(S, r, kFar, stk);                         // :157
-    nseg++;
-    if (depth == 0 && t_primary) *t_primary = h.t;
-    if (h.t >= kFar) { Lend = (fl & kSkybox) ? sample_sky(S, r.D) : v3(0.0f, 0.0f, 0.0f); break; }  // :159
-    const V3 I = r.O + h.t * r.D;                                                          // tiny_bvh.h:586
-    const V3 V = -r.D;
-    const HitAttr ha = hit_attributes(S, h.inst, h.prim, h.u, h.v, (fl & kNormalMap) != 0);
-    if (A.mode != 0) { Lend = debug_view(S, A.mode, ha, h.inst, h.prim); break; }        // :170-194
-    const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
-    const int kind = nee_kind(fl, seed);                                                  // :198-326
-    uint32_t vis = 0;
-    V3 f[4];
-    const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed, [&](int k, const Ray& sr, float tmax, V3 fk) {
-      f[k] = fk;
-      nshadow++;
-      if (!Trav<BV>::template anyhit<kBlock>(S, sr, tmax, stk)) vis |= 1u << k;
-    });
-    const V3 result = nee_resolve(kind, vis, e, brdf, f, fl);
-    if (depth == A.bounces - 1) { Lend = result; break; }                                 // :329
-    V3 dir, thr;
-    if (!sample_bounce(ha.m, V, ha.N, seed, dir, thr)) { Lend = result; break; }          // :376-399
-    R[nd] = result;
-    T[nd] = thr;
-    nd++;
-    r = make_ray(I + dir * kEpsilon, dir);                                                 // :404
-  }
-  V3 L = Lend;
-  for (int k = nd - 1; k >= 0; k--) L = R[k] + L * T[k];
-  return L;
-}
-
-template <int BV>
-__global__ void __launch_bounds__(kBlock) k_trace_frames(SceneDev S, TraceArgs A, TileMap M, float4* __restrict__ out,
-                                                         Counters* __restrict__ cnt) {
-  __shared__ uint32_t lds_stack[Trav<BV>::kWords * kBlock];
-  uint32_t* stk = lds_stack + threadIdx.x;
-  const uint64_t item = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint64_t total = (uint64_t)M.items * (uint64_t)A.frames;
-  uint32_t nseg = 0, nsh = 0;
-  if (item < total) {
-    const uint32_t f = (uint32_t)(item / M.items), r = (uint32_t)(item % M.items);
-    int32_t x, y;
-    if (item_pixel(M, r, x, y)) {
-      const uint32_t p = (uint32_t)(y * A.W + x);
-      uint32_t seed = init_seed(A.seed + p + (uint32_t)A.W * (uint32_t)A.H * (A.frame_index + f));
-      float t1 = kFar;
-      const Ray r1 = primary_ray(S, (float)x, (float)y, A.W, A.H);
-      V3 res;
-      if (A.flags & kAA) {                                                                 // :59-66
-        const float jx = random_float(seed), jy = random_float(seed);
-        const Ray r2 = primary_ray(S, (float)x + jx, (float)y + jy, A.W, A.H);
-        const V3 s1 = trace_path<BV>(S, A, r1, seed, &t1, nseg, nsh, stk);
-        const V3 s2 = trace_path<BV>(S, A, r2, seed, nullptr, nseg, nsh, stk);
-        res = 0.5f * (s1 + s2);
-      } else {
-        res = trace_path<BV>(S, A, r1, seed, &t1, nseg, nsh, stk);
-      }
-      if (A.flags & kGamma) res = v3(sqrtf(res.x), sqrtf(res.y), sqrtf(res.z));          // :73-79
-      out[item] = make_float4(res.x, res.y, res.z, t1);
-    } else {
-      out[item] = make_float4(0.0f, 0.0f, 0.0f, kFar);
-    }
-  }
-  wave_count(cnt, nseg, nsh);
 }
 
 // Core/Renderer.cpp:81-104,137.  tiles_out != null: write the average in item (tile-compact) order.
@@ -206,10 +123,9 @@ __global__ void __launch_bounds__(kBlock) k_postfx(PostDev P, const float4* __re
 
 // ---- geometry-only kernels
 
-template <int BV>
 __global__ void __launch_bounds__(kBlock) k_primary_hits(SceneDev S, TileMap M, HitOut* __restrict__ out,
                                                          Counters* __restrict__ cnt) {
-  __shared__ uint32_t lds_stack[Trav<BV>::kWords * kBlock];
+  __shared__ uint32_t lds_stack[kQueryWords * kBlock];
   uint32_t* stk = lds_stack + threadIdx.x;
   const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
   uint32_t nseg = 0;
@@ -217,7 +133,7 @@ __global__ void __launch_bounds__(kBlock) k_primary_hits(SceneDev S, TileMap M, 
     int32_t x, y;
     if (item_pixel(M, r, x, y)) {
       const Ray ray = primary_ray(S, (float)x, (float)y, M.W, M.H);
-      const Hit h = Trav<BV>::template closest<kBlock>(S, ray, kFar, stk);
+      const Hit h = scene_closest8<kQueryStack, kBlock>(S, ray, kFar, stk);
       nseg = 1;
       HitOut o;
       o.t = h.t; o.u = h.u; o.v = h.v; o.prim = h.prim; o.inst = h.inst;
@@ -227,51 +143,33 @@ __global__ void __launch_bounds__(kBlock) k_primary_hits(SceneDev S, TileMap M, 
   wave_count(cnt, nseg, 0);
 }
 
-template <int BV>
 __global__ void __launch_bounds__(kBlock) k_intersect(SceneDev S, int32_t n, const float* __restrict__ O,
                                                       const float* __restrict__ D, const float* __restrict__ tmax,
                                                       HitOut* __restrict__ out) {
-  __shared__ uint32_t lds_stack[Trav<BV>::kWords * kBlock];
+  __shared__ uint32_t lds_stack[kQueryWords * kBlock];
   uint32_t* stk = lds_stack + threadIdx.x;
   const int32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const Ray r = make_ray(v3(O[3 * i], O[3 * i + 1], O[3 * i + 2]), v3(D[3 * i], D[3 * i + 1], D[3 * i + 2]));
-  const Hit h = Trav<BV>::template closest<kBlock>(S, r, tmax ? tmax[i] : kFar, stk);
+  const Hit h = scene_closest8<kQueryStack, kBlock>(S, r, tmax ? tmax[i] : kFar, stk);
   HitOut o;
   o.t = h.t; o.u = h.u; o.v = h.v; o.prim = h.prim; o.inst = h.inst;
   out[i] = o;
 }
 
-template <int BV>
 __global__ void __launch_bounds__(kBlock) k_occluded(SceneDev S, int32_t n, const float* __restrict__ O,
                                                      const float* __restrict__ D, const float* __restrict__ tmax,
                                                      int32_t* __restrict__ out) {
-  __shared__ uint32_t lds_stack[Trav<BV>::kWords * kBlock];
+  __shared__ uint32_t lds_stack[kQueryWords * kBlock];
   uint32_t* stk = lds_stack + threadIdx.x;
   const int32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const Ray r = make_ray(v3(O[3 * i], O[3 * i + 1], O[3 * i + 2]), v3(D[3 * i], D[3 * i + 1], D[3 * i + 2]));
-  out[i] = Trav<BV>::template anyhit<kBlock>(S, r, tmax[i], stk) ? 1 : 0;
+  out[i] = scene_anyhit8<kQueryStack, kBlock>(S, r, tmax[i], stk) ? 1 : 0;
 }
 
 // ---- launchers (host)
 static inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
-
-// launch kernel template K<layout> (4 = Node4, 8 = Node8, 9 = Node8H)
-#define PRT_BY_LAYOUT(layout, K, ...)                           \
-  do {                                                          \
-    if ((layout) == 4) hipLaunchKernelGGL(K<4>, __VA_ARGS__);   \
-    else if ((layout) == 9) hipLaunchKernelGGL(K<9>, __VA_ARGS__); \
-    else hipLaunchKernelGGL(K<8>, __VA_ARGS__);                 \
-  } while (0)
-
-hipError_t launch_trace_frames(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
-                               float4* out, Counters* cnt) {
-  const uint64_t total = (uint64_t)M.items * (uint64_t)A.frames;
-  if (total == 0) return hipSuccess;
-  PRT_BY_LAYOUT(c.layout, k_trace_frames, dim3(grid_of(total)), dim3(kBlock), 0, c.stream, S, A, M, out, cnt);
-  return hipGetLastError();
-}
 
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,
                              float4* acc, int32_t* nsamp, float* dist, float4* avg, uint32_t* rgb8, float4* tiles,
@@ -302,21 +200,21 @@ hipError_t launch_untile(const LaunchCfg& c, int32_t W, int32_t H, int32_t ts, i
 
 hipError_t launch_primary_hits(const LaunchCfg& c, const SceneDev& S, const TileMap& M, HitOut* out, Counters* cnt) {
   if (M.items == 0) return hipSuccess;
-  PRT_BY_LAYOUT(c.layout, k_primary_hits, dim3(grid_of(M.items)), dim3(kBlock), 0, c.stream, S, M, out, cnt);
+  hipLaunchKernelGGL(k_primary_hits, dim3(grid_of(M.items)), dim3(kBlock), 0, c.stream, S, M, out, cnt);
   return hipGetLastError();
 }
 
 hipError_t launch_intersect(const LaunchCfg& c, const SceneDev& S, int32_t n, const float* O, const float* D,
                             const float* tmax, HitOut* out) {
   if (n <= 0) return hipSuccess;
-  PRT_BY_LAYOUT(c.layout, k_intersect, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
+  hipLaunchKernelGGL(k_intersect, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
   return hipGetLastError();
 }
 
 hipError_t launch_occluded(const LaunchCfg& c, const SceneDev& S, int32_t n, const float* O, const float* D,
                            const float* tmax, int32_t* out) {
   if (n <= 0) return hipSuccess;
-  PRT_BY_LAYOUT(c.layout, k_occluded, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
+  hipLaunchKernelGGL(k_occluded, dim3(grid_of(n)), dim3(kBlock), 0, c.stream, S, n, O, D, tmax, out);
   return hipGetLastError();
 }
 

@@ -1,6 +1,6 @@
 // prt_scene.h -- device-resident scene layout (HBM) shared by host and kernels.
 //
-//   nodes   Node4[]    128 B each, all meshes' BLASes concatenated (bvh_build.h)
+//   nodes8  Node8[]    80 B each, all meshes' BLASes concatenated (bvh_build.h)
 //   tris    TriMT[]    48 B each, leaf order, MT-ready {v0,prim | e1 | e2}
 //   stri    ShadeTri[T] everything shading reads for one primitive in one 128-B line, prim order
 //                       (global prim = mesh.prim_base + prim): Model::fixedNormals, fixedTextureCoords,
@@ -36,7 +36,7 @@ struct alignas(16) ShadeTri {
 static_assert(sizeof(ShadeTri) == 128, "ShadeTri must be one 128-byte line");
 
 struct MeshDev {
-  uint32_t root;       // Node4 index of the BLAS root
+  uint32_t root;       // Node8 index of the BLAS root
   uint32_t prim_base;  // offset into the per-triangle shading arrays
   uint32_t vert_base;  // unused (kept for layout)
   uint32_t tri_count;
@@ -52,9 +52,7 @@ struct TexDev {
 constexpr int kMaxInstances = 64;
 
 struct SceneDev {
-  const Node4* nodes;
-  const Node8* nodes8;    // Node8 BLASes (layout 8); root indices in MeshDev.root refer to the active layout
-  const Node8H* nodes8h;  // Node8H BLASes (layout 9)
+  const Node8* nodes8;    // all BLASes; MeshDev.root indexes it
   const TriMT* tris;
   const ShadeTri* stri;
   const uint32_t* texels;

@@ -48,67 +48,6 @@ __device__ __forceinline__ uint32_t node8_hits(const uint4& a, const uint4& c, c
   return hits;
 }
 
-// child k alone (k lane-varying): the same arithmetic as bit k of node8_hits
-__device__ __forceinline__ bool node8_child_hit(const uint4& a, const uint4& c, const uint4& d, const uint4& e,
-                                                uint32_t k, const V3& O, const V3& rD, float tlimit) {
-  const float sx = __uint_as_float((a.w & 0xFFu) << 23), sy = __uint_as_float(((a.w >> 8) & 0xFFu) << 23),
-              sz = __uint_as_float(((a.w >> 16) & 0xFFu) << 23);
-  const float ax = (__uint_as_float(a.x) - O.x) * rD.x, ay = (__uint_as_float(a.y) - O.y) * rD.y,
-              az = (__uint_as_float(a.z) - O.z) * rD.z;
-  const float bx = sx * rD.x, by = sy * rD.y, bz = sz * rD.z;
-  const bool px = rD.x >= 0.0f, py = rD.y >= 0.0f, pz = rD.z >= 0.0f, lo = k < 4;
-  const uint32_t sh = 8u * (k & 3u);
-  const uint32_t wx0 = lo ? c.x : c.y, wx1 = lo ? d.z : d.w;  // lo / hi plane words of child k
-  const uint32_t wy0 = lo ? c.z : c.w, wy1 = lo ? e.x : e.y;
-  const uint32_t wz0 = lo ? d.x : d.y, wz1 = lo ? e.z : e.w;
-  const float qnx = (float)(((px ? wx0 : wx1) >> sh) & 0xFFu), qfx = (float)(((px ? wx1 : wx0) >> sh) & 0xFFu);
-  const float qny = (float)(((py ? wy0 : wy1) >> sh) & 0xFFu), qfy = (float)(((py ? wy1 : wy0) >> sh) & 0xFFu);
-  const float qnz = (float)(((pz ? wz0 : wz1) >> sh) & 0xFFu), qfz = (float)(((pz ? wz1 : wz0) >> sh) & 0xFFu);
-  const float tnx = __builtin_fmaf(qnx, bx, ax), tfx = __builtin_fmaf(qfx, bx, ax);
-  const float tny = __builtin_fmaf(qny, by, ay), tfy = __builtin_fmaf(qfy, by, ay);
-  const float tnz = __builtin_fmaf(qnz, bz, az), tfz = __builtin_fmaf(qfz, bz, az);
-  const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f)) * kNearPad;
-  const float tf = fminf(fminf(tfx, tfy), tfz) * kFarPad;
-  return tn <= tf && tn <= tlimit;
-}
-
-// Node8H: fp16 integer child bounds; the near/far block of each axis is picked by the direction sign at
-// load time and every half goes straight into v_fma_mix_f32 (no byte / half conversions)
-__device__ __forceinline__ float half_lo(uint32_t w) {
-  return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xFFFFu));
-}
-__device__ __forceinline__ float half_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
-__device__ __forceinline__ uint32_t word_of(const uint4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
-
-__device__ __forceinline__ uint32_t node8h_hits(const uint4* __restrict__ np, const uint4& a, const V3& O, const V3& rD,
-                                                float tlimit) {
-  const float sx = __uint_as_float((a.w & 0xFFu) << 23), sy = __uint_as_float(((a.w >> 8) & 0xFFu) << 23),
-              sz = __uint_as_float(((a.w >> 16) & 0xFFu) << 23);
-  const float ax = (__uint_as_float(a.x) - O.x) * rD.x, ay = (__uint_as_float(a.y) - O.y) * rD.y,
-              az = (__uint_as_float(a.z) - O.z) * rD.z;
-  const float bx = sx * rD.x, by = sy * rD.y, bz = sz * rD.z;
-  const int px = rD.x >= 0.0f ? 0 : 1, py = rD.y >= 0.0f ? 0 : 1, pz = rD.z >= 0.0f ? 0 : 1;
-  const uint4 nx = np[2 + px], fx = np[3 - px], ny = np[4 + py], fy = np[5 - py], nz = np[6 + pz], fz = np[7 - pz];
-  uint32_t hits = 0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const int w = k >> 1;
-    const bool hi = (k & 1) != 0;
-    const uint32_t wnx = word_of(nx, w), wfx = word_of(fx, w), wny = word_of(ny, w), wfy = word_of(fy, w),
-                   wnz = word_of(nz, w), wfz = word_of(fz, w);
-    const float tnx = __builtin_fmaf(hi ? half_hi(wnx) : half_lo(wnx), bx, ax);
-    const float tfx = __builtin_fmaf(hi ? half_hi(wfx) : half_lo(wfx), bx, ax);
-    const float tny = __builtin_fmaf(hi ? half_hi(wny) : half_lo(wny), by, ay);
-    const float tfy = __builtin_fmaf(hi ? half_hi(wfy) : half_lo(wfy), by, ay);
-    const float tnz = __builtin_fmaf(hi ? half_hi(wnz) : half_lo(wnz), bz, az);
-    const float tfz = __builtin_fmaf(hi ? half_hi(wfz) : half_lo(wfz), bz, az);
-    const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f)) * kNearPad;
-    const float tf = fminf(fminf(tfx, tfy), tfz) * kFarPad;
-    if (tn <= tf && tn <= tlimit) hits |= 1u << k;
-  }
-  return hits;
-}
-
 // physical-slot mask -> traversal-order mask (bit k ^ oct)
 __device__ __forceinline__ uint32_t order_mask(uint32_t m, uint32_t oct) {
   if (oct & 1u) m = ((m & 0x55u) << 1) | ((m >> 1) & 0x55u);
@@ -117,8 +56,8 @@ __device__ __forceinline__ uint32_t order_mask(uint32_t m, uint32_t oct) {
   return m;
 }
 
-template <int STACK, int BLOCK, bool ANY, bool HALF>
-__device__ __forceinline__ bool blas_traverse8(const void* __restrict__ nodes, const TriMT* __restrict__ tris,
+template <int STACK, int BLOCK, bool ANY>
+__device__ __forceinline__ bool blas_traverse8(const Node8* __restrict__ nodes, const TriMT* __restrict__ tris,
                                                uint32_t root, const V3& O, const V3& D, const V3& rD, uint32_t inst,
                                                Hit& h, uint32_t* __restrict__ stk) {
   const uint32_t oct = (rD.x < 0.0f ? 1u : 0u) | (rD.y < 0.0f ? 2u : 0u) | (rD.z < 0.0f ? 4u : 0u);
@@ -127,10 +66,10 @@ __device__ __forceinline__ bool blas_traverse8(const void* __restrict__ nodes, c
   int sp = 0;
   while (true) {
     {
-      const uint4* np = reinterpret_cast<const uint4*>(nodes) + (size_t)node * (HALF ? 8 : 5);
+      const uint4* np = reinterpret_cast<const uint4*>(nodes + node);
       const uint4 a = np[0], b = np[1];
       const uint32_t imask = a.w >> 24;
-      const uint32_t hits = HALF ? node8h_hits(np, a, O, rD, h.t) : node8_hits(a, np[2], np[3], np[4], O, rD, h.t);
+      const uint32_t hits = node8_hits(a, np[2], np[3], np[4], O, rD, h.t);
       uint32_t lhit = hits & ~imask;
       while (lhit) {  // leaf children: test their triangles now
         const uint32_t k = __builtin_ctz(lhit);
@@ -177,7 +116,7 @@ __device__ __forceinline__ bool blas_traverse8(const void* __restrict__ nodes, c
   return false;
 }
 
-template <int STACK, int BLOCK, bool HALF>
+template <int STACK, int BLOCK>
 __device__ __forceinline__ Hit scene_closest8(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
   Hit h;
   h.t = tmax; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;
@@ -186,12 +125,12 @@ __device__ __forceinline__ Hit scene_closest8(const SceneDev& S, const Ray& r, f
     if (slab1(I.bmin, I.bmax, r.O, r.rD, h.t) >= kFar) continue;
     const V3 Oi = xform_point(r.O, I.inv), Di = xform_vector(r.D, I.inv);
     const V3 rDi = v3(safercp(Di.x), safercp(Di.y), safercp(Di.z));
-    blas_traverse8<STACK, BLOCK, false, HALF>(HALF ? (const void*)S.nodes8h : (const void*)S.nodes8, S.tris, S.mesh[I.mesh].root, Oi, Di, rDi, (uint32_t)i, h, stk);
+    blas_traverse8<STACK, BLOCK, false>(S.nodes8, S.tris, S.mesh[I.mesh].root, Oi, Di, rDi, (uint32_t)i, h, stk);
   }
   return h;
 }
 
-template <int STACK, int BLOCK, bool HALF>
+template <int STACK, int BLOCK>
 __device__ __forceinline__ bool scene_anyhit8(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
   for (int i = 0; i < S.ninst; i++) {
     const InstDev& I = S.inst[i];
@@ -200,54 +139,13 @@ __device__ __forceinline__ bool scene_anyhit8(const SceneDev& S, const Ray& r, f
     const V3 rDi = v3(safercp(Di.x), safercp(Di.y), safercp(Di.z));
     Hit h;
     h.t = tmax;
-    if (blas_traverse8<STACK, BLOCK, true, HALF>(HALF ? (const void*)S.nodes8h : (const void*)S.nodes8, S.tris, S.mesh[I.mesh].root, Oi, Di, rDi, 0u, h, stk)) return true;
+    if (blas_traverse8<STACK, BLOCK, true>(S.nodes8, S.tris, S.mesh[I.mesh].root, Oi, Di, rDi, 0u, h, stk)) return true;
   }
   return false;
 }
 
-// BLAS layout selection for the kernels: 4 = Node4 (128-B fp32 nodes, per-node LDS stack of 48
-// entries), 8 = Node8 (80-B 8-bit-quantised nodes), 9 = Node8H (128-B fp16-quantised nodes); the 8-wide
-// layouts keep 16 two-word group entries.  kWords = LDS words / lane.
-template <int LAYOUT>
-struct Trav;
-template <>
-struct Trav<4> {
-  static constexpr int kWords = 48;
-  static constexpr int kMaxDepth = 16;  // 3 pushes per level
-  template <int BLOCK>
-  __device__ static __forceinline__ Hit closest(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
-    return scene_closest<48, BLOCK>(S, r, tmax, stk);
-  }
-  template <int BLOCK>
-  __device__ static __forceinline__ bool anyhit(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
-    return scene_anyhit<48, BLOCK>(S, r, tmax, stk);
-  }
-};
-template <>
-struct Trav<8> {
-  static constexpr int kWords = 32;
-  static constexpr int kMaxDepth = 16;  // one group per level
-  template <int BLOCK>
-  __device__ static __forceinline__ Hit closest(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
-    return scene_closest8<16, BLOCK, false>(S, r, tmax, stk);
-  }
-  template <int BLOCK>
-  __device__ static __forceinline__ bool anyhit(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
-    return scene_anyhit8<16, BLOCK, false>(S, r, tmax, stk);
-  }
-};
-template <>
-struct Trav<9> {
-  static constexpr int kWords = 32;
-  static constexpr int kMaxDepth = 16;
-  template <int BLOCK>
-  __device__ static __forceinline__ Hit closest(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
-    return scene_closest8<16, BLOCK, true>(S, r, tmax, stk);
-  }
-  template <int BLOCK>
-  __device__ static __forceinline__ bool anyhit(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
-    return scene_anyhit8<16, BLOCK, true>(S, r, tmax, stk);
-  }
-};
+// stack words per lane of the one-ray-per-lane query kernels (16 two-word groups: one per tree level)
+constexpr int kQueryStack = 16;
+constexpr int kQueryWords = 2 * kQueryStack;
 
 }  // namespace prt

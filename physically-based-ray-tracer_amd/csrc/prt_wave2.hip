@@ -1,7 +1,12 @@
-// prt_wave2.hip -- merged-trace wavefront pipeline (default) for gfx950.
+// prt_wave2.hip -- the merged-trace wavefront path tracer for gfx950.
 //
-// Same estimator, RNG stream and per-item state as prt_wave.hip; the difference is where the path's
-// next ray is decided.  Every random number of a path is drawn in the shading stage, so the shading
+// The reference's recursive per-pixel Renderer::Trace (Core/Renderer.cpp:150-406) is re-cut into stages over
+// queues of live work items.  One item = one pixel x reference frame; it traces its AA path pair
+// sequentially, so the canonical RNG stream of SURVEY Appendix B is preserved.  All per-item state is SoA in
+// HBM.  Queues are split into kNSub sub-queues, each with its own counter on its own 128-B line; appends are
+// block-aggregated (one atomic per block), consumers read the kNSub counts into an LDS prefix table.
+//
+// Every random number of a path is drawn in the shading stage, so the shading
 // of iteration i already knows the ray of iteration i+1 (the sampled bounce, or the AA path-2 primary
 // ray when path 1 ends) and queues it at once.  The closest-hit rays of iteration i+1 and the shadow
 // rays of iteration i are then traced by ONE persistent launch, and the NEE resolve of iteration i
@@ -25,10 +30,44 @@
 
 namespace prt {
 
+// ---- init: items -> primary rays, appended to queue 0 (sub-queue = block % kNSub)
+__global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, TileMap M, WaveBufs B,
+                                                      float4* __restrict__ out) {
+  __shared__ uint32_t sm[8];
+  const uint32_t sub = blockIdx.x % kNSub;
+  uint32_t* cnt = qcounter(B.ctr, 0, 0, sub);
+  for (uint32_t c = blockIdx.x; c * kBlock < B.n; c += gridDim.x) {
+    const uint32_t i = c * kBlock + threadIdx.x;
+    bool enq = false;
+    if (i < B.n) {
+      const uint32_t gi = B.base + i;  // item index within the call (batches cover consecutive ranges)
+      const uint32_t f = gi / M.items, r = gi % M.items;
+      int32_t x, y;
+      const bool valid = item_pixel(M, r, x, y);
+      if (valid && A.bounces > 0) {
+        const uint32_t p = (uint32_t)(y * A.W + x);
+        uint32_t seed = init_seed(A.seed + p + (uint32_t)A.W * (uint32_t)A.H * (A.frame_index + f));
+        float jx = 0.0f, jy = 0.0f;
+        if (A.flags & kAA) { jx = random_float(seed); jy = random_float(seed); }         // :61
+        const Ray r1 = primary_ray(S, (float)x, (float)y, A.W, A.H);
+        B.seed[i] = seed;
+        B.jit[i] = make_float2(jx, jy);
+        B.ro[i] = make_float4(r1.O.x, r1.O.y, r1.O.z, 0.0f);
+        B.rd[i] = make_float4(r1.D.x, r1.D.y, r1.D.z, 0.0f);
+        B.info[i] = 0u;
+        B.s1[i] = make_float4(0.0f, 0.0f, 0.0f, kFar);
+        enq = true;
+      } else {
+        out[i] = make_float4(0.0f, 0.0f, 0.0f, kFar);  // bounces == 0: Trace returns 0, t1 stays BVH_FAR
+      }
+    }
+    const uint32_t slot = block_append(cnt, enq ? 1u : 0u, sm);
+    if (enq) B.q0[sub * B.qcap + slot] = i;
+  }
+}
+
 // ---- one traversal launch: closest hits of P(iter) (iter < iters) + any hits of S(iter - 1) (iter > 0)
-// GTAIL: the opt-in group tail (PRT_TAIL=2/3, measured slower) is compiled into the default 7-wave form only: in
-// the others its registers would cost scratch spills
-template <bool HALF, int REFILL, int STACK, int WAVES, int TAILN, bool GTAIL = false>
+template <int REFILL, int STACK, int WAVES, int TAILN>
 __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, uint32_t iter, uint32_t iters) {
   __shared__ uint32_t lds_stack[2 * STACK * 64];
   __shared__ uint32_t prefP[kNSub + 1], prefS[kNSub + 1];
@@ -38,21 +77,17 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   const uint32_t nP = iter < iters ? load_prefix(B.ctr, iter, 0, prefP) : 0u;
   const uint32_t nS = iter > 0 ? load_prefix(B.ctr, iter - 1, 1, prefS) : 0u;
   const uint32_t total = nP + nS;
-  // a launch with fewer rays than lanes spreads them: at most `cap` (>= 8) per fetch, so a small queue gives
-  // many waves a few rays each (at <= 8 they go straight to the group tail) instead of few waves 64 each
-  const uint32_t gtail = GTAIL ? (uint32_t)B.group_tail : 0u;
-  const uint32_t cap = gtail ? max(8u, (total + gridDim.x - 1u) / gridDim.x) : 64u;
-  if (blockIdx.x * min(cap, 64u) >= total) return;
+  if (blockIdx.x * 64u >= total) return;
   uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
   uint32_t part = xcc_id();
   // timeline diagnostic (s_memrealtime, one record per wave: start, first empty fetch, exit)
   unsigned long long* tl = B.tl ? B.tl + ((size_t)iter * kTlWaves + blockIdx.x) * 4 : nullptr;
   bool seen_drain = false;
   if (tl && threadIdx.x == 0) tl[0] = __builtin_amdgcn_s_memrealtime();
-  trav8_persistent<2, HALF, STACK, REFILL, TAILN>(
+  trav8_persistent<2, STACK, REFILL, TAILN>(
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) {
-        const uint32_t got = fetch_some(fctr, total, part, base, min(want, cap));
+        const uint32_t got = fetch_some(fctr, total, part, base, want);
         if (tl && got == 0 && !seen_drain) {
           seen_drain = true;
           if (threadIdx.x == 0) tl[1] = __builtin_amdgcn_s_memrealtime();
@@ -91,7 +126,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
           B.hit[h] = make_float4(hit.t, hit.u, hit.v, __uint_as_float(hit.prim | (hit.inst << 26)));
         }
       },
-      B.coop_tail ? tail_lds : nullptr, gtail);
+      B.coop_tail ? tail_lds : nullptr);
   if (tl && threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -411,34 +446,19 @@ __global__ void __launch_bounds__(kBlock) k_resolve2(SceneDev S, TraceArgs A, Wa
 
 // LDS per wave (one block): 2 x STACK x 256 B of stack + 264 B of prefix tables + the tail slots, within
 // 160 KB / (4 x WAVES) blocks per CU
-template <int REFILL, int STACK, int WAVES, int TAILN>
+template <int STACK, int WAVES, int TAILN>
 void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
-  if constexpr (WAVES == 7 && REFILL == 32) {
-    if (c.layout != 9 && B.group_tail) {
-      hipLaunchKernelGGL((k_trace2<false, REFILL, STACK, WAVES, TAILN, true>), dim3(256u * 4u * WAVES), dim3(64), 0,
-                         c.stream, S, B, it, iters);
-      return;
-    }
-  }
   static_assert(2 * STACK * 256 + 264 + 4 * 3 * TAILN <= 163840 / (4 * WAVES), "LDS over the occupancy budget");
-  const dim3 grid(256u * 4u * WAVES);
-  if (c.layout == 9)
-    hipLaunchKernelGGL((k_trace2<true, REFILL, STACK, WAVES, TAILN>), grid, dim3(64), 0, c.stream, S, B, it, iters);
-  else
-    hipLaunchKernelGGL((k_trace2<false, REFILL, STACK, WAVES, TAILN>), grid, dim3(64), 0, c.stream, S, B, it, iters);
+  hipLaunchKernelGGL((k_trace2<32, STACK, WAVES, TAILN>), dim3(256u * 4u * WAVES), dim3(64), 0, c.stream, S, B, it,
+                     iters);
 }
+// persistent traversal occupancy (waves/SIMD) -> LDS stack groups per lane
 static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
-  if (c.occ == 8) {
-    if (c.trav == 16) launch_t2<16, 8, 8, 32>(c, S, B, it, iters); else launch_t2<32, 8, 8, 32>(c, S, B, it, iters);
-  } else if (c.occ == 7) {
-    if (c.trav == 16) launch_t2<16, 9, 7, 64>(c, S, B, it, iters); else launch_t2<32, 9, 7, 64>(c, S, B, it, iters);
-  } else if (c.occ == 6) {
-    if (c.trav == 16) launch_t2<16, 11, 6, 64>(c, S, B, it, iters); else launch_t2<32, 11, 6, 64>(c, S, B, it, iters);
-  } else if (c.occ == 5) {
-    if (c.trav == 16) launch_t2<16, 14, 5, 32>(c, S, B, it, iters); else launch_t2<32, 14, 5, 32>(c, S, B, it, iters);
-  } else {
-    if (c.trav == 16) launch_t2<16, 18, 4, 32>(c, S, B, it, iters); else launch_t2<32, 18, 4, 32>(c, S, B, it, iters);
-  }
+  if (c.occ == 8) launch_t2<8, 8, 32>(c, S, B, it, iters);
+  else if (c.occ == 7) launch_t2<9, 7, 64>(c, S, B, it, iters);
+  else if (c.occ == 6) launch_t2<11, 6, 64>(c, S, B, it, iters);
+  else if (c.occ == 5) launch_t2<14, 5, 32>(c, S, B, it, iters);
+  else launch_t2<18, 4, 32>(c, S, B, it, iters);
 }
 
 // one iteration of the merged pipeline: trace P(it) + S(it - 1), resolve P(it - 1), miss + shade P(it)
@@ -466,15 +486,10 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
   return hipGetLastError();
 }
 
-hipError_t launch_wavefront2(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
-                             const WaveBufs& B, float4* out, WaveTimers* tm) {
-  if (B.n == 0) return hipSuccess;
-  hipError_t e = launch_wave_init(c, S, A, M, B, out);
-  if (e != hipSuccess) return e;
-  const uint32_t iters = wave_iters(S.has_diel != 0, A.bounces, A.flags);
-  for (uint32_t it = 0; it <= iters; it++)
-    if ((e = launch_wave2_iter(c, S, A, M, B, out, tm, it)) != hipSuccess) return e;
-  return hipSuccess;
+hipError_t launch_wave_init(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
+                            const WaveBufs& B, float4* out) {
+  hipLaunchKernelGGL(k_wave_init, dim3(256u * 4u), dim3(kBlock), 0, c.stream, S, A, M, B, out);
+  return hipGetLastError();
 }
 
 }  // namespace prt

@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIBPATH = os.path.join(HERE, "libprt.so")
 
 PRT_OK = 0
-ABI_VERSION = 3  # PRT_ABI_VERSION of the include/prt.h these structs mirror
+ABI_VERSION = 4  # PRT_ABI_VERSION of the include/prt.h these structs mirror
 FLAG_AA, FLAG_ACCUMULATE, FLAG_GAMMA, FLAG_NORMALMAP, FLAG_SKYBOX, FLAG_LIGHTED, FLAG_STOCHASTIC = (1 << i for i in range(7))
 FLAGS_DEFAULT = 0x7F
 OUT_DEVICE = 1
@@ -25,8 +25,11 @@ EXPORTS = [
     "prt_camera_look_at", "prt_postfx_preset", "prt_set_postfx", "prt_render", "prt_reset_accumulation", "prt_tile_buffer_pixels", "prt_tile_pixel_map",
     "prt_render_tiles",
     "prt_untile", "prt_trace_primary", "prt_intersect", "prt_occluded", "prt_get_scene_info", "prt_set_bvh_builder",
-    "prt_set_instance_materials", "prt_set_area_lights",
+    "prt_set_instance_materials", "prt_set_area_lights", "prt_shard_unique_id", "prt_shard_init_rccl",
+    "prt_shard_attach_rccl", "prt_create_group", "prt_get_shard_info",
 ]
+SHARD_ID_BYTES = 128
+SHARD_NONE, SHARD_RCCL, SHARD_GROUP = 0, 1, 2  # prt_shard_info.transport
 
 # instance material kinds (prt_set_instance_materials; the reference's dead Scene.cpp:193-205 branches)
 MAT_TEXTURED, MAT_DIELECTRIC, MAT_MIRROR = 0, 1, 2
@@ -83,11 +86,15 @@ class Stats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("shadow_rays", C.c_uint64), ("paths", C.c_uint64), ("ms", C.c_double),
                 ("ms_trace", C.c_double), ("ms_closest", C.c_double), ("ms_anyhit", C.c_double),
                 ("pipeline", C.c_int32), ("iterations", C.c_int32),
-                ("batches", C.c_int32), ("reserved", C.c_int32)]
+                ("batches", C.c_int32), ("ranks", C.c_int32)]
 
 
 class Hit(C.Structure):
     _fields_ = [("t", C.c_float), ("u", C.c_float), ("v", C.c_float), ("prim", C.c_uint32), ("inst", C.c_uint32)]
+
+
+class ShardInfo(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("tile_size", C.c_int32), ("transport", C.c_int32)]
 
 
 class SceneInfo(C.Structure):
@@ -143,6 +150,11 @@ def load():
         "prt_set_bvh_builder": ([vp, i32], C.c_int),
         "prt_set_instance_materials": ([vp, vp, i32], C.c_int),
         "prt_set_area_lights": ([vp, C.POINTER(AreaLight), i32], C.c_int),
+        "prt_shard_unique_id": ([vp], C.c_int),
+        "prt_shard_init_rccl": ([vp, vp, i32, i32, i32], C.c_int),
+        "prt_shard_attach_rccl": ([vp, vp, i32], C.c_int),
+        "prt_create_group": ([C.POINTER(DeviceDesc), i32, i32, C.POINTER(vp)], C.c_int),
+        "prt_get_shard_info": ([vp, C.POINTER(ShardInfo)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -118,17 +118,46 @@ class Scene:
 class Context:
     """One prt_ctx on one HIP device (one process per GPU)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, group=None, tile: int = 32):
+        """group: a list of device ordinals -> one context over several GPUs of this process
+        (prt_create_group: pixel tiles rendered concurrently, gathered on the first device); a device may
+        repeat, which runs several shards on one GPU."""
         L = _lib.load()
         n = C.c_int32(0)
         check(L.prt_device_count(C.byref(n)))
         if n.value <= 0:
             raise _lib.PrtError("no HIP device visible (the product path has no CPU fallback)")
         h = C.c_void_p()
-        check(L.prt_create(C.byref(_lib.DeviceDesc(device, 0)), C.byref(h)))
+        if group is None:
+            check(L.prt_create(C.byref(_lib.DeviceDesc(device, 0)), C.byref(h)))
+        else:
+            devs = (_lib.DeviceDesc * len(group))(*[_lib.DeviceDesc(int(d), 0) for d in group])
+            check(L.prt_create_group(devs, len(group), tile, C.byref(h)))
+            device = int(group[0])
         self.L = L
         self.h = h
         self.device = device
+
+    # -- multi-GPU inside the boundary (include/prt.h, prt_shard_*)
+    @staticmethod
+    def shard_unique_id() -> bytes:
+        """A fresh RCCL id (rank 0 makes it, the caller carries the bytes to the other ranks)."""
+        buf = (C.c_uint8 * _lib.SHARD_ID_BYTES)()
+        check(_lib.load().prt_shard_unique_id(buf))
+        return bytes(buf)
+
+    def shard_rccl(self, uid: bytes, rank: int, world: int, tile: int = 32):
+        """Join the RCCL communicator of `uid` as `rank` of `world`: prt_render then renders this rank's
+        pixel tiles and gathers the frame on rank 0 (one ncclGather per frame, on the context stream)."""
+        if len(uid) != _lib.SHARD_ID_BYTES:
+            raise ValueError("RCCL id must be %d bytes" % _lib.SHARD_ID_BYTES)
+        buf = (C.c_uint8 * _lib.SHARD_ID_BYTES).from_buffer_copy(uid)
+        check(self.L.prt_shard_init_rccl(self.h, buf, rank, world, tile))
+
+    def shard_info(self):
+        si = _lib.ShardInfo()
+        check(self.L.prt_get_shard_info(self.h, C.byref(si)))
+        return si
 
     def close(self):
         if self.h:

@@ -5,7 +5,9 @@ One process per GPU.  Tiles of tile x tile pixels, numbered row-major, go round-
 (rank r: tiles r, r+world, ...).  Every rank renders all samples of its tiles into a compact float4
 buffer [local tile][tile*tile] (prt_render_tiles), the buffers meet on rank 0 in ONE RCCL gather per
 frame, and rank 0 scatters them back into the W x H image (prt_untile).  Pixels are independent, so
-there is no other exchange.
+there is no other exchange.  join_rccl puts all of that inside the context (the RCCL communicator is the
+context's; prt_render does the tile render, the gather and the untile); ShardedFrame is the same frame
+with the gather done by the caller's torch.distributed group.
 """
 from __future__ import annotations
 
@@ -42,16 +44,34 @@ def untile_host(gathered: np.ndarray, width: int, height: int, tile: int) -> np.
     return img
 
 
-class ShardedFrame:
-    """Renders one frame split over a torch.distributed group (backend "nccl" = RCCL on ROCm).
+def join_rccl(ctx, dist, tile: int = 32):
+    """Shard `ctx` over the ranks of a torch.distributed group, inside the boundary: rank 0 makes the RCCL
+    id (prt_shard_unique_id), the group carries its bytes to the other ranks, and every rank's context joins
+    the communicator it then owns (prt_shard_init_rccl).  After this, ctx.render() on every rank renders
+    that rank's tiles and leaves the whole frame in rank 0's outputs."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    box = [ctx.shard_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    ctx.shard_rccl(box[0], rank, world, tile)
+    return ctx.shard_info()
 
-    ctx: this rank's prt.Context (its own GPU); tiles and gathered buffers live on that GPU.
+
+class ShardedFrame:
+    """The caller-side transport: one frame split over a torch.distributed group (prt_render_tiles, one
+    dist.gather to rank 0, prt_untile) -- what a host whose framework owns the collectives uses instead of
+    join_rccl.
+
+    ctx: this rank's prt.Context (its own GPU); tiles and gathered buffers live on that GPU.  On a GPU the
+    context is moved onto torch's current stream, so the gather (queued there by torch) is ordered after
+    the tile render and before the untile.
     render() returns this rank's prt_stats; rank 0's avg/rgb8 device buffers hold the full frame."""
 
     def __init__(self, ctx, dist, width: int, height: int, tile: int = 32, device=None):
         import torch
         self.ctx, self.dist, self.W, self.H, self.tile = ctx, dist, width, height, tile
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        if device is not None and torch.device(device).type == "cuda":
+            ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
         per = tile_buffer_pixels(width, height, tile, self.world)
         self.tiles = torch.zeros((per, 4), dtype=torch.float32, device=device)
         self.gathered = (torch.zeros((self.world, per, 4), dtype=torch.float32, device=device)

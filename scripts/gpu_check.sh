@@ -25,9 +25,9 @@ step() {  # step <name> <timeout> <cmd...>
 if [ "$what" = "tests" ] || [ "$what" = "all" ]; then
   step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
   if [ -n "$kexpr" ]; then
-    step pytest_gpu 1200 python -m pytest tests -m gpu -x -q -k "$kexpr"
+    step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$kexpr"
   else
-    step pytest_gpu 1200 python -m pytest tests -m gpu -q
+    step pytest_gpu 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
   fi
 fi
 if [ "$what" = "bench" ] || [ "$what" = "all" ]; then
@@ -51,6 +51,23 @@ if [ "$what" = "pmc" ]; then
   tag=${3:-pmc}
   step "pmc_$tag" 900 rocprofv3 --pmc $kexpr --output-format csv -d "gpurun_out/pmc_$tag" -o run -- \
     python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline
+fi
+if [ "$what" = "valu" ] || [ "$what" = "prof" ]; then
+  # VALU issue counters of the roofline (scripts/summarize_pmc.py valu): 5 SQ + 1 GRBM counters, one pass
+  export TMPDIR=/tmp
+  step pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES \
+    GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_valu -o run -- \
+    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline
+fi
+if [ "$what" = "calib" ]; then
+  # FETCH_SIZE / WRITE_SIZE against known bytes (scripts/fetch_calibration.hip; scripts/summarize_pmc.py calib)
+  export TMPDIR=/tmp
+  step calib_known 120 scripts/bin/fetch_calibration
+  tail -n 1 gpurun_out/calib_known.log > gpurun_out/calib_known.json
+  step calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib_fetch -o run -- \
+    scripts/bin/fetch_calibration
+  step calib_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/calib_write -o run -- \
+    scripts/bin/fetch_calibration
 fi
 if [ "$what" = "listpmc" ]; then
   step listpmc 300 rocprofv3 -L

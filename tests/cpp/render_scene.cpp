@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -31,7 +32,7 @@ struct Reader {
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    std::fprintf(stderr, "usage: render_scene <scene.bin> <out.bin> <ticks> <bounces> [flags]\n");
+    std::fprintf(stderr, "usage: render_scene <scene.bin> <out.bin> <ticks> <bounces> [flags] [shards]\n");
     return 2;
   }
   try {
@@ -46,7 +47,11 @@ int main(int argc, char** argv) {
     for (float& v : tgt) v = r.get<float>();
     const float aspect = r.get<float>();
 
-    prt::Renderer R(W, H, 0);
+    // shards > 1: one local group of that many tile shards on device 0 (prt_create_group)
+    const int shards = argc > 6 ? std::atoi(argv[6]) : 1;
+    std::unique_ptr<prt::Renderer> owner = shards > 1 ? std::make_unique<prt::Renderer>(W, H, std::vector<int32_t>(shards, 0), 16)
+                                                       : std::make_unique<prt::Renderer>(W, H, 0);
+    prt::Renderer& R = *owner;
     prt::Scene& S = R.scene;
     float* lw = &S.lights.point_pos[0][0];  // prt_lights is 39 consecutive floats
     for (int k = 0; k < 39; k++) lw[k] = r.get<float>();

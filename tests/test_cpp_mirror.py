@@ -27,8 +27,10 @@ def test_cpp_mirror_compiles_and_links(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ext", [False, True])
-def test_cpp_mirror_matches_python_mirror(tmp_path, ext):
+@pytest.mark.parametrize("ext,shards", [(False, 1), (True, 1), (False, 3)])
+def test_cpp_mirror_matches_python_mirror(tmp_path, ext, shards):
+    """shards > 1: the C++ Renderer built over a local group of tile shards (prt_create_group) renders the
+    same frames as the unsharded Python mirror."""
     import prt
     from prt import scenes
     exe = _build(tmp_path)
@@ -37,7 +39,8 @@ def test_cpp_mirror_matches_python_mirror(tmp_path, ext):
         sd = scenes.with_extensions(sd, materials=[0, 1, 2], area_light=scenes.ceiling_light())
     W, H, ticks, bounces = 80, 56, 3, 3
     dump_scene(sd, W, H, str(tmp_path / "scene.bin"))
-    r = subprocess.run([exe, str(tmp_path / "scene.bin"), str(tmp_path / "out.bin"), str(ticks), str(bounces)],
+    r = subprocess.run([exe, str(tmp_path / "scene.bin"), str(tmp_path / "out.bin"), str(ticks), str(bounces),
+                        str(0x7F), str(shards)],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     raw = np.fromfile(str(tmp_path / "out.bin"), np.uint8)

@@ -147,17 +147,11 @@ def test_extensions_tiles_match_full_frame(gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_extensions_refusals(gpu_ctx, monkeypatch):
-    """The extensions run on the merged pipeline only; dielectric path trees beyond the iteration limit
-    are refused, not truncated."""
+def test_extensions_refusals(gpu_ctx):
+    """Dielectric path trees beyond the iteration limit are refused, not truncated."""
     sd = _ext_scene("all")
     W, H = 32, 24
     gpu_scene(gpu_ctx, sd, W, H)
     with pytest.raises(_lib.PrtError):
         gpu_ctx.render(W, H, 2, 6)  # 2 paths x 63 segments > 32 iterations
-    for pipe in ("mega", "wave1", "stream"):
-        monkeypatch.setenv("PRT_PIPELINE", pipe)
-        with pytest.raises(_lib.PrtError):
-            gpu_ctx.render(W, H, 2, 3)
-    monkeypatch.delenv("PRT_PIPELINE")
     gpu_ctx.render(W, H, 2, 3)

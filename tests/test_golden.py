@@ -76,9 +76,7 @@ def test_oracle_trace_matches_golden(oracle_mod):
 # ---------------------------------------------------------------- HIP path (GPU)
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bvh", ["8", "4"])
-def test_gpu_c2_primary_matches_golden(gpu_ctx, monkeypatch, bvh):
-    monkeypatch.setenv("PRT_BVH", bvh)
+def test_gpu_c2_primary_matches_golden(gpu_ctx):
     sd, z = _c2()
     W, H = int(z["W"]), int(z["H"])
     gpu_scene(gpu_ctx, sd, W, H)
@@ -87,9 +85,7 @@ def test_gpu_c2_primary_matches_golden(gpu_ctx, monkeypatch, bvh):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bvh", ["8", "4"])
-def test_gpu_multi_rays_match_golden(gpu_ctx, monkeypatch, bvh):
-    monkeypatch.setenv("PRT_BVH", bvh)
+def test_gpu_multi_rays_match_golden(gpu_ctx):
     sd, z = _multi()
     gpu_scene(gpu_ctx, sd, 64, 64)
     g = gpu_ctx.intersect(z["O"], z["D"])
