@@ -470,9 +470,14 @@ static inline int mt_test(const float* q, f3 O, f3 D, float* t_out, float* u_out
     return 0;
 }
 
+/* Hit rule: closest t; an equal t goes to the smaller instance, then to the LARGER prim.  tinybvh's BVH8_CPU leaf
+ * keeps the highest lane among equal minima (Core/tiny_bvh.h:6436, __bfind of the equality mask) and its leaves
+ * hold primitives in ascending order, so the two triangles of a quad tied on their shared edge resolve to the
+ * larger index, as here; ties across leaves (first found there, :6440 strict <) remain BVH-dependent (about 2 rays
+ * per million on C4, tests/golden/make_golden.py).  The rule is order-independent, so any BVH gives the same hit. */
 static inline int better(float t, uint32_t inst, uint32_t prim, const hit_t* h) {
     if (t < h->t) return 1;
-    if (t == h->t && (inst < h->inst || (inst == h->inst && prim < h->prim))) return 1;
+    if (t == h->t && (inst < h->inst || (inst == h->inst && prim > h->prim))) return 1;
     return 0;
 }
 

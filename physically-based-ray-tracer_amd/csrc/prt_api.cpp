@@ -399,7 +399,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   c->last_iters = iters;
   c->last_timers = timers;
-  c->last_paths = (uint64_t)M.items * (uint64_t)F * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
+  c->last_paths = tile_image_pixels(M) * (uint64_t)F * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
   return PRT_OK;
 }
 

@@ -38,6 +38,18 @@ __host__ __device__ inline bool item_pixel(const TileMap& m, uint32_t r, int32_t
   return px < m.W && py < m.H;
 }
 
+// pixels of the image inside rank's tiles (items minus the overhang of partial tiles at the right / bottom edge)
+inline uint64_t tile_image_pixels(const TileMap& m) {
+  uint64_t n = 0;
+  for (int32_t lt = 0; lt < m.local_tiles; lt++) {
+    const int32_t g = m.rank + lt * m.world, gx = g % m.tiles_x, gy = g / m.tiles_x;
+    const int32_t w = m.W - gx * m.ts < m.ts ? m.W - gx * m.ts : m.ts;
+    const int32_t h = m.H - gy * m.ts < m.ts ? m.H - gy * m.ts : m.ts;
+    n += (uint64_t)w * (uint64_t)h;
+  }
+  return n;
+}
+
 struct TraceArgs {
   int32_t W, H;
   int32_t bounces;

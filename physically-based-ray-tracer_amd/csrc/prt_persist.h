@@ -12,7 +12,7 @@
 //   triangle   lanes with pending leaf triangles test one of them (Moeller-Trumbore, prt_traverse.h)
 // so node visits and triangle tests of different lanes share iterations instead of serialising.
 // Results are those of blas_traverse8: the hit rule is order-independent (closest t, then smaller
-// (instance, prim)) and the box tests are conservative, so visiting order cannot change a hit.
+// instance, then larger prim) and the box tests are conservative, so visiting order cannot change a hit.
 //
 // Cooperative tail (tail != nullptr).  Once the queue is drained a launch lasts as long as its slowest
 // rays: a lone wave still spends ~0.5-1 us per iteration (a wave64 node visit is ~220 VALU), and the
@@ -160,7 +160,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
         return true;
       }
     } else if (hit && (t < h.t || (t == h.t && ((uint32_t)inst < h.inst ||
-                                                ((uint32_t)inst == h.inst && prim < h.prim))))) {
+                                                ((uint32_t)inst == h.inst && prim > h.prim))))) {
       h.t = t; h.u = u; h.v = v; h.prim = prim; h.inst = (uint32_t)inst;
       found = true;
     }
@@ -228,7 +228,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     // tstate: helpers still walking (low 16 bits) | any-hit: some team lane hit (kFoundBit)
     constexpr uint32_t kFoundBit = 1u << 16;
     uint32_t* tstate = tail;
-    unsigned long long* tkey = reinterpret_cast<unsigned long long*>(tail + TAILN);  // best (t, prim)
+    unsigned long long* tkey = reinterpret_cast<unsigned long long*>(tail + TAILN);  // best (t, ~prim)
     bool helper = false;
     uint32_t slot = (uint32_t)__popcll(__ballot(active) & lanes_below);
     if (active) {
@@ -241,9 +241,9 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       const unsigned long long k = tkey[slot];
       tkey[slot] = ~0ull;
       const float kt = __uint_as_float((uint32_t)(k >> 32));
-      const uint32_t kp = (uint32_t)k;
+      const uint32_t kp = ~(uint32_t)k;  // the key holds ~prim: the larger prim wins an equal t
       if (k != ~0ull && (kt < h.t || (kt == h.t && ((uint32_t)inst < h.inst ||
-                                                   ((uint32_t)inst == h.inst && kp < h.prim))))) {
+                                                   ((uint32_t)inst == h.inst && kp > h.prim))))) {
         const uint32_t g = S.stri[S.mesh[S.inst[inst].mesh].prim_base + kp].pad[0];
         float t, u, v;
         uint32_t prim;
@@ -258,7 +258,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       bool busy = member && (node != kNoNode || lhit != 0 || tcnt != 0);
       // ---- helpers done with their subtree: publish, leave the team
       if (helper && !busy) {
-        if (!any && found) atomicMin(&tkey[slot], ((unsigned long long)__float_as_uint(h.t) << 32) | h.prim);
+        if (!any && found) atomicMin(&tkey[slot], ((unsigned long long)__float_as_uint(h.t) << 32) | (~h.prim & 0xFFFFFFFFull));
         atomicSub(&tstate[slot], 1u);
         helper = false;
       }

@@ -5,8 +5,10 @@
 //
 // Hit rule (identical in the oracle): Moeller-Trumbore exactly as the BVH8_CPU leaf lane math
 // (:6412-6440; det eps 1e-6, u in [0,1], v >= 0, u+v <= 1, t > 0; any-hit adds t < tmax), closest
-// t wins and equal t is broken by the smaller (instance, prim).  Box tests are conservative
-// (inflated boxes, padded slab interval), so the result does not depend on the BVH's shape.
+// t wins; an equal t goes to the smaller instance, then to the LARGER prim -- what BVH8_CPU's leaf does with
+// the two triangles of a quad sharing an edge (:6436 __bfind keeps the highest lane among equal minima, and
+// the leaves hold primitives in ascending order).  Box tests are conservative (inflated boxes, padded slab
+// interval), so the result does not depend on the BVH's shape.
 //
 // Shared pieces of the traversal kernels: ray / hit records, the leaf test, the instance-box slab.
 #pragma once

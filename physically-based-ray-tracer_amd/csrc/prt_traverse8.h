@@ -82,7 +82,7 @@ __device__ __forceinline__ bool blas_traverse8(const Node8* __restrict__ nodes, 
           if (mt_test(tris + first + i, O, D, t, u, v, prim)) {
             if (ANY) {
               if (t < h.t) return true;  // tiny_bvh.h:6594 (h.t holds tmax)
-            } else if (t < h.t || (t == h.t && (inst < h.inst || (inst == h.inst && prim < h.prim)))) {
+            } else if (t < h.t || (t == h.t && (inst < h.inst || (inst == h.inst && prim > h.prim)))) {
               h.t = t; h.u = u; h.v = v; h.prim = prim; h.inst = inst;
             }
           }

@@ -202,6 +202,14 @@ def load_model(path: str) -> Mesh:
         UV[:, 1] = np.float32(1.0) - UV[:, 1]  # aiProcess_FlipUVs
     else:
         UV = np.zeros((n, 2), F32)
+    return mesh_from_indexed(P, N, UV, tri)
+
+
+def mesh_from_indexed(P: np.ndarray, N: np.ndarray, UV: np.ndarray, tri: np.ndarray) -> Mesh:
+    """Model's arrays (Core/Model.cpp:25-119) from indexed float32 positions / normals / (flipped) UVs and
+    (T, 3) corner indices: fat corners in face order, face normals = tmpl8 normalize(cross(e1, e2))."""
+    P, N, UV = (np.ascontiguousarray(a, F32) for a in (P, N, UV))
+    tri = np.asarray(tri, np.int64).reshape(-1, 3)
     T = tri.shape[0]
     corner = tri.reshape(-1)
     triangles = np.zeros((3 * T, 4), F32)

@@ -44,6 +44,7 @@ def test_group_matches_single(gpu_ctx, world, post):
         g.set_postfx(pf)
         a, r, st = g.render(W, H, 4, 3)
         assert np.array_equal(a, a_full) and np.array_equal(r, r_full)
+        assert s_full.paths == W * H * 4  # camera paths of in-image pixels only (not the tiles' overhang)
         assert (st.segments, st.shadow_rays, st.paths) == (s_full.segments, s_full.shadow_rays, s_full.paths)
         assert st.ranks == world
         a2, r2, _ = g.render(W, H, 4, 3, frame_index=2)
