@@ -294,8 +294,9 @@ def main():
             roof = {"bound": "valu", "achieved": round(valu_rate, 1), "peak": VALU_PEAK_GINST,
                     "unit": "G VALU wave-instructions/s", "frac": round(valu_rate / VALU_PEAK_GINST, 4),
                     "traffic": traffic, "valu_insts_per_launch": int(valu["SQ_INSTS_VALU"]), "source": valu_src}
-            if "valu_busy" in valu:
-                roof["valu_busy_pmc"] = round(valu["valu_busy"], 4)
+            if "valu_busy" in valu:  # SQ_ACTIVE_INST_VALU x 4 / SIMD cycles: waves with a VALU instruction in
+                # flight (a lone wave holds its SIMD 4 cycles per instruction), not the 2-cycle issue peak above
+                roof["wave_valu_active_pmc"] = round(valu["valu_busy"], 4)
         else:  # no VALU pass for this config: price the measured HBM bytes (or nothing)
             roof = {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": hbm["frac"], "traffic": traffic}
@@ -305,7 +306,8 @@ def main():
             "algorithmic_bytes_per_launch": round(ref_bytes),
             "reference_layout_equiv_GBps": round(ref_bytes / (kern_ms / 1e3) / 1e9, 1),
             "own_layout_GBps": round(own_bytes / (kern_ms / 1e3) / 1e9, 1) if own_bytes else None,
-            "basis": "frac = PMC-measured VALU issue rate over the VALU issue peak (the kernel is VALU-bound); "
+            "basis": "frac = PMC-measured VALU wave-instructions (SQ_INSTS_VALU) per second over the issue peak "
+                     "(1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction, MI355X_MICROARCH.md); "
                      "hbm = PMC-measured HBM bytes over the HBM peak; reference_layout_equiv_GBps = SURVEY 8d "
                      "bytes in the reference's BVH8_CPU layout over the launch time (not HBM traffic)",
             "bytes_per_ray": {k: round(v, 1) for k, v in bpr.items()},

@@ -209,8 +209,10 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
         active = false;
       }
     }
-    // ---- one node visit for lanes without pending triangles
-    if (active && node != kNoNode && lhit == 0 && tcnt == 0) node_step();
+    // ---- one node visit for lanes whose leaf children have all been started: the remaining triangles of
+    // the current leaf (tcur, tcnt) are tested alongside the next node visits (order-independent hit rule;
+    // measured 1.5-2.5 % faster per launch on C4 than waiting for the leaf to finish)
+    if (active && node != kNoNode && lhit == 0) node_step();
     // ---- one triangle test for lanes with pending leaf triangles
     if (active && (lhit | tcnt)) {
       if (tri_step()) {
