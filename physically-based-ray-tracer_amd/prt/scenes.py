@@ -274,3 +274,22 @@ def config_c1(root: str = REFERENCE_ROOT) -> SceneData:
 
 
 C1_FLAGS = 0x7F & ~(1 << 4) & ~(1 << 0)  # reference defaults without SKYBOX (C1) and AA (1 spp)
+
+
+def config_spaceship(root: str = REFERENCE_ROOT) -> SceneData:
+    """The reference's textured Spaceship (Core/assets/prefabs/models/Spaceship: 12,490 triangles, 1024x1024
+    albedo / normal / metalness PNGs, Core/Model.cpp:183-204) as scene1's model 0: the XShip game object
+    (~pi about Y) plus a second, untransformed copy beside it (a two-instance TLAS), the C3/C4 lights and sky,
+    a camera framing both ships.  Needs the reference's asset files (`root`); tests use the committed
+    fixture tests/golden/spaceship.npz made from it."""
+    from . import ingest
+    model = os.path.join(root, "Core", "assets", "prefabs", "models", "Spaceship", "Spaceship.gltf")
+    if not os.path.exists(model):
+        raise FileNotFoundError(f"the Spaceship scene needs the reference assets ({model})")
+    sd = ingest.load_scene([model], os.path.join(root, "assets", "scene1"),
+                           os.path.join(root, "Core", "assets", "prefabs", "camera.json"), name="spaceship-textured")
+    beside = IDENTITY.copy()
+    beside[0, 3], beside[2, 3] = 0.6, 0.2
+    return dataclasses.replace(sd, instances=sd.instances + [(0, beside)], lights=scene1_lights(),
+                               sky=procedural_sky(), cam_pos=np.array([0.55, 0.3, -0.75], F32),
+                               cam_target=np.array([0.3, -0.02, 0.0], F32))

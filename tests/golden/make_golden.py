@@ -18,9 +18,12 @@ The headline configs, through the same reference traversal (`make_golden.py ref`
   c2_ref_1280x720.npz  C2 primary rays at the full 1280x720: prim per pixel, digests of t / u / v
   c1_scene1.npz        C1 as data (the SciFiHelmet arrays the ingest reads from the reference's glTF, scene1's
                        instance / lights / camera, stand-in maps) + its 256x256 1 spp depth-1 renders
+  spaceship.npz        the textured Spaceship (scenes.config_spaceship) as data -- indexed mesh arrays, the three
+                       1024x1024 maps as decoded texels, two instances, lights, sky, camera -- plus its
+                       reference-traversal renders at 160x160: shaded (4 spp, depth 3), albedo and shading-normal views
 Every fixture records a digest of the scene arrays it was made from, so a change of scenes.py is caught.
 
-usage: python tests/golden/make_golden.py [small] [ref]
+usage: python tests/golden/make_golden.py [small] [ref] [ship]
 """
 import hashlib
 import os
@@ -204,6 +207,49 @@ def c1_scene1():
     return {k: v.tolist() for k, v in out.items() if k.endswith("counts")}
 
 
+SHIP_RENDERS = (("shaded", 0, 4, 3), ("albedo", 1, 1, 1), ("normal", 3, 1, 1))
+SHIP_WH = 160
+
+
+def indexed(m):
+    """(P, N, UV, tri) of a Mesh whose corners were expanded from an indexed model (ingest.mesh_from_indexed)."""
+    P = m.vertices.reshape(-1, 3)
+    tri = m.indices.reshape(-1, 3)
+    N = np.zeros_like(P)
+    UV = np.zeros((P.shape[0], 2), np.float32)
+    N[m.indices] = m.fixed_normals.reshape(-1, 4)[:, :3]
+    UV[m.indices] = m.fixed_uvs.reshape(-1, 2)
+    return P, N, UV, tri
+
+
+def spaceship():
+    """The textured Spaceship scene as data, and its reference-traversal renders (SHIP_RENDERS)."""
+    sd = scenes.config_spaceship()
+    m = sd.meshes[0]
+    P, N, UV, tri = indexed(m)
+    from prt import ingest
+    m2 = ingest.mesh_from_indexed(P, N, UV, tri)
+    for f in ("triangles", "fixed_normals", "fixed_uvs", "indices", "vertices", "face_normals"):
+        assert np.array_equal(getattr(m, f), getattr(m2, f)), f
+    W = H = SHIP_WH
+    out = {}
+    for name, mode, spp, bounces in SHIP_RENDERS:
+        avg, rgb8, _, st = _ref_render(sd, W, H, spp, bounces, mode=mode)
+        out[f"{name}_avg"] = avg[:, :3].copy()
+        out[f"{name}_rgb8"] = rgb8
+        out[f"{name}_counts"] = np.array([st.segments, st.shadow_rays], np.int64)
+    L = sd.lights
+    np.savez_compressed(os.path.join(HERE, "spaceship.npz"), P=P, N=N, UV=UV, tri=tri.astype(np.int32),
+                        albedo=m.albedo, normal=m.normal, metalness=m.metalness, emission=m.emission,
+                        tex0=sd.textures[0], tex1=sd.textures[1], tex2=sd.textures[2],
+                        xf=np.stack([x for _, x in sd.instances]).astype(np.float32),
+                        xf_mesh=np.array([mi for mi, _ in sd.instances], np.int32),
+                        point_pos=L.point_pos, point_col=L.point_col, dir_pos=L.dir_pos, dir_col=L.dir_col,
+                        spot_pos=L.spot_pos, spot_col=L.spot_col, spot_rot=L.spot_rot, sky=sd.sky,
+                        cam_pos=sd.cam_pos, cam_target=sd.cam_target, W=W, H=H, digest=scene_digest(sd), **out)
+    return {k: v.tolist() for k, v in out.items() if k.endswith("counts")}
+
+
 def main():
     if oracle.reflib() is None:
         sys.exit("oracle/_ref/libref_tinybvh.so is missing: run `make -C oracle ref` where /root/reference exists")
@@ -217,6 +263,8 @@ def main():
         print("c3_ref rays", c3_ref())
         print("c2_ref_full hits", c2_ref_full())
         print("c1_scene1", c1_scene1())
+    if "ship" in which or "ref" in which:
+        print("spaceship", spaceship())
 
 
 if __name__ == "__main__":

@@ -1,6 +1,7 @@
 """The headline configs pinned to the reference's own traversal (tests/golden/make_golden.py `ref`): frames rendered
 by the restated Trace on tinybvh v1.4.2's BVH8_CPU + TLAS (compiled unmodified from /root/reference into oracle/_ref),
-committed as data.  C4 and C3 are the BASELINE workloads, C2 the primary-ray config, C1 scene1's SciFiHelmet.
+committed as data.  C4 and C3 are the BASELINE workloads, C2 the primary-ray config, C1 scene1's SciFiHelmet, and
+the textured Spaceship (1024x1024 albedo / normal / metalness maps) the real-asset case of the ingest row.
 
 Bar (BASELINE.json north star): per-channel RMSE <= 1e-4 against the reference-traversal image, identical ray
 counts.  The remaining differences are tinybvh's BVH-dependent choices (an exact-t tie across two leaves goes to
@@ -13,9 +14,9 @@ import numpy as np
 import pytest
 
 import oracle
-from golden.make_golden import C1_RENDERS, c1_lit, scene_digest
+from golden.make_golden import C1_RENDERS, SHIP_RENDERS, c1_lit, scene_digest
 from helpers import RMSE_TOL, gpu_scene, rmse
-from prt import ingest, scenes
+from prt import _lib, ingest, scenes
 from prt.scenes import Lights, SceneData
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -55,7 +56,27 @@ def c1_scene():
     return sd, z
 
 
+def ship_scene():
+    """SceneData of the textured Spaceship rebuilt from the committed fixture (no reference tree needed)."""
+    z = np.load(os.path.join(GOLDEN, "spaceship.npz"))
+    m = ingest.mesh_from_indexed(z["P"], z["N"], z["UV"], z["tri"])
+    m.albedo, m.normal, m.metalness, m.emission = (int(z[k]) for k in ("albedo", "normal", "metalness", "emission"))
+    tex = [z[f"tex{i}"] for i in range(3)]
+    L = Lights(z["point_pos"], z["point_col"], z["dir_pos"], z["dir_col"], z["spot_pos"], z["spot_col"], z["spot_rot"])
+    inst = [(int(mi), x) for mi, x in zip(z["xf_mesh"], z["xf"])]
+    sd = SceneData([m], tex, inst, L, z["sky"], z["cam_pos"], z["cam_target"], "spaceship-textured")
+    assert scene_digest(sd) == str(z["digest"])
+    return sd, z
+
+
 # ---------------------------------------------------------------- fixtures vs the reference asset tree (CPU)
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(scenes.REFERENCE_ROOT, "Core", "assets")),
+                    reason="reference asset tree absent")
+def test_spaceship_fixture_is_the_ingested_scene():
+    sd, _ = ship_scene()
+    assert scene_digest(sd) == scene_digest(scenes.config_spaceship())
+    assert all(t.shape == (1024, 1024) for t in sd.textures) and sd.meshes[0].tri_count == 12490
 
 @pytest.mark.skipif(not os.path.exists(os.path.join(scenes.REFERENCE_ROOT, "Core", "assets")),
                     reason="reference asset tree absent")
@@ -79,6 +100,19 @@ def test_oracle_c1_matches_reference_traversal(oracle_mod):
         assert err <= RMSE_TOL
         assert [st.segments, st.shadow_rays] == z[f"{variant}{mode}_counts"].tolist()
     assert z["lit0_avg"].max() > 0 and z["shipped1_avg"].max() > 0  # non-black images are part of the pin
+
+
+def test_oracle_spaceship_matches_reference_traversal(oracle_mod):
+    sd, z = ship_scene()
+    W, H = int(z["W"]), int(z["H"])
+    for name, mode, spp, bounces in SHIP_RENDERS:
+        osc = oracle_mod.OracleScene(sd, W, H)
+        avg, rgb8, _, st = osc.render(W, H, spp=spp, bounces=bounces, mode=mode, nthreads=THREADS)
+        err, _ = _report(f"Spaceship {name}", z[f"{name}_avg"], avg)
+        assert err <= RMSE_TOL
+        assert [st.segments, st.shadow_rays] == z[f"{name}_counts"].tolist()
+    # the albedo view samples the ship's texture: many distinct colours, not a stand-in map
+    assert len(np.unique(z["albedo_rgb8"])) > 1000
 
 
 def test_oracle_c3_matches_reference_traversal(oracle_mod):
@@ -131,6 +165,22 @@ def test_gpu_c1_matches_reference_traversal(gpu_ctx):
         err, _ = _report(f"GPU C1 {variant} mode {mode}", z[f"{variant}{mode}_avg"], avg)
         assert err <= RMSE_TOL
         assert [st.segments, st.shadow_rays] == z[f"{variant}{mode}_counts"].tolist()
+
+
+@pytest.mark.gpu
+def test_gpu_spaceship_matches_reference_traversal(gpu_ctx):
+    """The textured Spaceship (two instances, 1024x1024 maps) through libprt.so: shaded, albedo, shading normal."""
+    sd, z = ship_scene()
+    W, H = int(z["W"]), int(z["H"])
+    gpu_scene(gpu_ctx, sd, W, H)
+    for name, mode, spp, bounces in SHIP_RENDERS:
+        gpu_ctx.reset_accumulation(full=True)
+        flags = _lib.FLAGS_DEFAULT if spp > 1 else _lib.FLAGS_DEFAULT & ~_lib.FLAG_AA  # 1 spp: AA off (SURVEY 8d)
+        avg, rgb8, st = gpu_ctx.render(W, H, spp, bounces, flags=flags, mode=mode)
+        err, exact = _report(f"GPU Spaceship {name}", z[f"{name}_avg"], avg)
+        assert err <= RMSE_TOL
+        assert [st.segments, st.shadow_rays] == z[f"{name}_counts"].tolist()
+        assert np.mean(rgb8 == z[f"{name}_rgb8"]) > 0.999
 
 
 @pytest.mark.gpu
