@@ -288,7 +288,7 @@ typedef struct {
     int32_t triangles;
     double  build_ms;       /* wall time of the last prt_set_meshes (BLAS builds + uploads) */
     int32_t builder;        /* PRT_BUILDER_* used by the last prt_set_meshes */
-    int32_t pad;
+    int32_t tlas_depth;     /* levels of the instance BVH the rays walk (0: instances tested as a linear list) */
 } prt_scene_info;
 int prt_get_scene_info(prt_ctx* ctx, prt_scene_info* info);
 

@@ -394,4 +394,27 @@ BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf) {
   return out;
 }
 
+BuiltTlas8 build_tlas8(const float* boxes, int32_t n) {
+  // each instance box as a degenerate "triangle" {lo, hi, lo}: its bounds are the box, its centroid the box centre
+  std::vector<float> fat(12 * (size_t)n, 0.0f);
+  for (int32_t i = 0; i < n; i++) {
+    const float* b = boxes + 6 * (size_t)i;
+    float* t = fat.data() + 12 * (size_t)i;
+    for (int k = 0; k < 3; k++) { t[k] = b[k]; t[4 + k] = b[3 + k]; t[8 + k] = b[k]; }
+  }
+  BuiltBlas8 w;
+  build_wide8<Node8, Fmt8>(fat.data(), n, 1, w);
+  BuiltTlas8 out;
+  out.depth = w.depth;
+  out.nodes = std::move(w.nodes);
+  out.slot.assign(8 * out.nodes.size(), 0xFFFFFFFFu);
+  for (size_t j = 0; j < out.nodes.size(); j++) {
+    Node8& nd = out.nodes[j];
+    for (int s = 0; s < 8; s++)
+      if (!((nd.imask >> s) & 1u) && nd.meta[s]) out.slot[8 * j + s] = w.tris[nd.tri_base + (nd.meta[s] >> 3)].prim;
+    nd.tri_base = (uint32_t)(8 * j);
+  }
+  return out;
+}
+
 }  // namespace prt

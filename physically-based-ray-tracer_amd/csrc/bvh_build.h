@@ -47,6 +47,17 @@ struct BuiltBlas8 {
 };
 BuiltBlas8 build_blas8(const float* triangles, int32_t tri_count, int max_leaf = 3);
 
+// ---- TLAS over instance world boxes (replaces BVH::Build over BLASInstances, Core/tiny_bvh.h:1732-1770): the same
+// binned SAH + SAH-optimal 8-wide collapse with one instance per leaf slot.  A TLAS node's leaf slot s names its
+// instance in slot[8 * node + s] (node.tri_base = 8 * node), so the traversal addresses an instance group like an
+// interior group: base + slot.
+struct BuiltTlas8 {
+  std::vector<Node8> nodes;     // node 0 = root
+  std::vector<uint32_t> slot;   // 8 per node: instance id of each leaf slot (0xFFFFFFFF elsewhere)
+  int depth = 0;
+};
+BuiltTlas8 build_tlas8(const float* boxes, int32_t n);  // boxes: n x {lo[3], hi[3]} world AABBs (inflated)
+
 // Same inflation rule the traversal relies on (see bvh_build.cpp).
 void inflate_box(float* lo, float* hi);
 

@@ -105,6 +105,11 @@ struct prt_ctx {
   std::vector<uint32_t> inst_kind;  // prt_set_instance_materials (PRT_MAT_*), textured by default
   std::vector<InstSrc> inst_stage;  // host side of the refit input (prt_refit.h)
   DevBuf inst, inst_src;
+  // instance BVH (more than kLinearInstances instances, or PRT_TLAS=1): rebuilt on the host with the instances
+  bool use_tlas = false;
+  int tlas_depth = 0;
+  BuiltTlas8 tlas_host;
+  DevBuf tlas8, tlas_slot;
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
   float al[16] = {};
   int32_t area = 0, area_two_sided = 0;
@@ -149,7 +154,10 @@ namespace {
 // The LDS traversal stacks hold one group per tree level below the root: up to 16 levels (18 groups at
 // 4 waves/SIMD, 16 in the query kernels)
 constexpr int kMaxBvhDepth = 16;
-bool depth_ok(const prt_ctx* c) { return c->max_depth <= kMaxBvhDepth; }
+// tree levels one lane's stack must cover: the deepest BLAS, plus the instance BVH's levels when it is walked
+// (its groups sit below the BLAS's: at most one per TLAS level, the last one the remaining instances of a leaf)
+int stack_depth(const prt_ctx* c) { return c->max_depth + (c->use_tlas ? c->tlas_depth : 0); }
+bool depth_ok(const prt_ctx* c) { return stack_depth(c) <= kMaxBvhDepth; }
 
 // finish the frames queued on the context stream before a setter overwrites (or frees) resident buffers
 int drain(prt_ctx* c) {
@@ -163,10 +171,11 @@ int drain(prt_ctx* c) {
 int occ_for(const prt_ctx* c) {
   const char* e = std::getenv("PRT_OCC");
   int want = e ? std::atoi(e) : 7;
-  if (want >= 8 && c->max_depth <= 9) return 8;
-  if (want >= 7 && c->max_depth <= 10) return 7;
-  if (want >= 6 && c->max_depth <= 12) return 6;
-  if (want >= 5 && c->max_depth <= 15) return 5;
+  const int d = stack_depth(c);
+  if (want >= 8 && d <= 9) return 8;
+  if (want >= 7 && d <= 10) return 7;
+  if (want >= 6 && d <= 12) return 6;
+  if (want >= 5 && d <= 15) return 5;
   return 4;
 }
 
@@ -188,10 +197,42 @@ int ensure_instances(prt_ctx* c) {
     s.mesh = m;
     s.kind = i < (int32_t)c->inst_kind.size() ? c->inst_kind[i] : 0u;
   }
-  HIP_TRY(c->inst.ensure(sizeof(InstDev) * kMaxInstances));
-  HIP_TRY(c->inst_src.ensure(sizeof(InstSrc) * kMaxInstances));
+  // buffers sized for n (at least the linear-list size); growing them frees what queued frames read: drain first
+  const size_t cap = (size_t)std::max(n, kLinearInstances);
+  if (c->inst.bytes < sizeof(InstDev) * cap || c->inst_src.bytes < sizeof(InstSrc) * cap) {
+    const int rc = drain(c);
+    if (rc) return rc;
+    HIP_TRY(c->inst.ensure(sizeof(InstDev) * cap));
+    HIP_TRY(c->inst_src.ensure(sizeof(InstSrc) * cap));
+  }
   HIP_TRY(hipMemcpyAsync(c->inst_src.p, src.data(), sizeof(InstSrc) * n, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(launch_refit(c->stream, c->inst_src.as<InstSrc>(), n, c->inst.as<InstDev>()));
+  // instance BVH over the refit's world boxes (the same refit_instance on the host), BVH::Build over the
+  // BLASInstances every frame as the reference does (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770)
+  const char* te = std::getenv("PRT_TLAS");
+  c->use_tlas = n > kLinearInstances || (te && std::atoi(te) == 1);
+  if (c->use_tlas) {
+    std::vector<float> boxes(6 * (size_t)n);
+    for (int32_t i = 0; i < n; i++) {
+      InstDev I;
+      refit_instance(src[i], I);
+      std::memcpy(&boxes[6 * (size_t)i], I.bmin, 12);
+      std::memcpy(&boxes[6 * (size_t)i + 3], I.bmax, 12);
+    }
+    c->tlas_host = build_tlas8(boxes.data(), n);
+    c->tlas_depth = c->tlas_host.depth;
+    const size_t nb = c->tlas_host.nodes.size() * sizeof(Node8), sb = c->tlas_host.slot.size() * 4;
+    if (c->tlas8.bytes < nb || c->tlas_slot.bytes < sb) {
+      const int rc = drain(c);
+      if (rc) return rc;
+      HIP_TRY(c->tlas8.ensure(nb));
+      HIP_TRY(c->tlas_slot.ensure(sb));
+    }
+    HIP_TRY(hipMemcpyAsync(c->tlas8.p, c->tlas_host.nodes.data(), nb, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->tlas_slot.p, c->tlas_host.slot.data(), sb, hipMemcpyHostToDevice, c->stream));
+  } else {
+    c->tlas_depth = 0;
+  }
   c->inst_dirty = false;
   return PRT_OK;
 }
@@ -199,7 +240,6 @@ int ensure_instances(prt_ctx* c) {
 int scene_ready(prt_ctx* c, SceneDev& S) {
   if (c->mesh_host.empty()) return fail(PRT_ERR_NOT_READY, "no meshes: call prt_set_meshes");
   if (c->inst_mesh.empty()) return fail(PRT_ERR_NOT_READY, "no instances: call prt_set_instances");
-  if ((int)c->inst_mesh.size() > kMaxInstances) return fail(PRT_ERR_UNSUPPORTED, "more than 64 instances");
   int rc = ensure_instances(c);
   if (rc) return rc;
   std::memset(&S, 0, sizeof(S));
@@ -213,6 +253,18 @@ int scene_ready(prt_ctx* c, SceneDev& S) {
   S.mesh = c->mesh.as<MeshDev>();
   S.sky = (c->skyw > 0) ? c->sky.as<float>() : nullptr;
   S.ninst = (int32_t)c->inst_mesh.size();
+  S.tlas = c->use_tlas ? 1 : 0;
+  S.tlas8 = c->use_tlas ? c->tlas8.as<Node8>() : nullptr;
+  S.tlas_slot = c->use_tlas ? c->tlas_slot.as<uint32_t>() : nullptr;
+  {  // packed hit word: prim bits for the largest mesh, instance bits above
+    uint32_t maxt = 1;
+    for (const MeshDev& m : c->mesh_host) maxt = std::max(maxt, m.tri_count);
+    uint32_t pb = 1, ib = 0;
+    while (pb < 32 && (1ull << pb) < maxt) pb++;
+    while ((1ull << ib) < (uint64_t)S.ninst) ib++;
+    if (pb + ib > 32) return fail(PRT_ERR_UNSUPPORTED, "mesh size x instance count exceed the 32-bit hit word");
+    S.pbits = pb;
+  }
   S.skyw = c->skyw;
   S.skyh = c->skyh;
   const prt_lights& L = c->lights;
@@ -831,7 +883,7 @@ int prt_set_bvh_builder(prt_ctx* c, int32_t builder) {
 
 int prt_set_instances(prt_ctx* c, const float* xf, const uint32_t* mi, int32_t n) {
   if (!c || !xf || !mi || n <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad instances");
-  if (n > kMaxInstances) return fail(PRT_ERR_UNSUPPORTED, "more than 64 instances");
+  if (n > kMaxInstances) return fail(PRT_ERR_UNSUPPORTED, "more than 2^24 instances");
   c->inst_xf.assign(xf, xf + 16 * (size_t)n);
   if ((size_t)n != c->inst_mesh.size()) c->inst_kind.clear();  // materials survive transform updates only
   c->inst_mesh.assign(mi, mi + n);
@@ -1249,6 +1301,7 @@ int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
     info->triangles += m.tris;
   }
   info->max_depth = c->max_depth;
+  info->tlas_depth = c->use_tlas ? c->tlas_depth : 0;
   info->build_ms = c->build_ms;
   info->builder = c->built_with;
   info->device_bytes = (int64_t)(c->nodes8.bytes + c->tris.bytes + c->stri.bytes + c->texels.bytes + c->sky.bytes +

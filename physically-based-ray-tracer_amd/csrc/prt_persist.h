@@ -32,6 +32,7 @@
 namespace prt {
 
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
+constexpr uint32_t kInstGroup = 0x100u;  // gimask flag: the group's children are instances (TLAS walk)
 // a drained wave with at most TAILN rays turns cooperative; its LDS: TAILN x {count | found << 16, key lo, key hi}
 constexpr uint32_t tail_lds_words(int tailn) { return 3u * (uint32_t)tailn; }
 
@@ -59,8 +60,8 @@ __device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
 // tail: tail_lds_words(TAILN) words of LDS for the cooperative tail, or nullptr (no tail mode).
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
-template <int MODE, int STACK, int REFILL, int TAILN = 32, class Fetch, class Load, class Reload, class Finish,
-          class Tick>
+template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, class Fetch, class Load, class Reload,
+          class Finish, class Tick>
 __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                    Load load, Reload reload, Finish finish, Tick tick,
                                                    uint32_t* __restrict__ tail = nullptr) {
@@ -79,27 +80,54 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   uint32_t* st = stk;  // the LDS stack column this lane walks with
   uint32_t lhit = 0, ltri = 0, lmeta0 = 0, lmeta1 = 0, tcur = 0, tcnt = 0;  // pending leaf triangles
   bool found = false;  // tail: this lane improved its closest hit
-  // enter the first instance >= i0 whose world box the ray hits before h.t (tiny_bvh.h:2500-2565 TLAS
-  // walk as a linear loop over <= 64 instance boxes); false when there is none
-  auto enter = [&](int i0, const V3& Ow, const V3& Dw) -> bool {
-    const V3 rDw = v3(safercp(Dw.x), safercp(Dw.y), safercp(Dw.z));
-    int i = i0;
-    while (i < S.ninst && slab1(S.inst[i].bmin, S.inst[i].bmax, Ow, rDw, h.t) >= kFar) i++;
-    if (i >= S.ninst) return false;
-    const InstDev& I = S.inst[i];
-    inst = i;
-    O = xform_point(Ow, I.inv);
-    D = xform_vector(Dw, I.inv);
+  // TLAS walk (TLAS = true): O / D / rD / oct hold the world ray while inst < 0 and the instance ray while
+  // inst >= 0.  Groups of the instance BVH sit on the same LDS stack below those of the BLAS being walked (tsp:
+  // the stack level where that BLAS began); an instance group (kInstGroup in gimask) names instances by slot.
+  int tsp = 0;
+  auto set_ray = [&](const V3& Oi, const V3& Di) {
+    O = Oi;
+    D = Di;
     rD = v3(safercp(D.x), safercp(D.y), safercp(D.z));
     oct = (rD.x < 0.0f ? 1u : 0u) | (rD.y < 0.0f ? 2u : 0u) | (rD.z < 0.0f ? 4u : 0u);
-    node = S.mesh[I.mesh].root;
-    gmask = 0;
-    sp = 0;
-    return true;
   };
-  // next child of the current group, or the next stacked group, or done with this BLAS
+  // enter the first instance >= i0 whose world box the ray hits before h.t (tiny_bvh.h:2500-2565 TLAS
+  // walk as a linear loop over <= kLinearInstances instance boxes); false when there is none.  TLAS: start
+  // the instance-BVH walk at its root.
+  auto enter = [&](int i0, const V3& Ow, const V3& Dw) -> bool {
+    if constexpr (TLAS) {
+      set_ray(Ow, Dw);
+      inst = -1;
+      node = 0;
+      gmask = 0;
+      sp = 0;
+      tsp = 0;
+      return true;
+    } else {
+      const V3 rDw = v3(safercp(Dw.x), safercp(Dw.y), safercp(Dw.z));
+      int i = i0;
+      while (i < S.ninst && slab1(S.inst[i].bmin, S.inst[i].bmax, Ow, rDw, h.t) >= kFar) i++;
+      if (i >= S.ninst) return false;
+      const InstDev& I = S.inst[i];
+      inst = i;
+      set_ray(xform_point(Ow, I.inv), xform_vector(Dw, I.inv));
+      node = S.mesh[I.mesh].root;
+      gmask = 0;
+      sp = 0;
+      return true;
+    }
+  };
+  auto push_cur = [&]() {
+    if (gmask && sp < STACK) {
+      st[(2 * sp) * 64] = gbase;
+      st[(2 * sp + 1) * 64] = gmask | (gimask << 8);
+      sp++;
+    }
+  };
+  // next child of the current group, or the next stacked group, or done with this BLAS (TLAS: with this BLAS,
+  // or with the instance BVH when inst < 0).  TLAS: an instance child is entered here (world -> instance ray).
   auto next_node = [&]() {
-    if (!gmask && sp > 0) {
+    const int base = TLAS && inst >= 0 ? tsp : 0;
+    if (!gmask && sp > base) {
       sp--;
       gbase = st[(2 * sp) * 64];
       const uint32_t m = st[(2 * sp + 1) * 64];
@@ -110,7 +138,19 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       const uint32_t bit = __builtin_ctz(gmask);
       gmask &= gmask - 1u;
       const uint32_t k = bit ^ oct;
-      node = gbase + __builtin_popcount(gimask & ((1u << k) - 1u));
+      node = gbase + __builtin_popcount(gimask & ((1u << k) - 1u) & 0xFFu);
+      if constexpr (TLAS) {
+        if (gimask & kInstGroup) {
+          const int id = (int)S.tlas_slot[node];
+          push_cur();  // the remaining instances of the group
+          tsp = sp;
+          inst = id;
+          const InstDev& I = S.inst[id];
+          set_ray(xform_point(O, I.inv), xform_vector(D, I.inv));
+          node = S.mesh[I.mesh].root;
+          gmask = 0;
+        }
+      }
     } else {
       node = kNoNode;
     }
@@ -118,24 +158,44 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   // interior children hit at a visited node: stack the rest of the current group, descend into the new one
   auto push_group = [&](uint32_t ihit, uint32_t imask, uint32_t child_base) {
     if (ihit) {
-      if (gmask && sp < STACK) {
-        st[(2 * sp) * 64] = gbase;
-        st[(2 * sp + 1) * 64] = gmask | (gimask << 8);
-        sp++;
-      }
+      push_cur();
       gbase = child_base;
       gmask = order_mask(ihit, oct);
       gimask = imask;
     }
     next_node();
   };
+  // leave the BLAS of instance `inst` (its walk and triangle tests done): the world ray again, then the next
+  // instance-BVH child; false when the instance BVH is done too
+  auto leave_blas = [&]() -> bool {
+    V3 Ow, Dw;
+    reload(handle, any, Ow, Dw);
+    set_ray(Ow, Dw);
+    inst = -1;
+    next_node();
+    return node != kNoNode;
+  };
   // one node visit (lanes without pending triangles)
   auto node_step = [&]() {
-    const uint4* np = reinterpret_cast<const uint4*>(S.nodes8 + node);
+    const bool top = TLAS && inst < 0;  // a node of the instance BVH
+    const uint4* np = reinterpret_cast<const uint4*>((top ? S.tlas8 : S.nodes8) + node);
     const uint4 a = np[0], b = np[1];
     const uint4 c = np[2], d = np[3], e = np[4];
     const uint32_t hits = node8_hits(a, c, d, e, O, rD, h.t);
     const uint32_t imask = a.w >> 24;
+    if (TLAS && top) {  // instance children: one group addressed by slot (tlas_slot[b.y + slot])
+      const uint32_t ih = hits & imask, lh = hits & ~imask;
+      if (ih) {
+        push_cur();
+        gbase = b.x; gmask = order_mask(ih, oct); gimask = imask;
+      }
+      if (lh) {
+        push_cur();
+        gbase = b.y; gmask = order_mask(lh, oct); gimask = 0xFFu | kInstGroup;
+      }
+      next_node();
+      return;
+    }
     lhit = hits & ~imask;
     ltri = b.y; lmeta0 = b.z; lmeta1 = b.w;
     push_group(hits & imask, imask, b.x);
@@ -199,7 +259,9 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     // ---- BLAS done: next instance, or the ray is finished
     if (active && node == kNoNode && lhit == 0 && tcnt == 0) {
       bool more = false;
-      if (inst + 1 < S.ninst) {
+      if constexpr (TLAS) {
+        if (inst >= 0) more = leave_blas();
+      } else if (inst + 1 < S.ninst) {
         V3 Ow, Dw;
         reload(handle, any, Ow, Dw);
         more = enter(inst + 1, Ow, Dw);
@@ -271,7 +333,9 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
         if (occl || (ts & 0xFFFFu) == 0u) {
           if (!any) merge_team();
           bool more = false;
-          if (!occl && inst + 1 < S.ninst) {
+          if constexpr (TLAS) {
+            if (!occl && inst >= 0) more = leave_blas();
+          } else if (!occl && inst + 1 < S.ninst) {
             V3 Ow, Dw;
             reload(handle, any, Ow, Dw);
             more = enter(inst + 1, Ow, Dw);
@@ -287,13 +351,14 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       if (__ballot(active) == 0) break;  // helpers always belong to a live owner
       // ---- free lanes take a pending group from a walking lane: its top stack entry or its sibling group
       const uint64_t freem = __ballot(!active && !helper);
-      const uint64_t donm = __ballot((active || helper) && busy && (sp > 0 || gmask != 0) &&
-                                     !(any && (tstate[slot] & kFoundBit)));
+      // (TLAS: only groups of the BLAS being walked are handed out: a helper walks instance-space subtrees)
+      const uint64_t donm = __ballot((active || helper) && busy && (!TLAS || inst >= 0) &&
+                                     (sp > (TLAS ? tsp : 0) || gmask != 0) && !(any && (tstate[slot] & kFoundBit)));
       if (freem && donm) {
         const uint32_t npair = min((uint32_t)__popcll(freem), (uint32_t)__popcll(donm));
         uint32_t ub = 0, um = 0, ui = 0;
         if (((donm >> lane) & 1ull) && (uint32_t)__popcll(donm & lanes_below) < npair) {
-          if (sp > 0) {
+          if (sp > (TLAS ? tsp : 0)) {
             sp--;
             ub = stk[(2 * sp) * 64];
             const uint32_t m = stk[(2 * sp + 1) * 64];
@@ -327,7 +392,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
           slot = sslot;
           h.t = tt; h.prim = shp; h.inst = shi;
           gbase = sb; gmask = sm; gimask = si;
-          sp = 0; lhit = 0; tcnt = 0;
+          sp = 0; tsp = 0; lhit = 0; tcnt = 0;
           found = false;
           next_node();
           atomicAdd(&tstate[slot], 1u);
@@ -343,11 +408,13 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   }
 }
 
-template <int MODE, int STACK, int REFILL, int TAILN = 32, class Fetch, class Load, class Reload, class Finish>
+template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, class Fetch, class Load, class Reload,
+          class Finish>
 __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                  Load load, Reload reload, Finish finish,
                                                  uint32_t* __restrict__ tail = nullptr) {
-  trav8_persistent_t<MODE, STACK, REFILL, TAILN>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {}, tail);
+  trav8_persistent_t<MODE, STACK, REFILL, TAILN, TLAS>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {},
+                                                        tail);
 }
 
 }  // namespace prt

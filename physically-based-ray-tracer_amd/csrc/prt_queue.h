@@ -89,7 +89,13 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, uint32_t n, 
   return off + before;
 }
 
-__device__ __forceinline__ uint32_t pack_hit(uint32_t prim, uint32_t inst) { return prim | (inst << 26); }
+// hit record word: prim in the low S.pbits bits (enough for the largest mesh), instance above (prt_api.cpp
+// checks that both fit in 32 bits)
+__device__ __forceinline__ uint32_t pack_hit(const SceneDev& S, uint32_t prim, uint32_t inst) {
+  return prim | (inst << S.pbits);
+}
+__device__ __forceinline__ uint32_t hit_prim(const SceneDev& S, uint32_t pk) { return pk & ((1u << S.pbits) - 1u); }
+__device__ __forceinline__ uint32_t hit_inst(const SceneDev& S, uint32_t pk) { return pk >> S.pbits; }
 
 // wave-uniform fetch of up to `want` consecutive live-range entries from the XCD-partitioned counters
 __device__ __forceinline__ uint32_t fetch_some(uint32_t* fctr, uint32_t total, uint32_t& part, uint32_t* base,

@@ -49,7 +49,10 @@ struct TexDev {
   int32_t pad;
 };
 
-constexpr int kMaxInstances = 64;
+// up to kLinearInstances instances are tested as a linear list of world boxes; above that (or with PRT_TLAS=1)
+// the rays walk an 8-wide BVH over the instance boxes (the reference's TLAS, Core/tiny_bvh.h:2500-2565)
+constexpr int kLinearInstances = 64;
+constexpr int kMaxInstances = 1 << 24;
 
 struct SceneDev {
   const Node8* nodes8;    // all BLASes; MeshDev.root indexes it
@@ -61,9 +64,13 @@ struct SceneDev {
   const MeshDev* mesh;
   const float* sky;
   const float* srgb;  // srgbToLinear(byte / 255) for byte 0..255
+  const Node8* tlas8;          // instance BVH (root = node 0; bvh_build.h build_tlas8), when tlas != 0
+  const uint32_t* tlas_slot;   // 8 per TLAS node: instance id of each leaf slot
   int32_t ninst;
   int32_t skyw, skyh;
-  int32_t pad0;
+  uint32_t pbits;   // prim bits of a packed hit word (prt_queue.h pack_hit)
+  int32_t pad0[3];
+  int32_t tlas;     // 1: rays walk tlas8 (more than kLinearInstances instances, or PRT_TLAS=1); 0: linear list
   // lights (Core/Renderer.cpp:216-310) and camera (Core/Camera.cpp:29-36)
   float ppos[12], pcol[12];
   float dpos[3], dcol[3], spos[3], scol[3], srot[3];

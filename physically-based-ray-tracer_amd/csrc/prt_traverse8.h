@@ -59,7 +59,7 @@ __device__ __forceinline__ uint32_t order_mask(uint32_t m, uint32_t oct) {
 template <int STACK, int BLOCK, bool ANY>
 __device__ __forceinline__ bool blas_traverse8(const Node8* __restrict__ nodes, const TriMT* __restrict__ tris,
                                                uint32_t root, const V3& O, const V3& D, const V3& rD, uint32_t inst,
-                                               Hit& h, uint32_t* __restrict__ stk) {
+                                               Hit& h, uint32_t* __restrict__ stk, int cap = STACK) {
   const uint32_t oct = (rD.x < 0.0f ? 1u : 0u) | (rD.y < 0.0f ? 2u : 0u) | (rD.z < 0.0f ? 4u : 0u);
   uint32_t gbase = 0, gmask = 0, gimask = 0;  // current group: unvisited interior children (ordered bits)
   uint32_t node = root;
@@ -87,6 +87,60 @@ __device__ __forceinline__ bool blas_traverse8(const Node8* __restrict__ nodes, 
             }
           }
         }
+      }
+      const uint32_t ihit = hits & imask;
+      if (ihit) {
+        if (gmask && sp < cap) {
+          stk[(2 * sp) * BLOCK] = gbase;
+          stk[(2 * sp + 1) * BLOCK] = gmask | (gimask << 8);
+          sp++;
+        }
+        gbase = b.x;
+        gmask = order_mask(ihit, oct);
+        gimask = imask;
+      }
+    }
+    if (!gmask) {
+      if (sp == 0) break;
+      sp--;
+      gbase = stk[(2 * sp) * BLOCK];
+      const uint32_t m = stk[(2 * sp + 1) * BLOCK];
+      gmask = m & 0xFFu;
+      gimask = m >> 8;
+    }
+    const uint32_t bit = __builtin_ctz(gmask);
+    gmask &= gmask - 1u;
+    const uint32_t k = bit ^ oct;
+    node = gbase + __builtin_popcount(gimask & ((1u << k) - 1u));
+  }
+  return false;
+}
+
+// instance BVH walk (S.tlas): TLAS groups on the stack below, each hit instance's BLAS walked at once on the
+// stack space above them (tiny_bvh.h:2500-2565 / 2611-2673 with an 8-wide TLAS; bvh_build.h build_tlas8)
+template <int STACK, int BLOCK, bool ANY>
+__device__ __forceinline__ bool tlas_traverse8(const SceneDev& S, const Ray& r, Hit& h, uint32_t* __restrict__ stk) {
+  const uint32_t oct = (r.rD.x < 0.0f ? 1u : 0u) | (r.rD.y < 0.0f ? 2u : 0u) | (r.rD.z < 0.0f ? 4u : 0u);
+  uint32_t gbase = 0, gmask = 0, gimask = 0;
+  uint32_t node = 0;
+  int sp = 0;
+  while (true) {
+    {
+      const uint4* np = reinterpret_cast<const uint4*>(S.tlas8 + node);
+      const uint4 a = np[0], b = np[1];
+      const uint32_t imask = a.w >> 24;
+      const uint32_t hits = node8_hits(a, np[2], np[3], np[4], r.O, r.rD, h.t);
+      uint32_t lh = order_mask(hits & ~imask, oct);
+      while (lh) {  // instances of this node, near to far
+        const uint32_t k = __builtin_ctz(lh) ^ oct;
+        lh &= lh - 1u;
+        const uint32_t i = S.tlas_slot[b.y + k];
+        const InstDev& I = S.inst[i];
+        const V3 Oi = xform_point(r.O, I.inv), Di = xform_vector(r.D, I.inv);
+        const V3 rDi = v3(safercp(Di.x), safercp(Di.y), safercp(Di.z));
+        if (blas_traverse8<STACK, BLOCK, ANY>(S.nodes8, S.tris, S.mesh[I.mesh].root, Oi, Di, rDi, i, h,
+                                              stk + 2 * sp * BLOCK, STACK - sp) && ANY)
+          return true;
       }
       const uint32_t ihit = hits & imask;
       if (ihit) {
@@ -120,6 +174,10 @@ template <int STACK, int BLOCK>
 __device__ __forceinline__ Hit scene_closest8(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
   Hit h;
   h.t = tmax; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;
+  if (S.tlas) {
+    (void)tlas_traverse8<STACK, BLOCK, false>(S, r, h, stk);
+    return h;
+  }
   for (int i = 0; i < S.ninst; i++) {
     const InstDev& I = S.inst[i];
     if (slab1(I.bmin, I.bmax, r.O, r.rD, h.t) >= kFar) continue;
@@ -132,6 +190,11 @@ __device__ __forceinline__ Hit scene_closest8(const SceneDev& S, const Ray& r, f
 
 template <int STACK, int BLOCK>
 __device__ __forceinline__ bool scene_anyhit8(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
+  if (S.tlas) {
+    Hit h;
+    h.t = tmax; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;
+    return tlas_traverse8<STACK, BLOCK, true>(S, r, h, stk);
+  }
   for (int i = 0; i < S.ninst; i++) {
     const InstDev& I = S.inst[i];
     if (slab1(I.bmin, I.bmax, r.O, r.rD, tmax) >= kFar) continue;

@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, T
 }
 
 // ---- one traversal launch: closest hits of P(iter) (iter < iters) + any hits of S(iter - 1) (iter > 0)
-template <int REFILL, int STACK, int WAVES, int TAILN>
+template <int REFILL, int STACK, int WAVES, int TAILN, bool TLAS>
 __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, uint32_t iter, uint32_t iters) {
   __shared__ uint32_t lds_stack[2 * STACK * 64];
   __shared__ uint32_t prefP[kNSub + 1], prefS[kNSub + 1];
@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   unsigned long long* tl = B.tl ? B.tl + ((size_t)iter * kTlWaves + blockIdx.x) * 4 : nullptr;
   bool seen_drain = false;
   if (tl && threadIdx.x == 0) tl[0] = __builtin_amdgcn_s_memrealtime();
-  trav8_persistent<2, STACK, REFILL, TAILN>(
+  trav8_persistent<2, STACK, REFILL, TAILN, TLAS>(
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) {
         const uint32_t got = fetch_some(fctr, total, part, base, want);
@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
         if (any) {
           if (!occluded) vis8[__float_as_uint(B.shd[h].w)] = 1;
         } else {
-          B.hit[h] = make_float4(hit.t, hit.u, hit.v, __uint_as_float(hit.prim | (hit.inst << 26)));
+          B.hit[h] = make_float4(hit.t, hit.u, hit.v, __uint_as_float(pack_hit(S, hit.prim, hit.inst)));
         }
       },
       B.coop_tail ? tail_lds : nullptr);
@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
       const uint32_t pk = __float_as_uint(hh.w);
       const V3 I = v3(o.x, o.y, o.z) + hh.x * D;                                             // tiny_bvh.h:586
       const V3 V = -D;
-      const HitAttr ha = hit_attributes(S, pk >> 26, pk & 0x03FFFFFFu, hh.y, hh.z, (fl & kNormalMap) != 0);
+      const HitAttr ha = hit_attributes(S, hit_inst(S, pk), hit_prim(S, pk), hh.y, hh.z, (fl & kNormalMap) != 0);
       const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
       B.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
       const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed, [&](int k, const Ray& sr, float tmax, V3 fk) {
@@ -342,8 +342,8 @@ __global__ void __launch_bounds__(kBlock) k_shade2_debug(SceneDev S, TraceArgs A
       if ((info & 0x1FFu) == 0) B.s1[item].w = hh.x;
       if (hh.x < kFar) {  // misses keep k_miss2's sky value
         const uint32_t pk = __float_as_uint(hh.w);
-        const HitAttr ha = hit_attributes(S, pk >> 26, pk & 0x03FFFFFFu, hh.y, hh.z, (A.flags & kNormalMap) != 0);
-        const V3 L = debug_view(S, A.mode, ha, pk >> 26, pk & 0x03FFFFFFu);
+        const HitAttr ha = hit_attributes(S, hit_inst(S, pk), hit_prim(S, pk), hh.y, hh.z, (A.flags & kNormalMap) != 0);
+        const V3 L = debug_view(S, A.mode, ha, hit_inst(S, pk), hit_prim(S, pk));
         B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
       }
       B.rinfo[item] = info & 0x1FFu;  // kStEndValue
@@ -449,8 +449,12 @@ __global__ void __launch_bounds__(kBlock) k_resolve2(SceneDev S, TraceArgs A, Wa
 template <int STACK, int WAVES, int TAILN>
 void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
   static_assert(2 * STACK * 256 + 264 + 4 * 3 * TAILN <= 163840 / (4 * WAVES), "LDS over the occupancy budget");
-  hipLaunchKernelGGL((k_trace2<32, STACK, WAVES, TAILN>), dim3(256u * 4u * WAVES), dim3(64), 0, c.stream, S, B, it,
-                     iters);
+  if (S.tlas)
+    hipLaunchKernelGGL((k_trace2<32, STACK, WAVES, TAILN, true>), dim3(256u * 4u * WAVES), dim3(64), 0, c.stream, S, B,
+                       it, iters);
+  else
+    hipLaunchKernelGGL((k_trace2<32, STACK, WAVES, TAILN, false>), dim3(256u * 4u * WAVES), dim3(64), 0, c.stream, S,
+                       B, it, iters);
 }
 // persistent traversal occupancy (waves/SIMD) -> LDS stack groups per lane
 static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {

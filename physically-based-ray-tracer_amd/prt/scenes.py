@@ -237,6 +237,29 @@ def multi_instance(base: SceneData) -> SceneData:
     return dataclasses.replace(base, instances=inst, name=base.name + "+inst")
 
 
+def instance_field(n: int = 300, seed: int = 5) -> SceneData:
+    """Many instances (the reference's TLAS over up to 2^32 BLASInstances, Core/tiny_bvh.h:103-104,1732-1770): the
+    small heightfield as instance 0 plus `n` copies of a 576-triangle torus scattered over it with random
+    rotation about Y, tilt and scale -- more than kLinearInstances, so the rays walk the instance BVH."""
+    base = config_small(40, 30)
+    albedo, metalness, normal, emis = procedural_textures()
+    tor = torus(24, 12, 0.22, 0.08)
+    tor.albedo, tor.metalness = 0, 2
+    rng = np.random.default_rng(seed)
+    inst = list(base.instances)
+    for _ in range(n):
+        a, b, sc = rng.uniform(0, 2 * np.pi), rng.uniform(-0.6, 0.6), rng.uniform(0.5, 1.6)
+        ca, sa, cb, sb = np.cos(a), np.sin(a), np.cos(b), np.sin(b)
+        Ry = np.array([[ca, 0, sa], [0, 1, 0], [-sa, 0, ca]])
+        Rx = np.array([[1, 0, 0], [0, cb, -sb], [0, sb, cb]])
+        M = np.eye(4)
+        M[:3, :3] = (Ry @ Rx) * sc
+        M[:3, 3] = (rng.uniform(-4.5, 4.5), rng.uniform(0.25, 1.2), rng.uniform(-4.5, 4.5))
+        inst.append((1, M.astype(F32)))
+    return dataclasses.replace(base, meshes=list(base.meshes) + [tor], instances=inst,
+                               name=f"instance-field-{n}")
+
+
 def ceiling_light(corner=(-1.5, 4.0, -1.0), edge_u=(3.0, 0.0, 0.0), edge_v=(0.0, 0.0, 2.0), radiance=(8.0, 7.0, 6.0),
                   two_sided=False) -> dict:
     """One quad area light (extension; the reference's AreaLight is never sampled): by default a 3 x 2 panel

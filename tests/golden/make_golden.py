@@ -12,6 +12,8 @@ outputs only, so the parity tests run anywhere (CPU here, GPU box) without the r
   trace_64x48.npz  the oracle's Trace (Core/Renderer.cpp:150-406 restated) running on tinybvh's BVH8_CPU
                    traversal: avg RGBA, RGB8, segment / shadow-ray counts.  The traversal half is the
                    reference's; the shading half is the restatement (BRDF.cpp is unbuildable here).
+  many_inst.npz    scenes.instance_field(300) (301 instances: tinybvh's TLAS over them), 8192 random rays:
+                   closest-hit records and IsOccluded as multi_rays; plus a 96x64, 2 spp, depth 3 render
 The headline configs, through the same reference traversal (`make_golden.py ref`):
   c4_ref_crop.npz      C4 1920x1080, 4 spp, depth 4: whole-frame ray counts + digests, a 480x270 window's pixels
   c3_ref_480x270.npz   C3 at 480x270, 4 spp, depth 4: the whole frame
@@ -23,7 +25,7 @@ The headline configs, through the same reference traversal (`make_golden.py ref`
                        reference-traversal renders at 160x160: shaded (4 spp, depth 3), albedo and shading-normal views
 Every fixture records a digest of the scene arrays it was made from, so a change of scenes.py is caught.
 
-usage: python tests/golden/make_golden.py [small] [ref] [ship]
+usage: python tests/golden/make_golden.py [small] [inst] [ref] [ship]
 """
 import hashlib
 import os
@@ -86,6 +88,21 @@ def multi_rays():
     np.savez_compressed(os.path.join(HERE, "multi_rays.npz"), O=O, D=D, t=t, u=u, v=v, prim=p, inst=i, tmax=tmax,
                         occ=occ, digest=scene_digest(sd))
     return int((t < 1e30).sum())
+
+
+def many_inst():
+    sd = scenes.instance_field(300)
+    O, D = random_rays(sd, 8192, seed=13)
+    ref = oracle.RefScene(sd)
+    t, u, v, p, i = ref.intersect(O, D)
+    tmax = np.where(np.arange(len(t)) % 3 == 0, np.float32(1e30), t * np.float32(0.999)).astype(np.float32)
+    occ = ref.occluded(O, D, tmax)
+    W, H = 96, 64
+    avg, rgb8, _, st = _ref_render(sd, W, H, 2, 3)
+    np.savez_compressed(os.path.join(HERE, "many_inst.npz"), O=O, D=D, t=t, u=u, v=v, prim=p, inst=i, tmax=tmax, occ=occ,
+                        W=W, H=H, avg=avg[:, :3].copy(), rgb8=rgb8, segments=int(st.segments),
+                        shadow_rays=int(st.shadow_rays), digest=scene_digest(sd))
+    return int((t < 1e30).sum()), int((i[t < 1e30] > 0).sum())
 
 
 def trace_small():
@@ -258,6 +275,8 @@ def main():
         print("c2_primary hits", c2_primary())
         print("multi_rays hits", multi_rays())
         print("trace segments", trace_small())
+    if "small" in which or "inst" in which:
+        print("many_inst hits (all, on tori)", many_inst())
     if "ref" in which:
         print("c4_ref_crop rays", c4_ref_crop())
         print("c3_ref rays", c3_ref())
