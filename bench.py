@@ -30,7 +30,7 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # VALU issue peak: 256 CUs x 4 SIMD-32 x 2.4 GHz, one wave64 VALU instruction per 2 cycles per SIMD
 # (MI355X_MICROARCH.md, Execution model) = 1228.8 G wave-instructions/s
-VALU_PEAK_GINST = 256 * 4 * 2.4 / 2 * 1000.0
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # G wave64 VALU instructions/s: 1024 SIMDs x 2.4 GHz / 2 cycles each
 VISITS_JSON = os.path.join(ROOT, "profiles", "reference_visits_c4.json")
 TRACE_KERNEL = "k_trace2"
 

@@ -228,6 +228,11 @@ SHIP_RENDERS = (("shaded", 0, 4, 3), ("albedo", 1, 1, 1), ("normal", 3, 1, 1))
 SHIP_WH = 160
 
 
+def ship_flags(spp):
+    """reference defaults; a 1-spp render has AA off (SURVEY 8d canonical estimator)"""
+    return oracle.DEFAULT_FLAGS if spp > 1 else oracle.DEFAULT_FLAGS & ~1
+
+
 def indexed(m):
     """(P, N, UV, tri) of a Mesh whose corners were expanded from an indexed model (ingest.mesh_from_indexed)."""
     P = m.vertices.reshape(-1, 3)
@@ -251,7 +256,7 @@ def spaceship():
     W = H = SHIP_WH
     out = {}
     for name, mode, spp, bounces in SHIP_RENDERS:
-        avg, rgb8, _, st = _ref_render(sd, W, H, spp, bounces, mode=mode)
+        avg, rgb8, _, st = _ref_render(sd, W, H, spp, bounces, flags=ship_flags(spp), mode=mode)
         out[f"{name}_avg"] = avg[:, :3].copy()
         out[f"{name}_rgb8"] = rgb8
         out[f"{name}_counts"] = np.array([st.segments, st.shadow_rays], np.int64)

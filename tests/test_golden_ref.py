@@ -14,9 +14,9 @@ import numpy as np
 import pytest
 
 import oracle
-from golden.make_golden import C1_RENDERS, SHIP_RENDERS, c1_lit, scene_digest
+from golden.make_golden import C1_RENDERS, SHIP_RENDERS, c1_lit, scene_digest, ship_flags
 from helpers import RMSE_TOL, gpu_scene, rmse
-from prt import _lib, ingest, scenes
+from prt import ingest, scenes
 from prt.scenes import Lights, SceneData
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -107,7 +107,8 @@ def test_oracle_spaceship_matches_reference_traversal(oracle_mod):
     W, H = int(z["W"]), int(z["H"])
     for name, mode, spp, bounces in SHIP_RENDERS:
         osc = oracle_mod.OracleScene(sd, W, H)
-        avg, rgb8, _, st = osc.render(W, H, spp=spp, bounces=bounces, mode=mode, nthreads=THREADS)
+        avg, rgb8, _, st = osc.render(W, H, spp=spp, bounces=bounces, flags=ship_flags(spp), mode=mode,
+                                      nthreads=THREADS)
         err, _ = _report(f"Spaceship {name}", z[f"{name}_avg"], avg)
         assert err <= RMSE_TOL
         assert [st.segments, st.shadow_rays] == z[f"{name}_counts"].tolist()
@@ -175,8 +176,7 @@ def test_gpu_spaceship_matches_reference_traversal(gpu_ctx):
     gpu_scene(gpu_ctx, sd, W, H)
     for name, mode, spp, bounces in SHIP_RENDERS:
         gpu_ctx.reset_accumulation(full=True)
-        flags = _lib.FLAGS_DEFAULT if spp > 1 else _lib.FLAGS_DEFAULT & ~_lib.FLAG_AA  # 1 spp: AA off
-        avg, rgb8, st = gpu_ctx.render(W, H, spp, bounces, flags=flags, mode=mode)
+        avg, rgb8, st = gpu_ctx.render(W, H, spp, bounces, flags=ship_flags(spp), mode=mode)
         err, exact = _report(f"GPU Spaceship {name}", z[f"{name}_avg"], avg)
         assert err <= RMSE_TOL
         assert [st.segments, st.shadow_rays] == z[f"{name}_counts"].tolist()
