@@ -22,9 +22,10 @@ struct Box {
   void grow(const Box& b) {
     for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], b.lo[k]); hi[k] = std::max(hi[k], b.hi[k]); }
   }
-  float area() const {
-    float e0 = hi[0] - lo[0], e1 = hi[1] - lo[1], e2 = hi[2] - lo[2];
-    if (e0 < 0 || e1 < 0 || e2 < 0) return 0.0f;
+  // in double: boxes of extent above ~1e19 overflow a float area (and every SAH cost built on it)
+  double area() const {
+    const double e0 = (double)hi[0] - lo[0], e1 = (double)hi[1] - lo[1], e2 = (double)hi[2] - lo[2];
+    if (e0 < 0 || e1 < 0 || e2 < 0) return 0.0;
     return e0 * e1 + e1 * e2 + e2 * e0;
   }
 };
@@ -79,7 +80,7 @@ struct Builder {
     nodes[ni].box = b;
     if (count <= 1) return;
     // binned SAH over centroid bins (C_trav = 1, C_int = 1 per triangle)
-    float best = 1e30f;
+    double best = 1e300;
     int bax = -1, bsplit = -1;
     for (int ax = 0; ax < 3; ax++) {
       const float lo = cb.lo[ax], hi = cb.hi[ax];
@@ -94,7 +95,7 @@ struct Builder {
         cnt[k]++;
         bins[k].grow(tb[p]);
       }
-      float la[kBins - 1], ra[kBins - 1];
+      double la[kBins - 1], ra[kBins - 1];
       int lc[kBins - 1], rc[kBins - 1];
       Box acc; acc.reset();
       int c = 0;
@@ -111,13 +112,13 @@ struct Builder {
       }
       for (int k = 0; k < kBins - 1; k++) {
         if (!lc[k] || !rc[k]) continue;
-        float cost = la[k] * lc[k] + ra[k] * rc[k];
+        const double cost = la[k] * lc[k] + ra[k] * rc[k];
         if (cost < best) { best = cost; bax = ax; bsplit = k; }
       }
     }
-    const float parea = b.area();
-    const float leaf_cost = (float)count;                      // C_int * n
-    const float split_cost = parea > 0 ? 1.0f + best / parea : 1e30f;  // C_trav + SAH
+    const double parea = b.area();
+    const double leaf_cost = (double)count;                     // C_int * n
+    const double split_cost = parea > 0 ? 1.0 + best / parea : 1e300;  // C_trav + SAH
     if (count <= max_leaf && (bax < 0 || leaf_cost <= split_cost)) return;
     int32_t mid;
     if (bax < 0) {
@@ -186,7 +187,7 @@ struct Fmt8 {
 // is either a leaf (<= max_leaf triangles, cost A(n) * c_tri * count) or a wide node (A(n) * c_node + the
 // best distribution of its 8 slots over the two binary children).  Costs are area-weighted (SAH).
 struct WideDp {
-  std::vector<std::array<float, 9>> C;     // C[n][i], i = 1..8
+  std::vector<std::array<double, 9>> C;    // C[n][i], i = 1..8
   std::vector<std::array<int8_t, 9>> Dk;   // best left share k of D(n, j) = C(l, k) + C(r, j - k), j = 2..8
   std::vector<std::array<uint8_t, 9>> prev;  // C(n, i) == C(n, i - 1) (use fewer slots)
   std::vector<uint8_t> leaf1;              // the single-slot form of n is a leaf
@@ -199,22 +200,23 @@ struct WideDp {
     leaf1.assign(N, 0);
     for (size_t n = N; n-- > 0;) {  // children are stored after their parent
       const Node2& x = B.nodes[n];
-      const float A = std::max(x.box.area(), 1e-30f);
-      const float leafc = x.count <= B.max_leaf ? A * c_tri * (float)x.count : 3e38f;
+      const double A = std::max(x.box.area(), 1e-30);
+      const double leafc = x.count <= B.max_leaf ? A * c_tri * (double)x.count : 1e300;
       if (x.leaf()) {
         for (int i = 1; i <= 8; i++) { C[n][i] = leafc; prev[n][i] = i > 1; }
         leaf1[n] = 1;
         continue;
       }
-      float D[9];
+      double D[9];
       for (int j = 2; j <= 8; j++) {
-        D[j] = 3e38f;
+        D[j] = 1e300;
+        Dk[n][j] = 1;
         for (int k = 1; k < j; k++) {
-          const float c = C[x.left][k] + C[x.right][j - k];
+          const double c = C[x.left][k] + C[x.right][j - k];
           if (c < D[j]) { D[j] = c; Dk[n][j] = (int8_t)k; }
         }
       }
-      const float intc = A * c_node + D[8];
+      const double intc = A * c_node + D[8];
       leaf1[n] = leafc <= intc;
       C[n][1] = std::min(leafc, intc);
       for (int i = 2; i <= 8; i++) {
@@ -283,7 +285,7 @@ void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out) {
       ch[nc++] = root.right;
       while (nc < 8) {
         int bi = -1;
-        float ba = -1.0f;
+        double ba = -1.0;
         for (int i = 0; i < nc; i++) {
           const Node2& c = B.nodes[ch[i]];
           if (!c.leaf() && c.box.area() > ba) { ba = c.box.area(); bi = i; }

@@ -110,6 +110,7 @@ struct prt_ctx {
   int tlas_depth = 0;
   BuiltTlas8 tlas_host;
   DevBuf tlas8, tlas_slot;
+  DevBuf spill;  // traversal stack levels beyond the LDS ones (BVHs deeper than 17 levels)
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
   float al[16] = {};
   int32_t area = 0, area_two_sided = 0;
@@ -151,9 +152,9 @@ struct prt_ctx {
 
 namespace {
 
-// The LDS traversal stacks hold one group per tree level below the root: up to 16 levels (18 groups at
-// 4 waves/SIMD, 16 in the query kernels)
-constexpr int kMaxBvhDepth = 16;
+// The traversal stacks hold one group per tree level below the root: 8-18 in LDS (by occupancy; 16 in the query
+// kernels), deeper levels in HBM spill columns (ensure_spill), up to tinybvh's 64-entry stack (tiny_bvh.h:6315)
+constexpr int kMaxBvhDepth = 64;
 // tree levels one lane's stack must cover: the deepest BLAS, plus the instance BVH's levels when it is walked
 // (its groups sit below the BLAS's: at most one per TLAS level, the last one the remaining instances of a leaf)
 int stack_depth(const prt_ctx* c) { return c->max_depth + (c->use_tlas ? c->tlas_depth : 0); }
@@ -234,6 +235,25 @@ int ensure_instances(prt_ctx* c) {
     c->tlas_depth = 0;
   }
   c->inst_dirty = false;
+  return PRT_OK;
+}
+
+// HBM spill columns for BVHs deeper than the LDS stacks hold (prt_traverse8.h LaneStack): levels beyond the
+// query kernels' 16 (the persistent spill form holds 18 in LDS, so this covers it too), one uint2 per level for
+// every thread of the launch: `threads` for a query, the persistent spill grid for renders
+int ensure_spill(prt_ctx* c, SceneDev& S, size_t threads) {
+  const int levels = stack_depth(c) - 1 - kQueryStack;
+  S.spill = nullptr;
+  S.spill_levels = 0;
+  if (levels <= 0) return PRT_OK;
+  const size_t need = sizeof(uint2) * (size_t)levels * std::max<size_t>(threads, (size_t)kSpillTraceBlocks * 64u);
+  if (c->spill.bytes < need) {
+    const int rc = drain(c);
+    if (rc) return rc;
+    HIP_TRY(c->spill.ensure(need));
+  }
+  S.spill = c->spill.as<uint2>();
+  S.spill_levels = levels;
   return PRT_OK;
 }
 
@@ -390,7 +410,9 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   if (rc) return rc;
   if (!c->have_camera) return fail(PRT_ERR_NOT_READY, "no camera: call prt_set_camera");
   if (!c->have_lights) return fail(PRT_ERR_NOT_READY, "no lights: call prt_set_lights");
-  if (!depth_ok(c)) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep for the LDS traversal stack");
+  if (!depth_ok(c)) return fail(PRT_ERR_UNSUPPORTED, "BVH deeper than 64 levels");
+  rc = ensure_spill(c, S, 0);
+  if (rc) return rc;
   rc = ensure_state(c, p->width, p->height);
   if (rc) return rc;
   const int32_t F = frames_of(p);
@@ -1126,9 +1148,11 @@ int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t 
   int rc = scene_ready(c, S);
   if (rc) return rc;
   if (!c->have_camera) return fail(PRT_ERR_NOT_READY, "no camera");
-  if (!depth_ok(c)) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
+  if (!depth_ok(c)) return fail(PRT_ERR_UNSUPPORTED, "BVH deeper than 64 levels");
   const TileMap M = make_tilemap(W, H, 8, 0, 1);
   const size_t n = (size_t)W * H;
+  rc = ensure_spill(c, S, (size_t)M.items + 256);
+  if (rc) return rc;
   HitOut* out = reinterpret_cast<HitOut*>(hits);
   const bool dev_out = (out_flags & PRT_OUT_DEVICE) != 0;
   if (!dev_out) { HIP_TRY(c->hits.ensure(n * sizeof(HitOut))); out = c->hits.as<HitOut>(); }
@@ -1164,7 +1188,9 @@ static int ray_query(prt_ctx* c, int32_t n, const float* O, const float* D, cons
   SceneDev S;
   int rc = scene_ready(c, S);
   if (rc) return rc;
-  if (!depth_ok(c)) return fail(PRT_ERR_UNSUPPORTED, "BVH too deep");
+  if (!depth_ok(c)) return fail(PRT_ERR_UNSUPPORTED, "BVH deeper than 64 levels");
+  rc = ensure_spill(c, S, (size_t)n + 256);
+  if (rc) return rc;
   DevBuf dO, dD, dT, dOut;
   auto cleanup = [&]() { dO.release(); dD.release(); dT.release(); dOut.release(); };
   const size_t outb = (size_t)n * (any ? 4 : sizeof(HitOut));

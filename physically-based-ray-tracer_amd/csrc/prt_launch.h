@@ -88,7 +88,11 @@ hipError_t launch_postfx(const LaunchCfg& c, const PostDev& P, const float4* acc
 hipError_t launch_untile(const LaunchCfg& c, int32_t W, int32_t H, int32_t ts, int32_t world, uint32_t per_rank,
                          const float4* gathered, float4* avg, uint32_t* rgb8, const PostDev* post);
 struct InstSrc;
-// device refit of n <= kMaxInstances instances (prt_refit.h)
+// persistent traversal grid when the stacks spill to HBM (4 waves/SIMD: 256 CUs x 4 SIMDs x 4), and the LDS
+// stack levels of that form and of the one-ray query kernels (prt_traverse8.h kQueryStack)
+constexpr uint32_t kSpillTraceBlocks = 256u * 4u * 4u;
+constexpr int kSpillTraceStack = 18;
+// device refit of the instances (prt_refit.h)
 hipError_t launch_refit(hipStream_t s, const InstSrc* src, int32_t n, InstDev* out);
 hipError_t launch_primary_hits(const LaunchCfg& c, const SceneDev& S, const TileMap& M, HitOut* out, Counters* cnt);
 hipError_t launch_intersect(const LaunchCfg& c, const SceneDev& S, int32_t n, const float* O, const float* D,

@@ -60,8 +60,8 @@ __device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
 // tail: tail_lds_words(TAILN) words of LDS for the cooperative tail, or nullptr (no tail mode).
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
-template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, class Fetch, class Load, class Reload,
-          class Finish, class Tick>
+template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, bool SPILL = false, class Fetch,
+          class Load, class Reload, class Finish, class Tick>
 __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                    Load load, Reload reload, Finish finish, Tick tick,
                                                    uint32_t* __restrict__ tail = nullptr) {
@@ -78,6 +78,25 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   uint32_t node = kNoNode, gbase = 0, gmask = 0, gimask = 0;
   int sp = 0;
   uint32_t* st = stk;  // the LDS stack column this lane walks with
+  // SPILL: levels past STACK go to the lane's HBM spill column (BVHs deeper than the LDS stack holds)
+  const LaneStack ls = lane_stack<STACK, 64>(S, stk);
+  const int cap = SPILL ? ls.cap : STACK;
+  auto put = [&](int lvl, uint32_t a, uint32_t b) {
+    if (SPILL) {
+      stack_put<STACK, 64>(ls, lvl, a, b);
+    } else {
+      st[(2 * lvl) * 64] = a;
+      st[(2 * lvl + 1) * 64] = b;
+    }
+  };
+  auto get = [&](int lvl, uint32_t& a, uint32_t& b) {
+    if (SPILL) {
+      stack_get<STACK, 64>(ls, lvl, a, b);
+    } else {
+      a = st[(2 * lvl) * 64];
+      b = st[(2 * lvl + 1) * 64];
+    }
+  };
   uint32_t lhit = 0, ltri = 0, lmeta0 = 0, lmeta1 = 0, tcur = 0, tcnt = 0;  // pending leaf triangles
   bool found = false;  // tail: this lane improved its closest hit
   // TLAS walk (TLAS = true): O / D / rD / oct hold the world ray while inst < 0 and the instance ray while
@@ -117,9 +136,8 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     }
   };
   auto push_cur = [&]() {
-    if (gmask && sp < STACK) {
-      st[(2 * sp) * 64] = gbase;
-      st[(2 * sp + 1) * 64] = gmask | (gimask << 8);
+    if (gmask && sp < cap) {
+      put(sp, gbase, gmask | (gimask << 8));
       sp++;
     }
   };
@@ -129,8 +147,8 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     const int base = TLAS && inst >= 0 ? tsp : 0;
     if (!gmask && sp > base) {
       sp--;
-      gbase = st[(2 * sp) * 64];
-      const uint32_t m = st[(2 * sp + 1) * 64];
+      uint32_t m;
+      get(sp, gbase, m);
       gmask = m & 0xFFu;
       gimask = m >> 8;
     }
@@ -360,8 +378,8 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
         if (((donm >> lane) & 1ull) && (uint32_t)__popcll(donm & lanes_below) < npair) {
           if (sp > (TLAS ? tsp : 0)) {
             sp--;
-            ub = stk[(2 * sp) * 64];
-            const uint32_t m = stk[(2 * sp + 1) * 64];
+            uint32_t m;
+            get(sp, ub, m);
             um = m & 0xFFu;
             ui = m >> 8;
           } else {
@@ -408,12 +426,12 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   }
 }
 
-template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, class Fetch, class Load, class Reload,
-          class Finish>
+template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, bool SPILL = false, class Fetch,
+          class Load, class Reload, class Finish>
 __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                  Load load, Reload reload, Finish finish,
                                                  uint32_t* __restrict__ tail = nullptr) {
-  trav8_persistent_t<MODE, STACK, REFILL, TAILN, TLAS>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {},
+  trav8_persistent_t<MODE, STACK, REFILL, TAILN, TLAS, SPILL>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {},
                                                         tail);
 }
 

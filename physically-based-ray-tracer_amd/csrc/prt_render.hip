@@ -126,7 +126,7 @@ __global__ void __launch_bounds__(kBlock) k_postfx(PostDev P, const float4* __re
 __global__ void __launch_bounds__(kBlock) k_primary_hits(SceneDev S, TileMap M, HitOut* __restrict__ out,
                                                          Counters* __restrict__ cnt) {
   __shared__ uint32_t lds_stack[kQueryWords * kBlock];
-  uint32_t* stk = lds_stack + threadIdx.x;
+  const LaneStack stk = lane_stack<kQueryStack, kBlock>(S, lds_stack + threadIdx.x);
   const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
   uint32_t nseg = 0;
   if (r < M.items) {
@@ -147,7 +147,7 @@ __global__ void __launch_bounds__(kBlock) k_intersect(SceneDev S, int32_t n, con
                                                       const float* __restrict__ D, const float* __restrict__ tmax,
                                                       HitOut* __restrict__ out) {
   __shared__ uint32_t lds_stack[kQueryWords * kBlock];
-  uint32_t* stk = lds_stack + threadIdx.x;
+  const LaneStack stk = lane_stack<kQueryStack, kBlock>(S, lds_stack + threadIdx.x);
   const int32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const Ray r = make_ray(v3(O[3 * i], O[3 * i + 1], O[3 * i + 2]), v3(D[3 * i], D[3 * i + 1], D[3 * i + 2]));
@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(kBlock) k_occluded(SceneDev S, int32_t n, cons
                                                      const float* __restrict__ D, const float* __restrict__ tmax,
                                                      int32_t* __restrict__ out) {
   __shared__ uint32_t lds_stack[kQueryWords * kBlock];
-  uint32_t* stk = lds_stack + threadIdx.x;
+  const LaneStack stk = lane_stack<kQueryStack, kBlock>(S, lds_stack + threadIdx.x);
   const int32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const Ray r = make_ray(v3(O[3 * i], O[3 * i + 1], O[3 * i + 2]), v3(D[3 * i], D[3 * i + 1], D[3 * i + 2]));

@@ -69,7 +69,8 @@ struct SceneDev {
   int32_t ninst;
   int32_t skyw, skyh;
   uint32_t pbits;   // prim bits of a packed hit word (prt_queue.h pack_hit)
-  int32_t pad0[3];
+  int32_t spill_levels;  // traversal stack levels beyond the LDS ones, in HBM (prt_traverse8.h LaneStack)
+  uint2* spill;          // level-major spill columns (nullptr: the BVH fits the LDS stacks)
   int32_t tlas;     // 1: rays walk tlas8 (more than kLinearInstances instances, or PRT_TLAS=1); 0: linear list
   // lights (Core/Renderer.cpp:216-310) and camera (Core/Camera.cpp:29-36)
   float ppos[12], pcol[12];

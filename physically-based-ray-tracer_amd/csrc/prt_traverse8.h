@@ -56,10 +56,50 @@ __device__ __forceinline__ uint32_t order_mask(uint32_t m, uint32_t oct) {
   return m;
 }
 
+// One lane's traversal stack: levels [0, STACK) in LDS (stk[2 * level * BLOCK], one column per lane), deeper
+// levels in the lane's HBM spill column (S.spill, level-major so a wave's entries of one level are contiguous;
+// S.spill_levels levels, 0 = no spill: the host sizes both from the BVH depth, prt_api.cpp stack_depth)
+struct LaneStack {
+  uint32_t* lds;
+  uint2* spill;
+  uint32_t tid, stride;
+  int cap;  // STACK + spill levels
+};
+template <int STACK, int BLOCK>
+__device__ __forceinline__ LaneStack lane_stack(const SceneDev& S, uint32_t* lds) {
+  LaneStack L;
+  L.lds = lds;
+  L.spill = S.spill;
+  L.tid = blockIdx.x * blockDim.x + threadIdx.x;
+  L.stride = gridDim.x * blockDim.x;
+  L.cap = STACK + (S.spill ? S.spill_levels : 0);
+  return L;
+}
+template <int STACK, int BLOCK>
+__device__ __forceinline__ void stack_put(const LaneStack& L, int lvl, uint32_t a, uint32_t b) {
+  if (lvl < STACK) {
+    L.lds[(2 * lvl) * BLOCK] = a;
+    L.lds[(2 * lvl + 1) * BLOCK] = b;
+  } else {
+    L.spill[(size_t)(lvl - STACK) * L.stride + L.tid] = make_uint2(a, b);
+  }
+}
+template <int STACK, int BLOCK>
+__device__ __forceinline__ void stack_get(const LaneStack& L, int lvl, uint32_t& a, uint32_t& b) {
+  if (lvl < STACK) {
+    a = L.lds[(2 * lvl) * BLOCK];
+    b = L.lds[(2 * lvl + 1) * BLOCK];
+  } else {
+    const uint2 v = L.spill[(size_t)(lvl - STACK) * L.stride + L.tid];
+    a = v.x;
+    b = v.y;
+  }
+}
+
 template <int STACK, int BLOCK, bool ANY>
 __device__ __forceinline__ bool blas_traverse8(const Node8* __restrict__ nodes, const TriMT* __restrict__ tris,
                                                uint32_t root, const V3& O, const V3& D, const V3& rD, uint32_t inst,
-                                               Hit& h, uint32_t* __restrict__ stk, int cap = STACK) {
+                                               Hit& h, const LaneStack& stk, int lvl0 = 0) {
   const uint32_t oct = (rD.x < 0.0f ? 1u : 0u) | (rD.y < 0.0f ? 2u : 0u) | (rD.z < 0.0f ? 4u : 0u);
   uint32_t gbase = 0, gmask = 0, gimask = 0;  // current group: unvisited interior children (ordered bits)
   uint32_t node = root;
@@ -90,9 +130,8 @@ __device__ __forceinline__ bool blas_traverse8(const Node8* __restrict__ nodes, 
       }
       const uint32_t ihit = hits & imask;
       if (ihit) {
-        if (gmask && sp < cap) {
-          stk[(2 * sp) * BLOCK] = gbase;
-          stk[(2 * sp + 1) * BLOCK] = gmask | (gimask << 8);
+        if (gmask && lvl0 + sp < stk.cap) {
+          stack_put<STACK, BLOCK>(stk, lvl0 + sp, gbase, gmask | (gimask << 8));
           sp++;
         }
         gbase = b.x;
@@ -103,8 +142,8 @@ __device__ __forceinline__ bool blas_traverse8(const Node8* __restrict__ nodes, 
     if (!gmask) {
       if (sp == 0) break;
       sp--;
-      gbase = stk[(2 * sp) * BLOCK];
-      const uint32_t m = stk[(2 * sp + 1) * BLOCK];
+      uint32_t m;
+      stack_get<STACK, BLOCK>(stk, lvl0 + sp, gbase, m);
       gmask = m & 0xFFu;
       gimask = m >> 8;
     }
@@ -119,7 +158,7 @@ __device__ __forceinline__ bool blas_traverse8(const Node8* __restrict__ nodes, 
 // instance BVH walk (S.tlas): TLAS groups on the stack below, each hit instance's BLAS walked at once on the
 // stack space above them (tiny_bvh.h:2500-2565 / 2611-2673 with an 8-wide TLAS; bvh_build.h build_tlas8)
 template <int STACK, int BLOCK, bool ANY>
-__device__ __forceinline__ bool tlas_traverse8(const SceneDev& S, const Ray& r, Hit& h, uint32_t* __restrict__ stk) {
+__device__ __forceinline__ bool tlas_traverse8(const SceneDev& S, const Ray& r, Hit& h, const LaneStack& stk) {
   const uint32_t oct = (r.rD.x < 0.0f ? 1u : 0u) | (r.rD.y < 0.0f ? 2u : 0u) | (r.rD.z < 0.0f ? 4u : 0u);
   uint32_t gbase = 0, gmask = 0, gimask = 0;
   uint32_t node = 0;
@@ -138,15 +177,14 @@ __device__ __forceinline__ bool tlas_traverse8(const SceneDev& S, const Ray& r, 
         const InstDev& I = S.inst[i];
         const V3 Oi = xform_point(r.O, I.inv), Di = xform_vector(r.D, I.inv);
         const V3 rDi = v3(safercp(Di.x), safercp(Di.y), safercp(Di.z));
-        if (blas_traverse8<STACK, BLOCK, ANY>(S.nodes8, S.tris, S.mesh[I.mesh].root, Oi, Di, rDi, i, h,
-                                              stk + 2 * sp * BLOCK, STACK - sp) && ANY)
+        if (blas_traverse8<STACK, BLOCK, ANY>(S.nodes8, S.tris, S.mesh[I.mesh].root, Oi, Di, rDi, i, h, stk, sp) &&
+            ANY)
           return true;
       }
       const uint32_t ihit = hits & imask;
       if (ihit) {
-        if (gmask && sp < STACK) {
-          stk[(2 * sp) * BLOCK] = gbase;
-          stk[(2 * sp + 1) * BLOCK] = gmask | (gimask << 8);
+        if (gmask && sp < stk.cap) {
+          stack_put<STACK, BLOCK>(stk, sp, gbase, gmask | (gimask << 8));
           sp++;
         }
         gbase = b.x;
@@ -157,8 +195,8 @@ __device__ __forceinline__ bool tlas_traverse8(const SceneDev& S, const Ray& r, 
     if (!gmask) {
       if (sp == 0) break;
       sp--;
-      gbase = stk[(2 * sp) * BLOCK];
-      const uint32_t m = stk[(2 * sp + 1) * BLOCK];
+      uint32_t m;
+      stack_get<STACK, BLOCK>(stk, sp, gbase, m);
       gmask = m & 0xFFu;
       gimask = m >> 8;
     }
@@ -171,7 +209,7 @@ __device__ __forceinline__ bool tlas_traverse8(const SceneDev& S, const Ray& r, 
 }
 
 template <int STACK, int BLOCK>
-__device__ __forceinline__ Hit scene_closest8(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
+__device__ __forceinline__ Hit scene_closest8(const SceneDev& S, const Ray& r, float tmax, const LaneStack& stk) {
   Hit h;
   h.t = tmax; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;
   if (S.tlas) {
@@ -189,7 +227,7 @@ __device__ __forceinline__ Hit scene_closest8(const SceneDev& S, const Ray& r, f
 }
 
 template <int STACK, int BLOCK>
-__device__ __forceinline__ bool scene_anyhit8(const SceneDev& S, const Ray& r, float tmax, uint32_t* stk) {
+__device__ __forceinline__ bool scene_anyhit8(const SceneDev& S, const Ray& r, float tmax, const LaneStack& stk) {
   if (S.tlas) {
     Hit h;
     h.t = tmax; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;

@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, T
 }
 
 // ---- one traversal launch: closest hits of P(iter) (iter < iters) + any hits of S(iter - 1) (iter > 0)
-template <int REFILL, int STACK, int WAVES, int TAILN, bool TLAS>
+template <int REFILL, int STACK, int WAVES, int TAILN, bool TLAS, bool SPILL = false>
 __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, uint32_t iter, uint32_t iters) {
   __shared__ uint32_t lds_stack[2 * STACK * 64];
   __shared__ uint32_t prefP[kNSub + 1], prefS[kNSub + 1];
@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   unsigned long long* tl = B.tl ? B.tl + ((size_t)iter * kTlWaves + blockIdx.x) * 4 : nullptr;
   bool seen_drain = false;
   if (tl && threadIdx.x == 0) tl[0] = __builtin_amdgcn_s_memrealtime();
-  trav8_persistent<2, STACK, REFILL, TAILN, TLAS>(
+  trav8_persistent<2, STACK, REFILL, TAILN, TLAS, SPILL>(
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) {
         const uint32_t got = fetch_some(fctr, total, part, base, want);
@@ -456,9 +456,17 @@ void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_
     hipLaunchKernelGGL((k_trace2<32, STACK, WAVES, TAILN, false>), dim3(256u * 4u * WAVES), dim3(64), 0, c.stream, S,
                        B, it, iters);
 }
-// persistent traversal occupancy (waves/SIMD) -> LDS stack groups per lane
+// persistent traversal occupancy (waves/SIMD) -> LDS stack groups per lane; a BVH deeper than the 18 LDS
+// groups at 4 waves/SIMD hold runs the 4-wave form with the HBM spill columns (S.spill)
 static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
-  if (c.occ == 8) launch_t2<8, 8, 32>(c, S, B, it, iters);
+  if (S.spill) {
+    if (S.tlas)
+      hipLaunchKernelGGL((k_trace2<32, 18, 4, 32, true, true>), dim3(kSpillTraceBlocks), dim3(64), 0, c.stream, S, B,
+                         it, iters);
+    else
+      hipLaunchKernelGGL((k_trace2<32, 18, 4, 32, false, true>), dim3(kSpillTraceBlocks), dim3(64), 0, c.stream, S,
+                         B, it, iters);
+  } else if (c.occ == 8) launch_t2<8, 8, 32>(c, S, B, it, iters);
   else if (c.occ == 7) launch_t2<9, 7, 64>(c, S, B, it, iters);
   else if (c.occ == 6) launch_t2<11, 6, 64>(c, S, B, it, iters);
   else if (c.occ == 5) launch_t2<14, 5, 32>(c, S, B, it, iters);

@@ -260,6 +260,24 @@ def instance_field(n: int = 300, seed: int = 5) -> SceneData:
                                name=f"instance-field-{n}")
 
 
+def deep_bvh(n: int = 1000, r: float = 1.04) -> SceneData:
+    """A pathological mesh whose SAH tree is 23 levels deep (deeper than the LDS traversal stacks hold, so the
+    HIP path spills to HBM, prt_traverse8.h LaneStack): n nested triangles in the planes z = 0.01 k, triangle k
+    spanning r^k around the origin, so every box on the spine contains the rays and its siblings are stacked."""
+    from . import ingest
+    k = np.arange(n, dtype=np.float64)
+    a, z = r ** k, 0.01 * k
+    P = np.stack([np.stack([-a, -a, z], 1), np.stack([2 * a, -a, z], 1), np.stack([-a, 2 * a, z], 1)], 1)
+    P = P.reshape(-1, 3).astype(F32)
+    N = np.tile(np.array([0.0, 0.0, -1.0], F32), (3 * n, 1))
+    UV = np.tile(np.array([[0.1, 0.1], [0.9, 0.1], [0.1, 0.9]], F32), (n, 1))
+    m = ingest.mesh_from_indexed(P, N, UV, np.arange(3 * n).reshape(-1, 3))
+    albedo, metalness, normal, emis = procedural_textures()
+    m.albedo, m.metalness = 0, 1
+    return SceneData([m], [albedo, metalness], [(0, IDENTITY.copy())], scene1_lights(), procedural_sky(),
+                     np.array([0.4, 0.3, -3.0], F32), np.array([0.0, 0.0, 0.5], F32), f"deep-bvh-{n}")
+
+
 def ceiling_light(corner=(-1.5, 4.0, -1.0), edge_u=(3.0, 0.0, 0.0), edge_v=(0.0, 0.0, 2.0), radiance=(8.0, 7.0, 6.0),
                   two_sided=False) -> dict:
     """One quad area light (extension; the reference's AreaLight is never sampled): by default a 3 x 2 panel

@@ -325,3 +325,32 @@ def test_dynamic_instances_stream_ordered(gpu_ctx):
     for sd, o in ((sd0, out[0]), (sd1, out[1])):
         a_o, _, _, _ = oracle.OracleScene(sd, W, H).render(W, H, spp=2, bounces=3, flags=flags)
         assert np.array_equal(o.cpu().numpy(), a_o)
+
+
+def test_deep_bvh_spills_to_hbm(gpu_ctx):
+    """A BLAS deeper than every LDS stack (scenes.deep_bvh: 23 levels against 16 in the query kernels and 18 in the
+    4-wave persistent form): the traversal stacks continue in HBM spill columns (tinybvh walks with a 64-entry
+    stack, tiny_bvh.h:6315), and results equal the oracle's -- hit records and a rendered frame."""
+    sd = scenes.deep_bvh()
+    W, H = 64, 48
+    gpu_scene(gpu_ctx, sd, W, H)
+    assert gpu_ctx.scene_info().max_depth > 19  # past the 4-wave persistent LDS stack too
+    osc = oracle.OracleScene(sd, W, H)
+    rng = np.random.default_rng(3)
+    O = np.tile(np.array([0.0, 0.0, -2.0], np.float32), (20000, 1))
+    O[:, :2] = rng.uniform(-0.5, 0.5, (20000, 2)).astype(np.float32)
+    D = np.zeros_like(O)
+    D[:, :2] = rng.uniform(-0.3, 0.3, (20000, 2)).astype(np.float32)
+    D[:, 2] = 1.0
+    t, u, v, prim, inst = osc.intersect(O, D)
+    g = gpu_ctx.intersect(O, D)
+    hit = t < 1e30
+    assert hit.sum() > 10000
+    assert np.array_equal(hit, g["t"] < 1e30) and np.array_equal(prim[hit], g["prim"][hit])
+    assert np.array_equal(t[hit], g["t"][hit])
+    tmax = np.where(hit, t * np.float32(0.999), np.float32(1e30)).astype(np.float32)
+    assert np.array_equal(osc.occluded(O, D, tmax), gpu_ctx.occluded(O, D, tmax))
+    a_o, r_o, _, s_o = osc.render(W, H, spp=2, bounces=3)
+    a_g, r_g, s_g = gpu_ctx.render(W, H, 2, 3)
+    assert (s_g.segments, s_g.shadow_rays) == (s_o.segments, s_o.shadow_rays)
+    assert np.array_equal(a_o[:, :3], a_g[:, :3]) and np.array_equal(r_o, r_g)
