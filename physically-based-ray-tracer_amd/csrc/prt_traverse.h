@@ -36,6 +36,9 @@ __device__ __forceinline__ Ray make_ray(V3 origin, V3 dir) {
 
 constexpr float kNearPad = 0.99999f;
 constexpr float kFarPad = 1.00001f;
+// both pads on the near side: tn * kPadRatio <= tf accepts whatever tn * kNearPad <= tf * kFarPad accepts
+// (kPadRatio < kNearPad / kFarPad), and tn * kPadRatio <= tlimit whatever tn * kNearPad <= tlimit does
+constexpr float kPadRatio = 0.99998f;
 
 // BVH8_CPU leaf lane arithmetic, same operation order (Core/tiny_bvh.h:6413-6430)
 __device__ __forceinline__ bool mt_test(const TriMT* __restrict__ tp, const V3& O, const V3& D, float& t_out,

@@ -41,8 +41,8 @@ __device__ __forceinline__ uint32_t node8_hits(const uint4& a, const uint4& c, c
     const float tnx = __builtin_fmaf(byte_f(wnx, b), bx, ax), tfx = __builtin_fmaf(byte_f(wfx, b), bx, ax);
     const float tny = __builtin_fmaf(byte_f(wny, b), by, ay), tfy = __builtin_fmaf(byte_f(wfy, b), by, ay);
     const float tnz = __builtin_fmaf(byte_f(wnz, b), bz, az), tfz = __builtin_fmaf(byte_f(wfz, b), bz, az);
-    const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f)) * kNearPad;
-    const float tf = fminf(fminf(tfx, tfy), tfz) * kFarPad;
+    const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.0f)) * kPadRatio;  // both pads (prt_traverse.h)
+    const float tf = fminf(fminf(tfx, tfy), tfz);
     if (tn <= tf && tn <= tlimit) hits |= 1u << k;
   }
   return hits;
