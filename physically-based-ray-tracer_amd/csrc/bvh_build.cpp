@@ -143,6 +143,257 @@ struct Builder {
   }
 };
 
+// ---- spatial-split binary builder (SBVH: Stich, Friedrich, Dietrich 2009, "Spatial Splits in Bounding Volume
+// Hierarchies"; what the reference's BVH::BuildHQ does, Core/tiny_bvh.h:1968-2284).  A node may split its
+// references at a plane, cutting the triangles that straddle it: each side keeps the bounds of its part of the
+// triangle (clipped against the plane, inside the reference's box), so a triangle can sit in several leaves.
+// Spatial splits are tried only where the best object split's children overlap by more than alpha of the root
+// area, and duplication stops once the references reach kSbvhSlack x the triangle count.  The output is the
+// same binary tree form as Builder (nodes with children after their parent, leaf ranges of idx).
+constexpr double kSbvhAlpha = 1e-5;
+constexpr double kSbvhSlack = 1.5;
+
+struct SpatialBuilder {
+  struct Ref {
+    uint32_t prim;
+    Box box;
+  };
+  const float* tri = nullptr;
+  int max_leaf = 3;
+  size_t refs_total = 0, refs_cap = 0;
+  double root_area = 0;
+  std::vector<Node2>* nodes = nullptr;
+  std::vector<uint32_t>* idx = nullptr;
+
+  // bounds of the part of triangle `p` with lo <= x[ax] <= hi, intersected with `clip` (double arithmetic)
+  Box clip_part(uint32_t p, int ax, double lo, double hi, const Box& clip) const {
+    const float* a = tri + 12 * (size_t)p;
+    double v[3][3];
+    for (int j = 0; j < 3; j++)
+      for (int k = 0; k < 3; k++) v[j][k] = a[4 * j + k];
+    double blo[3] = {1e300, 1e300, 1e300}, bhi[3] = {-1e300, -1e300, -1e300};
+    auto grow = [&](const double* q) {
+      for (int k = 0; k < 3; k++) { blo[k] = std::min(blo[k], q[k]); bhi[k] = std::max(bhi[k], q[k]); }
+    };
+    for (int j = 0; j < 3; j++) {
+      const double* P = v[j];
+      const double* Q = v[(j + 1) % 3];
+      if (P[ax] >= lo && P[ax] <= hi) grow(P);
+      for (const double c : {lo, hi}) {
+        if ((P[ax] < c && Q[ax] > c) || (P[ax] > c && Q[ax] < c)) {
+          const double t = (c - P[ax]) / (Q[ax] - P[ax]);
+          double X[3];
+          for (int k = 0; k < 3; k++) X[k] = P[k] + t * (Q[k] - P[k]);
+          X[ax] = c;
+          grow(X);
+        }
+      }
+    }
+    Box b;
+    for (int k = 0; k < 3; k++) {
+      // outward rounding to float, then the reference's own box
+      b.lo[k] = std::max(clip.lo[k], std::nextafter((float)blo[k], -3e38f));
+      b.hi[k] = std::min(clip.hi[k], std::nextafter((float)bhi[k], 3e38f));
+    }
+    return b;
+  }
+
+  void build(int32_t T, std::vector<Node2>& out_nodes, std::vector<uint32_t>& out_idx) {
+    nodes = &out_nodes;
+    idx = &out_idx;
+    std::vector<Ref> refs(T);
+    Box root;
+    root.reset();
+    for (int32_t i = 0; i < T; i++) {
+      const float* a = tri + 12 * (size_t)i;
+      refs[i].prim = (uint32_t)i;
+      refs[i].box.reset();
+      refs[i].box.grow(a); refs[i].box.grow(a + 4); refs[i].box.grow(a + 8);
+      root.grow(refs[i].box);
+    }
+    root_area = std::max(root.area(), 1e-30);
+    refs_total = (size_t)T;
+    refs_cap = (size_t)((double)T * kSbvhSlack);
+    nodes->clear();
+    nodes->reserve(2 * (size_t)T);
+    idx->clear();
+    nodes->push_back(Node2());
+    struct Work { int32_t ni; std::vector<Ref> refs; };
+    std::vector<Work> work;
+    work.push_back({0, std::move(refs)});
+    while (!work.empty()) {
+      Work w = std::move(work.back());
+      work.pop_back();
+      split(w.ni, w.refs, work);
+    }
+  }
+
+  template <class W>
+  void split(int32_t ni, std::vector<Ref>& refs, W& work) {
+    const int32_t count = (int32_t)refs.size();
+    Box b, cb;
+    b.reset(); cb.reset();
+    for (const Ref& r : refs) {
+      b.grow(r.box);
+      float c[3];
+      for (int k = 0; k < 3; k++) c[k] = 0.5f * (r.box.lo[k] + r.box.hi[k]);
+      cb.grow(c);
+    }
+    (*nodes)[ni].box = b;
+    // subtrees are finished depth first, so this node's leaves are idx[first, first + count) whatever its form
+    (*nodes)[ni].first = (int32_t)idx->size();
+    (*nodes)[ni].count = count;
+    auto make_leaf = [&]() {
+      for (const Ref& r : refs) idx->push_back(r.prim);
+    };
+    if (count <= 1) { make_leaf(); return; }
+    // object split: binned SAH over the reference centroids
+    double best = 1e300;
+    int bax = -1, bsplit = -1;
+    Box bl_best, br_best;
+    for (int ax = 0; ax < 3; ax++) {
+      const float lo = cb.lo[ax], hi = cb.hi[ax];
+      if (!(hi > lo)) continue;
+      Box bins[kBins];
+      int cnt[kBins] = {0};
+      for (int k = 0; k < kBins; k++) bins[k].reset();
+      const float sc = kBins / (hi - lo);
+      for (const Ref& r : refs) {
+        const float c = 0.5f * (r.box.lo[ax] + r.box.hi[ax]);
+        const int k = std::min(kBins - 1, std::max(0, (int)((c - lo) * sc)));
+        cnt[k]++;
+        bins[k].grow(r.box);
+      }
+      Box lacc[kBins - 1];
+      int lc[kBins - 1];
+      Box acc; acc.reset();
+      int c = 0;
+      for (int k = 0; k < kBins - 1; k++) {
+        if (cnt[k]) acc.grow(bins[k]);
+        c += cnt[k];
+        lacc[k] = acc; lc[k] = c;
+      }
+      acc.reset(); c = 0;
+      for (int k = kBins - 1; k > 0; k--) {
+        if (cnt[k]) acc.grow(bins[k]);
+        c += cnt[k];
+        if (!lc[k - 1] || !c) continue;
+        const double cost = lacc[k - 1].area() * lc[k - 1] + acc.area() * c;
+        if (cost < best) { best = cost; bax = ax; bsplit = k - 1; bl_best = lacc[k - 1]; br_best = acc; }
+      }
+    }
+    // spatial split: only where the object split's children overlap noticeably, within the duplication budget
+    double sbest = 1e300;
+    int sax = -1;
+    double splane = 0;
+    if (bax >= 0 && count > 2 * max_leaf && refs_total < refs_cap) {
+      Box ov;
+      for (int k = 0; k < 3; k++) { ov.lo[k] = std::max(bl_best.lo[k], br_best.lo[k]); ov.hi[k] = std::min(bl_best.hi[k], br_best.hi[k]); }
+      if (ov.area() / root_area > kSbvhAlpha) {
+        for (int ax = 0; ax < 3; ax++) {
+          const double lo = b.lo[ax], hi = b.hi[ax], w = (hi - lo) / kBins;
+          if (!(w > 0)) continue;
+          Box bins[kBins];
+          int enter[kBins] = {0}, leave[kBins] = {0};
+          for (int k = 0; k < kBins; k++) bins[k].reset();
+          auto bin_of = [&](double x) { return std::min(kBins - 1, std::max(0, (int)((x - lo) / w))); };
+          for (const Ref& r : refs) {
+            const int b0 = bin_of(r.box.lo[ax]), b1 = bin_of(r.box.hi[ax]);
+            if (b0 == b1) {
+              bins[b0].grow(r.box);
+            } else {
+              // binning prices the reference's box cut at the bin planes (the exact triangle clip is done only for
+              // the chosen plane, below): an upper bound of each part, at a fraction of the cost
+              for (int k = b0; k <= b1; k++) {
+                Box part = r.box;
+                if (k > b0) part.lo[ax] = std::max(part.lo[ax], (float)(lo + k * w));
+                if (k < b1) part.hi[ax] = std::min(part.hi[ax], (float)(lo + (k + 1) * w));
+                bins[k].grow(part);
+              }
+            }
+            enter[b0]++;
+            leave[b1]++;
+          }
+          Box lacc[kBins - 1];
+          int lcnt[kBins - 1];
+          Box acc; acc.reset();
+          int c = 0;
+          for (int k = 0; k < kBins - 1; k++) {
+            acc.grow(bins[k]);
+            c += enter[k];
+            lacc[k] = acc; lcnt[k] = c;
+          }
+          acc.reset(); c = 0;
+          for (int k = kBins - 1; k > 0; k--) {
+            acc.grow(bins[k]);
+            c += leave[k];
+            if (!lcnt[k - 1] || !c || (lcnt[k - 1] == count && c == count)) continue;
+            const double cost = lacc[k - 1].area() * lcnt[k - 1] + acc.area() * c;
+            if (cost < sbest) { sbest = cost; sax = ax; splane = lo + k * w; }
+          }
+        }
+      }
+    }
+    const double parea = b.area();
+    const double leaf_cost = (double)count;
+    const double obj_cost = parea > 0 && bax >= 0 ? 1.0 + best / parea : 1e300;
+    const double sp_cost = parea > 0 && sax >= 0 ? 1.0 + sbest / parea : 1e300;
+    if (count <= max_leaf && leaf_cost <= std::min(obj_cost, sp_cost)) { make_leaf(); return; }
+    std::vector<Ref> L, R;
+    if (sax >= 0 && sp_cost < obj_cost) {
+      // cut at splane: references entirely on one side stay whole, straddling ones are clipped into both
+      const float s = (float)splane;
+      for (const Ref& r : refs) {
+        if (r.box.hi[sax] <= s) {
+          L.push_back(r);
+        } else if (r.box.lo[sax] >= s) {
+          R.push_back(r);
+        } else {
+          Ref a = r, c = r;
+          a.box = clip_part(r.prim, sax, -1e300, splane, r.box);
+          c.box = clip_part(r.prim, sax, splane, 1e300, r.box);
+          const bool ea = a.box.lo[0] <= a.box.hi[0] && a.box.lo[1] <= a.box.hi[1] && a.box.lo[2] <= a.box.hi[2];
+          const bool ec = c.box.lo[0] <= c.box.hi[0] && c.box.lo[1] <= c.box.hi[1] && c.box.lo[2] <= c.box.hi[2];
+          if (ea) L.push_back(a);
+          if (ec) R.push_back(c);
+          if (!ea && !ec) L.push_back(r);  // degenerate clip: keep the whole reference
+          if (ea && ec) refs_total++;
+        }
+      }
+      if (L.empty() || R.empty() || ((int32_t)L.size() == count && (int32_t)R.size() == count)) {
+        L.clear(); R.clear();
+        sax = -1;  // no progress: object split instead
+      }
+    }
+    if (L.empty() && R.empty()) {
+      if (bax < 0) {  // coincident centroids: halve the list
+        L.assign(refs.begin(), refs.begin() + count / 2);
+        R.assign(refs.begin() + count / 2, refs.end());
+      } else {
+        const float lo = cb.lo[bax], sc = kBins / (cb.hi[bax] - lo);
+        for (const Ref& r : refs) {
+          const float c = 0.5f * (r.box.lo[bax] + r.box.hi[bax]);
+          const int k = std::min(kBins - 1, std::max(0, (int)((c - lo) * sc)));
+          (k <= bsplit ? L : R).push_back(r);
+        }
+        if (L.empty() || R.empty()) {
+          std::vector<Ref> all = std::move(L.empty() ? R : L);
+          L.assign(all.begin(), all.begin() + count / 2);
+          R.assign(all.begin() + count / 2, all.end());
+        }
+      }
+    }
+    std::vector<Ref>().swap(refs);
+    const int32_t l = (int32_t)nodes->size();
+    nodes->push_back(Node2());
+    nodes->push_back(Node2());
+    (*nodes)[ni].left = l;
+    (*nodes)[ni].right = l + 1;
+    work.push_back({l + 1, std::move(R)});
+    work.push_back({l, std::move(L)});
+  }
+};
+
 }  // namespace
 
 // Conservative inflation: the traversal must never cull a box that holds a triangle the MT test
@@ -250,11 +501,18 @@ struct WideDp {
 constexpr float kWideNodeCost = 1.0f, kWideTriCost = 1.0f;  // tri cost swept 0.15-5 on C4: flat above 1
 
 template <class NodeT, class Fmt, class Out>
-void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out) {
+void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out, bool spatial = false) {
   Builder B;
   B.tri = triangles;
   B.max_leaf = std::max(1, std::min(4, max_leaf));
-  B.build(T);
+  if (spatial) {
+    SpatialBuilder SB;
+    SB.tri = triangles;
+    SB.max_leaf = B.max_leaf;
+    SB.build(T, B.nodes, B.idx);
+  } else {
+    B.build(T);
+  }
   for (int k = 0; k < 3; k++) { out.bmin[k] = B.nodes[0].box.lo[k]; out.bmax[k] = B.nodes[0].box.hi[k]; }
   out.tris.reserve(T);
   const char* ce = std::getenv("PRT_COLLAPSE");
@@ -390,9 +648,9 @@ void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out) {
 
 }  // namespace
 
-BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf) {
+BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf, bool spatial) {
   BuiltBlas8 out;
-  build_wide8<Node8, Fmt8>(triangles, T, max_leaf, out);
+  build_wide8<Node8, Fmt8>(triangles, T, max_leaf, out, spatial);
   return out;
 }
 

@@ -45,7 +45,9 @@ struct BuiltBlas8 {
   int depth = 0;
   int64_t leaves = 0;
 };
-BuiltBlas8 build_blas8(const float* triangles, int32_t tri_count, int max_leaf = 3);
+// spatial: spatial-split binary build (SBVH, as the reference's BuildHQ) instead of binned object splits; a
+// triangle may then be referenced by several leaves (tris holds one record per reference)
+BuiltBlas8 build_blas8(const float* triangles, int32_t tri_count, int max_leaf = 3, bool spatial = false);
 
 // ---- TLAS over instance world boxes (replaces BVH::Build over BLASInstances, Core/tiny_bvh.h:1732-1770): the same
 // binned SAH + SAH-optimal 8-wide collapse with one instance per leaf slot.  A TLAS node's leaf slot s names its

@@ -1,4 +1,4 @@
-// bvh_gpu.h -- on-device BLAS build (bvh_gpu.hip): LBVH + greedy 8-wide collapse into Node8 / TriMT.
+// bvh_gpu.h -- on-device BLAS build (bvh_gpu.hip): LBVH + SAH-optimal 8-wide collapse into Node8 / TriMT.
 #pragma once
 #include <hip/hip_runtime.h>
 

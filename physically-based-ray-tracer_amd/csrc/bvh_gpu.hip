@@ -8,16 +8,22 @@
 //   4. boxes bottom-up: one thread per leaf walks towards the root; the second child to arrive at a node
 //      (agent atomic) unions both boxes.  Boxes are stored write-through (sc1) and read with sc1 loads
 //      after the atomic, the in-launch hand-off of MI355X_MICROARCH.md (per-XCD L2s are not coherent)
-//   5. greedy 8-wide collapse, one launch per level: a wide node opens its largest-area child with more
-//      than max_leaf triangles until it has 8 children; subtrees of <= max_leaf triangles become leaf
-//      children.  Nodes are quantised and laid out exactly as the host builder's Node8 (bvh_build.h):
-//      interior children contiguous (one atomic per node), leaf triangles contiguous (one atomic per node)
+//      In the same bottom-up pass, the SAH-optimal 8-wide collapse table of every internal node (Ylitie, Karras,
+//      Laine 2017 sec. 3.1, as bvh_build.cpp WideDp): C(n, i) = cheapest cost of subtree n in at most i slots,
+//      from its children's tables, in double, with the chosen split of the slots (Dk) and the leaf decision
+//   5. 8-wide collapse, one launch per level: a wide node takes the <= 8 slots the table chose for it (a slot
+//      whose single-slot form is a leaf becomes a leaf child with all its triangles, contiguous in key order).
+//      PRT_COLLAPSE=greedy instead opens the largest-area child with more than max_leaf triangles until 8.
+//      Nodes are quantised and laid out exactly as the host builder's Node8 (bvh_build.h): interior
+//      children contiguous (one atomic per node), leaf triangles contiguous (one atomic per node)
 // The result is a different tree from the host's SAH build, so traversal cost differs; hits do not (the
 // hit rule is BVH-independent), which is what the GPU tests check.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 
 #include "bvh_build.h"
 #include "bvh_gpu.h"
@@ -49,6 +55,27 @@ __device__ __forceinline__ void st_sc1(float* p, float v) {
 __device__ __forceinline__ float ld_sc1(const float* p) {
   return __uint_as_float(__hip_atomic_load(reinterpret_cast<uint32_t*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1_d(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1_d(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<double*>(p)),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// collapse table of one internal node: C[1..8] (slot 0 unused), and in `dec` the decisions:
+// bits 0-23: Dk[j] for j = 2..8 (3 bits each: the left child's share 1..7), bits 24-30: prev[i] for i = 2..8
+// (C(n, i) == C(n, i - 1): use fewer slots), bit 31: leaf1 (the single-slot form of n is a leaf)
+struct DpTab {
+  double* C;      // 8 per internal node: C(n, i) at [8 n + i - 1]
+  uint32_t* dec;  // 1 per internal node
+};
+constexpr double kDpNode = 1.0, kDpTri = 1.0;  // bvh_build.cpp kWideNodeCost / kWideTriCost
+__device__ __forceinline__ double area6d(const float* b) {
+  const double dx = (double)b[3] - b[0], dy = (double)b[4] - b[1], dz = (double)b[5] - b[2];
+  return dx * dy + dy * dz + dz * dx;
 }
 
 // ---- 1. centroid bounds
@@ -133,7 +160,7 @@ __global__ void __launch_bounds__(kB) k_radix_tree(const unsigned long long* __r
 __global__ void __launch_bounds__(kB) k_boxes(const float4* __restrict__ tri, const unsigned long long* __restrict__ keys,
                                               int n, const int* __restrict__ left, const int* __restrict__ right,
                                               const int* __restrict__ parent, float* box, uint32_t* flag,
-                                              uint32_t* first, uint32_t* count) {
+                                              uint32_t* first, uint32_t* count, DpTab dp, int max_leaf) {
   const int i = (int)(blockIdx.x * kB + threadIdx.x);
   if (i >= n) return;
   const uint32_t prim = (uint32_t)keys[i];
@@ -154,11 +181,45 @@ __global__ void __launch_bounds__(kB) k_boxes(const float4* __restrict__ tri, co
     const int p = parent[node];
     if (p < 0 || p >= n - 1) return;                    // malformed tree: the host checks the node count
     if (atomicAdd(flag + p, 1u) == 0u) return;          // the sibling's thread finishes the parent
-    const float* l = box + 6 * (size_t)left[p];
-    const float* r = box + 6 * (size_t)right[p];
+    const int lc = left[p], rc = right[p];
+    const float* l = box + 6 * (size_t)lc;
+    const float* r = box + 6 * (size_t)rc;
     float* o = box + 6 * (size_t)p;
-    for (int k = 0; k < 3; k++) st_sc1(o + k, fminf(ld_sc1(l + k), ld_sc1(r + k)));
-    for (int k = 3; k < 6; k++) st_sc1(o + k, fmaxf(ld_sc1(l + k), ld_sc1(r + k)));
+    float pb[6], lb[6], rb[6];
+    for (int k = 0; k < 6; k++) { lb[k] = ld_sc1(l + k); rb[k] = ld_sc1(r + k); }
+    for (int k = 0; k < 3; k++) { pb[k] = fminf(lb[k], rb[k]); st_sc1(o + k, pb[k]); }
+    for (int k = 3; k < 6; k++) { pb[k] = fmaxf(lb[k], rb[k]); st_sc1(o + k, pb[k]); }
+    if (dp.C) {  // collapse table of p from its children's (a binary leaf: one triangle, every C = its leaf cost)
+      double cl[9], cr[9];
+      const double al = area6d(lb) * kDpTri, ar = area6d(rb) * kDpTri;
+      for (int i = 1; i <= 8; i++) {
+        cl[i] = lc >= n - 1 ? al : ld_sc1_d(dp.C + 8 * (size_t)lc + i - 1);
+        cr[i] = rc >= n - 1 ? ar : ld_sc1_d(dp.C + 8 * (size_t)rc + i - 1);
+      }
+      const double A = fmax(area6d(pb), 1e-30);
+      const double leafc = (int)count[p] <= max_leaf ? A * kDpTri * (double)count[p] : 1e300;
+      double D[9];
+      uint32_t dec = 0;
+      for (int j = 2; j <= 8; j++) {
+        D[j] = 1e300;
+        uint32_t bk = 1;
+        for (int k = 1; k < j; k++) {
+          const double c = cl[k] + cr[j - k];
+          if (c < D[j]) { D[j] = c; bk = (uint32_t)k; }
+        }
+        dec |= bk << (3 * (j - 2));
+      }
+      const double intc = A * kDpNode + D[8];
+      if ((int)count[p] <= max_leaf && leafc <= intc) dec |= 1u << 31;
+      double C = fmin(leafc, intc);
+      st_sc1_d(dp.C + 8 * (size_t)p, C);
+      for (int i = 2; i <= 8; i++) {
+        if (C <= D[i]) dec |= 1u << (24 + i - 2);
+        else C = D[i];
+        st_sc1_d(dp.C + 8 * (size_t)p + i - 1, C);
+      }
+      dp.dec[p] = dec;
+    }
     node = p;
   }
 }
@@ -194,16 +255,37 @@ __global__ void __launch_bounds__(kB) k_collapse(const float4* __restrict__ tri,
                                                  const float* __restrict__ box, const uint32_t* __restrict__ first,
                                                  const uint32_t* __restrict__ count, int max_leaf,
                                                  const Task* __restrict__ tasks, uint32_t ntasks, Task* next,
-                                                 uint32_t* ctr, Node8* nodes, TriMT* tris) {
+                                                 uint32_t* ctr, Node8* nodes, TriMT* tris, DpTab dp) {
   const uint32_t t = blockIdx.x * kB + threadIdx.x;
   if (t >= ntasks) return;
   const Task tk = tasks[t];
   const int nn = 2 * n - 1;
   if (tk.n2 < 0 || tk.n2 >= nn || tk.n8 >= (uint32_t)n) { atomicOr(ctr + 3, 0x80000000u); return; }
-  auto is_leaf = [&](int v) { return v >= n - 1 || (int)count[v] <= max_leaf; };
+  // a child slot's form: leaf (all its triangles) or a wide node of its own
+  auto is_leaf = [&](int v) { return v >= n - 1 || (dp.dec ? (dp.dec[v] >> 31) != 0 : (int)count[v] <= max_leaf); };
   int ch[8];
   int nc = 0;
-  if (is_leaf(tk.n2)) {
+  if (dp.dec && !is_leaf(tk.n2)) {
+    // the slots the table chose: expand(n) = collect(left, Dk[n][8]) + collect(right, 8 - Dk[n][8]), where
+    // collect(v, i) = v if i == 1 or v is a leaf / its own form; collect(v, i - 1) if prev; else split again
+    int st_n[16], st_i[16], sp = 0;
+    const uint32_t d0 = dp.dec[tk.n2];
+    const int k0 = (int)((d0 >> 18) & 7u);  // Dk[n][8]
+    st_n[sp] = right[tk.n2]; st_i[sp++] = 8 - k0;
+    st_n[sp] = left[tk.n2]; st_i[sp++] = k0;
+    while (sp > 0 && nc < 8) {
+      const int v = st_n[--sp];
+      int i = st_i[sp];
+      if (v >= n - 1 || i <= 1) { ch[nc++] = v; continue; }
+      const uint32_t d = dp.dec[v];
+      while (i > 1 && ((d >> (24 + i - 2)) & 1u)) i--;
+      if (i <= 1) { ch[nc++] = v; continue; }
+      const int k = (int)((d >> (3 * (i - 2))) & 7u);
+      if (sp + 2 > 16) { atomicOr(ctr + 3, 0x80000000u); return; }
+      st_n[sp] = right[v]; st_i[sp++] = i - k;
+      st_n[sp] = left[v]; st_i[sp++] = k;
+    }
+  } else if (is_leaf(tk.n2)) {
     ch[nc++] = tk.n2;
   } else {
     ch[nc++] = left[tk.n2];
@@ -355,6 +437,7 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
   int *left = nullptr, *right = nullptr, *parent = nullptr;
   uint32_t *first = nullptr, *count = nullptr, *flag = nullptr, *ctr = nullptr, *cb = nullptr;
   float* box = nullptr;
+  DpTab dp{nullptr, nullptr};
   Task *ta = nullptr, *tb = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -363,6 +446,7 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
     (void)hipFree(keys); (void)hipFree(keys2); (void)hipFree(left); (void)hipFree(right); (void)hipFree(parent);
     (void)hipFree(first); (void)hipFree(count); (void)hipFree(flag); (void)hipFree(ctr); (void)hipFree(cb);
     (void)hipFree(box); (void)hipFree(ta); (void)hipFree(tb); (void)hipFree(tmp);
+    (void)hipFree(dp.C); (void)hipFree(dp.dec);
     return e;
   };
   const float4* tri = reinterpret_cast<const float4*>(tri_dev);
@@ -372,6 +456,12 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
       (err = hipMalloc(&box, 24 * nn)) || (err = hipMalloc(&ta, sizeof(Task) * (size_t)n)) ||
       (err = hipMalloc(&tb, sizeof(Task) * (size_t)n)) || (err = hipMalloc(&ctr, 16)) || (err = hipMalloc(&cb, 24)))
     return fail(err);
+  const char* ce = std::getenv("PRT_COLLAPSE");
+  if (!(ce && std::strcmp(ce, "greedy") == 0) && n > 1) {
+    if ((err = hipMalloc(&dp.C, 8 * sizeof(double) * (size_t)(n - 1))) ||
+        (err = hipMalloc(&dp.dec, sizeof(uint32_t) * (size_t)(n - 1))))
+      return fail(err);
+  }
   const uint32_t init_cb[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
   if ((err = hipMemcpyAsync(cb, init_cb, 24, hipMemcpyHostToDevice, s))) return fail(err);
   hipLaunchKernelGGL(k_centroid_bounds, dim3(grid_of(n)), dim3(kB), 0, s, tri, (uint32_t)n, cb);
@@ -384,7 +474,7 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
     hipLaunchKernelGGL(k_radix_tree, dim3(grid_of(n - 1)), dim3(kB), 0, s, keys2, n, left, right, parent, first, count);
   if ((err = hipMemsetAsync(flag, 0, 4 * nn, s))) return fail(err);
   hipLaunchKernelGGL(k_boxes, dim3(grid_of(n)), dim3(kB), 0, s, tri, keys2, n, left, right, parent, box, flag, first,
-                     count);
+                     count, dp, max_leaf);
   // collapse, level by level from the binary root (node 0; the single leaf when n == 1)
   const Task t0{0, 0u};  // binary root: internal node 0, or the single leaf (node n - 1 = 0) when n == 1
   const uint32_t c0[4] = {1u, 0u, 0u, 0u};  // wide nodes used (the root), triangles used, next tasks
@@ -397,7 +487,7 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
     const uint32_t zero = 0;
     if ((err = hipMemcpyAsync(ctr + 2, &zero, 4, hipMemcpyHostToDevice, s))) return fail(err);
     hipLaunchKernelGGL(k_collapse, dim3(grid_of(ntasks)), dim3(kB), 0, s, tri, keys2, n, left, right, box, first,
-                       count, max_leaf, ta, ntasks, tb, ctr, nodes_out, tris_out);
+                       count, max_leaf, ta, ntasks, tb, ctr, nodes_out, tris_out, dp);
     if ((err = hipGetLastError())) return fail(err);
     uint32_t c[4];
     if ((err = hipMemcpyAsync(c, ctr, 16, hipMemcpyDeviceToHost, s)) || (err = hipStreamSynchronize(s)))

@@ -96,7 +96,7 @@ struct prt_ctx {
   std::vector<MeshHost> mesh_info;
   DevBuf nodes8, tris, stri, mesh;
   int max_depth = 0;
-  int builder = -1;  // BLAS builder: PRT_BUILDER_HOST_SAH / PRT_BUILDER_GPU_LBVH (-1: PRT_BUILDER env, else host)
+  int builder = -1;  // BLAS builder: PRT_BUILDER_HOST_SAH / _GPU_LBVH / _HOST_SBVH (-1: PRT_BUILDER env, else host)
   double build_ms = 0;  // wall time of the last prt_set_meshes BLAS builds
   int built_with = PRT_BUILDER_HOST_SAH;
   // instances
@@ -751,7 +751,9 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
   int builder = c->builder;
   if (builder < 0) {
     const char* e = std::getenv("PRT_BUILDER");
-    builder = (e && std::strcmp(e, "gpu") == 0) ? PRT_BUILDER_GPU_LBVH : PRT_BUILDER_HOST_SAH;
+    builder = (e && std::strcmp(e, "gpu") == 0)    ? PRT_BUILDER_GPU_LBVH
+              : (e && std::strcmp(e, "sbvh") == 0) ? PRT_BUILDER_HOST_SBVH
+                                                   : PRT_BUILDER_HOST_SAH;
   }
   const bool gpu = builder == PRT_BUILDER_GPU_LBVH;
   int rc = drain(c);
@@ -825,7 +827,7 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
         depth = built.depth; nnodes = (int64_t)built.nodes.size(); nleaves = built.leaves;
         return true;
       };
-      const bool ok = append(build_blas8(M.triangles, M.tri_count, 3), nodes8);
+      const bool ok = append(build_blas8(M.triangles, M.tri_count, 3, builder == PRT_BUILDER_HOST_SBVH), nodes8);
       if (!ok) return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
     }
     mh[i].prim_base = (uint32_t)stri.size();
@@ -896,7 +898,7 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
 }
 
 int prt_set_bvh_builder(prt_ctx* c, int32_t builder) {
-  if (!c || (builder != PRT_BUILDER_HOST_SAH && builder != PRT_BUILDER_GPU_LBVH))
+  if (!c || (builder != PRT_BUILDER_HOST_SAH && builder != PRT_BUILDER_GPU_LBVH && builder != PRT_BUILDER_HOST_SBVH))
     return fail(PRT_ERR_INVALID_ARGUMENT, "bad BLAS builder");
   c->builder = builder;
   PRT_FOR_MEMBERS(prt_set_bvh_builder(m, builder));

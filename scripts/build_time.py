@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """BLAS build time and traversal rate per builder: the host SAH + SAH-optimal collapse
-against the device LBVH + greedy collapse, on the bench scene (C4, 1M triangles) at the bench workload."""
+against the device LBVH + SAH-optimal collapse (and its greedy collapse, PRT_COLLAPSE=greedy), on the bench scene (C4, 1M triangles) at the bench workload."""
 import os
 import sys
 import time
@@ -12,15 +12,27 @@ import torch  # noqa: E402
 import prt  # noqa: E402
 from prt import _lib, scenes  # noqa: E402
 
-sd = scenes.config_c4() if "c3" not in sys.argv else scenes.config_c3()
+if "ship" in sys.argv:  # the textured Spaceship fixture (two instances; long thin triangles)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from test_golden_ref import ship_scene
+    sd = ship_scene()[0]
+else:
+    sd = scenes.config_c4() if "c3" not in sys.argv else scenes.config_c3()
 W, H = 1920, 1080
 ctx = prt.Context(0)
 ctx.set_stream(torch.cuda.current_stream().cuda_stream)
 scene = prt.Scene.from_data(sd)
 avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
 rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
-print("BLAS builders (C4):", flush=True)
-for name, b in (("host SAH", _lib.BUILDER_HOST_SAH), ("GPU LBVH", _lib.BUILDER_GPU_LBVH)):
+print(f"BLAS builders ({sd.name}):", flush=True)
+for name, b, col in (("host SAH", _lib.BUILDER_HOST_SAH, None), ("host SBVH", _lib.BUILDER_HOST_SBVH, None),
+                     ("GPU LBVH + optimal collapse", _lib.BUILDER_GPU_LBVH, None),
+                     ("GPU LBVH + greedy collapse", _lib.BUILDER_GPU_LBVH, "greedy")):
+    if col:
+        os.environ["PRT_COLLAPSE"] = col
+    else:
+        os.environ.pop("PRT_COLLAPSE", None)
     ctx.set_bvh_builder(b)
     ctx.set_scene(scene)
     ctx.set_scene(scene)  # second upload: warm caches / kernels

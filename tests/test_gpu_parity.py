@@ -276,15 +276,16 @@ def test_postfx_matches_oracle(gpu_ctx, preset, over, flags):
 
 @pytest.mark.parametrize("which", ["small_multi", "c2", "c3"])
 def test_gpu_builder_renders_identical(gpu_ctx, which):
-    """The device LBVH builder (PRT_BUILDER_GPU_LBVH) gives a different tree, but the hit rule is
-    BVH-independent: primary hits and rendered frames equal the host SAH build's bit for bit."""
+    """The device LBVH builder (PRT_BUILDER_GPU_LBVH) and the spatial-split host builder (PRT_BUILDER_HOST_SBVH,
+    triangles referenced from several leaves) give different trees, but the hit rule is BVH-independent:
+    primary hits and rendered frames equal the host SAH build's bit for bit."""
     import prt
     from prt import _lib
     sd = {"small_multi": lambda: scenes.multi_instance(scenes.config_small(60, 40)),
           "c2": scenes.config_c2, "c3": scenes.config_c3}[which]()
     W, H = 160, 96
     out = {}
-    for b in (_lib.BUILDER_HOST_SAH, _lib.BUILDER_GPU_LBVH):
+    for b in (_lib.BUILDER_HOST_SAH, _lib.BUILDER_GPU_LBVH, _lib.BUILDER_HOST_SBVH):
         gpu_ctx.set_bvh_builder(b)
         gpu_scene(gpu_ctx, sd, W, H)
         info = gpu_ctx.scene_info()
@@ -293,11 +294,12 @@ def test_gpu_builder_renders_identical(gpu_ctx, which):
         a, r, st = gpu_ctx.render(W, H, 4, 3)
         out[b] = (hits, a, r, st)
     gpu_ctx.set_bvh_builder(_lib.BUILDER_HOST_SAH)
-    h0, h1 = out[0][0], out[1][0]
-    for f in ("t", "u", "v", "prim", "inst"):
-        assert np.array_equal(h0[f], h1[f]), f
-    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])
-    assert out[0][3].segments == out[1][3].segments and out[0][3].shadow_rays == out[1][3].shadow_rays
+    for b in (1, 2):
+        h0, h1 = out[0][0], out[b][0]
+        for f in ("t", "u", "v", "prim", "inst"):
+            assert np.array_equal(h0[f], h1[f]), (b, f)
+        assert np.array_equal(out[0][1], out[b][1]) and np.array_equal(out[0][2], out[b][2])
+        assert out[0][3].segments == out[b][3].segments and out[0][3].shadow_rays == out[b][3].shadow_rays
 
 
 def test_dynamic_instances_stream_ordered(gpu_ctx):
