@@ -15,14 +15,15 @@
 //   k_wave_init                                   P(0) = primary rays r1
 //   for i = 0 .. iters:
 //     k_trace2(i)    closest hits of P(i)  +  any hits of S(i-1)         (one launch, mixed lanes)
-//     k_resolve2(i-1) NEE result of iteration i-1, (result, throughput) stack, path end, frame write
-//     k_miss2(i)     sky radiance of this iteration's misses (before shading rewrites the ray)
+//     k_resmiss2(i)  over P(i-1): NEE result of iteration i-1, (result, throughput) stack, path end, frame write;
+//                    then, for the items k_shade2(i-1) queued into P(i) (P(i) is a subset of P(i-1)), the sky
+//                    radiance of this iteration's misses (i = 0: k_miss2 over P(0))
 //     k_shade2(i)    hit attributes, NEE set-up -> S(i), BRDF sample or path-2 start -> P(i+1)
 //
-// Hazards (all kernels on one stream): P(i+1) reuses P(i-1)'s buffer after k_resolve2(i-1) read it;
-// S(i) reuses S(i-1)'s buffer after k_trace2(i) read it; k_resolve2(i-1) reads ne/nb/nf/vis/R/T of its
-// items before k_miss2(i) / k_shade2(i) overwrite them; rinfo keeps iteration i-1's status while info
-// already holds the state of the queued next ray.
+// Hazards (all kernels on one stream): P(i+1) reuses P(i-1)'s buffer after k_resmiss2(i) read it;
+// S(i) reuses S(i-1)'s buffer after k_trace2(i) read it; k_resmiss2(i) reads ne/nb/nf/vis/R/T of an item for
+// iteration i-1 before it (misses) or k_shade2(i) (hits) overwrites them; rinfo keeps iteration i-1's status
+// (and whether the item was queued) while info already holds the state of the queued next ray.
 #include "prt_launch.h"
 #include "prt_path.h"
 #include "prt_persist.h"
@@ -133,6 +134,32 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
 // ---- misses of P(iter) (:159): sky radiance (or 0) into ne, before k_shade2 replaces the ray.  EXT: a ray
 // that reaches the area light before any geometry ends there (ne = its MIS-weighted radiance, hit = miss).
 template <bool EXT>
+__device__ __forceinline__ void miss_item(const SceneDev& S, const TraceArgs& A, const WaveBufs& B, uint32_t item) {
+  float4 hh = B.hit[item];
+  if constexpr (EXT) {
+    if (S.area) {
+      const float4 o = B.ro[item], d = B.rd[item];
+      const AreaLight AL = area_light(S);
+      float tq, cl;
+      if (area_hit(AL, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), hh.x, tq, cl)) {
+        const uint32_t depth = B.info[item] & 0xFFu;
+        const float pdf = depth == 0 ? kFar : B.T[(size_t)(depth - 1) * B.n + item].w;
+        const V3 L = area_seen(AL, tq, cl, pdf);
+        B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
+        B.hit[item] = make_float4(kFar, 0.0f, 0.0f, 0.0f);
+        return;
+      }
+    }
+  }
+  if (hh.x < kFar) return;
+  V3 L = v3(0.0f, 0.0f, 0.0f);
+  if (A.flags & kSkybox) {
+    const float4 d = B.rd[item];
+    L = sample_sky(S, v3(d.x, d.y, d.z));
+  }
+  B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
+}
+template <bool EXT>
 __global__ void __launch_bounds__(kBlock) k_miss2(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter) {
   __shared__ uint32_t pref[kNSub + 1];
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
@@ -140,30 +167,7 @@ __global__ void __launch_bounds__(kBlock) k_miss2(SceneDev S, TraceArgs A, WaveB
   for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
     const uint32_t g = c * kBlock + threadIdx.x;
     if (g >= total) continue;
-    const uint32_t item = q[map_slot(pref, g, B.qcap)];
-    float4 hh = B.hit[item];
-    if constexpr (EXT) {
-      if (S.area) {
-        const float4 o = B.ro[item], d = B.rd[item];
-        const AreaLight AL = area_light(S);
-        float tq, cl;
-        if (area_hit(AL, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), hh.x, tq, cl)) {
-          const uint32_t depth = B.info[item] & 0xFFu;
-          const float pdf = depth == 0 ? kFar : B.T[(size_t)(depth - 1) * B.n + item].w;
-          const V3 L = area_seen(AL, tq, cl, pdf);
-          B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
-          B.hit[item] = make_float4(kFar, 0.0f, 0.0f, 0.0f);
-          continue;
-        }
-      }
-    }
-    if (hh.x < kFar) continue;
-    V3 L = v3(0.0f, 0.0f, 0.0f);
-    if (A.flags & kSkybox) {
-      const float4 d = B.rd[item];
-      L = sample_sky(S, v3(d.x, d.y, d.z));
-    }
-    B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
+    miss_item<EXT>(S, A, B, q[map_slot(pref, g, B.qcap)]);
   }
 }
 
@@ -310,11 +314,11 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
       }
     }
     if (active) {
-      B.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20);
       if (status != kStNeeCont) {
         if (EXT && S.has_diel) next = diel_next(B, item, depth, path);
         if (!next) next = start_path2(S, A, M, B, item, path);
       }
+      B.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20) | (next ? kRiQueued : 0u);
     }
     const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
     if (next) qn[sub * B.qcap + slot] = item;
@@ -346,8 +350,8 @@ __global__ void __launch_bounds__(kBlock) k_shade2_debug(SceneDev S, TraceArgs A
         const V3 L = debug_view(S, A.mode, ha, hit_inst(S, pk), hit_prim(S, pk));
         B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
       }
-      B.rinfo[item] = info & 0x1FFu;  // kStEndValue
       next = start_path2(S, A, M, B, item, (info >> 8) & 1u);
+      B.rinfo[item] = (info & 0x1FFu) | (next ? kRiQueued : 0u);  // kStEndValue
     }
     const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
     if (next) qn[sub * B.qcap + slot] = item;
@@ -356,91 +360,102 @@ __global__ void __launch_bounds__(kBlock) k_shade2_debug(SceneDev S, TraceArgs A
 
 // ---- NEE resolve of P(iter) (after k_trace2(iter + 1) traced S(iter)), stack, path end, frame write
 template <bool EXT>
-__global__ void __launch_bounds__(kBlock) k_resolve2(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter,
-                                                     float4* __restrict__ out) {
-  __shared__ uint32_t pref[kNSub + 1];
-  const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
-  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
+__device__ __forceinline__ void resolve_item(const SceneDev& S, const TraceArgs& A, const WaveBufs& B, uint32_t item,
+                                             float4* __restrict__ out) {
   const uint32_t fl = A.flags;
+  const uint32_t ri = B.rinfo[item];
+  const uint32_t depth = ri & 0xFFu, path = (ri >> 8) & 1u, status = (ri >> 16) & 3u, kind = (ri >> 20) & 3u;
+  const float4 ne = B.ne[item];
+  V3 L = v3(ne.x, ne.y, ne.z);
+  if (status == kStNeeEnd || status == kStNeeCont) {
+    const float4 nb = B.nb[item];
+    const uint32_t vw = B.vis[item];
+    const uint32_t vis = ((vw & 0xFFu) ? 1u : 0u) | ((vw & 0xFF00u) ? 2u : 0u) | ((vw & 0xFF0000u) ? 4u : 0u) |
+                         ((vw & 0xFF000000u) ? 8u : 0u);
+    V3 f[4];
+    const uint32_t nr = kind == 0 ? 4u : 1u;
+    for (uint32_t k = 0; k < 4; k++) {
+      if (k < nr) {
+        const float4 fk = B.nf[4 * (size_t)item + k];
+        f[k] = v3(fk.x, fk.y, fk.z);
+      } else {
+        f[k] = v3(0.0f, 0.0f, 0.0f);
+      }
+    }
+    V3 result = nee_resolve((int)kind, vis, L, v3(nb.x, nb.y, nb.z), f, fl);
+    if constexpr (EXT) {
+      if (reinterpret_cast<const uint8_t*>(B.vis)[4 * (size_t)B.n + item]) {  // area light unoccluded
+        const float4 a = B.na[item];
+        result = result + v3(a.x, a.y, a.z);
+      }
+    }
+    if (status == kStNeeCont) {  // the path goes on: result joins the stack
+      B.R[(size_t)depth * B.n + item] = make_float4(result.x, result.y, result.z, 0.0f);
+      return;
+    }
+    L = result;
+  }
+  if constexpr (EXT) {
+    // unwind through dielectric nodes: the end of a reflection subtree parks its radiance in T[level] and
+    // stops (the refraction subtree is already queued); the end of a refraction subtree combines (:369)
+    uint32_t ds = S.has_diel ? B.dst[item] : 0u;
+    bool parked = false;
+    for (int k = (int)depth - 1; k >= 0; k--) {
+      const size_t e = (size_t)k * B.n + item;
+      const uint32_t bit = 1u << k;
+      if (ds & bit) {
+        const float F = B.dro[e].w;
+        if (ds & (bit << 24)) {
+          L = dielectric_combine(F, L, v3(0.0f, 0.0f, 0.0f));
+        } else if (!(ds & (bit << 16))) {
+          B.T[e] = make_float4(L.x, L.y, L.z, kFar);
+          ds |= bit << 16;
+          parked = true;
+          break;
+        } else {
+          const float4 Lr = B.T[e];
+          L = dielectric_combine(F, v3(Lr.x, Lr.y, Lr.z), L);
+        }
+        ds &= ~(0x01010101u << k);
+        continue;
+      }
+      const float4 Rk = B.R[e], Tk = B.T[e];
+      L = v3(Rk.x, Rk.y, Rk.z) + L * v3(Tk.x, Tk.y, Tk.z);
+    }
+    if (S.has_diel) B.dst[item] = ds;
+    if (parked) return;
+  } else {
+    for (int k = (int)depth - 1; k >= 0; k--) {                                            // result + Trace(..) * throughput
+      const float4 Rk = B.R[(size_t)k * B.n + item], Tk = B.T[(size_t)k * B.n + item];
+      L = v3(Rk.x, Rk.y, Rk.z) + L * v3(Tk.x, Tk.y, Tk.z);
+    }
+  }
+  const float4 s1 = B.s1[item];
+  if (path == 0 && (fl & kAA)) {  // path 2 was queued by k_shade2; keep path 1's radiance
+    B.s1[item] = make_float4(L.x, L.y, L.z, s1.w);
+  } else {
+    V3 res = (fl & kAA) ? 0.5f * (v3(s1.x, s1.y, s1.z) + L) : L;                           // :65
+    if (fl & kGamma) res = v3(sqrtf(res.x), sqrtf(res.y), sqrtf(res.z));                  // :73-79
+    out[item] = make_float4(res.x, res.y, res.z, s1.w);
+  }
+}
+// ---- resolve of P(iter - 1) and the misses of P(iter) in one pass over P(iter - 1): P(iter) is the subset
+// k_shade2(iter - 1) queued (rinfo bit kRiQueued), so each of its items is visited once, resolved first (it
+// reads ne / T of iteration iter - 1) and then given its sky value (ne of iteration iter), the order of the
+// separate kernels
+template <bool EXT>
+__global__ void __launch_bounds__(kBlock) k_resmiss2(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter,
+                                                     uint32_t iters, float4* __restrict__ out) {
+  __shared__ uint32_t pref[kNSub + 1];
+  const uint32_t* q = ((iter - 1) & 1) ? B.q1 : B.q0;
+  const uint32_t total = load_prefix(B.ctr, iter - 1, 0, pref);
   for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
     const uint32_t g = c * kBlock + threadIdx.x;
     if (g >= total) continue;
     const uint32_t item = q[map_slot(pref, g, B.qcap)];
-    const uint32_t ri = B.rinfo[item];
-    const uint32_t depth = ri & 0xFFu, path = (ri >> 8) & 1u, status = (ri >> 16) & 3u, kind = (ri >> 20) & 3u;
-    const float4 ne = B.ne[item];
-    V3 L = v3(ne.x, ne.y, ne.z);
-    if (status == kStNeeEnd || status == kStNeeCont) {
-      const float4 nb = B.nb[item];
-      const uint32_t vw = B.vis[item];
-      const uint32_t vis = ((vw & 0xFFu) ? 1u : 0u) | ((vw & 0xFF00u) ? 2u : 0u) | ((vw & 0xFF0000u) ? 4u : 0u) |
-                           ((vw & 0xFF000000u) ? 8u : 0u);
-      V3 f[4];
-      const uint32_t nr = kind == 0 ? 4u : 1u;
-      for (uint32_t k = 0; k < 4; k++) {
-        if (k < nr) {
-          const float4 fk = B.nf[4 * (size_t)item + k];
-          f[k] = v3(fk.x, fk.y, fk.z);
-        } else {
-          f[k] = v3(0.0f, 0.0f, 0.0f);
-        }
-      }
-      V3 result = nee_resolve((int)kind, vis, L, v3(nb.x, nb.y, nb.z), f, fl);
-      if constexpr (EXT) {
-        if (reinterpret_cast<const uint8_t*>(B.vis)[4 * (size_t)B.n + item]) {  // area light unoccluded
-          const float4 a = B.na[item];
-          result = result + v3(a.x, a.y, a.z);
-        }
-      }
-      if (status == kStNeeCont) {  // the path goes on: result joins the stack
-        B.R[(size_t)depth * B.n + item] = make_float4(result.x, result.y, result.z, 0.0f);
-        continue;
-      }
-      L = result;
-    }
-    if constexpr (EXT) {
-      // unwind through dielectric nodes: the end of a reflection subtree parks its radiance in T[level] and
-      // stops (the refraction subtree is already queued); the end of a refraction subtree combines (:369)
-      uint32_t ds = S.has_diel ? B.dst[item] : 0u;
-      bool parked = false;
-      for (int k = (int)depth - 1; k >= 0; k--) {
-        const size_t e = (size_t)k * B.n + item;
-        const uint32_t bit = 1u << k;
-        if (ds & bit) {
-          const float F = B.dro[e].w;
-          if (ds & (bit << 24)) {
-            L = dielectric_combine(F, L, v3(0.0f, 0.0f, 0.0f));
-          } else if (!(ds & (bit << 16))) {
-            B.T[e] = make_float4(L.x, L.y, L.z, kFar);
-            ds |= bit << 16;
-            parked = true;
-            break;
-          } else {
-            const float4 Lr = B.T[e];
-            L = dielectric_combine(F, v3(Lr.x, Lr.y, Lr.z), L);
-          }
-          ds &= ~(0x01010101u << k);
-          continue;
-        }
-        const float4 Rk = B.R[e], Tk = B.T[e];
-        L = v3(Rk.x, Rk.y, Rk.z) + L * v3(Tk.x, Tk.y, Tk.z);
-      }
-      if (S.has_diel) B.dst[item] = ds;
-      if (parked) continue;
-    } else {
-      for (int k = (int)depth - 1; k >= 0; k--) {                                            // result + Trace(..) * throughput
-        const float4 Rk = B.R[(size_t)k * B.n + item], Tk = B.T[(size_t)k * B.n + item];
-        L = v3(Rk.x, Rk.y, Rk.z) + L * v3(Tk.x, Tk.y, Tk.z);
-      }
-    }
-    const float4 s1 = B.s1[item];
-    if (path == 0 && (fl & kAA)) {  // path 2 was queued by k_shade2; keep path 1's radiance
-      B.s1[item] = make_float4(L.x, L.y, L.z, s1.w);
-    } else {
-      V3 res = (fl & kAA) ? 0.5f * (v3(s1.x, s1.y, s1.z) + L) : L;                           // :65
-      if (fl & kGamma) res = v3(sqrtf(res.x), sqrtf(res.y), sqrtf(res.z));                  // :73-79
-      out[item] = make_float4(res.x, res.y, res.z, s1.w);
-    }
+    const bool queued = (B.rinfo[item] & kRiQueued) != 0;
+    resolve_item<EXT>(S, A, B, item, out);
+    if (iter < iters && queued) miss_item<EXT>(S, A, B, item);
   }
 }
 
@@ -483,13 +498,14 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
   launch_trace2(c, S, B, it, iters);
   if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
   const bool ext = (S.area || S.has_diel) && A.mode == 0;
-  if (it > 0) {
-    if (ext) hipLaunchKernelGGL(k_resolve2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it - 1, out);
-    else hipLaunchKernelGGL(k_resolve2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it - 1, out);
-  }
-  if (it < iters) {
+  if (it > 0) {  // resolve of P(it - 1) + misses of P(it), one pass
+    if (ext) hipLaunchKernelGGL(k_resmiss2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it, iters, out);
+    else hipLaunchKernelGGL(k_resmiss2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it, iters, out);
+  } else {
     if (ext) hipLaunchKernelGGL(k_miss2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
     else hipLaunchKernelGGL(k_miss2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
+  }
+  if (it < iters) {
     if (A.mode != 0) hipLaunchKernelGGL(k_shade2_debug, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
     else if (ext) hipLaunchKernelGGL(k_shade2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
     else hipLaunchKernelGGL(k_shade2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
