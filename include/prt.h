@@ -278,6 +278,7 @@ int prt_occluded(prt_ctx* ctx, int32_t n, const float* origins, const float* dir
 #define PRT_BUILDER_HOST_SAH 0
 #define PRT_BUILDER_GPU_LBVH 1
 #define PRT_BUILDER_HOST_SBVH 2  /* spatial splits (BVH::BuildHQ, Core/tiny_bvh.h:1968-2284) + SAH-optimal collapse */
+#define PRT_BUILDER_GPU_PLOC 3   /* device PLOC clustering + SAH-optimal collapse */
 int prt_set_bvh_builder(prt_ctx* ctx, int32_t builder);
 
 /* ---- introspection ---- */

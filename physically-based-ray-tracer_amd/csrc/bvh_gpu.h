@@ -1,4 +1,4 @@
-// bvh_gpu.h -- on-device BLAS build (bvh_gpu.hip): LBVH + SAH-optimal 8-wide collapse into Node8 / TriMT.
+// bvh_gpu.h -- on-device BLAS build (bvh_gpu.hip): LBVH or PLOC + SAH-optimal 8-wide collapse into Node8 / TriMT.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -16,8 +16,9 @@ struct GpuBlasInfo {
 
 // tri_dev: fat triangles float4 x 3T in device memory.  nodes_out: room for T Node8; tris_out: T TriMT.
 // Synchronises on stream s once per tree level.  Child / triangle offsets are relative to the mesh.
+// ploc: PLOC clustering (bvh_gpu.hip) instead of the LBVH radix tree for the binary tree
 hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, int max_leaf, Node8* nodes_out,
-                           TriMT* tris_out, GpuBlasInfo* info);
+                           TriMT* tris_out, GpuBlasInfo* info, bool ploc = false);
 // rebase a mesh's nodes into the concatenated arrays (in place) and record ShadeTri.pad[0] for its primitives
 hipError_t gpu_blas_finish(hipStream_t s, Node8* nodes, uint32_t n_nodes, uint32_t node_base, const TriMT* tris,
                            uint32_t n_tris, uint32_t tri_base, ShadeTri* stri, uint32_t prim_base);

@@ -156,6 +156,42 @@ __global__ void __launch_bounds__(kB) k_radix_tree(const unsigned long long* __r
   count[i] = (uint32_t)(hi - lo + 1);
 }
 
+// collapse table of internal node p from its children's (a binary leaf, id >= n - 1: one triangle, every C its
+// leaf cost); children's tables were written earlier in this launch (sc1, after the arrival atomic) or by an
+// earlier launch
+__device__ __forceinline__ void dp_node(const DpTab& dp, int p, int lc, int rc, const float* pb, const float* lb,
+                                        const float* rb, int cnt, int n, int max_leaf) {
+  double cl[9], cr[9];
+  const double al = area6d(lb) * kDpTri, ar = area6d(rb) * kDpTri;
+  for (int i = 1; i <= 8; i++) {
+    cl[i] = lc >= n - 1 ? al : ld_sc1_d(dp.C + 8 * (size_t)lc + i - 1);
+    cr[i] = rc >= n - 1 ? ar : ld_sc1_d(dp.C + 8 * (size_t)rc + i - 1);
+  }
+  const double A = fmax(area6d(pb), 1e-30);
+  const double leafc = cnt <= max_leaf ? A * kDpTri * (double)cnt : 1e300;
+  double D[9];
+  uint32_t dec = 0;
+  for (int j = 2; j <= 8; j++) {
+    D[j] = 1e300;
+    uint32_t bk = 1;
+    for (int k = 1; k < j; k++) {
+      const double c = cl[k] + cr[j - k];
+      if (c < D[j]) { D[j] = c; bk = (uint32_t)k; }
+    }
+    dec |= bk << (3 * (j - 2));
+  }
+  const double intc = A * kDpNode + D[8];
+  if (cnt <= max_leaf && leafc <= intc) dec |= 1u << 31;
+  double C = fmin(leafc, intc);
+  st_sc1_d(dp.C + 8 * (size_t)p, C);
+  for (int i = 2; i <= 8; i++) {
+    if (C <= D[i]) dec |= 1u << (24 + i - 2);
+    else C = D[i];
+    st_sc1_d(dp.C + 8 * (size_t)p + i - 1, C);
+  }
+  dp.dec[p] = dec;
+}
+
 // ---- 4. boxes bottom-up (flag[] zeroed before the launch)
 __global__ void __launch_bounds__(kB) k_boxes(const float4* __restrict__ tri, const unsigned long long* __restrict__ keys,
                                               int n, const int* __restrict__ left, const int* __restrict__ right,
@@ -189,39 +225,99 @@ __global__ void __launch_bounds__(kB) k_boxes(const float4* __restrict__ tri, co
     for (int k = 0; k < 6; k++) { lb[k] = ld_sc1(l + k); rb[k] = ld_sc1(r + k); }
     for (int k = 0; k < 3; k++) { pb[k] = fminf(lb[k], rb[k]); st_sc1(o + k, pb[k]); }
     for (int k = 3; k < 6; k++) { pb[k] = fmaxf(lb[k], rb[k]); st_sc1(o + k, pb[k]); }
-    if (dp.C) {  // collapse table of p from its children's (a binary leaf: one triangle, every C = its leaf cost)
-      double cl[9], cr[9];
-      const double al = area6d(lb) * kDpTri, ar = area6d(rb) * kDpTri;
-      for (int i = 1; i <= 8; i++) {
-        cl[i] = lc >= n - 1 ? al : ld_sc1_d(dp.C + 8 * (size_t)lc + i - 1);
-        cr[i] = rc >= n - 1 ? ar : ld_sc1_d(dp.C + 8 * (size_t)rc + i - 1);
-      }
-      const double A = fmax(area6d(pb), 1e-30);
-      const double leafc = (int)count[p] <= max_leaf ? A * kDpTri * (double)count[p] : 1e300;
-      double D[9];
-      uint32_t dec = 0;
-      for (int j = 2; j <= 8; j++) {
-        D[j] = 1e300;
-        uint32_t bk = 1;
-        for (int k = 1; k < j; k++) {
-          const double c = cl[k] + cr[j - k];
-          if (c < D[j]) { D[j] = c; bk = (uint32_t)k; }
-        }
-        dec |= bk << (3 * (j - 2));
-      }
-      const double intc = A * kDpNode + D[8];
-      if ((int)count[p] <= max_leaf && leafc <= intc) dec |= 1u << 31;
-      double C = fmin(leafc, intc);
-      st_sc1_d(dp.C + 8 * (size_t)p, C);
-      for (int i = 2; i <= 8; i++) {
-        if (C <= D[i]) dec |= 1u << (24 + i - 2);
-        else C = D[i];
-        st_sc1_d(dp.C + 8 * (size_t)p + i - 1, C);
-      }
-      dp.dec[p] = dec;
-    }
+    if (dp.C) dp_node(dp, p, lc, rc, pb, lb, rb, (int)count[p], n, max_leaf);
     node = p;
   }
+}
+
+// ---- PLOC (Meister, Bittner 2018, "Parallel Locally-Ordered Clustering for Bounding Volume Hierarchy
+// Construction"): clusters start as the Morton-ordered triangles; every iteration each cluster finds the
+// neighbour within kPlocR places (in the current cluster order) whose merged box has the smallest surface area,
+// mutual nearest neighbours merge into a new internal node, and the survivors are compacted in order.  Ties are
+// broken by the pair's indices, so the globally best pair is always mutual and every iteration merges.
+// Internal nodes take ids n-2, n-3, ... as they are created, so the root (created last) is node 0 and the
+// LBVH node numbering (leaves n-1+i) and the collapse below apply unchanged; the collapse table of a node is
+// filled when it is created, from its children's (created in earlier launches).
+constexpr int kPlocR = 16;
+
+__global__ void __launch_bounds__(kB) k_ploc_leaves(const float4* __restrict__ tri,
+                                                    const unsigned long long* __restrict__ keys, int n, float* box,
+                                                    uint32_t* count, int* clus) {
+  const int i = (int)(blockIdx.x * kB + threadIdx.x);
+  if (i >= n) return;
+  const uint32_t prim = (uint32_t)keys[i];
+  const float4 a = tri[3 * prim], b = tri[3 * prim + 1], c = tri[3 * prim + 2];
+  float* bx = box + 6 * (size_t)(n - 1 + i);
+  bx[0] = fminf(fminf(a.x, b.x), c.x); bx[1] = fminf(fminf(a.y, b.y), c.y); bx[2] = fminf(fminf(a.z, b.z), c.z);
+  bx[3] = fmaxf(fmaxf(a.x, b.x), c.x); bx[4] = fmaxf(fmaxf(a.y, b.y), c.y); bx[5] = fmaxf(fmaxf(a.z, b.z), c.z);
+  count[n - 1 + i] = 1u;
+  clus[i] = n - 1 + i;
+}
+
+// nearest neighbour of every cluster (by merged surface area) within kPlocR places; the block's boxes (plus the
+// kPlocR on either side) staged in LDS
+__global__ void __launch_bounds__(kB) k_ploc_nn(const int* __restrict__ clus, int m, const float* __restrict__ box,
+                                                int* nn) {
+  __shared__ float sb[6 * (kB + 2 * kPlocR)];
+  const int b0 = (int)(blockIdx.x * kB) - kPlocR;
+  for (int t = threadIdx.x; t < kB + 2 * kPlocR; t += kB) {
+    const int j = b0 + t;
+    if (j >= 0 && j < m) {
+      const float* bx = box + 6 * (size_t)clus[j];
+      for (int k = 0; k < 6; k++) sb[6 * t + k] = bx[k];
+    }
+  }
+  __syncthreads();
+  const int i = (int)(blockIdx.x * kB + threadIdx.x);
+  if (i >= m) return;
+  const float* bi = sb + 6 * (i - b0);
+  float best = 3.4e38f;
+  int bj = -1;
+  for (int j = max(0, i - kPlocR); j <= min(m - 1, i + kPlocR); j++) {
+    if (j == i) continue;
+    const float* bj6 = sb + 6 * (j - b0);
+    const float dx = fmaxf(bi[3], bj6[3]) - fminf(bi[0], bj6[0]);
+    const float dy = fmaxf(bi[4], bj6[4]) - fminf(bi[1], bj6[1]);
+    const float dz = fmaxf(bi[5], bj6[5]) - fminf(bi[2], bj6[2]);
+    const float a = dx * dy + dy * dz + dz * dx;
+    // ties: the pair (min index, max index) that sorts first, the same order from both ends of a pair
+    const bool better = a < best || (a == best && bj >= 0 && (min(i, j) < min(i, bj) ||
+                                                              (min(i, j) == min(i, bj) && max(i, j) < max(i, bj))));
+    if (bj < 0 || better) { best = a; bj = j; }
+  }
+  nn[i] = bj;
+}
+
+// mutual nearest neighbours merge (the lower index creates the node and keeps the slot); ctr[0] counts down the
+// internal node ids
+__global__ void __launch_bounds__(kB) k_ploc_merge(const int* __restrict__ clus, int m, const int* __restrict__ nn,
+                                                   float* box, int* left, int* right, uint32_t* count, int* out,
+                                                   int* keep, uint32_t* ctr, DpTab dp, int n, int max_leaf) {
+  const int i = (int)(blockIdx.x * kB + threadIdx.x);
+  if (i >= m) return;
+  const int j = nn[i];
+  const bool mutual = j >= 0 && nn[j] == i;
+  if (mutual && i > j) {  // merged into the cluster at j
+    keep[i] = 0;
+    return;
+  }
+  keep[i] = 1;
+  if (!mutual) {
+    out[i] = clus[i];
+    return;
+  }
+  const int lc = clus[i], rc = clus[j];
+  const int p = (int)atomicSub(ctr, 1u) - 1;
+  if (p < 0) { atomicOr(ctr + 3, 0x80000000u); out[i] = lc; return; }
+  float lb[6], rb[6], pb[6];
+  for (int k = 0; k < 6; k++) { lb[k] = box[6 * (size_t)lc + k]; rb[k] = box[6 * (size_t)rc + k]; }
+  for (int k = 0; k < 3; k++) { pb[k] = fminf(lb[k], rb[k]); pb[3 + k] = fmaxf(lb[3 + k], rb[3 + k]); }
+  for (int k = 0; k < 6; k++) box[6 * (size_t)p + k] = pb[k];
+  left[p] = lc;
+  right[p] = rc;
+  count[p] = count[lc] + count[rc];
+  if (dp.C) dp_node(dp, p, lc, rc, pb, lb, rb, (int)count[p], n, max_leaf);
+  out[i] = p;
 }
 
 // ---- 5. greedy 8-wide collapse, one level per launch
@@ -382,9 +478,29 @@ __global__ void __launch_bounds__(kB) k_collapse(const float4* __restrict__ tri,
     }
     const int c = ch[i];
     if (is_leaf(c)) {
-      const uint32_t f = c >= n - 1 ? (uint32_t)(c - (n - 1)) : first[c], cnt = count[c];
+      // the leaf child's triangles: a key range (LBVH subtrees are contiguous in Morton order), or (PLOC,
+      // first == nullptr) the binary leaves under c, at most max_leaf of them
+      uint32_t kidx[8];
+      uint32_t cnt = 0;
+      if (c >= n - 1) {
+        kidx[cnt++] = (uint32_t)(c - (n - 1));
+      } else if (first) {
+        cnt = min(count[c], 8u);
+        for (uint32_t j = 0; j < cnt; j++) kidx[j] = first[c] + j;
+      } else {
+        int st[8], sp = 0;
+        st[sp++] = c;
+        while (sp > 0 && cnt < 8) {
+          const int v = st[--sp];
+          if (v >= n - 1) { kidx[cnt++] = (uint32_t)(v - (n - 1)); continue; }
+          if (sp + 2 > 8) break;
+          st[sp++] = right[v];
+          st[sp++] = left[v];
+        }
+      }
+      if (cnt != count[c] || cnt > 7) { atomicOr(ctr + 3, 0x80000000u); return; }
       for (uint32_t j = 0; j < cnt; j++) {
-        const uint32_t pr = (uint32_t)keys[f + j];
+        const uint32_t pr = (uint32_t)keys[kidx[j]];
         const float4 a = tri[3 * pr], b = tri[3 * pr + 1], d = tri[3 * pr + 2];
         TriMT m;
         m.v0[0] = a.x; m.v0[1] = a.y; m.v0[2] = a.z;
@@ -428,7 +544,7 @@ __global__ void __launch_bounds__(kB) k_rebase(Node8* nodes, uint32_t n, uint32_
   } while (0)
 
 hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, int max_leaf, Node8* nodes_out,
-                           TriMT* tris_out, GpuBlasInfo* info) {
+                           TriMT* tris_out, GpuBlasInfo* info, bool ploc) {
   const int n = n_tris;
   if (n <= 0) return hipErrorInvalidValue;
   const size_t nn = 2 * (size_t)n - 1;
@@ -469,12 +585,54 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
   if ((err = hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, keys2, n, 0, 64, s))) return fail(err);
   if ((err = hipMalloc(&tmp, tmp_bytes))) return fail(err);
   if ((err = hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, keys2, n, 0, 64, s))) return fail(err);
-  if ((err = hipMemsetAsync(parent, 0xFF, 4 * nn, s))) return fail(err);
-  if (n > 1)
-    hipLaunchKernelGGL(k_radix_tree, dim3(grid_of(n - 1)), dim3(kB), 0, s, keys2, n, left, right, parent, first, count);
-  if ((err = hipMemsetAsync(flag, 0, 4 * nn, s))) return fail(err);
-  hipLaunchKernelGGL(k_boxes, dim3(grid_of(n)), dim3(kB), 0, s, tri, keys2, n, left, right, parent, box, flag, first,
-                     count, dp, max_leaf);
+  if (ploc) {
+    // clusters: the Morton-ordered leaves; iterate nearest-neighbour / merge / compact down to the root
+    int *clus = nullptr, *clus2 = nullptr, *nnb = nullptr, *keep = nullptr, *nsel = nullptr;
+    void* stmp = nullptr;
+    size_t stmp_bytes = 0;
+    auto pfree = [&]() {
+      (void)hipFree(clus); (void)hipFree(clus2); (void)hipFree(nnb); (void)hipFree(keep); (void)hipFree(nsel);
+      (void)hipFree(stmp);
+    };
+    if ((err = hipMalloc(&clus, 4 * (size_t)n)) || (err = hipMalloc(&clus2, 4 * (size_t)n)) ||
+        (err = hipMalloc(&nnb, 4 * (size_t)n)) || (err = hipMalloc(&keep, 4 * (size_t)n)) ||
+        (err = hipMalloc(&nsel, 4)) ||
+        (err = hipcub::DeviceSelect::Flagged(nullptr, stmp_bytes, clus2, keep, clus, nsel, n, s)) ||
+        (err = hipMalloc(&stmp, stmp_bytes))) {
+      pfree();
+      return fail(err);
+    }
+    const uint32_t c0p[4] = {(uint32_t)(n - 1), 0u, 0u, 0u};
+    if ((err = hipMemcpyAsync(ctr, c0p, 16, hipMemcpyHostToDevice, s))) { pfree(); return fail(err); }
+    hipLaunchKernelGGL(k_ploc_leaves, dim3(grid_of(n)), dim3(kB), 0, s, tri, keys2, n, box, count, clus);
+    int m = n;
+    while (m > 1 && !err) {
+      hipLaunchKernelGGL(k_ploc_nn, dim3(grid_of(m)), dim3(kB), 0, s, clus, m, box, nnb);
+      hipLaunchKernelGGL(k_ploc_merge, dim3(grid_of(m)), dim3(kB), 0, s, clus, m, nnb, box, left, right, count, clus2,
+                         keep, ctr, dp, n, max_leaf);
+      if ((err = hipcub::DeviceSelect::Flagged(stmp, stmp_bytes, clus2, keep, clus, nsel, m, s))) break;
+      int mm = 0;
+      if ((err = hipMemcpyAsync(&mm, nsel, 4, hipMemcpyDeviceToHost, s)) || (err = hipStreamSynchronize(s))) break;
+      if (mm >= m) err = hipErrorInvalidValue;  // no merge: cannot happen (the best pair is always mutual)
+      m = mm;
+    }
+    uint32_t c[4];
+    if (!err && !(err = hipMemcpyAsync(c, ctr, 16, hipMemcpyDeviceToHost, s)) && !(err = hipStreamSynchronize(s)) &&
+        (c[0] != 0u || (c[3] & 0x80000000u)))
+      err = hipErrorInvalidValue;  // not exactly n - 1 internal nodes
+    pfree();
+    if (err) return fail(err);
+    (void)hipFree(first);
+    first = nullptr;  // PLOC subtrees are not key ranges: the collapse walks them
+  } else {
+    if ((err = hipMemsetAsync(parent, 0xFF, 4 * nn, s))) return fail(err);
+    if (n > 1)
+      hipLaunchKernelGGL(k_radix_tree, dim3(grid_of(n - 1)), dim3(kB), 0, s, keys2, n, left, right, parent, first,
+                         count);
+    if ((err = hipMemsetAsync(flag, 0, 4 * nn, s))) return fail(err);
+    hipLaunchKernelGGL(k_boxes, dim3(grid_of(n)), dim3(kB), 0, s, tri, keys2, n, left, right, parent, box, flag, first,
+                       count, dp, max_leaf);
+  }
   // collapse, level by level from the binary root (node 0; the single leaf when n == 1)
   const Task t0{0, 0u};  // binary root: internal node 0, or the single leaf (node n - 1 = 0) when n == 1
   const uint32_t c0[4] = {1u, 0u, 0u, 0u};  // wide nodes used (the root), triangles used, next tasks

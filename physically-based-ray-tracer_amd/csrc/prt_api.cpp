@@ -752,10 +752,11 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
   if (builder < 0) {
     const char* e = std::getenv("PRT_BUILDER");
     builder = (e && std::strcmp(e, "gpu") == 0)    ? PRT_BUILDER_GPU_LBVH
+              : (e && std::strcmp(e, "ploc") == 0) ? PRT_BUILDER_GPU_PLOC
               : (e && std::strcmp(e, "sbvh") == 0) ? PRT_BUILDER_HOST_SBVH
                                                    : PRT_BUILDER_HOST_SAH;
   }
-  const bool gpu = builder == PRT_BUILDER_GPU_LBVH;
+  const bool gpu = builder == PRT_BUILDER_GPU_LBVH || builder == PRT_BUILDER_GPU_PLOC;
   int rc = drain(c);
   if (rc) return rc;
   const auto t_build0 = std::chrono::steady_clock::now();
@@ -791,13 +792,14 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
     float bmin[3], bmax[3];
     int depth = 0;
     int64_t nnodes = 0, nleaves = 0;
-    if (gpu) {  // LBVH + greedy 8-wide collapse on the device (bvh_gpu.hip)
+    if (gpu) {  // LBVH or PLOC + SAH-optimal 8-wide collapse on the device (bvh_gpu.hip)
       GpuMesh& g = gm[i];
       DevBuf fat;
       HIP_TRY(upload(fat, M.triangles, 48ull * (size_t)M.tri_count));
       HIP_TRY(g.nodes.ensure(sizeof(Node8) * (size_t)M.tri_count));
       HIP_TRY(g.tris.ensure(sizeof(TriMT) * (size_t)M.tri_count));
-      HIP_TRY(gpu_build_blas8(c->stream, fat.as<float>(), M.tri_count, 3, g.nodes.as<Node8>(), g.tris.as<TriMT>(), &g.gi));
+      HIP_TRY(gpu_build_blas8(c->stream, fat.as<float>(), M.tri_count, 3, g.nodes.as<Node8>(), g.tris.as<TriMT>(), &g.gi,
+                              builder == PRT_BUILDER_GPU_PLOC));
       fat.release();
       if ((uint64_t)gpu_nodes + g.gi.nodes >= (1ull << 32) || (uint64_t)gpu_tris + g.gi.tris >= (1ull << 32))
         return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
@@ -898,7 +900,7 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
 }
 
 int prt_set_bvh_builder(prt_ctx* c, int32_t builder) {
-  if (!c || (builder != PRT_BUILDER_HOST_SAH && builder != PRT_BUILDER_GPU_LBVH && builder != PRT_BUILDER_HOST_SBVH))
+  if (!c || builder < PRT_BUILDER_HOST_SAH || builder > PRT_BUILDER_GPU_PLOC)
     return fail(PRT_ERR_INVALID_ARGUMENT, "bad BLAS builder");
   c->builder = builder;
   PRT_FOR_MEMBERS(prt_set_bvh_builder(m, builder));

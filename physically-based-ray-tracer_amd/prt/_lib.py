@@ -13,7 +13,7 @@ ABI_VERSION = 4  # PRT_ABI_VERSION of the include/prt.h these structs mirror
 FLAG_AA, FLAG_ACCUMULATE, FLAG_GAMMA, FLAG_NORMALMAP, FLAG_SKYBOX, FLAG_LIGHTED, FLAG_STOCHASTIC = (1 << i for i in range(7))
 FLAGS_DEFAULT = 0x7F
 OUT_DEVICE = 1
-BUILDER_HOST_SAH, BUILDER_GPU_LBVH, BUILDER_HOST_SBVH = 0, 1, 2
+BUILDER_HOST_SAH, BUILDER_GPU_LBVH, BUILDER_HOST_SBVH, BUILDER_GPU_PLOC = 0, 1, 2, 3
 
 # Renderer::RENDER_STATES (Core/Renderer.h:37-46)
 MODE_BRDF, MODE_BASECOLOR, MODE_GEOMETRYNORMAL, MODE_SHADINGNORMAL, MODE_METAL, MODE_ROUGHNESS, MODE_EMISSIVE = range(7)

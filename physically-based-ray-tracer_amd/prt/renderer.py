@@ -248,8 +248,8 @@ class Context:
         check(self.L.prt_set_postfx(self.h, C.byref(pf)))
 
     def set_bvh_builder(self, builder):
-        """BLAS builder for the next set_scene: _lib.BUILDER_HOST_SAH (default), _lib.BUILDER_GPU_LBVH or
-        _lib.BUILDER_HOST_SBVH (spatial splits)."""
+        """BLAS builder for the next set_scene: _lib.BUILDER_HOST_SAH (default), _lib.BUILDER_GPU_LBVH,
+        _lib.BUILDER_HOST_SBVH (spatial splits) or _lib.BUILDER_GPU_PLOC."""
         check(self.L.prt_set_bvh_builder(self.h, builder))
 
     def scene_info(self):

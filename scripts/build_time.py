@@ -28,6 +28,7 @@ rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
 print(f"BLAS builders ({sd.name}):", flush=True)
 for name, b, col in (("host SAH", _lib.BUILDER_HOST_SAH, None), ("host SBVH", _lib.BUILDER_HOST_SBVH, None),
                      ("GPU LBVH + optimal collapse", _lib.BUILDER_GPU_LBVH, None),
+                     ("GPU PLOC + optimal collapse", _lib.BUILDER_GPU_PLOC, None),
                      ("GPU LBVH + greedy collapse", _lib.BUILDER_GPU_LBVH, "greedy")):
     if col:
         os.environ["PRT_COLLAPSE"] = col

@@ -276,8 +276,8 @@ def test_postfx_matches_oracle(gpu_ctx, preset, over, flags):
 
 @pytest.mark.parametrize("which", ["small_multi", "c2", "c3"])
 def test_gpu_builder_renders_identical(gpu_ctx, which):
-    """The device LBVH builder (PRT_BUILDER_GPU_LBVH) and the spatial-split host builder (PRT_BUILDER_HOST_SBVH,
-    triangles referenced from several leaves) give different trees, but the hit rule is BVH-independent:
+    """The device LBVH and PLOC builders (PRT_BUILDER_GPU_LBVH / _GPU_PLOC) and the spatial-split host builder
+    (PRT_BUILDER_HOST_SBVH, triangles referenced from several leaves) give different trees, but the hit rule is BVH-independent:
     primary hits and rendered frames equal the host SAH build's bit for bit."""
     import prt
     from prt import _lib
@@ -285,7 +285,7 @@ def test_gpu_builder_renders_identical(gpu_ctx, which):
           "c2": scenes.config_c2, "c3": scenes.config_c3}[which]()
     W, H = 160, 96
     out = {}
-    for b in (_lib.BUILDER_HOST_SAH, _lib.BUILDER_GPU_LBVH, _lib.BUILDER_HOST_SBVH):
+    for b in (_lib.BUILDER_HOST_SAH, _lib.BUILDER_GPU_LBVH, _lib.BUILDER_HOST_SBVH, _lib.BUILDER_GPU_PLOC):
         gpu_ctx.set_bvh_builder(b)
         gpu_scene(gpu_ctx, sd, W, H)
         info = gpu_ctx.scene_info()
@@ -294,7 +294,7 @@ def test_gpu_builder_renders_identical(gpu_ctx, which):
         a, r, st = gpu_ctx.render(W, H, 4, 3)
         out[b] = (hits, a, r, st)
     gpu_ctx.set_bvh_builder(_lib.BUILDER_HOST_SAH)
-    for b in (1, 2):
+    for b in (1, 2, 3):
         h0, h1 = out[0][0], out[b][0]
         for f in ("t", "u", "v", "prim", "inst"):
             assert np.array_equal(h0[f], h1[f]), (b, f)
