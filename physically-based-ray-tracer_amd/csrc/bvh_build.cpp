@@ -328,6 +328,8 @@ struct SpatialBuilder {
             acc.grow(bins[k]);
             c += leave[k];
             if (!lcnt[k - 1] || !c || (lcnt[k - 1] == count && c == count)) continue;
+            // the references this plane cuts must fit the remaining duplication budget
+            if (refs_total + (size_t)(lcnt[k - 1] + c - count) > refs_cap) continue;
             const double cost = lacc[k - 1].area() * lcnt[k - 1] + acc.area() * c;
             if (cost < sbest) { sbest = cost; sax = ax; splane = lo + k * w; }
           }
