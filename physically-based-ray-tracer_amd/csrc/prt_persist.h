@@ -194,12 +194,12 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     return node != kNoNode;
   };
   // one node visit (lanes without pending triangles)
-  auto node_step = [&]() {
+  auto node_step = [&](float tlimit) {
     const bool top = TLAS && inst < 0;  // a node of the instance BVH
     const uint4* np = reinterpret_cast<const uint4*>((top ? S.tlas8 : S.nodes8) + node);
     const uint4 a = np[0], b = np[1];
     const uint4 c = np[2], d = np[3], e = np[4];
-    const uint32_t hits = node8_hits(a, c, d, e, O, rD, h.t);
+    const uint32_t hits = node8_hits(a, c, d, e, O, rD, tlimit);
     const uint32_t imask = a.w >> 24;
     if (TLAS && top) {  // instance children: one group addressed by slot (tlas_slot[b.y + slot])
       const uint32_t ih = hits & imask, lh = hits & ~imask;
@@ -292,7 +292,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     // ---- one node visit for lanes whose leaf children have all been started: the remaining triangles of
     // the current leaf (tcur, tcnt) are tested alongside the next node visits (order-independent hit rule;
     // measured 1.5-2.5 % faster per launch on C4 than waiting for the leaf to finish)
-    if (active && node != kNoNode && lhit == 0) node_step();
+    if (active && node != kNoNode && lhit == 0) node_step(h.t);
     // ---- one triangle test for lanes with pending leaf triangles
     if (active && (lhit | tcnt)) {
       if (tri_step()) {
@@ -418,9 +418,21 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
         }
       }
       // ---- one node visit / one triangle test per walking lane, as in the main loop
-      if (busy && node != kNoNode && lhit == 0 && tcnt == 0) node_step();
+      // closest hit: boxes are culled against the team's best t so far (the owner's and every helper's hits
+      // are published as they are found), not only this lane's; a box entered at exactly that t is still
+      // visited, so ties still reach the hit rule
+      float tlim = h.t;
+      if (busy && !any) {
+        const unsigned long long k = tkey[slot];
+        if (k != ~0ull) tlim = fminf(tlim, __uint_as_float((uint32_t)(k >> 32)));
+      }
+      if (busy && node != kNoNode && lhit == 0 && tcnt == 0) node_step(tlim);
       if (busy && (lhit | tcnt)) {
+        const float t0 = h.t;
+        const uint32_t p0 = h.prim;
         if (tri_step()) atomicOr(&tstate[slot], kFoundBit);
+        if (!any && (h.t != t0 || h.prim != p0))
+          atomicMin(&tkey[slot], ((unsigned long long)__float_as_uint(h.t) << 32) | (~h.prim & 0xFFFFFFFFull));
       }
     }
   }
