@@ -446,7 +446,13 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     HIP_TRY(hipMemsetAsync(c->tl.p, 0, tlb, c->stream));
     c->wb.tl = c->tl.as<unsigned long long>();
   }
-  HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * kCtrWords, c->stream));
+  {  // the queue counters and the fetch counters of the iterations this call uses (kMaxIters is the capacity)
+    const size_t qw = (size_t)(iters + 2) * 2 * kNSub * kCtrStride;
+    const size_t fbase = (size_t)(kMaxIters + 2) * 2 * kNSub * kCtrStride;
+    const size_t fw = (size_t)(iters + 2) * 2 * kParts * kCtrStride;
+    HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * qw, c->stream));
+    HIP_TRY(hipMemsetAsync(c->wb.ctr + fbase, 0, 4 * fw, c->stream));
+  }
   if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(c->wb.dst, 0, 4ull * c->wb.n, c->stream));
   float4* frames = c->frames.as<float4>();
   HIP_TRY(launch_wave_init(L, S, A, M, c->wb, frames));
@@ -484,8 +490,9 @@ int read_stats(prt_ctx* c, prt_stats* stats) {
   {
     std::memset(stats, 0, sizeof(*stats));
     // per-launch traversal times summed over every launch
-    std::vector<uint32_t> ctr(kCtrWords);
     const bool dump = std::getenv("PRT_DEBUG_QUEUES") != nullptr;
+    // the queue counters of the iterations this render used (the whole array with the queue dump)
+    std::vector<uint32_t> ctr(dump ? kCtrWords : (size_t)(iters + 2) * 2 * kNSub * kCtrStride);
     HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const WaveTimers& wt = c->wt;

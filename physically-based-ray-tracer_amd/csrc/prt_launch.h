@@ -58,13 +58,14 @@ struct WaveBufs {
   int32_t coop_tail;       // cooperative traversal tail (prt_persist.h)
   int32_t pad;
 };
-constexpr int kMaxIters = 32;
+constexpr uint32_t kParts = 8;  // XCD parts of a traversal launch's live range, one fetch counter each (prt_queue.h)
+constexpr int kMaxIters = 128;  // wavefront iterations per call: bounces <= 64 (AA) / 6 with dielectrics (AA)
 // wavefront iterations of one call: one per path segment, paths x bounces; with dielectric instances a path
 // is a binary tree walked depth first (one segment per iteration), at most 2^bounces - 1 segments per path
 inline uint32_t wave_iters(bool dielectric, int bounces, uint32_t flags) {
   const uint32_t paths = (flags & 1u) ? 2u : 1u;  // PRT_FLAG_AA: two camera paths per reference frame
   if (!dielectric) return paths * (uint32_t)bounces;
-  return bounces >= 6 ? 0xFFFFFFFFu : paths * ((1u << bounces) - 1u);
+  return bounces > 8 ? 0xFFFFFFFFu : paths * ((1u << bounces) - 1u);  // dst holds 4 bits per level for 8 levels
 }
 constexpr int kTlWaves = 256 * 4 * 8;  // timeline records per traversal launch (max persistent grid)
 struct WaveTimers {

@@ -43,7 +43,6 @@ __device__ __forceinline__ uint32_t map_slot(const uint32_t* pref, uint32_t g, u
 // into kParts contiguous parts, each with its own fetch counter; a wave starts on the part of its XCD
 // (HW_REG_XCC_ID) and steals from the others once that part is drained.  Returns false when all parts
 // are drained.  Wave-uniform.
-constexpr uint32_t kParts = 8;
 __device__ __forceinline__ uint32_t xcc_id() {
   uint32_t v;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));

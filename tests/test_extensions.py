@@ -153,5 +153,21 @@ def test_extensions_refusals(gpu_ctx):
     W, H = 32, 24
     gpu_scene(gpu_ctx, sd, W, H)
     with pytest.raises(_lib.PrtError):
-        gpu_ctx.render(W, H, 2, 6)  # 2 paths x 63 segments > 32 iterations
+        gpu_ctx.render(W, H, 2, 7)  # 2 paths x 127 segments > 128 iterations
     gpu_ctx.render(W, H, 2, 3)
+
+
+@pytest.mark.gpu
+def test_deep_dielectric_trees_match_oracle(gpu_ctx):
+    """Dielectric path trees up to the iteration limit (6 bounces with AA: 2 x 63 iterations; the reference's
+    recursion, Core/Renderer.cpp:331-372, has no limit of its own) equal the oracle's recursion."""
+    sd = _ext_scene("all")
+    W, H = 40, 30
+    gpu_scene(gpu_ctx, sd, W, H)
+    for spp, bounces, flags in ((2, 6, oracle.DEFAULT_FLAGS), (1, 7, NO_AA)):
+        gpu_ctx.reset_accumulation(full=True)
+        a_o, _, _, s_o = oracle.OracleScene(sd, W, H).render(W, H, spp=spp, bounces=bounces, flags=flags)
+        a_g, _, s_g = gpu_ctx.render(W, H, spp, bounces, flags)
+        assert rmse(a_o, a_g) <= RMSE_TOL
+        assert np.array_equal(a_o[:, :3], a_g[:, :3])
+        assert (s_o.segments, s_o.shadow_rays) == (s_g.segments, s_g.shadow_rays)
