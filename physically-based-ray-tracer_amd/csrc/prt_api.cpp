@@ -140,6 +140,7 @@ struct prt_ctx {
   uint32_t last_iters = 0;
   bool last_timers = false;
   uint64_t last_paths = 0;
+  uint64_t carry_segments = 0, carry_shadow = 0;  // ray counts of a call's earlier frame passes
   // sharding (prt_shard_init_rccl / prt_shard_attach_rccl / prt_create_group)
   int32_t sh_kind = 0;  // 0 none, 1 RCCL, 2 local group (this context is member 0)
   int32_t sh_rank = 0, sh_world = 1, sh_tile = 32;
@@ -416,12 +417,22 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   rc = ensure_state(c, p->width, p->height);
   if (rc) return rc;
   const int32_t F = frames_of(p);
-  const uint64_t n = (uint64_t)M.items * (uint64_t)F;
-  if (n >= (1ull << 30)) return fail(PRT_ERR_UNSUPPORTED, "too many work items in one call (split spp)");
-  HIP_TRY(c->frames.ensure(sizeof(float4) * (size_t)std::max<uint64_t>(n, 1)));
+  // work items are pixels x reference frames (≈ 390 B of wavefront state each); a call holding more than 2^27 of
+  // them (≈ 52 GB of state) runs its frames in passes of up to 2^27 items (at least one frame), each folded into
+  // the accumulation state in order (the reference's frame sequence).  PRT_MAX_ITEMS sets the pass size (tests
+  // run the multi-pass path at small sizes)
+  const uint64_t per = (uint64_t)M.items;
+  if (per >= (1ull << 30)) return fail(PRT_ERR_UNSUPPORTED, "more than 2^30 pixels in one frame");
+  const char* emi = std::getenv("PRT_MAX_ITEMS");
+  const uint64_t max_items = emi ? std::min<uint64_t>(std::max<uint64_t>(std::strtoull(emi, nullptr, 10), 1), 1ull << 30)
+                                 : (1ull << 27);
+  const int32_t fmax = (int32_t)std::max<uint64_t>(1, (max_items - 1) / std::max<uint64_t>(per, 1));
+  const int32_t npass = F > fmax ? (F + fmax - 1) / fmax : 1;
+  const int32_t F0 = std::min(F, fmax);
+  HIP_TRY(c->frames.ensure(sizeof(float4) * (size_t)std::max<uint64_t>(per * (uint64_t)F0, 1)));
   TraceArgs A;
   A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
-  A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F;
+  A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F0;
   LaunchCfg L{c->stream, occ_for(c)};
   // extensions (area light, dielectric instances) take the EXT instantiations of the shading kernels
   const bool ext = (S.area || S.has_diel) && p->render_mode == 0;
@@ -430,51 +441,72 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     return fail(PRT_ERR_UNSUPPORTED, S.has_diel ? "dielectric path trees exceed the wavefront iteration limit (lower bounces)"
                                                 : "too many wavefront iterations");
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  rc = ensure_wave(c, (uint32_t)n, p->bounces, ext);
+  rc = ensure_wave(c, (uint32_t)(per * (uint64_t)F0), p->bounces, ext);
   if (rc) return rc;
   // PRT_TAIL=0 switches the cooperative traversal tail off (prt_persist.h; A/B runs only)
   const char* et = std::getenv("PRT_TAIL");
   c->wb.coop_tail = (et && std::atoi(et) == 0) ? 0 : 1;
   c->wb.tl = nullptr;
   // per-launch traversal timers (HIP events around every k_trace launch) with stats, unless
-  // PRT_LAUNCH_TIMERS=0: each event record costs a few us between kernels
+  // PRT_LAUNCH_TIMERS=0: each event record costs a few us between kernels (one-pass calls only)
   const char* elt = std::getenv("PRT_LAUNCH_TIMERS");
-  const bool timers = want_stats && !(elt && std::strcmp(elt, "0") == 0);
+  const bool timers = want_stats && npass == 1 && !(elt && std::strcmp(elt, "0") == 0);
   if (want_stats && std::getenv("PRT_DEBUG_QUEUES")) {
     const size_t tlb = 32ull * kTlWaves * (kMaxIters + 2);
     HIP_TRY(c->tl.ensure(tlb));
     HIP_TRY(hipMemsetAsync(c->tl.p, 0, tlb, c->stream));
     c->wb.tl = c->tl.as<unsigned long long>();
   }
-  {  // the queue counters and the fetch counters of the iterations this call uses (kMaxIters is the capacity)
-    const size_t qw = (size_t)(iters + 2) * 2 * kNSub * kCtrStride;
-    const size_t fbase = (size_t)(kMaxIters + 2) * 2 * kNSub * kCtrStride;
-    const size_t fw = (size_t)(iters + 2) * 2 * kParts * kCtrStride;
-    HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * qw, c->stream));
-    HIP_TRY(hipMemsetAsync(c->wb.ctr + fbase, 0, 4 * fw, c->stream));
-  }
-  if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(c->wb.dst, 0, 4ull * c->wb.n, c->stream));
-  float4* frames = c->frames.as<float4>();
-  HIP_TRY(launch_wave_init(L, S, A, M, c->wb, frames));
-  for (uint32_t it = 0; it <= iters; it++)
-    HIP_TRY(launch_wave2_iter(L, S, A, M, c->wb, frames, timers ? &c->wt : nullptr, it));
-  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-  // post-processing (single-GPU image): the screen pass needs the average and, for the aberration, the
-  // accumulator before the last frame
+  c->carry_segments = c->carry_shadow = 0;
   const bool post = c->pfx.enabled && !tiles_dev && rgb8_dev && F > 0;
-  float4* acc_prev = nullptr;
-  if (post) {
-    const size_t np = (size_t)p->width * p->height;
-    if (!avg_dev) { HIP_TRY(c->avg.ensure(np * 16)); avg_dev = c->avg.as<float4>(); }
-    if (c->pfx.aberration != 0) { HIP_TRY(c->accprev.ensure(np * 16)); acc_prev = c->accprev.as<float4>(); }
-  }
-  HIP_TRY(launch_accumulate(L, M, F, p->flags, frames, c->acc.as<float4>(), c->nsamp.as<int32_t>(),
-                            c->dist.as<float>(), avg_dev, post ? nullptr : rgb8_dev, tiles_dev, acc_prev));
-  if (post) {
-    // with !accumulates the accumulator held this frame's value until the end-of-frame memset
-    const float4* acc_new = (p->flags & PRT_FLAG_ACCUMULATE) ? c->acc.as<float4>() : avg_dev;
-    HIP_TRY(launch_postfx(L, post_params(c, p->width, p->height), acc_new, acc_prev, c->nsamp.as<int32_t>(), avg_dev,
-                          rgb8_dev));
+  for (int32_t pass = 0; pass < npass; pass++) {
+    const int32_t f0 = pass * fmax, Fb = npass == 1 ? F : std::min(fmax, F - f0);
+    const bool last = pass == npass - 1;
+    A.frame_index = p->frame_index + f0;
+    A.frames = Fb;
+    if (npass > 1) {
+      rc = ensure_wave(c, (uint32_t)(per * (uint64_t)Fb), p->bounces, ext);
+      if (rc) return rc;
+    }
+    {  // the queue counters and the fetch counters of the iterations this call uses (kMaxIters is the capacity)
+      const size_t qw = (size_t)(iters + 2) * 2 * kNSub * kCtrStride;
+      const size_t fbase = (size_t)(kMaxIters + 2) * 2 * kNSub * kCtrStride;
+      const size_t fw = (size_t)(iters + 2) * 2 * kParts * kCtrStride;
+      HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * qw, c->stream));
+      HIP_TRY(hipMemsetAsync(c->wb.ctr + fbase, 0, 4 * fw, c->stream));
+    }
+    if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(c->wb.dst, 0, 4ull * c->wb.n, c->stream));
+    float4* frames = c->frames.as<float4>();
+    HIP_TRY(launch_wave_init(L, S, A, M, c->wb, frames));
+    for (uint32_t it = 0; it <= iters; it++)
+      HIP_TRY(launch_wave2_iter(L, S, A, M, c->wb, frames, timers ? &c->wt : nullptr, it));
+    if (last) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    // post-processing (single-GPU image): the screen pass needs the average and, for the aberration, the
+    // accumulator before the last frame
+    float4* acc_prev = nullptr;
+    if (post && last) {
+      const size_t np = (size_t)p->width * p->height;
+      if (!avg_dev) { HIP_TRY(c->avg.ensure(np * 16)); avg_dev = c->avg.as<float4>(); }
+      if (c->pfx.aberration != 0) { HIP_TRY(c->accprev.ensure(np * 16)); acc_prev = c->accprev.as<float4>(); }
+    }
+    HIP_TRY(launch_accumulate(L, M, Fb, p->flags, frames, c->acc.as<float4>(), c->nsamp.as<int32_t>(),
+                              c->dist.as<float>(), avg_dev, post ? nullptr : rgb8_dev, tiles_dev, acc_prev));
+    if (post && last) {
+      // with !accumulates the accumulator held this frame's value until the end-of-frame memset
+      const float4* acc_new = (p->flags & PRT_FLAG_ACCUMULATE) ? c->acc.as<float4>() : avg_dev;
+      HIP_TRY(launch_postfx(L, post_params(c, p->width, p->height), acc_new, acc_prev, c->nsamp.as<int32_t>(),
+                            avg_dev, rgb8_dev));
+    }
+    if (want_stats && !last) {  // this pass's ray counts, before the next pass clears the counters
+      std::vector<uint32_t> ctr((size_t)(iters + 2) * 2 * kNSub * kCtrStride);
+      HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      for (uint32_t k = 0; k < iters; k++)
+        for (uint32_t s2 = 0; s2 < kNSub; s2++) {
+          c->carry_segments += ctr[((k * 2 + 0) * kNSub + s2) * kCtrStride];
+          c->carry_shadow += ctr[((k * 2 + 1) * kNSub + s2) * kCtrStride];
+        }
+    }
   }
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   c->last_iters = iters;
@@ -535,6 +567,8 @@ int read_stats(prt_ctx* c, prt_stats* stats) {
                      q(0.99), ex.empty() ? 0.0 : ex.back());
       }
     }
+    stats->segments += c->carry_segments;  // earlier passes of a call above 2^30 work items
+    stats->shadow_rays += c->carry_shadow;
     stats->pipeline = 2;
     stats->iterations = (int32_t)(iters + 1);  // traversal launches
     stats->batches = 1;

@@ -356,3 +356,18 @@ def test_deep_bvh_spills_to_hbm(gpu_ctx):
     a_g, r_g, s_g = gpu_ctx.render(W, H, 2, 3)
     assert (s_g.segments, s_g.shadow_rays) == (s_o.segments, s_o.shadow_rays)
     assert np.array_equal(a_o[:, :3], a_g[:, :3]) and np.array_equal(r_o, r_g)
+
+
+def test_frame_passes_match_one_pass(gpu_ctx, monkeypatch):
+    """A call holding more than 2^30 work items (pixels x reference frames) runs its frames in passes, each folded
+    into the accumulation state in order; PRT_MAX_ITEMS shrinks the pass so the split runs at test size: the image,
+    RGB8 and ray counts equal the one-pass render's."""
+    sd = scenes.multi_instance(scenes.config_small(50, 40))
+    W, H, spp = 96, 64, 12  # 6 reference frames
+    gpu_scene(gpu_ctx, sd, W, H)
+    a1, r1, s1 = gpu_ctx.render(W, H, spp, 3)
+    monkeypatch.setenv("PRT_MAX_ITEMS", str(W * H * 2 + 7))  # 2 frames per pass: 3 passes
+    gpu_ctx.reset_accumulation(full=True)
+    a2, r2, s2 = gpu_ctx.render(W, H, spp, 3)
+    assert np.array_equal(a1, a2) and np.array_equal(r1, r2)
+    assert (s1.segments, s1.shadow_rays) == (s2.segments, s2.shadow_rays)
