@@ -217,6 +217,20 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
   float4* shd = B.shd + (size_t)sub * B.scap;
   const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
   const uint32_t fl = A.flags;
+  // software pipeline over the grid-stride chunks: the next chunk's item, info, hit and seed are loaded while this
+  // chunk's item is shaded
+  uint32_t item_n = 0, info_n = 0, seed_n = 0;
+  float4 hh_n = make_float4(kFar, 0.0f, 0.0f, 0.0f);
+  auto prefetch = [&](uint32_t cc) {
+    const uint32_t gg = cc * kBlock + threadIdx.x;
+    if (gg < total) {
+      item_n = q[map_slot(pref, gg, B.qcap)];
+      info_n = B.info[item_n];
+      hh_n = B.hit[item_n];
+      seed_n = B.seed[item_n];
+    }
+  };
+  prefetch(blockIdx.x);
   for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
     const uint32_t g = c * kBlock + threadIdx.x;
     uint32_t item = 0, info = 0, seed = 0, nr = 0;
@@ -224,16 +238,16 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
     float4 hh = make_float4(kFar, 0.0f, 0.0f, 0.0f);
     const bool active = g < total;
     if (active) {
-      item = q[map_slot(pref, g, B.qcap)];
-      info = B.info[item];
-      hh = B.hit[item];
+      item = item_n; info = info_n; hh = hh_n;
+      const uint32_t sd = seed_n;
       if ((info & 0x1FFu) == 0) B.s1[item].w = hh.x;                                        // r1.hit.t
       if (hh.x < kFar) {
-        seed = B.seed[item];
+        seed = sd;
         kind = nee_kind(fl, seed);                                                           // :198-214
         nr = (uint32_t)nee_rays(kind);
       }
     }
+    prefetch(c + gridDim.x);
     const uint32_t s0 = block_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic
     const uint32_t depth = info & 0xFFu, path = (info >> 8) & 1u;
     uint32_t status = kStMiss;
