@@ -375,11 +375,9 @@ __global__ void __launch_bounds__(kBlock) k_shade2_debug(SceneDev S, TraceArgs A
 // ---- NEE resolve of P(iter) (after k_trace2(iter + 1) traced S(iter)), stack, path end, frame write
 template <bool EXT>
 __device__ __forceinline__ void resolve_item(const SceneDev& S, const TraceArgs& A, const WaveBufs& B, uint32_t item,
-                                             float4* __restrict__ out) {
+                                             uint32_t ri, float4 ne, float4* __restrict__ out) {
   const uint32_t fl = A.flags;
-  const uint32_t ri = B.rinfo[item];
   const uint32_t depth = ri & 0xFFu, path = (ri >> 8) & 1u, status = (ri >> 16) & 3u, kind = (ri >> 20) & 3u;
-  const float4 ne = B.ne[item];
   V3 L = v3(ne.x, ne.y, ne.z);
   if (status == kStNeeEnd || status == kStNeeCont) {
     const float4 nb = B.nb[item];
@@ -463,13 +461,27 @@ __global__ void __launch_bounds__(kBlock) k_resmiss2(SceneDev S, TraceArgs A, Wa
   __shared__ uint32_t pref[kNSub + 1];
   const uint32_t* q = ((iter - 1) & 1) ? B.q1 : B.q0;
   const uint32_t total = load_prefix(B.ctr, iter - 1, 0, pref);
+  // software pipeline over the grid-stride chunks: the next chunk's item, rinfo and ne are loaded while this
+  // chunk's item is resolved
+  uint32_t item_n = 0, ri_n = 0;
+  float4 ne_n = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  auto prefetch = [&](uint32_t cc) {
+    const uint32_t gg = cc * kBlock + threadIdx.x;
+    if (gg < total) {
+      item_n = q[map_slot(pref, gg, B.qcap)];
+      ri_n = B.rinfo[item_n];
+      ne_n = B.ne[item_n];
+    }
+  };
+  prefetch(blockIdx.x);
   for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
     const uint32_t g = c * kBlock + threadIdx.x;
+    const uint32_t item = item_n, ri = ri_n;
+    const float4 ne = ne_n;
+    prefetch(c + gridDim.x);
     if (g >= total) continue;
-    const uint32_t item = q[map_slot(pref, g, B.qcap)];
-    const bool queued = (B.rinfo[item] & kRiQueued) != 0;
-    resolve_item<EXT>(S, A, B, item, out);
-    if (iter < iters && queued) miss_item<EXT>(S, A, B, item);
+    resolve_item<EXT>(S, A, B, item, ri, ne, out);
+    if (iter < iters && (ri & kRiQueued)) miss_item<EXT>(S, A, B, item);
   }
 }
 
