@@ -147,8 +147,11 @@ def cpu_baseline(sd, W, H, spp, bounces):
         legs.append({"kind": kind, "value": round(rays / dt / 1e6, 2), "unit": "Mrays/s", "seconds": round(dt, 2),
                      "rays": int(rays)})
     ref = legs[1] if legs[1].get("value") else legs[0]
+    # the pool runs one GPU's job on its share of the host's CPUs (OMP_NUM_THREADS); the whole host is only
+    # extrapolated, linearly in threads (an upper bound: the row loop shares memory bandwidth), not measured
+    whole = round(ref["value"] * nproc / max(threads, 1), 1) if ref.get("value") else None
     return {"value": ref["value"], "unit": "Mrays/s", "cores": threads, "kind": ref["kind"],
-            "model": model, "host_logical_cpus": nproc,
+            "model": model, "host_logical_cpus": nproc, "whole_host_linear_estimate": whole,
             "sample": f"{sd.name}: {what}, {spp} spp, depth {bounces}, {threads} threads "
                       f"(this GPU's CPU share of a {nproc}-CPU host)",
             "legs": legs}
