@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-rank frame time of the pixel-tile sharding on ONE GPU: rank 0's share of the C4 frame for
-world = 1, 2, 4, 8 (what each GPU of an N-GPU node renders), to estimate strong scaling without a node."""
+world = 1, 2, 4, 8 (what each GPU of an N-GPU node renders), to estimate strong scaling without a node.
+`rank_time.py [c5] [worlds...]`: c5 = 3840x2160, 16 spp, depth 8 with the area light (bench.py --scene c5)."""
 import os
 import sys
 import time
@@ -12,24 +13,29 @@ import torch  # noqa: E402
 import prt  # noqa: E402
 from prt import scenes  # noqa: E402
 
-sd = scenes.config_c4()
-W, H = 1920, 1080
+args = sys.argv[1:]
+C5 = bool(args) and args[0] == "c5"
+if C5:
+    args = args[1:]
+sd = scenes.config_c5() if C5 else scenes.config_c4()
+W, H, SPP, BOUNCES = (3840, 2160, 16, 8) if C5 else (1920, 1080, 4, 4)
+FPC = SPP // 2
 ctx = prt.Context(0)
 ctx.set_stream(torch.cuda.current_stream().cuda_stream)
 ctx.set_scene(prt.Scene.from_data(sd))
 ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
 base = None
-WORLDS = [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]
+WORLDS = [int(a) for a in args] or [1, 2, 4, 8]
 for world in WORLDS:
     per = ctx.tile_buffer_pixels(W, H, 32, world)
     tiles = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
-    for i in range(2):
-        ctx.render_tiles(W, H, 4, 4, 32, 0, world, tiles.data_ptr(), frame_index=2 * i)
+    for i in range(1 if C5 else 2):
+        ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i)
     torch.cuda.synchronize()
-    n = 5
+    n = 2 if C5 else 5
     t0 = time.perf_counter()
     for i in range(n):
-        st = ctx.render_tiles(W, H, 4, 4, 32, 0, world, tiles.data_ptr(), frame_index=2 * i, stats=True)
+        st = ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i, stats=True)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / n
     base = base or ms * world
