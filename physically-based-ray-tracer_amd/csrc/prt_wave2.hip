@@ -519,6 +519,14 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
                              const WaveBufs& B, float4* out, WaveTimers* tm, uint32_t it) {
   if (B.n == 0) return hipSuccess;
   const unsigned gprod = 256u * 4u;  // producer blocks (multiple of kNSub)
+  // k_shade2 over 4x the resident blocks when a call holds >= 2^21 items: the extra blocks queue behind the
+  // resident ones and even out the kernel's end (C4 frame -1 to -2 %); below that the extra launch width costs
+  // more than it evens out (world-8 shares). PRT_SHADE_GRID overrides (A/B runs).
+#ifndef PRT_SHADE_GRID
+  const unsigned gshade = B.n >= (1u << 21) ? 4u * gprod : gprod;
+#else
+  const unsigned gshade = PRT_SHADE_GRID;
+#endif
   const uint32_t iters = wave_iters(S.has_diel != 0, A.bounces, A.flags);
   if (tm) (void)hipEventRecord(tm->ev[4 * it + 0], c.stream);
   launch_trace2(c, S, B, it, iters);
@@ -533,8 +541,8 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
   }
   if (it < iters) {
     if (A.mode != 0) hipLaunchKernelGGL(k_shade2_debug, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
-    else if (ext) hipLaunchKernelGGL(k_shade2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
-    else hipLaunchKernelGGL(k_shade2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
+    else if (ext) hipLaunchKernelGGL(k_shade2<true>, dim3(gshade), dim3(kBlock), 0, c.stream, S, A, M, B, it);
+    else hipLaunchKernelGGL(k_shade2<false>, dim3(gshade), dim3(kBlock), 0, c.stream, S, A, M, B, it);
   }
   if (tm) tm->iters = iters + 1;
   return hipGetLastError();
