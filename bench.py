@@ -72,6 +72,21 @@ def _pmc_kernel(path, kernel):
     return None, None
 
 
+def current_code_hash(kernel):
+    """Hash of `kernel`'s machine code in the libprt.so being timed (prt/codeobj.py: the gfx950 code objects
+    of the library's .hip_fatbin, the kernel's .text bytes + kernel descriptor, all instantiations)."""
+    from prt import _lib, codeobj
+    try:
+        return codeobj.base_hashes(_lib.LIBPATH).get(kernel)
+    except (OSError, ValueError):
+        return None
+
+
+def fresh(d, live_hash):
+    """A committed PMC record prices the timed library only when it carries the same code hash."""
+    return bool(d) and live_hash is not None and d.get("code_hash") == live_hash
+
+
 def measured_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/traffic_current.json;
     FETCH_SIZE x2 gfx950 correction of MI355X_MICROARCH.md, checked for this kernel's gathers by
@@ -134,27 +149,46 @@ def cpu_baseline(sd, W, H, spp, bounces):
     what = "the full frame" if scale == 1 else f"the same camera at {w}x{h} (1/{scale * scale} of the pixels)"
     legs = []
     osc = oracle.OracleScene(sd, w, h)
-    for kind in ("port", "reference"):
-        if kind == "reference":
-            if oracle.reflib() is None:
-                legs.append({"kind": kind, "value": None, "why": "oracle/_ref/libref_tinybvh.so not built"})
-                continue
-            osc.use_reference_traversal()
+
+    def timed(nthreads):
         t0 = time.perf_counter()
-        _, _, _, st = osc.render(w, h, spp=spp, bounces=bounces, nthreads=threads)
+        _, _, _, st = osc.render(w, h, spp=spp, bounces=bounces, nthreads=nthreads)
         dt = time.perf_counter() - t0
         rays = st.segments + st.shadow_rays
-        legs.append({"kind": kind, "value": round(rays / dt / 1e6, 2), "unit": "Mrays/s", "seconds": round(dt, 2),
-                     "rays": int(rays)})
+        return {"value": round(rays / dt / 1e6, 2), "unit": "Mrays/s", "seconds": round(dt, 3), "rays": int(rays),
+                "threads": nthreads}
+
+    legs.append(dict(kind="port", **timed(threads)))
+    ref_ok = oracle.reflib() is not None
+    if ref_ok:
+        osc.use_reference_traversal()
+        points = [timed(t) for t in sorted({1, min(4, threads), threads})]
+        legs.append(dict(kind="reference", **points[-1]))
+    else:
+        legs.append({"kind": "reference", "value": None, "why": "oracle/_ref/libref_tinybvh.so not built"})
+        points = []
     ref = legs[1] if legs[1].get("value") else legs[0]
-    # the pool runs one GPU's job on its share of the host's CPUs (OMP_NUM_THREADS); the whole host is only
-    # extrapolated, linearly in threads (an upper bound: the row loop shares memory bandwidth), not measured
-    whole = round(ref["value"] * nproc / max(threads, 1), 1) if ref.get("value") else None
-    return {"value": ref["value"], "unit": "Mrays/s", "cores": threads, "kind": ref["kind"],
-            "model": model, "host_logical_cpus": nproc, "whole_host_linear_estimate": whole,
-            "sample": f"{sd.name}: {what}, {spp} spp, depth {bounces}, {threads} threads "
-                      f"(this GPU's CPU share of a {nproc}-CPU host)",
-            "legs": legs}
+    out = {"value": ref["value"], "unit": "Mrays/s", "cores": threads, "kind": ref["kind"],
+           "model": model, "host_logical_cpus": nproc,
+           "sample": f"{sd.name}: {what}, {spp} spp, depth {bounces}, {threads} threads "
+                     f"(this GPU's CPU share of a {nproc}-CPU host)",
+           "legs": legs}
+    if len(points) >= 2:
+        # whole host: not measured (the pool gives one GPU's job its share of the CPUs).  The reference leg's
+        # measured thread points are fitted with Amdahl's t(p) = a + b / p (least squares in 1/p) and the fit
+        # is evaluated at every logical CPU of the host -- an estimate, derived from the points listed
+        x = np.array([1.0 / p["threads"] for p in points])
+        y = np.array([p["seconds"] for p in points])
+        b, a = np.polyfit(x, y, 1)
+        a = max(a, 0.0)
+        rays = points[-1]["rays"]
+        t_host = a + b / nproc
+        out["thread_points"] = [{"threads": p["threads"], "value": p["value"], "seconds": p["seconds"]} for p in points]
+        out["amdahl_fit"] = {"serial_s": round(a, 4), "parallel_s": round(b, 4),
+                             "serial_fraction": round(a / (a + b), 4) if a + b > 0 else None}
+        out["whole_host_estimate"] = {"value": round(rays / t_host / 1e6, 1), "threads": nproc,
+                                      "how": "Amdahl fit of thread_points evaluated at host_logical_cpus (not measured)"}
+    return out
 
 
 def spawn_ranks(n):
@@ -284,6 +318,17 @@ def main():
         c4 = args.scene == "c4" and W == 1920 and H == 1080 and world == 1  # the PMC passes are of this config
         valu, valu_src = measured_valu(TRACE_KERNEL) if c4 else (None, None)
         traffic, traffic_src = measured_traffic(TRACE_KERNEL) if c4 else (None, None)
+        # the committed counters count only if they were taken on this very k_trace2 (code-object hash):
+        # otherwise frac is withheld and the line says the profile is stale
+        live_hash = current_code_hash(TRACE_KERNEL)
+        tr_rec, _ = _pmc_kernel(os.path.join(ROOT, "profiles", "traffic_current.json"), TRACE_KERNEL) if c4 else (None, None)
+        stale = {"valu": bool(valu) and not fresh(valu, live_hash),
+                 "traffic": bool(traffic) and not fresh(tr_rec, live_hash)}
+        valu_stale_rec = valu if stale["valu"] else None
+        if stale["valu"]:
+            valu = None
+        if stale["traffic"]:
+            traffic = None
         valu_rate = valu["SQ_INSTS_VALU"] / (kern_ms / 1e3) / 1e9 if valu else None
         hbm_rate = traffic / (kern_ms / 1e3) / 1e9 if traffic else None
         bpr = algorithmic_bytes_per_ray()
@@ -292,17 +337,28 @@ def main():
         own_bytes = (seg_f * own["closest"] + sh_f * own["anyhit"]) / launches if own else None
         hbm = {"achieved": round(hbm_rate, 1) if hbm_rate else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": round(hbm_rate / HBM_PEAK_GBS, 4) if hbm_rate else None, "traffic": traffic,
-               "source": traffic_src}
+               "source": traffic_src, "stale_profile": stale["traffic"]}
         if valu_rate is not None:
             roof = {"bound": "valu", "achieved": round(valu_rate, 1), "peak": VALU_PEAK_GINST,
                     "unit": "G VALU wave-instructions/s", "frac": round(valu_rate / VALU_PEAK_GINST, 4),
-                    "traffic": traffic, "valu_insts_per_launch": int(valu["SQ_INSTS_VALU"]), "source": valu_src}
+                    "traffic": traffic, "valu_insts_per_launch": int(valu["SQ_INSTS_VALU"]), "source": valu_src,
+                    # the single-wave issue rate (4 cycles per wave64 instruction, MI355X_MICROARCH.md
+                    # constants table) bounds a SIMD holding one wave; k_trace2 holds 7, so frac uses 2 cycles
+                    "frac_vs_single_wave_issue": round(2 * valu_rate / VALU_PEAK_GINST, 4)}
             if "valu_busy" in valu:  # SQ_ACTIVE_INST_VALU x 4 / SIMD cycles: waves with a VALU instruction in
                 # flight (a lone wave holds its SIMD 4 cycles per instruction), not the 2-cycle issue peak above
                 roof["wave_valu_active_pmc"] = round(valu["valu_busy"], 4)
-        else:  # no VALU pass for this config: price the measured HBM bytes (or nothing)
-            roof = {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": hbm["frac"], "traffic": traffic}
+            if valu.get("clock_ghz"):  # effective clock of the PMC pass (GRBM_GUI_ACTIVE / 8 / dispatch time)
+                roof["pmc_clock_ghz"] = round(valu["clock_ghz"], 3)
+                roof["frac_at_pmc_clock"] = round(valu_rate / (VALU_PEAK_GINST * valu["clock_ghz"] / 2.4), 4)
+        else:  # no fresh VALU pass for this config: price the measured HBM bytes (or nothing)
+            roof = {"bound": "valu" if valu_stale_rec else "hbm",
+                    "achieved": None if valu_stale_rec else hbm["achieved"],
+                    "peak": VALU_PEAK_GINST if valu_stale_rec else HBM_PEAK_GBS,
+                    "unit": "G VALU wave-instructions/s" if valu_stale_rec else "GB/s",
+                    "frac": None if valu_stale_rec else hbm["frac"], "traffic": traffic}
+        roof["stale_profile"] = stale["valu"] or stale["traffic"]
+        roof["code_hash"] = live_hash[:16] if live_hash else None
         roof.update({
             "kernel": TRACE_KERNEL, "per": f"launch (avg of {launches} launches per frame)",
             "launch_ms": round(kern_ms, 4), "hbm": hbm,

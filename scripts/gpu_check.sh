@@ -33,6 +33,10 @@ fi
 if [ "$what" = "bench" ] || [ "$what" = "all" ]; then
   step bench 900 python bench.py --steps 5 --warmup 1
 fi
+if [ "$what" = "prof" ] || [ "$what" = "benchprof" ] || [ "$what" = "valu" ]; then
+  # the machine code these passes measure (prt/codeobj.py; scripts/summarize_*.py stamp it on the summaries)
+  (cd physically-based-ray-tracer_amd && python -m prt.codeobj) > gpurun_out/lib_hashes.json
+fi
 if [ "$what" = "prof" ] || [ "$what" = "benchprof" ]; then
   export TMPDIR=/tmp
   if [ "$what" = "benchprof" ]; then

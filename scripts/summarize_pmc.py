@@ -17,25 +17,39 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from summarize_prof import stamp  # noqa: E402
 
 
 def short(name):
     return name.split("(")[0].replace("void ", "").strip()
 
 
-def per_launch(path):
-    """{kernel: {counter: mean over dispatches of the per-dispatch sum}} and dispatch counts."""
+def per_launch(path, durations=None):
+    """{kernel: {counter: mean over dispatches of the per-dispatch sum}} and dispatch counts.  With a dict
+    `durations`, also {kernel: mean dispatch ns} of this pass when the CSV carries timestamps."""
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
+    span = collections.defaultdict(dict)
     for r in csv.DictReader(open(path)):
         k = short(r["Kernel_Name"])
         per[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
+        if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+            span[k][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    if durations is not None:
+        for k, d in span.items():
+            durations[k] = sum(d.values()) / len(d)
     return {k: {c: v / len(disp[k]) for c, v in d.items()} for k, d in per.items()}, {k: len(v) for k, v in disp.items()}
 
 
 def valu(name, src):
-    means, calls = per_launch(os.path.join(src, "pmc_valu", "run_counter_collection.csv"))
+    dur = {}
+    means, calls = per_launch(os.path.join(src, "pmc_valu", "run_counter_collection.csv"), dur)
+    stats = {}  # fallback durations: the --kernel-trace --stats pass of the same session
+    sf = os.path.join(src, "prof_stats", "run_kernel_stats.csv")
+    if os.path.exists(sf):
+        stats = {short(r["Name"]): float(r["AverageNs"]) for r in csv.DictReader(open(sf))}
     out = {"name": name, "source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES "
                                    "SQ_WAVES GRBM_GUI_ACTIVE -- python3 bench.py --steps 1 --warmup 1", "kernels": {}}
     for k, d in means.items():
@@ -45,7 +59,15 @@ def valu(name, src):
         rec["calls"] = calls[k]
         if d.get("GRBM_GUI_ACTIVE"):
             rec["valu_busy"] = d.get("SQ_ACTIVE_INST_VALU", 0.0) * 4 / (1024 * d["GRBM_GUI_ACTIVE"] / 8)
+            # effective shader clock of the pass (MI355X_MICROARCH.md, DVFS give-back: GRBM_GUI_ACTIVE / 8 XCDs
+            # / dispatch wall time); the dispatch time is this pass's own when the CSV has timestamps
+            ns, ns_src = (dur[k], "pmc pass timestamps") if k in dur else (stats.get(k), "kernel-trace stats")
+            if ns:
+                rec["dispatch_ns"] = ns
+                rec["clock_ghz"] = d["GRBM_GUI_ACTIVE"] / 8 / ns
+                rec["clock_source"] = ns_src
         out["kernels"][k] = rec
+    stamp(out, src)
     for fn in (f"{name}.json", "valu_current.json"):
         with open(os.path.join(ROOT, "profiles", fn), "w") as f:
             json.dump(out, f, indent=1)

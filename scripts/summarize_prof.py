@@ -15,6 +15,24 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "physically-based-ray-tracer_amd"))
+from prt import codeobj  # noqa: E402
+
+
+def stamp(out, src):
+    """Stamp every kernel record with the hash of the machine code it measured (codeobj.base_hashes): from
+    <src>/lib_hashes.json, written on the GPU box before the passes, else from the in-tree libprt.so."""
+    f = os.path.join(src, "lib_hashes.json")
+    if os.path.exists(f):
+        hashes, origin = json.load(open(f))["kernels"], "lib_hashes.json written on the GPU box"
+    else:
+        hashes = codeobj.base_hashes(os.path.join(ROOT, "physically-based-ray-tracer_amd", "prt", "libprt.so"))
+        origin = "in-tree libprt.so at summary time"
+    out["code_hash_source"] = origin
+    for k, d in out["kernels"].items():
+        h = hashes.get(codeobj.profile_kernel_base(k))
+        if h:
+            d["code_hash"] = h
 
 
 def short(name):
@@ -53,6 +71,7 @@ def main():
         if "hbm_fetch_bytes_per_launch" in d or "hbm_write_bytes_per_launch" in d:
             d["hbm_bytes_per_launch"] = d.get("hbm_fetch_bytes_per_launch", 0) + d.get("hbm_write_bytes_per_launch", 0)
             d["hbm_bytes_per_frame"] = d.get("hbm_fetch_bytes_per_frame", 0) + d.get("hbm_write_bytes_per_frame", 0)
+    stamp(out, src)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", f"{name}.json"), "w") as f:
         json.dump(out, f, indent=1)
