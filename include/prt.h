@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PRT_ABI_VERSION 4
+#define PRT_ABI_VERSION 5
 
 typedef enum {
     PRT_OK = 0,
@@ -142,13 +142,15 @@ typedef struct {
     uint64_t paths;         /* camera paths traced */
     double   ms;            /* device time of the render (HIP events) */
     double   ms_trace;      /* device time of the path-tracing kernel(s) only */
-    double   ms_closest;    /* device time of the traversal launches (pipeline 2: closest + shadow rays together;
-                               pipeline 3: the whole persistent launch, shading included) */
+    double   ms_closest;    /* device time of the traversal launches (closest + shadow rays together), summed */
     double   ms_anyhit;     /* reserved (0): shadow rays are traced inside the merged traversal launches */
     int32_t  pipeline;      /* 2 = the merged-trace wavefront (prt_wave2.hip) */
     int32_t  iterations;    /* traversal launches per call */
     int32_t  batches;       /* 1 */
     int32_t  ranks;         /* shards whose rays these stats count (1 unless a local group summed its members) */
+    uint64_t stack_overflows; /* traversal stack overflows since the context was created: a BVH node group that
+                                 found no free stack level (the host sizes the stacks from the BVH depth, so any
+                                 non-zero count is a builder / sizing bug; the results may have lost hits) */
 } prt_stats;
 
 /* closest-hit record, tinybvh::Intersection (Core/tiny_bvh.h:545-567) minus user data */
@@ -273,7 +275,8 @@ int prt_occluded(prt_ctx* ctx, int32_t n, const float* origins, const float* dir
 
 /* ---- BLAS builder (the reference builds on the CPU, Core/tiny_bvh.h:1968-2284,3706-3781)
  * HOST_SAH (default): binned SAH binary tree + SAH-optimal 8-wide collapse on the host.
- * GPU_LBVH: Morton-code LBVH (Karras 2012) + greedy 8-wide collapse on the device, Node8 layout only.
+ * GPU_LBVH: Morton-code LBVH (Karras 2012) + SAH-optimal 8-wide collapse on the device (PRT_COLLAPSE=greedy:
+ * the greedy collapse), Node8 layout only.
  * Applies to the next prt_set_meshes.  Hits do not depend on the builder (order-independent hit rule). */
 #define PRT_BUILDER_HOST_SAH 0
 #define PRT_BUILDER_GPU_LBVH 1

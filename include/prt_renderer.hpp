@@ -227,6 +227,9 @@ class Renderer {
     const prt_postfx pf = camera.PostFx(isPostProcessed);
     check(prt_set_postfx(ctx_, &pf));
     check(prt_render(ctx_, &p, accumulator.data(), screen.data(), 0u, &stats_));
+    if (stats_.stack_overflows)  // a dropped traversal stack group may have lost hits (prt_stats)
+      throw Error(PRT_ERR_HIP, "traversal stack overflow: " + std::to_string(stats_.stack_overflows) +
+                                        " node groups dropped");
     frame_ += (uint32_t)frames;
   }
 

@@ -111,6 +111,7 @@ struct prt_ctx {
   BuiltTlas8 tlas_host;
   DevBuf tlas8, tlas_slot;
   DevBuf spill;  // traversal stack levels beyond the LDS ones (BVHs deeper than 17 levels)
+  DevBuf diag;   // SceneDev::diag device counters ([0] traversal stack overflows, cumulative per context)
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
   float al[16] = {};
   int32_t area = 0, area_two_sided = 0;
@@ -169,7 +170,8 @@ int drain(prt_ctx* c) {
 }
 
 // waves/SIMD of the persistent traversal kernels: the LDS stack (8 / 9 / 11 / 14 / 18 groups at 8 / 7 / 6 / 5 / 4
-// waves) must hold max_depth - 1 groups; depth_ok caps the depth at 16
+// waves) must hold max_depth - 1 groups; deeper BVHs (depth_ok caps them at kMaxBvhDepth = 64 levels) run the
+// 4-wave form with HBM spill columns (ensure_spill)
 int occ_for(const prt_ctx* c) {
   const char* e = std::getenv("PRT_OCC");
   int want = e ? std::atoi(e) : 7;
@@ -264,6 +266,7 @@ int scene_ready(prt_ctx* c, SceneDev& S) {
   int rc = ensure_instances(c);
   if (rc) return rc;
   std::memset(&S, 0, sizeof(S));
+  S.diag = c->diag.as<uint32_t>();
   S.nodes8 = c->nodes8.as<Node8>();
   S.tris = c->tris.as<TriMT>();
   S.stri = c->stri.as<ShadeTri>();
@@ -515,6 +518,15 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   return PRT_OK;
 }
 
+// the context's traversal stack overflow count (SceneDev::diag[0]); waits for the context stream
+uint64_t diag_overflows(prt_ctx* c) {
+  uint32_t v = 0;
+  if (hipMemcpyAsync(&v, c->diag.p, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return ~0ull;  // unreadable counts as overflowed: never report a clean run that was not checked
+  return v;
+}
+
 // waits for the last render of run_render(..., want_stats = true) and fills its stats
 int read_stats(prt_ctx* c, prt_stats* stats) {
   const uint32_t iters = c->last_iters;
@@ -567,6 +579,7 @@ int read_stats(prt_ctx* c, prt_stats* stats) {
                      q(0.99), ex.empty() ? 0.0 : ex.back());
       }
     }
+    stats->stack_overflows = diag_overflows(c);
     stats->segments += c->carry_segments;  // earlier passes of a call above 2^30 work items
     stats->shadow_rays += c->carry_shadow;
     stats->pipeline = 2;
@@ -605,7 +618,21 @@ int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint
     if (per > M.items)  // the tail of a shorter rank's buffer
       HIP_TRY(hipMemsetAsync(m->shtiles.as<float4>() + M.items, 0, sizeof(float4) * (per - M.items), m->stream));
     int rc = run_render(m, p, M, nullptr, nullptr, m->shtiles.as<float4>(), stats != nullptr);
-    if (rc) return rc;
+    if (rc) {
+      // RCCL: the other ranks are already (or soon) inside this frame's ncclGather; post this rank's part
+      // (zeros) anyway so they complete, then report the local error
+      if (c->sh_kind == 1) {
+        const std::string why = g_err;
+        const Rccl* R = rccl(nullptr);
+        if (R && hipMemsetAsync(c->shtiles.p, 0, per * sizeof(float4), c->stream) == hipSuccess) {
+          float4* g = nullptr;
+          if (root && c->gathered.ensure((size_t)world * per * sizeof(float4)) == hipSuccess) g = c->gathered.as<float4>();
+          if (!root || g) (void)R->Gather(c->shtiles.p, g, per * 4, ncclFloat32, 0, c->comm, c->stream);
+        }
+        g_err = why;
+      }
+      return rc;
+    }
   }
   HIP_TRY(hipSetDevice(c->device));
   if (root) HIP_TRY(c->gathered.ensure((size_t)world * per * sizeof(float4)));
@@ -657,7 +684,14 @@ int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint
     }
     sum.ranks = (int32_t)all.size();
     HIP_TRY(hipSetDevice(c->device));
-    if (c->sh_kind == 1) HIP_TRY(hipStreamSynchronize(c->stream));  // the gather is part of the frame
+    if (c->sh_kind == 1) {
+      HIP_TRY(hipStreamSynchronize(c->stream));  // the gather is part of the frame
+      // a communicator that failed asynchronously (a peer's error, a lost link) is reported, not waited on
+      const Rccl* R = rccl(nullptr);
+      ncclResult_t ae = ncclSuccess;
+      if (R && R->CommGetAsyncError && R->CommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess)
+        return fail(PRT_ERR_HIP, std::string("RCCL communicator error: ") + R->GetErrorString(ae));
+    }
     *stats = sum;
   }
   return PRT_OK;
@@ -720,6 +754,10 @@ int prt_create(const prt_device_desc* desc, prt_ctx** out) {
     if (upload(c->srgb, lut, sizeof(lut)) != hipSuccess) {
       delete c;
       return fail(PRT_ERR_HIP, "srgb table upload failed");
+    }
+    if (c->diag.ensure(64) != hipSuccess || hipMemset(c->diag.p, 0, 64) != hipSuccess) {
+      delete c;
+      return fail(PRT_ERR_HIP, "diagnostics buffer allocation failed");
     }
   }
   for (auto& e : c->ev) {
@@ -1221,6 +1259,7 @@ int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t 
     stats->paths = n;
     stats->ms = ms;
     stats->ms_trace = ms;
+    stats->stack_overflows = diag_overflows(c);
   }
   return PRT_OK;
 }

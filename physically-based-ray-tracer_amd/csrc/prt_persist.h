@@ -55,8 +55,8 @@ __device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
 //   reload(uint32_t handle, bool any, V3& O, V3& D)        world ray again (next instance of the TLAS loop)
 //   finish(uint32_t handle, const Hit& h, bool any, bool hit)  closest: h; any-hit: hit = occluded
 //   tick(idle, drained)                                     wave-uniform, once at the top of every iteration:
-//                                                           idle lanes, no refill coming (the streaming
-//                                                           engine publishes finished rays there)
+//                                                           idle lanes, no refill coming (a hook for
+//                                                           per-iteration bookkeeping; k_trace2 passes none)
 // tail: tail_lds_words(TAILN) words of LDS for the cooperative tail, or nullptr (no tail mode).
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
@@ -139,6 +139,8 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     if (gmask && sp < cap) {
       put(sp, gbase, gmask | (gimask << 8));
       sp++;
+    } else if (gmask) {
+      stack_overflow(ls.ovf);
     }
   };
   // next child of the current group, or the next stacked group, or done with this BLAS (TLAS: with this BLAS,

@@ -62,14 +62,21 @@ __device__ __forceinline__ uint32_t order_mask(uint32_t m, uint32_t oct) {
 struct LaneStack {
   uint32_t* lds;
   uint2* spill;
+  uint32_t* ovf;  // overflow counter (SceneDev::diag)
   uint32_t tid, stride;
   int cap;  // STACK + spill levels
 };
+// a group that finds no free stack level is counted, never silently lost (the host sizes the stacks from the
+// BVH depth, so the count stays 0; prt_stats.stack_overflows reports it and the Python mirror raises on it)
+__device__ __forceinline__ void stack_overflow(uint32_t* ovf) {
+  if (ovf) atomicAdd(ovf, 1u);
+}
 template <int STACK, int BLOCK>
 __device__ __forceinline__ LaneStack lane_stack(const SceneDev& S, uint32_t* lds) {
   LaneStack L;
   L.lds = lds;
   L.spill = S.spill;
+  L.ovf = S.diag;
   L.tid = blockIdx.x * blockDim.x + threadIdx.x;
   L.stride = gridDim.x * blockDim.x;
   L.cap = STACK + (S.spill ? S.spill_levels : 0);
@@ -133,6 +140,8 @@ __device__ __forceinline__ bool blas_traverse8(const Node8* __restrict__ nodes, 
         if (gmask && lvl0 + sp < stk.cap) {
           stack_put<STACK, BLOCK>(stk, lvl0 + sp, gbase, gmask | (gimask << 8));
           sp++;
+        } else if (gmask) {
+          stack_overflow(stk.ovf);
         }
         gbase = b.x;
         gmask = order_mask(ihit, oct);
@@ -186,6 +195,8 @@ __device__ __forceinline__ bool tlas_traverse8(const SceneDev& S, const Ray& r, 
         if (gmask && sp < stk.cap) {
           stack_put<STACK, BLOCK>(stk, sp, gbase, gmask | (gimask << 8));
           sp++;
+        } else if (gmask) {
+          stack_overflow(stk.ovf);
         }
         gbase = b.x;
         gmask = order_mask(ihit, oct);

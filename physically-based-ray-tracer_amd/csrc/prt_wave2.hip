@@ -525,6 +525,9 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
 #ifndef PRT_SHADE_GRID
   const unsigned gshade = B.n >= (1u << 21) ? 4u * gprod : gprod;
 #else
+  // the sub-queue bound of ensure_wave (qcap) holds only when block b appends to sub-queue b % kNSub for
+  // chunks c == b (mod kNSub), i.e. for grids that are multiples of kNSub
+  static_assert(PRT_SHADE_GRID % kNSub == 0, "PRT_SHADE_GRID must be a multiple of kNSub");
   const unsigned gshade = PRT_SHADE_GRID;
 #endif
   const uint32_t iters = wave_iters(S.has_diel != 0, A.bounces, A.flags);

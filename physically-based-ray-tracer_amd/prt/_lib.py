@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIBPATH = os.path.join(HERE, "libprt.so")
 
 PRT_OK = 0
-ABI_VERSION = 4  # PRT_ABI_VERSION of the include/prt.h these structs mirror
+ABI_VERSION = 5  # PRT_ABI_VERSION of the include/prt.h these structs mirror
 FLAG_AA, FLAG_ACCUMULATE, FLAG_GAMMA, FLAG_NORMALMAP, FLAG_SKYBOX, FLAG_LIGHTED, FLAG_STOCHASTIC = (1 << i for i in range(7))
 FLAGS_DEFAULT = 0x7F
 OUT_DEVICE = 1
@@ -86,7 +86,7 @@ class Stats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("shadow_rays", C.c_uint64), ("paths", C.c_uint64), ("ms", C.c_double),
                 ("ms_trace", C.c_double), ("ms_closest", C.c_double), ("ms_anyhit", C.c_double),
                 ("pipeline", C.c_int32), ("iterations", C.c_int32),
-                ("batches", C.c_int32), ("ranks", C.c_int32)]
+                ("batches", C.c_int32), ("ranks", C.c_int32), ("stack_overflows", C.c_uint64)]
 
 
 class Hit(C.Structure):

@@ -205,9 +205,10 @@ def load_model(path: str) -> Mesh:
     return mesh_from_indexed(P, N, UV, tri)
 
 
-def mesh_from_indexed(P: np.ndarray, N: np.ndarray, UV: np.ndarray, tri: np.ndarray) -> Mesh:
+def mesh_from_indexed(P: np.ndarray, N: np.ndarray, UV: np.ndarray, tri: np.ndarray, face_normals=None) -> Mesh:
     """Model's arrays (Core/Model.cpp:25-119) from indexed float32 positions / normals / (flipped) UVs and
-    (T, 3) corner indices: fat corners in face order, face normals = tmpl8 normalize(cross(e1, e2))."""
+    (T, 3) corner indices: fat corners in face order, face normals = tmpl8 normalize(cross(e1, e2)), unless the
+    caller states them (synthetic meshes whose |cross|^2 leaves float range)."""
     P, N, UV = (np.ascontiguousarray(a, F32) for a in (P, N, UV))
     tri = np.asarray(tri, np.int64).reshape(-1, 3)
     T = tri.shape[0]
@@ -217,12 +218,14 @@ def mesh_from_indexed(P: np.ndarray, N: np.ndarray, UV: np.ndarray, tri: np.ndar
     fixed_normals = np.zeros((3 * T, 4), F32)
     fixed_normals[:, :3] = N[corner]
     fixed_uvs = UV[corner]
-    v0, v1, v2 = P[tri[:, 0]], P[tri[:, 1]], P[tri[:, 2]]
-    e1, e2 = (v1 - v0).astype(F32), (v2 - v0).astype(F32)
-    cr = np.stack([e1[:, 1] * e2[:, 2] - e1[:, 2] * e2[:, 1], e1[:, 2] * e2[:, 0] - e1[:, 0] * e2[:, 2],
-                   e1[:, 0] * e2[:, 1] - e1[:, 1] * e2[:, 0]], axis=1).astype(F32)  # tmpl8 cross
+    if face_normals is None:
+        v0, v1, v2 = P[tri[:, 0]], P[tri[:, 1]], P[tri[:, 2]]
+        e1, e2 = (v1 - v0).astype(F32), (v2 - v0).astype(F32)
+        cr = np.stack([e1[:, 1] * e2[:, 2] - e1[:, 2] * e2[:, 1], e1[:, 2] * e2[:, 0] - e1[:, 0] * e2[:, 2],
+                       e1[:, 0] * e2[:, 1] - e1[:, 1] * e2[:, 0]], axis=1).astype(F32)  # tmpl8 cross
+        face_normals = _normalize(cr)
     return Mesh(triangles.reshape(-1), fixed_normals.reshape(-1), fixed_uvs.reshape(-1).astype(F32),
-                corner.astype(np.int32), P.reshape(-1), _normalize(cr).reshape(-1))
+                corner.astype(np.int32), P.reshape(-1), np.ascontiguousarray(face_normals, F32).reshape(-1))
 
 
 def model_textures(path: str, ext: str = ".png") -> dict:

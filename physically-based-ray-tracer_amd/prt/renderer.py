@@ -272,7 +272,7 @@ class Context:
             pa, pr = avg, rgb8  # raw device pointers (ints) or None
         check(self.L.prt_render(self.h, C.byref(p), pa, pr, _lib.OUT_DEVICE if device_out else 0,
                                 C.byref(st) if st is not None else None))
-        return avg, rgb8, st
+        return avg, rgb8, _checked(st)
 
     def reset_accumulation(self, full=True):
         check(self.L.prt_reset_accumulation(self.h, 1 if full else 0))
@@ -282,7 +282,7 @@ class Context:
                                                ("inst", np.uint32)])
         st = _lib.Stats()
         check(self.L.prt_trace_primary(self.h, width, height, hits.ctypes.data, 0, C.byref(st)))
-        return hits, st
+        return hits, _checked(st)
 
     def intersect(self, O, D, tmax=None):
         O, D = _f32(O), _f32(D)
@@ -310,13 +310,21 @@ class Context:
         st = _lib.Stats() if stats else None
         check(self.L.prt_render_tiles(self.h, C.byref(p), tile, rank, world, tiles_dev_ptr,
                                       C.byref(st) if st is not None else None))
-        return st
+        return _checked(st)
 
     def untile(self, gathered_dev_ptr, width, height, tile, world, avg_dev_ptr, rgb8_dev_ptr):
         check(self.L.prt_untile(self.h, gathered_dev_ptr, width, height, tile, world, avg_dev_ptr, rgb8_dev_ptr))
 
     def set_stream(self, stream_ptr):
         check(self.L.prt_set_stream(self.h, stream_ptr))
+
+
+def _checked(st):
+    """Stats of a call whose context has dropped a traversal stack group (prt_stats.stack_overflows) raise:
+    such a render may have lost hits, and the host sizes the stacks so that it cannot happen."""
+    if st is not None and st.stack_overflows:
+        raise _lib.PrtError(f"traversal stack overflow: {st.stack_overflows} node groups dropped")
+    return st
 
 
 class Renderer:

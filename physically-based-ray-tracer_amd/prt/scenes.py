@@ -271,7 +271,11 @@ def deep_bvh(n: int = 1000, r: float = 1.04) -> SceneData:
     P = P.reshape(-1, 3).astype(F32)
     N = np.tile(np.array([0.0, 0.0, -1.0], F32), (3 * n, 1))
     UV = np.tile(np.array([[0.1, 0.1], [0.9, 0.1], [0.1, 0.9]], F32), (n, 1))
-    m = ingest.mesh_from_indexed(P, N, UV, np.arange(3 * n).reshape(-1, 3))
+    # face normals stated exactly: every triangle lies in a z plane with counter-clockwise corners seen from -z,
+    # so normalize(cross(e1, e2)) = (0, 0, 1); tmpl8's float normalize of the outer triangles' cross products
+    # (|c|^2 ~ 1e70) would overflow to zero-length normals
+    fn = np.tile(np.array([0.0, 0.0, 1.0], F32), (n, 1))
+    m = ingest.mesh_from_indexed(P, N, UV, np.arange(3 * n).reshape(-1, 3), face_normals=fn)
     albedo, metalness, normal, emis = procedural_textures()
     m.albedo, m.metalness = 0, 1
     return SceneData([m], [albedo, metalness], [(0, IDENTITY.copy())], scene1_lights(), procedural_sky(),

@@ -62,22 +62,38 @@ class ShardedFrame:
     join_rccl.
 
     ctx: this rank's prt.Context (its own GPU); tiles and gathered buffers live on that GPU.  On a GPU the
-    context is moved onto torch's current stream, so the gather (queued there by torch) is ordered after
-    the tile render and before the untile.
+    frame runs on a dedicated torch stream that the context is moved onto: the tile render, the gather
+    (queued there by torch) and the untile are ordered on it without a host sync.  A dedicated stream, not
+    torch's current one, because the current one may be the legacy default stream, which the context's
+    non-blocking stream (prt_set_stream(NULL)) does not order against.  The stream waits for the caller's
+    current stream on entry and the caller's stream waits for it on exit.
     render() returns this rank's prt_stats; rank 0's avg/rgb8 device buffers hold the full frame."""
 
     def __init__(self, ctx, dist, width: int, height: int, tile: int = 32, device=None):
         import torch
         self.ctx, self.dist, self.W, self.H, self.tile = ctx, dist, width, height, tile
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.stream = None
         if device is not None and torch.device(device).type == "cuda":
-            ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
+            self.stream = torch.cuda.Stream(device=device)
+            ctx.set_stream(self.stream.cuda_stream)
         per = tile_buffer_pixels(width, height, tile, self.world)
         self.tiles = torch.zeros((per, 4), dtype=torch.float32, device=device)
         self.gathered = (torch.zeros((self.world, per, 4), dtype=torch.float32, device=device)
                          if self.rank == 0 else None)
 
     def render(self, spp, bounces, avg_ptr, rgb8_ptr, frame_index=0, flags=_lib.FLAGS_DEFAULT, stats=True):
+        import torch
+        if self.stream is None:
+            return self._render(spp, bounces, avg_ptr, rgb8_ptr, frame_index, flags, stats)
+        caller = torch.cuda.current_stream(self.stream.device)
+        self.stream.wait_stream(caller)  # the caller's writes (buffers, scene updates) come first
+        with torch.cuda.stream(self.stream):
+            st = self._render(spp, bounces, avg_ptr, rgb8_ptr, frame_index, flags, stats)
+        caller.wait_stream(self.stream)  # the caller's later reads of avg / rgb8 come after the untile
+        return st
+
+    def _render(self, spp, bounces, avg_ptr, rgb8_ptr, frame_index, flags, stats):
         st = self.ctx.render_tiles(self.W, self.H, spp, bounces, self.tile, self.rank, self.world,
                                    self.tiles.data_ptr(), flags=flags, frame_index=frame_index, stats=stats)
         self.dist.gather(self.tiles, list(self.gathered.unbind(0)) if self.rank == 0 else None, dst=0)

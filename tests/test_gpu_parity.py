@@ -226,6 +226,25 @@ def test_c4_full_size_matches_oracle(gpu_ctx):
     assert (s_g.segments, s_g.shadow_rays) == (s_o.segments, s_o.shadow_rays)
 
 
+def test_c3_full_size_matches_oracle(gpu_ctx):
+    """Config C3 (the 100k-triangle scene) at its own size, 1920x1080, 4 spp, depth 4, full BRDF + shadow rays,
+    against the oracle: per-channel RMSE <= 1e-4 (BASELINE.json), >= 99.9 % bit-identical pixels, identical ray
+    counts (the reduced-size fixtures cover it against the reference traversal, tests/test_golden_ref.py)."""
+    import os
+    sd = scenes.config_c3()
+    W, H = 1920, 1080
+    gpu_scene(gpu_ctx, sd, W, H)
+    a_g, r_g, s_g = gpu_ctx.render(W, H, 4, 4)
+    osc = oracle.OracleScene(sd, W, H)
+    a_o, r_o, _, s_o = osc.render(W, H, spp=4, bounces=4, nthreads=min(16, os.cpu_count() or 1))
+    err = rmse(a_o, a_g)
+    exact = float(np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)))
+    assert err <= RMSE_TOL, (err, exact)
+    assert exact >= 0.999, (err, exact)
+    assert np.mean(r_o == r_g) >= 0.999
+    assert (s_g.segments, s_g.shadow_rays) == (s_o.segments, s_o.shadow_rays)
+
+
 def test_c5_quarter_matches_oracle(gpu_ctx):
     """Config C5 (C4 + the quad area light with MIS, 16 spp, depth 8) at a quarter of its pixels (1920x1080, the
     bench's CPU-baseline sample) against the oracle's extension restatement: RMSE <= 1e-4, >= 99.9 % identical

@@ -115,9 +115,13 @@ def test_rccl_world1_matches_single(gpu_ctx):
         c.close()
 
 
-def test_sharded_frame_torch_world1_no_stats(gpu_ctx):
-    """prt.tiles.ShardedFrame over a world-1 torch "nccl" group with stats off: the context follows torch's
-    stream, so tile render -> dist.gather -> untile are stream-ordered without a host sync."""
+@pytest.mark.parametrize("caller_stream", ["default", "side"])
+def test_sharded_frame_torch_world1_no_stats(gpu_ctx, caller_stream):
+    """prt.tiles.ShardedFrame over a world-1 torch "nccl" group with stats off: tile render -> dist.gather ->
+    untile run on the frame's own stream without a host sync, ordered after the caller's stream and before its
+    later reads, whether the caller is on the legacy default stream or a side stream."""
+    import contextlib
+
     import torch
     import torch.distributed as dist
     import prt
@@ -128,17 +132,89 @@ def test_sharded_frame_torch_world1_no_stats(gpu_ctx):
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     c = prt.Context(0)
+    side = torch.cuda.Stream() if caller_stream == "side" else None
     try:
         gpu_scene(c, sd, W, H)
-        shard = prt.tiles.ShardedFrame(c, dist, W, H, ts, device="cuda")
-        avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
-        rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
-        for _ in range(2):  # the second frame reuses the tile / gather buffers while nothing waits on the host
-            c.reset_accumulation(full=True)
-            shard.render(4, 3, avg.data_ptr(), rgb.data_ptr(), stats=False)
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            shard = prt.tiles.ShardedFrame(c, dist, W, H, ts, device="cuda")
+            avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+            rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+            for _ in range(2):  # the second frame reuses the tile / gather buffers while nothing waits on the host
+                c.reset_accumulation(full=True)
+                shard.render(4, 3, avg.data_ptr(), rgb.data_ptr(), stats=False)
+            out_avg, out_rgb = avg.clone(), rgb.clone()  # on the caller's stream: ordered after the untile
         torch.cuda.synchronize()
-        assert np.array_equal(avg.cpu().numpy(), a_full)
-        assert np.array_equal(rgb.cpu().numpy().view(np.uint32), r_full)
+        assert np.array_equal(out_avg.cpu().numpy(), a_full)
+        assert np.array_equal(out_rgb.cpu().numpy().view(np.uint32), r_full)
     finally:
         c.close()
         dist.destroy_process_group()
+
+
+def _visible_devices():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif("_visible_devices() < 2", reason="needs two visible GPUs (cross-device group / RCCL world 2)")
+def test_group_two_devices_matches_single(gpu_ctx):
+    """A local group over two devices (prt_create_group([0, 1])): member 1 renders on device 1 and its tile
+    buffer reaches member 0 by hipMemcpyPeerAsync, ordered by the cross-device events."""
+    import prt
+    sd = scenes.multi_instance(scenes.config_small(60, 40))
+    W, H, ts = 100, 70, 16
+    gpu_scene(gpu_ctx, sd, W, H)
+    a_full, r_full, s_full = gpu_ctx.render(W, H, 4, 3)
+    g = prt.Context(group=[0, 1], tile=ts)
+    try:
+        gpu_scene(g, sd, W, H)
+        for _ in range(2):  # the second frame's peer copy waits for the first frame's untile
+            g.reset_accumulation(full=True)
+            a, r, st = g.render(W, H, 4, 3)
+            assert np.array_equal(a, a_full) and np.array_equal(r, r_full)
+            assert (st.segments, st.shadow_rays) == (s_full.segments, s_full.shadow_rays)
+    finally:
+        g.close()
+
+
+def _rccl_rank(rank, world, port, out_path):
+    import torch
+    import torch.distributed as dist
+    import prt
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", rank))
+    sd = scenes.multi_instance(scenes.config_small(60, 40))
+    W, H = 100, 70
+    c = prt.Context(rank)
+    try:
+        gpu_scene(c, sd, W, H)
+        si = prt.tiles.join_rccl(c, dist, 16)
+        assert (si.rank, si.world) == (rank, world)
+        avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+        rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+        _, _, st = c.render(W, H, 4, 3, avg=avg.data_ptr(), rgb8=rgb.data_ptr(), device_out=True)
+        r = torch.tensor([st.segments, st.shadow_rays], dtype=torch.float64, device="cuda")
+        dist.all_reduce(r)
+        if rank == 0:
+            np.savez(out_path, avg=avg.cpu().numpy(), rgb=rgb.cpu().numpy().view(np.uint32),
+                     rays=r.cpu().numpy())
+    finally:
+        c.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif("_visible_devices() < 2", reason="needs two visible GPUs (RCCL refuses two ranks on one device)")
+def test_rccl_world2_matches_single(gpu_ctx, tmp_path):
+    """Two processes, one GPU each, one RCCL communicator inside the contexts: rank 1's tiles reach rank 0 through
+    ncclGather (NULL receive buffer on the non-root rank) and rank 0's frame equals the single-context frame."""
+    import torch.multiprocessing as mp
+    sd = scenes.multi_instance(scenes.config_small(60, 40))
+    W, H = 100, 70
+    gpu_scene(gpu_ctx, sd, W, H)
+    a_full, r_full, s_full = gpu_ctx.render(W, H, 4, 3)
+    out = str(tmp_path / "rank0.npz")
+    mp.spawn(_rccl_rank, args=(2, _free_port(), out), nprocs=2, join=True)
+    z = np.load(out)
+    assert np.array_equal(z["avg"], a_full) and np.array_equal(z["rgb"], r_full)
+    assert tuple(int(x) for x in z["rays"]) == (s_full.segments, s_full.shadow_rays)
