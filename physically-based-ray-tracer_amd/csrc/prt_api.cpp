@@ -39,7 +39,6 @@ int fail(int code, const std::string& msg) {
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
-  unsigned flags = 0;  // hipExtMallocWithFlags flags (hipDeviceMallocUncached for the streaming engine's state)
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
@@ -58,7 +57,7 @@ struct DevBuf {
   hipError_t ensure(size_t n) {
     if (n <= bytes && p) return hipSuccess;
     release();
-    hipError_t e = flags ? hipExtMallocWithFlags(&p, n ? n : 16, flags) : hipMalloc(&p, n ? n : 16);
+    hipError_t e = hipMalloc(&p, n ? n : 16);
     if (e == hipSuccess) bytes = n ? n : 16;
     return e;
   }
@@ -138,11 +137,6 @@ struct prt_ctx {
   uint32_t wave_n = 0, wave_levels = 0;
   bool wave_ext = false;
   WaveTimers wt = {};
-  // streaming engine (prt_stream.hip): item state + queues + control words, uncached
-  DevBuf sbuf;
-  StreamBufs sb = {};
-  uint32_t s_n = 0, s_levels = 0, s_iters = 0;
-  bool last_stream = false;
   // the last enqueued render, for its stats (read_stats)
   uint32_t last_iters = 0;
   bool last_timers = false;
@@ -411,53 +405,6 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces, bool ext) {
   return PRT_OK;
 }
 
-// Streaming engine (prt_stream.hip) buffers for n items: per-item state, the ray / shade queues (kParts partitions,
-// each able to take every entry of the call) and the control words, all in uncached device memory.  Queue entries
-// start empty (0xFF bytes) and the engine leaves them empty after a successful call.
-int ensure_stream(prt_ctx* c, uint32_t n, int bounces, uint32_t iters) {
-  const uint32_t levels = (uint32_t)std::max(1, bounces - 1);
-  const uint64_t cap_r = (uint64_t)n * iters * 5u + 64u, cap_s = 2ull * n * (iters + 2u) + 64u;
-  if (cap_r >= (1ull << 29) || cap_s >= (1ull << 29)) return fail(PRT_ERR_UNSUPPORTED, "too many items for the streaming queues");
-  StreamBufs& B = c->sb;
-  if (c->sbuf.p && c->s_n >= n && c->s_levels >= levels && c->s_iters >= iters) {
-    B.n = n;  // the SoA strides (R/T: depth * n + item) follow the current n; capacities stay
-    return PRT_OK;
-  }
-  size_t off = 0;
-  auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
-  const size_t o_ctl = take(4ull * kSqWords * kCtrStride), o_rq = take(4ull * kParts * cap_r), o_sq = take(4ull * kParts * cap_s);
-  const size_t o_seed = take(4ull * n), o_info = take(4ull * n), o_rinfo = take(4ull * n), o_pv = take(4ull * n),
-               o_ro = take(16ull * n), o_rd = take(16ull * n), o_R = take(16ull * n * levels), o_T = take(16ull * n * levels),
-               o_s1 = take(16ull * n), o_jit = take(8ull * n), o_hit = take(16ull * n), o_ne = take(16ull * n),
-               o_nb = take(16ull * n), o_nf = take(64ull * n), o_sho = take(64ull * n), o_shd = take(64ull * n);
-  c->sbuf.release();
-  const char* euc = std::getenv("PRT_STREAM_UC");  // A/B: 1 = uncached device memory
-  c->sbuf.flags = (euc && std::atoi(euc) == 1) ? hipDeviceMallocUncached : 0u;
-  HIP_TRY(c->sbuf.ensure(off));
-  char* b = c->sbuf.as<char>();
-  HIP_TRY(hipMemsetAsync(b + o_rq, 0xFF, o_seed - o_rq, c->stream));  // both queues: every entry empty
-  B.n = n; B.base = 0; B.cap_r = (uint32_t)cap_r; B.cap_s = (uint32_t)cap_s;
-  B.ctl = (uint32_t*)(b + o_ctl); B.rq = (uint32_t*)(b + o_rq); B.sq = (uint32_t*)(b + o_sq);
-  B.seed = (uint32_t*)(b + o_seed); B.info = (uint32_t*)(b + o_info); B.rinfo = (uint32_t*)(b + o_rinfo);
-  B.pv = (uint32_t*)(b + o_pv); B.ro = (float4*)(b + o_ro); B.rd = (float4*)(b + o_rd); B.R = (float4*)(b + o_R);
-  B.T = (float4*)(b + o_T); B.s1 = (float4*)(b + o_s1); B.jit = (float2*)(b + o_jit); B.hit = (float4*)(b + o_hit);
-  B.ne = (float4*)(b + o_ne); B.nb = (float4*)(b + o_nb); B.nf = (float4*)(b + o_nf); B.sho = (float4*)(b + o_sho);
-  B.shd = (float4*)(b + o_shd);
-  c->s_n = n; c->s_levels = levels; c->s_iters = iters;
-  return PRT_OK;
-}
-
-// Which engine renders a call: the streaming engine where it applies (reference features only: no area light,
-// dielectrics or debug views; BVHs within the LDS stacks; one pass) and PRT_STREAM asks for it (1: always, 0: never;
-// default: calls of at most kStreamAutoItems items, where the wavefront's straggler-bound launches dominate).
-constexpr uint64_t kStreamAutoItems = 0;
-bool use_stream(const SceneDev& S, const prt_render_params* p, bool ext, int32_t npass, uint64_t items) {
-  if (ext || p->render_mode != 0 || S.spill || npass != 1) return false;
-  const char* e = std::getenv("PRT_STREAM");
-  if (e) return std::atoi(e) != 0;
-  return items <= kStreamAutoItems;
-}
-
 // the shared trace + accumulate sequence for prt_render / prt_render_tiles
 // enqueues the render on the context stream; want_stats: per-launch timers + read_stats() afterwards
 int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4* avg_dev, uint32_t* rgb8_dev,
@@ -497,9 +444,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     return fail(PRT_ERR_UNSUPPORTED, S.has_diel ? "dielectric path trees exceed the wavefront iteration limit (lower bounces)"
                                                 : "too many wavefront iterations");
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  const bool streaming = use_stream(S, p, ext, npass, per * (uint64_t)F0);
-  rc = streaming ? ensure_stream(c, (uint32_t)(per * (uint64_t)F0), p->bounces, iters)
-                 : ensure_wave(c, (uint32_t)(per * (uint64_t)F0), p->bounces, ext);
+  rc = ensure_wave(c, (uint32_t)(per * (uint64_t)F0), p->bounces, ext);
   if (rc) return rc;
   // PRT_TAIL=0 switches the cooperative traversal tail off (prt_persist.h; A/B runs only)
   const char* et = std::getenv("PRT_TAIL");
@@ -526,25 +471,18 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
       rc = ensure_wave(c, (uint32_t)(per * (uint64_t)Fb), p->bounces, ext);
       if (rc) return rc;
     }
-    if (!streaming) {  // the queue counters and the fetch counters of the iterations this call uses (kMaxIters: capacity)
+    {  // the queue counters and the fetch counters of the iterations this call uses (kMaxIters is the capacity)
       const size_t qw = (size_t)(iters + 2) * 2 * kNSub * kCtrStride;
       const size_t fbase = (size_t)(kMaxIters + 2) * 2 * kNSub * kCtrStride;
       const size_t fw = (size_t)(iters + 2) * 2 * kParts * kCtrStride;
       HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * qw, c->stream));
       HIP_TRY(hipMemsetAsync(c->wb.ctr + fbase, 0, 4 * fw, c->stream));
     }
-    if (!streaming && ext && S.has_diel) HIP_TRY(hipMemsetAsync(c->wb.dst, 0, 4ull * c->wb.n, c->stream));
+    if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(c->wb.dst, 0, 4ull * c->wb.n, c->stream));
     float4* frames = c->frames.as<float4>();
-    if (streaming) {
-      HIP_TRY(hipMemsetAsync(c->sb.ctl, 0, 4ull * kSqWords * kCtrStride, c->stream));
-      if (timers) HIP_TRY(hipEventRecord(c->wt.ev[0], c->stream));
-      HIP_TRY(launch_stream(L, S, A, M, c->sb, frames));
-      if (timers) HIP_TRY(hipEventRecord(c->wt.ev[1], c->stream));
-    } else {
-      HIP_TRY(launch_wave_init(L, S, A, M, c->wb, frames));
-      for (uint32_t it = 0; it <= iters; it++)
-        HIP_TRY(launch_wave2_iter(L, S, A, M, c->wb, frames, timers ? &c->wt : nullptr, it));
-    }
+    HIP_TRY(launch_wave_init(L, S, A, M, c->wb, frames));
+    for (uint32_t it = 0; it <= iters; it++)
+      HIP_TRY(launch_wave2_iter(L, S, A, M, c->wb, frames, timers ? &c->wt : nullptr, it));
     if (last) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     // post-processing (single-GPU image): the screen pass needs the average and, for the aberration, the
     // accumulator before the last frame
@@ -576,7 +514,6 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   c->last_iters = iters;
   c->last_timers = timers;
-  c->last_stream = streaming;
   c->last_paths = tile_image_pixels(M) * (uint64_t)F * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
   return PRT_OK;
 }
@@ -594,41 +531,6 @@ uint64_t diag_overflows(prt_ctx* c) {
 int read_stats(prt_ctx* c, prt_stats* stats) {
   const uint32_t iters = c->last_iters;
   const bool timers = c->last_timers;
-  if (c->last_stream) {  // streaming engine: the ray counts and the error word are control words
-    std::memset(stats, 0, sizeof(*stats));
-    std::vector<uint32_t> ctl((size_t)kSqWords * kCtrStride);
-    HIP_TRY(hipMemcpyAsync(ctl.data(), c->sb.ctl, 4 * ctl.size(), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    const uint32_t err = ctl[(size_t)kSqError * kCtrStride];
-    uint32_t live = 0;
-    uint64_t seg = 0, sha = 0;
-    for (uint32_t p = 0; p < kParts; p++) {
-      live += ctl[(size_t)(kSqLive + p) * kCtrStride];
-      seg += ctl[(size_t)(kSqSegments + p) * kCtrStride];
-      sha += ctl[(size_t)(kSqShadow + p) * kCtrStride];
-    }
-    if (err || live) {
-      c->s_n = 0;  // queue entries may be left behind: the next call re-allocates and re-initialises them
-      return fail(PRT_ERR_HIP, std::string("streaming engine failed: ") +
-                                   ((err & 2u) ? "time limit" : (err & 1u) ? "queue capacity" : "items left unfinished"));
-    }
-    stats->segments = seg;
-    stats->shadow_rays = sha;
-    float a = 0, ms = 0, ms_trace = 0;
-    if (timers) HIP_TRY(hipEventElapsedTime(&a, c->wt.ev[0], c->wt.ev[1]));
-    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[2]));
-    HIP_TRY(hipEventElapsedTime(&ms_trace, c->ev[0], c->ev[1]));
-    stats->ms_closest = a;  // the whole persistent launch (shading included)
-    stats->stack_overflows = diag_overflows(c);
-    stats->pipeline = 3;
-    stats->iterations = 1;
-    stats->batches = 1;
-    stats->ranks = 1;
-    stats->paths = c->last_paths;
-    stats->ms = ms;
-    stats->ms_trace = ms_trace;
-    return PRT_OK;
-  }
   {
     std::memset(stats, 0, sizeof(*stats));
     // per-launch traversal times summed over every launch

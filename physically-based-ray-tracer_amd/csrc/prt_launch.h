@@ -73,44 +73,6 @@ struct WaveTimers {
   uint32_t iters;
 };
 
-// ---- streaming engine (prt_stream.hip): one persistent launch per call, items flow between traversal and
-// shading through queues instead of launch boundaries.  Every item lives on one XCD (its home partition): its
-// rays are traced and its shading done by waves of that XCD only, so all hand-offs of an item stay inside one
-// L2; readers skip their CU's L1 (non-temporal / sc1 loads) and writers drain their stores (s_waitcnt vmcnt(0))
-// before the atomic or queue entry that publishes them.
-constexpr uint32_t kStreamEmpty = 0xFFFFFFFFu;  // queue entry not yet written (entries are reset after use)
-enum : uint32_t {  // control words (kCtrStride apart), per partition where indexed
-  kSqRqTail = 0, kSqRqHead = kParts, kSqSqTail = 2 * kParts, kSqSqHead = 3 * kParts,
-  kSqLive = 4 * kParts, kSqSegments = 5 * kParts, kSqShadow = 6 * kParts, kSqError = 7 * kParts, kSqWords
-};
-struct StreamBufs {
-  uint32_t n;            // items of this call
-  uint32_t base;         // first item of the call's item range (0)
-  uint32_t cap_r, cap_s; // ray / shade queue capacity per partition (entries)
-  uint32_t* seed;
-  uint32_t* info;   // current closest ray: depth | path << 8
-  uint32_t* rinfo;  // what the item's next visit resolves: depth | path << 8 | status << 16 | kind << 20 | flags
-  uint32_t* pv;     // rays in flight (bits 0-7) | unoccluded shadow rays (bit 8 + k)
-  float4* ro;
-  float4* rd;
-  float4* R;        // (bounces - 1) x n
-  float4* T;
-  float4* s1;
-  float2* jit;
-  float4* hit;
-  float4* ne;
-  float4* nb;
-  float4* nf;       // 4 per item
-  float4* sho;      // 4 per item: shadow ray origin, tmax
-  float4* shd;      // 4 per item: direction
-  uint32_t* rq;     // ray queue entries [kParts][cap_r]: item << 3 | k (k < 4: shadow ray k, 4: closest ray)
-  uint32_t* sq;     // shade queue entries [kParts][cap_s]: item
-  uint32_t* ctl;    // control words
-};
-// items: primary rays into the ray queue; then the persistent launch until every item's frame value is written
-hipError_t launch_stream(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M, const StreamBufs& B,
-                         float4* out);
-
 hipError_t launch_wave_init(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                             const WaveBufs& B, float4* out);
 // merged pipeline (prt_wave2.hip): iteration `it` (0..iters) after launch_wave_init -- one traversal launch for

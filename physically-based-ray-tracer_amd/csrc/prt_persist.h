@@ -60,20 +60,11 @@ __device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
 // tail: tail_lds_words(TAILN) words of LDS for the cooperative tail, or nullptr (no tail mode).
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
-//
-// STREAM (prt_stream.hip): rays come from tickets instead of a launch's fixed range.  fetch(nullptr, want) claims
-// tickets for idle lanes and returns how many it got (0: the queue is empty for now); poll() returns the queue
-// entry of this lane's ticket once it is written (0xFFFFFFFF before), which load() turns into a ray.  Lanes poll in
-// the iteration of a claim and in the first iteration; the loop returns as soon as no lane holds a ray (the caller
-// shades, then calls again), and there is no cooperative tail.
-struct NoPoll {
-  __device__ uint32_t operator()() const { return 0xFFFFFFFFu; }
-};
-template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, bool SPILL = false, bool STREAM = false,
-          class Fetch, class Load, class Reload, class Finish, class Tick, class Poll = NoPoll>
+template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, bool SPILL = false, class Fetch,
+          class Load, class Reload, class Finish, class Tick>
 __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                    Load load, Reload reload, Finish finish, Tick tick,
-                                                   uint32_t* __restrict__ tail = nullptr, Poll poll = Poll{}) {
+                                                   uint32_t* __restrict__ tail = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   bool active = false, drained = false;
@@ -255,34 +246,11 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     }
     return false;
   };
-  bool first = true;
   while (true) {
     // ---- refill idle lanes from the queue
     const uint64_t idle = __ballot(!active);
     tick((uint32_t)__popcll(idle), drained);
-    if constexpr (STREAM) {
-      bool poll_now = first;
-      first = false;
-      if (!drained && __popcll(idle) >= (uint32_t)REFILL) {
-        if (fetch(nullptr, (uint32_t)__popcll(idle)) == 0) drained = true;
-        poll_now = true;
-      }
-      if (poll_now && !active) {
-        const uint32_t e = poll();
-        if (e != 0xFFFFFFFFu) {
-          V3 Ow, Dw;
-          float tmax;
-          bool a = MODE == 1;
-          handle = load(e, Ow, Dw, tmax, a);
-          if (MODE == 2) any = a;
-          h.t = tmax; h.u = 0.0f; h.v = 0.0f; h.prim = 0; h.inst = 0;
-          lhit = 0; tcnt = 0;
-          if (enter(0, Ow, Dw)) active = true;
-          else finish(handle, h, any, false);
-        }
-      }
-      if (__ballot(active) == 0) return;
-    } else if (!drained && __popcll(idle) >= (uint32_t)REFILL) {
+    if (!drained && __popcll(idle) >= (uint32_t)REFILL) {
       uint32_t base = 0;
       const uint32_t want = (uint32_t)__popcll(idle);
       const uint32_t got = fetch(&base, want);

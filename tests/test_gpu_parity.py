@@ -413,38 +413,3 @@ def test_frame_passes_match_one_pass(gpu_ctx, monkeypatch):
     a2, r2, s2 = gpu_ctx.render(W, H, spp, 3)
     assert np.array_equal(a1, a2) and np.array_equal(r1, r2)
     assert (s1.segments, s1.shadow_rays) == (s2.segments, s2.shadow_rays)
-
-
-@pytest.mark.parametrize("case", ["multi", "tlas", "noaa", "flat", "c3"])
-def test_streaming_engine_identical(gpu_ctx, monkeypatch, case):
-    """The streaming engine (prt_stream.hip: one persistent launch, items flowing between the ray and shade
-    queues, PRT_STREAM=1) renders the same frames as the merged wavefront (PRT_STREAM=0): image, RGB8 and ray
-    counts bit-identical, over the linear instance list and the instance BVH, with and without AA / stochastic
-    NEE, and on the C3 scene; its stats say pipeline 3."""
-    flags = oracle.DEFAULT_FLAGS
-    W, H, spp, bounces = 96, 64, 4, 4
-    if case == "multi":
-        sd = scenes.multi_instance(scenes.config_small(50, 40))
-    elif case == "tlas":
-        monkeypatch.setenv("PRT_TLAS", "1")
-        sd = scenes.multi_instance(scenes.config_small(50, 40))
-    elif case == "noaa":
-        sd, flags, spp = scenes.config_small(40, 30), oracle.DEFAULT_FLAGS & ~oracle.AA, 3
-    elif case == "flat":
-        sd, flags = scenes.config_small(40, 30), oracle.DEFAULT_FLAGS & ~(oracle.STOCHASTIC | oracle.SKYBOX)
-    else:
-        sd, W, H = scenes.config_c3(), 480, 270
-    gpu_scene(gpu_ctx, sd, W, H)
-    out = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("PRT_STREAM", mode)
-        gpu_ctx.reset_accumulation(full=True)
-        out[mode] = gpu_ctx.render(W, H, spp, bounces, flags)
-        gpu_ctx.render(W, H, spp, bounces, flags, frame_index=spp // 2)  # accumulating second call
-        out[mode + "b"] = gpu_ctx.render(W, H, spp, bounces, flags, frame_index=spp)
-    assert out["1"][2].pipeline == 3 and out["0"][2].pipeline == 2
-    for k in ("", "b"):
-        a0, r0, s0 = out["0" + k]
-        a1, r1, s1 = out["1" + k]
-        assert np.array_equal(a0, a1) and np.array_equal(r0, r1), k
-        assert (s0.segments, s0.shadow_rays) == (s1.segments, s1.shadow_rays), k
