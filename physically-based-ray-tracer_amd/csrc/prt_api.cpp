@@ -15,6 +15,7 @@
 #include "bvh_build.h"
 #include "bvh_gpu.h"
 #include "prt_launch.h"
+#include "prt_tlas.h"
 #include "prt_rccl.h"
 #include "prt_refit.h"
 
@@ -108,8 +109,10 @@ struct prt_ctx {
   // instance BVH (more than kLinearInstances instances, or PRT_TLAS=1): rebuilt on the host with the instances
   bool use_tlas = false;
   int tlas_depth = 0;
-  BuiltTlas8 tlas_host;
-  DevBuf tlas8, tlas_slot;
+  BuiltTlas8 tlas_host;  // the last host build (its topology is what the device refits)
+  TlasTopo tlas_topo;    // its nodes by depth, deepest first (prt_tlas.h)
+  int32_t tlas_n = -1;   // instance count of that build (-1: none)
+  DevBuf tlas8, tlas_slot, tlas_order, tlas_aabb;
   DevBuf spill;  // traversal stack levels beyond the LDS ones (BVHs deeper than 17 levels)
   DevBuf diag;   // SceneDev::diag device counters ([0] traversal stack overflows, cumulative per context)
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
@@ -215,7 +218,14 @@ int ensure_instances(prt_ctx* c) {
   // BLASInstances every frame as the reference does (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770)
   const char* te = std::getenv("PRT_TLAS");
   c->use_tlas = n > kLinearInstances || (te && std::atoi(te) == 1);
-  if (c->use_tlas) {
+  // the instance BVH: built by the host SAH builder when the set of instances changes (its count; or every call with
+  // PRT_TLAS_HOST=1, the A/B form), otherwise refitted on the device behind k_refit (prt_tlas.hip): the reference
+  // rebuilds it every frame (Core/Renderer.cpp:33-41); a per-frame update costs no host BVH work and no sync
+  const char* th = std::getenv("PRT_TLAS_HOST");
+  if (c->use_tlas && c->tlas_n == n && !(th && std::atoi(th) == 1)) {
+    HIP_TRY(launch_tlas_refit(c->stream, c->inst.as<InstDev>(), c->tlas_topo, c->tlas_order.as<uint32_t>(),
+                              c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(), c->tlas_aabb.as<float>()));
+  } else if (c->use_tlas) {
     std::vector<float> boxes(6 * (size_t)n);
     for (int32_t i = 0; i < n; i++) {
       InstDev I;
@@ -232,10 +242,21 @@ int ensure_instances(prt_ctx* c) {
       HIP_TRY(c->tlas8.ensure(nb));
       HIP_TRY(c->tlas_slot.ensure(sb));
     }
+    c->tlas_topo = tlas_topology(c->tlas_host.nodes);
+    const size_t ob = 4 * c->tlas_topo.order.size(), ab = 24 * c->tlas_host.nodes.size();
+    if (c->tlas_order.bytes < ob || c->tlas_aabb.bytes < ab) {
+      const int rc = drain(c);
+      if (rc) return rc;
+      HIP_TRY(c->tlas_order.ensure(ob));
+      HIP_TRY(c->tlas_aabb.ensure(ab));
+    }
     HIP_TRY(hipMemcpyAsync(c->tlas8.p, c->tlas_host.nodes.data(), nb, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->tlas_slot.p, c->tlas_host.slot.data(), sb, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->tlas_order.p, c->tlas_topo.order.data(), ob, hipMemcpyHostToDevice, c->stream));
+    c->tlas_n = n;
   } else {
     c->tlas_depth = 0;
+    c->tlas_n = -1;
   }
   c->inst_dirty = false;
   return PRT_OK;

@@ -413,3 +413,44 @@ def test_frame_passes_match_one_pass(gpu_ctx, monkeypatch):
     a2, r2, s2 = gpu_ctx.render(W, H, spp, 3)
     assert np.array_equal(a1, a2) and np.array_equal(r1, r2)
     assert (s1.segments, s1.shadow_rays) == (s2.segments, s2.shadow_rays)
+
+
+@pytest.mark.parametrize("n", [65, 1000])
+def test_device_tlas_moving_instances(gpu_ctx, monkeypatch, n):
+    """Above 64 instances the instance BVH is refitted on the device behind the instance refit (prt_tlas.hip), in
+    stream order, while the instance count stays: every instance moves before every frame, frames are queued back to
+    back with no host synchronisation, and each equals the oracle's render of its transforms; an instance BVH the host
+    rebuilds for every call (PRT_TLAS_HOST=1) renders the same."""
+    import dataclasses
+    import torch
+    sd0 = scenes.instance_field(n, seed=11)
+    W, H = 64, 48
+    flags = oracle.DEFAULT_FLAGS & ~oracle.ACCUMULATE
+    rng = np.random.default_rng(n)
+    frames = []
+    inst = [(m, np.array(T, np.float32)) for m, T in sd0.instances]
+    for f in range(3):
+        moved = []
+        for m, T in inst:
+            T = T.copy()
+            if m == 1:  # the tori move; the heightfield stays
+                T[0, 3] += np.float32(rng.uniform(-0.2, 0.2))
+                T[2, 3] += np.float32(rng.uniform(-0.2, 0.2))
+            moved.append((m, T))
+        inst = moved
+        frames.append(dataclasses.replace(sd0, instances=list(inst)))
+    gpu_scene(gpu_ctx, sd0, W, H)
+    assert gpu_ctx.scene_info().tlas_depth > 0
+    out = [torch.zeros((W * H, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    for sd, o in zip(frames, out):
+        gpu_ctx.set_instances(sd.instances)
+        gpu_ctx.render(W, H, 2, 3, flags, avg=o.data_ptr(), rgb8=rgb.data_ptr(), device_out=True, stats=False)
+    torch.cuda.synchronize()
+    for sd, o in zip(frames, out):
+        a_o, _, _, _ = oracle.OracleScene(sd, W, H).render(W, H, spp=2, bounces=3, flags=flags)
+        assert np.array_equal(o.cpu().numpy(), a_o)
+    monkeypatch.setenv("PRT_TLAS_HOST", "1")
+    gpu_ctx.set_instances(frames[-1].instances)
+    a_h, r_h, _ = gpu_ctx.render(W, H, 2, 3, flags)
+    assert np.array_equal(a_h, out[-1].cpu().numpy())
