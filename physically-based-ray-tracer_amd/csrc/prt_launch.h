@@ -44,8 +44,7 @@ struct WaveBufs {
   uint32_t* vis;    // 4 visibility bytes per item
   uint32_t* q0;
   uint32_t* q1;
-  float4* sho;      // shadow queue: O, tmax
-  float4* shd;      // shadow queue: D, bits(4 * item + slot)
+  float4* sho;      // shadow queue: hit point I, bits(light << 29 | visibility index) (prt_wave2.hip shadow_of)
   uint32_t* ctr;    // [iteration][path|shadow][sub-queue] counters, kCtrStride apart
   // extensions (area light / dielectric instances; merged pipeline only): vis holds 5 x n bytes, the area
   // light's shadow ray writes byte 4 * n + item
@@ -54,6 +53,8 @@ struct WaveBufs {
                     // 16-23 reflected radiance stored (in T[level]), 24-31 no refraction (k <= 0)
   float4* dro;      // per level: refraction ray origin, fresnel
   float4* drd;      // per level: refraction ray direction
+  float4* ao;       // the area light's shadow ray per item: origin, tmax (its NEE sample is random: stored whole)
+  float4* ad;       // ... direction
   unsigned long long* tl;  // PRT_DEBUG_QUEUES: [launch][wave] {start, first empty fetch, exit, -}
   int32_t coop_tail;       // cooperative traversal tail (prt_persist.h)
   int32_t pad;

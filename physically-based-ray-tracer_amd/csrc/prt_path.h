@@ -57,7 +57,36 @@ __device__ __forceinline__ int nee_kind(uint32_t fl, uint32_t& seed) {
 }
 __device__ __forceinline__ int nee_rays(int kind) { return kind == 0 ? 4 : 1; }
 
-// Builds the shadow rays of `kind` (emit(k, ray, tmax, f_k) per ray, in order, with f_k the ray's
+// The shadow ray towards light `light` (0-3: point light i, kLightDir: the directional light, kLightSpot: the
+// spot) from hit point I, as Core/Renderer.cpp:216-310 builds it; L gets the unit direction and dl the squared
+// distance (point) or the distance (directional / spot) that the contribution uses.  The shading kernel and the
+// traversal kernel both call this, so a queued shadow ray is only (I, light) and rebuilds bit for bit.
+constexpr uint32_t kLightDir = 4, kLightSpot = 5, kLightArea = 6;
+__device__ __forceinline__ void light_ray(const SceneDev& S, uint32_t light, V3 I, Ray& r, float& tmax, V3& L,
+                                          float& dl) {
+  if (light < 4) {                                                                          // :216-257
+    const int i = (int)light;
+    float Lx = S.ppos[3 * i] - I.x, Ly = S.ppos[3 * i + 1] - I.y, Lz = S.ppos[3 * i + 2] - I.z;
+    const float dsq = (Lx * Lx + Ly * Ly) + Lz * Lz;
+    const float dist = sqrtf(dsq);
+    const float invD = 1.0f / dist;  // _mm_rcp_ps restated as an exact reciprocal
+    Lx = Lx * invD; Ly = Ly * invD; Lz = Lz * invD;
+    L = v3(Lx, Ly, Lz);
+    dl = dsq;
+    r = make_ray(I + L * kEpsilon, L);
+    tmax = dsq - kEpsilon;                                                                  // tmax = squared distance (:257)
+    return;
+  }
+  const float* lp = (light == kLightSpot) ? S.spos : S.dpos;                                // :270-326
+  L = v3(lp[0], lp[1], lp[2]) - I;
+  const float distance = length(L);
+  L = L / distance;
+  dl = distance;
+  r = make_ray(I + L * kEpsilon, L);
+  tmax = distance - kEpsilon;
+}
+
+// Builds the shadow rays of `kind` (emit(k, light, ray, tmax, f_k) per ray, in order, with f_k the ray's
 // unoccluded contribution before the pick-probability division) and returns the BRDF value the reference
 // evaluates for this light class (0 when !LIGHTED).  Draws whichLight for point lights: the reference
 // draws it after tracing the four shadow rays (:267), which consume no random numbers, so drawing it
@@ -70,27 +99,26 @@ __device__ __forceinline__ V3 nee_lights(const SceneDev& S, uint32_t fl, int kin
     V3 Lw = v3(0.0f, 0.0f, 0.0f);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      float Lx = S.ppos[3 * i] - I.x, Ly = S.ppos[3 * i + 1] - I.y, Lz = S.ppos[3 * i + 2] - I.z;
-      const float dsq = (Lx * Lx + Ly * Ly) + Lz * Lz;
-      const float dist = sqrtf(dsq);
-      const float invD = 1.0f / dist;  // _mm_rcp_ps restated as an exact reciprocal
-      Lx = Lx * invD; Ly = Ly * invD; Lz = Lz * invD;
-      float cosa = (N.x * Lx + N.y * Ly) + N.z * Lz;
+      Ray r;
+      float tmax, dsq;
+      V3 L;
+      light_ray(S, (uint32_t)i, I, r, tmax, L, dsq);
+      const float invD = 1.0f / sqrtf(dsq);  // the same exact reciprocal light_ray scaled L by
+      float cosa = (N.x * L.x + N.y * L.y) + N.z * L.z;
       cosa = (cosa > 0.0f) ? cosa : 0.0f;  // _mm_max_ps(cosa, 0)
       const float k = invD * cosa;
-      const V3 L = v3(Lx, Ly, Lz);
       if (i == wl) Lw = L;
-      emit(i, make_ray(I + L * kEpsilon, L), dsq - kEpsilon,                                // tmax = squared distance (:257)
-           v3(S.pcol[3 * i] * k, S.pcol[3 * i + 1] * k, S.pcol[3 * i + 2] * k));
+      emit(i, (uint32_t)i, r, tmax, v3(S.pcol[3 * i] * k, S.pcol[3 * i + 1] * k, S.pcol[3 * i + 2] * k));
     }
     if (!(fl & kLighted)) return v3(0.0f, 0.0f, 0.0f);
     return eval_combined_brdf(N, Lw, V, m);
   }
-  const float* lp = (kind == 2) ? S.spos : S.dpos;                                          // :270-326
-  const float* lc = (kind == 2) ? S.scol : S.dcol;
-  V3 L = v3(lp[0], lp[1], lp[2]) - I;
-  const float distance = length(L);
-  L = L / distance;
+  const float* lc = (kind == 2) ? S.scol : S.dcol;                                          // :270-326
+  const uint32_t light = (kind == 2) ? kLightSpot : kLightDir;
+  Ray r;
+  float tmax, distance;
+  V3 L;
+  light_ray(S, light, I, r, tmax, L, distance);
   const float cosa = smax(0.0f, dot(N, L));
   V3 f0;
   if (kind == 2) {
@@ -100,7 +128,7 @@ __device__ __forceinline__ V3 nee_lights(const SceneDev& S, uint32_t fl, int kin
   } else {
     f0 = v3(lc[0], lc[1], lc[2]) * cosa;
   }
-  emit(0, make_ray(I + L * kEpsilon, L), distance - kEpsilon, f0);
+  emit(0, light, r, tmax, f0);
   return (fl & kLighted) ? eval_combined_brdf(N, L, V, m) : v3(0.0f, 0.0f, 0.0f);
 }
 

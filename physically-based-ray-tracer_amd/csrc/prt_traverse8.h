@@ -69,7 +69,9 @@ struct LaneStack {
 // a group that finds no free stack level is counted, never silently lost (the host sizes the stacks from the
 // BVH depth, so the count stays 0; prt_stats.stack_overflows reports it and the Python mirror raises on it)
 __device__ __forceinline__ void stack_overflow(uint32_t* ovf) {
+#ifndef PRT_NO_OVF_COUNT  // A/B only
   if (ovf) atomicAdd(ovf, 1u);
+#endif
 }
 template <int STACK, int BLOCK>
 __device__ __forceinline__ LaneStack lane_stack(const SceneDev& S, uint32_t* lds) {

@@ -67,6 +67,31 @@ __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, T
   }
 }
 
+// ---- a shadow-queue record -> its world ray: (I, light << 29 | index) rebuilt by light_ray exactly as the shading
+// kernel's NEE built it; the area light's rays (EXT, light kLightArea, index = item) are stored whole in ao / ad
+constexpr uint32_t kShIndexMask = (1u << 29) - 1u;
+__device__ __forceinline__ void shadow_of(const SceneDev& S, const WaveBufs& B, float4 e, V3& O, V3& D, float& tmax) {
+  const uint32_t code = __float_as_uint(e.w), light = code >> 29;
+  if (light == kLightArea) {
+    const float4 o = B.ao[code & kShIndexMask], d = B.ad[code & kShIndexMask];
+    O = v3(o.x, o.y, o.z);
+    D = v3(d.x, d.y, d.z);
+    tmax = o.w;
+    return;
+  }
+  Ray r;
+  V3 L;
+  float dl;
+  light_ray(S, light, v3(e.x, e.y, e.z), r, tmax, L, dl);
+  O = r.O;
+  D = r.D;
+}
+// the visibility byte of a shadow-queue record: 4 x item + k, or 4n + item for the area light's ray
+__device__ __forceinline__ uint32_t shadow_vis(const WaveBufs& B, float4 e) {
+  const uint32_t code = __float_as_uint(e.w);
+  return (code >> 29) == kLightArea ? 4u * B.n + (code & kShIndexMask) : (code & kShIndexMask);
+}
+
 // ---- one traversal launch: closest hits of P(iter) (iter < iters) + any hits of S(iter - 1) (iter > 0)
 template <int REFILL, int STACK, int WAVES, int TAILN, bool TLAS, bool SPILL = false>
 __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, uint32_t iter, uint32_t iters) {
@@ -106,23 +131,27 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
           any = false;
         } else {
           h = map_slot(prefS, g - nP, B.scap);
-          o = B.sho[h];
-          d = B.shd[h];
-          tmax = o.w;
           any = true;
+          shadow_of(S, B, B.sho[h], O, D, tmax);
+          return h;
         }
         O = v3(o.x, o.y, o.z);
         D = v3(d.x, d.y, d.z);
         return h;
       },
       [&](uint32_t h, bool any, V3& O, V3& D) {
-        const float4 o = any ? B.sho[h] : B.ro[h], d = any ? B.shd[h] : B.rd[h];
+        if (any) {
+          float tmax;
+          shadow_of(S, B, B.sho[h], O, D, tmax);
+          return;
+        }
+        const float4 o = B.ro[h], d = B.rd[h];
         O = v3(o.x, o.y, o.z);
         D = v3(d.x, d.y, d.z);
       },
       [&](uint32_t h, const Hit& hit, bool any, bool occluded) {
         if (any) {
-          if (!occluded) vis8[__float_as_uint(B.shd[h].w)] = 1;
+          if (!occluded) vis8[shadow_vis(B, B.sho[h])] = 1;
         } else {
           B.hit[h] = make_float4(hit.t, hit.u, hit.v, __uint_as_float(pack_hit(S, hit.prim, hit.inst)));
         }
@@ -214,7 +243,6 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
   uint32_t* shcnt = qcounter(B.ctr, iter, 1, sub);
   uint32_t* ncnt = qcounter(B.ctr, iter + 1, 0, sub);
   float4* sho = B.sho + (size_t)sub * B.scap;
-  float4* shd = B.shd + (size_t)sub * B.scap;
   const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
   const uint32_t fl = A.flags;
   // software pipeline over the grid-stride chunks: the next chunk's item, info, hit and seed are loaded while this
@@ -253,7 +281,6 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
     uint32_t status = kStMiss;
     bool next = false;
     bool area_ray = false;
-    float4 ar_o, ar_d;
     if (nr) {
       const float4 o = B.ro[item], d = B.rd[item];
       const V3 D = v3(d.x, d.y, d.z);
@@ -263,9 +290,10 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
       const HitAttr ha = hit_attributes(S, hit_inst(S, pk), hit_prim(S, pk), hh.y, hh.z, (fl & kNormalMap) != 0);
       const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
       B.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
-      const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed, [&](int k, const Ray& sr, float tmax, V3 fk) {
-        sho[s0 + k] = make_float4(sr.O.x, sr.O.y, sr.O.z, tmax);
-        shd[s0 + k] = make_float4(sr.D.x, sr.D.y, sr.D.z, __uint_as_float(4u * item + (uint32_t)k));
+      // a shadow ray is queued as (I, light, visibility index): the traversal kernel rebuilds it (shadow_of)
+      const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed,
+                                 [&](int k, uint32_t light, const Ray&, float, V3 fk) {
+        sho[s0 + k] = make_float4(I.x, I.y, I.z, __uint_as_float((light << 29) | (4u * item + (uint32_t)k)));
         B.nf[4 * (size_t)item + k] = make_float4(fk.x, fk.y, fk.z, 0.0f);
       });
       B.nb[item] = make_float4(brdf.x, brdf.y, brdf.z, 0.0f);
@@ -281,8 +309,8 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
           V3 fa;
           if (area_nee(area_light(S), I, ha.N, V, ha.m, xi1, xi2, sr, tmax, fa)) {
             area_ray = true;
-            ar_o = make_float4(sr.O.x, sr.O.y, sr.O.z, tmax);
-            ar_d = make_float4(sr.D.x, sr.D.y, sr.D.z, __uint_as_float(4u * B.n + item));
+            B.ao[item] = make_float4(sr.O.x, sr.O.y, sr.O.z, tmax);
+            B.ad[item] = make_float4(sr.D.x, sr.D.y, sr.D.z, 0.0f);
             B.na[item] = make_float4(fa.x, fa.y, fa.z, 0.0f);
           }
         }
@@ -322,10 +350,7 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
     }
     if constexpr (EXT) {  // the area-light shadow rays of the block, one more append
       const uint32_t a0 = block_append(shcnt, area_ray ? 1u : 0u, sm);
-      if (area_ray) {
-        sho[a0] = ar_o;
-        shd[a0] = ar_d;
-      }
+      if (area_ray) sho[a0] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((kLightArea << 29) | item));
     }
     if (active) {
       if (status != kStNeeCont) {
