@@ -541,13 +541,15 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   return PRT_OK;
 }
 
-// the context's traversal stack overflow count (SceneDev::diag[0]); waits for the context stream
-uint64_t diag_overflows(prt_ctx* c) {
-  uint32_t v = 0;
-  if (hipMemcpyAsync(&v, c->diag.p, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+// the context's traversal stack overflow count (SceneDev::diag[0]); waits for the context stream.  diag[1] != 0:
+// a kernel found its kernarg layout assumption broken (prt_wave2.hip Shade2Args) and did no work
+uint64_t diag_overflows(prt_ctx* c, bool* layout_ok = nullptr) {
+  uint32_t v[2] = {0, 0};
+  if (hipMemcpyAsync(v, c->diag.p, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return ~0ull;  // unreadable counts as overflowed: never report a clean run that was not checked
-  return v;
+  if (layout_ok) *layout_ok = v[1] == 0;
+  return v[0];
 }
 
 // waits for the last render of run_render(..., want_stats = true) and fills its stats
@@ -602,7 +604,9 @@ int read_stats(prt_ctx* c, prt_stats* stats) {
                      q(0.99), ex.empty() ? 0.0 : ex.back());
       }
     }
-    stats->stack_overflows = diag_overflows(c);
+    bool layout_ok = true;
+    stats->stack_overflows = diag_overflows(c, &layout_ok);
+    if (!layout_ok) return fail(PRT_ERR_HIP, "k_shade2: kernel-argument layout check failed (Shade2Args)");
     stats->segments += c->carry_segments;  // earlier passes of a call above 2^30 work items
     stats->shadow_rays += c->carry_shadow;
     stats->pipeline = 2;

@@ -71,7 +71,7 @@ struct SceneDev {
   uint32_t pbits;   // prim bits of a packed hit word (prt_queue.h pack_hit)
   int32_t spill_levels;  // traversal stack levels beyond the LDS ones, in HBM (prt_traverse8.h LaneStack)
   uint2* spill;          // level-major spill columns (nullptr: the BVH fits the LDS stacks)
-  uint32_t* diag;        // device diagnostics: [0] traversal stack overflows (a node group that found no stack
+  uint32_t* diag;        // device diagnostics ([1]: kernarg layout check failed): [0] traversal stack overflows (a node group that found no stack
                          // level was dropped; the host sizes the stacks so this stays 0, prt_stats.stack_overflows)
   int32_t tlas;     // 1: rays walk tlas8 (more than kLinearInstances instances, or PRT_TLAS=1); 0: linear list
   // lights (Core/Renderer.cpp:216-310) and camera (Core/Camera.cpp:29-36)

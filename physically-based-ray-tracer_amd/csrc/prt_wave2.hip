@@ -233,8 +233,23 @@ __device__ __forceinline__ bool diel_next(const WaveBufs& B, uint32_t item, uint
 }
 
 // ---- shading of P(iter): NEE set-up -> S(iter), BRDF sample or path-2 start -> P(iter + 1)
+// k_shade2's parameter list as the kernarg segment holds it (explicit arguments in order, each at its natural
+// alignment, as C lays out these members)
+struct Shade2Args {
+  SceneDev S;
+  TraceArgs A;
+  TileMap M;
+  WaveBufs B;
+  uint32_t iter;
+};
+typedef const __attribute__((address_space(4))) Shade2Args* Shade2ArgsPtr;
 template <bool EXT>
 __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, TileMap M, WaveBufs B, uint32_t iter) {
+  const Shade2ArgsPtr args = (Shade2ArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  if (args->iter != iter || args->B.n != B.n) {  // the layout above does not match this compiler's: fail the call
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(S.diag + 1, 1u);
+    return;
+  }
   __shared__ uint32_t pref[kNSub + 1];
   __shared__ uint32_t sm[8];
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
@@ -260,6 +275,13 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
   };
   prefetch(blockIdx.x);
   for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    // The scene and buffer descriptors are read from the kernarg segment inside each chunk (scalar loads, scalar
+    // cache) instead of being held in SGPRs across the loop: their ~90 live words spilled to VGPR lanes (378
+    // v_readlane in the loop) when hoisted.  The empty asm hides the pointer's loop invariance.
+    Shade2ArgsPtr ka = args;
+    asm volatile("" : "+s"(ka));
+    const SceneDev& Sc = *(const SceneDev*)&ka->S;
+    const WaveBufs& Bc = *(const WaveBufs*)&ka->B;
     const uint32_t g = c * kBlock + threadIdx.x;
     uint32_t item = 0, info = 0, seed = 0, nr = 0;
     int kind = 0;
@@ -268,7 +290,7 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
     if (active) {
       item = item_n; info = info_n; hh = hh_n;
       const uint32_t sd = seed_n;
-      if ((info & 0x1FFu) == 0) B.s1[item].w = hh.x;                                        // r1.hit.t
+      if ((info & 0x1FFu) == 0) Bc.s1[item].w = hh.x;                                        // r1.hit.t
       if (hh.x < kFar) {
         seed = sd;
         kind = nee_kind(fl, seed);                                                           // :198-214
@@ -282,52 +304,52 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
     bool next = false;
     bool area_ray = false;
     if (nr) {
-      const float4 o = B.ro[item], d = B.rd[item];
+      const float4 o = Bc.ro[item], d = Bc.rd[item];
       const V3 D = v3(d.x, d.y, d.z);
       const uint32_t pk = __float_as_uint(hh.w);
       const V3 I = v3(o.x, o.y, o.z) + hh.x * D;                                             // tiny_bvh.h:586
       const V3 V = -D;
-      const HitAttr ha = hit_attributes(S, hit_inst(S, pk), hit_prim(S, pk), hh.y, hh.z, (fl & kNormalMap) != 0);
+      const HitAttr ha = hit_attributes(Sc, hit_inst(Sc, pk), hit_prim(Sc, pk), hh.y, hh.z, (fl & kNormalMap) != 0);
       const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
-      B.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
+      Bc.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
       // a shadow ray is queued as (I, light, visibility index): the traversal kernel rebuilds it (shadow_of)
-      const V3 brdf = nee_lights(S, fl, kind, I, V, ha.N, ha.m, seed,
+      const V3 brdf = nee_lights(Sc, fl, kind, I, V, ha.N, ha.m, seed,
                                  [&](int k, uint32_t light, const Ray&, float, V3 fk) {
         sho[s0 + k] = make_float4(I.x, I.y, I.z, __uint_as_float((light << 29) | (4u * item + (uint32_t)k)));
-        B.nf[4 * (size_t)item + k] = make_float4(fk.x, fk.y, fk.z, 0.0f);
+        Bc.nf[4 * (size_t)item + k] = make_float4(fk.x, fk.y, fk.z, 0.0f);
       });
-      B.nb[item] = make_float4(brdf.x, brdf.y, brdf.z, 0.0f);
-      B.vis[item] = 0u;
+      Bc.nb[item] = make_float4(brdf.x, brdf.y, brdf.z, 0.0f);
+      Bc.vis[item] = 0u;
       status = kStNeeEnd;
       if constexpr (EXT) {
         // area-light sample (2 draws after the light-class NEE draws) at lit, non-delta, non-dielectric hits
-        reinterpret_cast<uint8_t*>(B.vis)[4 * (size_t)B.n + item] = 0;
-        if (S.area && (fl & kLighted) && ha.kind != kMatDielectric && !delta_lobe(ha.m)) {
+        reinterpret_cast<uint8_t*>(Bc.vis)[4 * (size_t)Bc.n + item] = 0;
+        if (Sc.area && (fl & kLighted) && ha.kind != kMatDielectric && !delta_lobe(ha.m)) {
           const float xi1 = random_float(seed), xi2 = random_float(seed);
           Ray sr;
           float tmax;
           V3 fa;
-          if (area_nee(area_light(S), I, ha.N, V, ha.m, xi1, xi2, sr, tmax, fa)) {
+          if (area_nee(area_light(Sc), I, ha.N, V, ha.m, xi1, xi2, sr, tmax, fa)) {
             area_ray = true;
-            B.ao[item] = make_float4(sr.O.x, sr.O.y, sr.O.z, tmax);
-            B.ad[item] = make_float4(sr.D.x, sr.D.y, sr.D.z, 0.0f);
-            B.na[item] = make_float4(fa.x, fa.y, fa.z, 0.0f);
+            Bc.ao[item] = make_float4(sr.O.x, sr.O.y, sr.O.z, tmax);
+            Bc.ad[item] = make_float4(sr.D.x, sr.D.y, sr.D.z, 0.0f);
+            Bc.na[item] = make_float4(fa.x, fa.y, fa.z, 0.0f);
           }
         }
       }
       if ((int)depth != A.bounces - 1) {                                                     // :329
         if (EXT && ha.kind == kMatDielectric) {                                              // :331-372
           const Dielectric dl = dielectric_split(I, D, ha.N);
-          const size_t e = (size_t)depth * B.n + item;
-          B.dro[e] = make_float4(dl.refr.O.x, dl.refr.O.y, dl.refr.O.z, dl.fresnel);
-          B.drd[e] = make_float4(dl.refr.D.x, dl.refr.D.y, dl.refr.D.z, 0.0f);
-          B.T[e] = make_float4(0.0f, 0.0f, 0.0f, kFar);  // w: the continuation is not BRDF-sampled
+          const size_t e = (size_t)depth * Bc.n + item;
+          Bc.dro[e] = make_float4(dl.refr.O.x, dl.refr.O.y, dl.refr.O.z, dl.fresnel);
+          Bc.drd[e] = make_float4(dl.refr.D.x, dl.refr.D.y, dl.refr.D.z, 0.0f);
+          Bc.T[e] = make_float4(0.0f, 0.0f, 0.0f, kFar);  // w: the continuation is not BRDF-sampled
           const uint32_t bit = 1u << depth, keep = ~(0x01010101u << depth);
-          B.dst[item] = (B.dst[item] & keep) | bit | (dl.has_refr ? 0u : (bit << 24));
+          Bc.dst[item] = (Bc.dst[item] & keep) | bit | (dl.has_refr ? 0u : (bit << 24));
           status = kStNeeCont;
-          B.ro[item] = make_float4(dl.refl.O.x, dl.refl.O.y, dl.refl.O.z, 0.0f);
-          B.rd[item] = make_float4(dl.refl.D.x, dl.refl.D.y, dl.refl.D.z, 0.0f);
-          B.info[item] = (depth + 1u) | (path << 8);
+          Bc.ro[item] = make_float4(dl.refl.O.x, dl.refl.O.y, dl.refl.O.z, 0.0f);
+          Bc.rd[item] = make_float4(dl.refl.D.x, dl.refl.D.y, dl.refl.D.z, 0.0f);
+          Bc.info[item] = (depth + 1u) | (path << 8);
           next = true;
         } else {
           V3 dir, thr;
@@ -336,17 +358,17 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
             status = kStNeeCont;
             float pdf = 0.0f;
             if constexpr (EXT)  // MIS density of the sampled direction (kFar: delta lobe or no light sampling)
-              pdf = (bp > 1.0f || !S.area || !(fl & kLighted)) ? kFar : brdf_pdf(ha.m, ha.N, V, dir, bp);
-            B.T[(size_t)depth * B.n + item] = make_float4(thr.x, thr.y, thr.z, pdf);
+              pdf = (bp > 1.0f || !Sc.area || !(fl & kLighted)) ? kFar : brdf_pdf(ha.m, ha.N, V, dir, bp);
+            Bc.T[(size_t)depth * Bc.n + item] = make_float4(thr.x, thr.y, thr.z, pdf);
             const Ray nr2 = make_ray(I + dir * kEpsilon, dir);                               // :404
-            B.ro[item] = make_float4(nr2.O.x, nr2.O.y, nr2.O.z, 0.0f);
-            B.rd[item] = make_float4(nr2.D.x, nr2.D.y, nr2.D.z, 0.0f);
-            B.info[item] = (depth + 1u) | (path << 8);
+            Bc.ro[item] = make_float4(nr2.O.x, nr2.O.y, nr2.O.z, 0.0f);
+            Bc.rd[item] = make_float4(nr2.D.x, nr2.D.y, nr2.D.z, 0.0f);
+            Bc.info[item] = (depth + 1u) | (path << 8);
             next = true;
           }
         }
       }
-      B.seed[item] = seed;
+      Bc.seed[item] = seed;
     }
     if constexpr (EXT) {  // the area-light shadow rays of the block, one more append
       const uint32_t a0 = block_append(shcnt, area_ray ? 1u : 0u, sm);
@@ -354,13 +376,13 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
     }
     if (active) {
       if (status != kStNeeCont) {
-        if (EXT && S.has_diel) next = diel_next(B, item, depth, path);
-        if (!next) next = start_path2(S, A, M, B, item, path);
+        if (EXT && Sc.has_diel) next = diel_next(Bc, item, depth, path);
+        if (!next) next = start_path2(Sc, A, M, Bc, item, path);
       }
-      B.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20) | (next ? kRiQueued : 0u);
+      Bc.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20) | (next ? kRiQueued : 0u);
     }
     const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
-    if (next) qn[sub * B.qcap + slot] = item;
+    if (next) qn[sub * Bc.qcap + slot] = item;
   }
 }
 

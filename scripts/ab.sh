@@ -10,6 +10,6 @@ for v in "$@"; do
   env $v timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > "gpurun_out/ab_$i.log" 2>&1
   rc=$?
   line=$(grep '"metric"' "gpurun_out/ab_$i.log" | tail -1)
-  python3 -c "import json,sys; d=json.loads(sys.argv[2]); r=d['roofline']['kernels']; print(sys.argv[1].ljust(36), d['value'], d['ms_per_step'], {k: v['launch_ms'] for k, v in r.items()})" "$v" "$line" 2>/dev/null || echo "$v: rc=$rc"
+  python3 -c "import json,sys; d=json.loads(sys.argv[2]); print(sys.argv[1].ljust(36), d['value'], d['ms_per_step'], d['roofline']['launch_ms'])" "$v" "$line" 2>/dev/null || echo "$v: rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
