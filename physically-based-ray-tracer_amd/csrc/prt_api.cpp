@@ -602,6 +602,35 @@ int read_stats(prt_ctx* c, prt_stats* stats) {
         std::fprintf(stderr, "prt: trace %u: %zu waves, queue empty after %.1f us; waves out at +%.1f / +%.1f / "
                      "+%.1f / +%.1f us (50/90/99/100 %%)\n", k, ex.size(), (d0 - s0) / 100.0, q(0.5), q(0.9),
                      q(0.99), ex.empty() ? 0.0 : ex.back());
+        // diagnostic builds (PRT_TAIL_STATS): where the waves that left last (top 5 %) spent the time after the
+        // queue emptied: main loop until their tail entry, then the cooperative tail
+        struct Late { double out, entry, tail; unsigned owners, iters; };
+        std::vector<Late> late;
+        for (int w = 0; w < kTlWaves; w++) {
+          const unsigned long long* r = t.data() + 4 * ((size_t)k * kTlWaves + w);
+          if (!r[0] || !r[2] || !r[3]) continue;
+          unsigned long long e = (r[2] & ~0xFFFFFFFFull) | (r[3] >> 32);
+          if (e > r[2]) e -= 1ull << 32;
+          late.push_back({((double)r[2] - (double)d0) / 100.0, ((double)e - (double)d0) / 100.0,
+                          ((double)r[2] - (double)e) / 100.0, (unsigned)(r[3] & 0xFF),
+                          (unsigned)((r[3] >> 8) & 0xFFFFFF)});
+        }
+        if (!late.empty()) {
+          std::sort(late.begin(), late.end(), [](const Late& a, const Late& b) { return a.out < b.out; });
+          for (size_t lo : {(size_t)0, late.size() * 95 / 100}) {
+            auto med = [&](auto f) {
+              std::vector<double> v;
+              for (size_t i = lo; i < late.size(); i++) v.push_back(f(late[i]));
+              std::sort(v.begin(), v.end());
+              return v[v.size() / 2];
+            };
+            std::fprintf(stderr, "prt:   tail %s: entry +%.1f us after the queue emptied, %.1f us in the tail, %.0f "
+                         "owners, %.0f tail iterations (medians over %zu waves)\n", lo ? "last 5%" : "all",
+                         med([](const Late& l) { return l.entry; }), med([](const Late& l) { return l.tail; }),
+                         med([](const Late& l) { return (double)l.owners; }),
+                         med([](const Late& l) { return (double)l.iters; }), late.size() - lo);
+          }
+        }
       }
     }
     bool layout_ok = true;

@@ -61,10 +61,11 @@ __device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
 template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, bool SPILL = false, class Fetch,
-          class Load, class Reload, class Finish, class Tick>
+          class Load, class Reload, class Finish, class Tick, class Drained>
 __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                    Load load, Reload reload, Finish finish, Tick tick,
-                                                   uint32_t* __restrict__ tail = nullptr) {
+                                                   Drained drained_elsewhere, uint32_t* __restrict__ tail = nullptr,
+                                                   unsigned long long* __restrict__ dbg = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   bool active = false, drained = false;
@@ -246,10 +247,16 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     }
     return false;
   };
+#ifdef PRT_DRAIN_POLL
+  uint32_t iter_no = 0;
+#endif
   while (true) {
     // ---- refill idle lanes from the queue
     const uint64_t idle = __ballot(!active);
     tick((uint32_t)__popcll(idle), drained);
+#ifdef PRT_DRAIN_POLL  // A/B: learn of the empty queue from other waves (measured slower: DESIGN.md 6)
+    if (tail && !drained && idle != 0 && (++iter_no & 3u) == 0 && drained_elsewhere()) drained = true;
+#endif
     if (!drained && __popcll(idle) >= (uint32_t)REFILL) {
       uint32_t base = 0;
       const uint32_t want = (uint32_t)__popcll(idle);
@@ -320,6 +327,13 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       tkey[slot] = ~0ull;
     }
     found = false;
+#ifdef PRT_TAIL_STATS  // diagnostic build (PRT_DEBUG_QUEUES timeline, word 3): owners at tail entry, tail
+                       // iterations, tail entry time (s_memrealtime, low 32 bits)
+    uint32_t ts_it = 0, ts_starve = 0, ts_full = 0, ts_hand = 0;
+    const uint32_t ts_a0 = (uint32_t)__popcll(__ballot(active));
+    const unsigned long long ts_t0 = __builtin_amdgcn_s_memrealtime();
+    (void)ts_starve; (void)ts_full; (void)ts_hand;
+#endif
     // an owner takes its helpers' best hit: (u, v) from the same triangle test on the same instance-space ray
     auto merge_team = [&]() {
       const unsigned long long k = tkey[slot];
@@ -369,11 +383,19 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
         }
       }
       if (__ballot(active) == 0) break;  // helpers always belong to a live owner
+#ifdef PRT_TAIL_STATS
+      ts_it++;
+#endif
       // ---- free lanes take a pending group from a walking lane: its top stack entry or its sibling group
       const uint64_t freem = __ballot(!active && !helper);
       // (TLAS: only groups of the BLAS being walked are handed out: a helper walks instance-space subtrees)
       const uint64_t donm = __ballot((active || helper) && busy && (!TLAS || inst >= 0) &&
                                      (sp > (TLAS ? tsp : 0) || gmask != 0) && !(any && (tstate[slot] & kFoundBit)));
+#ifdef PRT_TAIL_STATS
+      if (freem && !donm) ts_starve++;
+      if (!freem && donm) ts_full++;
+      if (freem && donm) ts_hand += min((uint32_t)__popcll(freem), (uint32_t)__popcll(donm));
+#endif
       if (freem && donm) {
         const uint32_t npair = min((uint32_t)__popcll(freem), (uint32_t)__popcll(donm));
         uint32_t ub = 0, um = 0, ui = 0;
@@ -437,16 +459,22 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
           atomicMin(&tkey[slot], ((unsigned long long)__float_as_uint(h.t) << 32) | (~h.prim & 0xFFFFFFFFull));
       }
     }
+#ifdef PRT_TAIL_STATS
+    if (dbg && lane == 0)
+      *dbg = (unsigned long long)ts_a0 | ((unsigned long long)min(ts_it, 0xFFFFFFu) << 8) |
+             ((unsigned long long)(uint32_t)ts_t0 << 32);
+#endif
   }
 }
 
 template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, bool SPILL = false, class Fetch,
-          class Load, class Reload, class Finish>
+          class Load, class Reload, class Finish, class Drained>
 __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
-                                                 Load load, Reload reload, Finish finish,
-                                                 uint32_t* __restrict__ tail = nullptr) {
+                                                 Load load, Reload reload, Finish finish, Drained drained_elsewhere,
+                                                 uint32_t* __restrict__ tail = nullptr,
+                                                 unsigned long long* __restrict__ dbg = nullptr) {
   trav8_persistent_t<MODE, STACK, REFILL, TAILN, TLAS, SPILL>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {},
-                                                        tail);
+                                                        drained_elsewhere, tail, dbg);
 }
 
 }  // namespace prt

@@ -105,6 +105,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   const uint32_t total = nP + nS;
   if (blockIdx.x * 64u >= total) return;
   uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
+  uint32_t* dflag = fetch_counters(B.ctr, iter, 1);  // set once some wave found the queue empty (cleared per call)
   uint32_t part = xcc_id();
   // timeline diagnostic (s_memrealtime, one record per wave: start, first empty fetch, exit)
   unsigned long long* tl = B.tl ? B.tl + ((size_t)iter * kTlWaves + blockIdx.x) * 4 : nullptr;
@@ -114,6 +115,10 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) {
         const uint32_t got = fetch_some(fctr, total, part, base, want);
+#ifdef PRT_DRAIN_POLL  // A/B: the first empty fetch of a wave tells the other waves
+        if (got == 0 && !seen_drain && threadIdx.x == 0)
+          __hip_atomic_store(dflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         if (tl && got == 0 && !seen_drain) {
           seen_drain = true;
           if (threadIdx.x == 0) tl[1] = __builtin_amdgcn_s_memrealtime();
@@ -156,7 +161,8 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
           B.hit[h] = make_float4(hit.t, hit.u, hit.v, __uint_as_float(pack_hit(S, hit.prim, hit.inst)));
         }
       },
-      B.coop_tail ? tail_lds : nullptr);
+      [&]() -> bool { return __hip_atomic_load(dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u; },
+      B.coop_tail ? tail_lds : nullptr, tl ? tl + 3 : nullptr);
   if (tl && threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
 
