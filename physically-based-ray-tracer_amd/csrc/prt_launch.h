@@ -44,7 +44,8 @@ struct WaveBufs {
   uint32_t* vis;    // 4 visibility bytes per item
   uint32_t* q0;
   uint32_t* q1;
-  float4* sho;      // shadow queue: hit point I, bits(light << 29 | visibility index) (prt_wave2.hip shadow_of)
+  uint32_t* shq;    // shadow queue: light << 29 | visibility index (prt_wave2.hip shadow_of)
+  float4* hp;       // the hit point I of the item's last shading (its shadow rays' origin before the offset)
   uint32_t* ctr;    // [iteration][path|shadow][sub-queue] counters, kCtrStride apart
   // extensions (area light / dielectric instances; merged pipeline only): vis holds 5 x n bytes, the area
   // light's shadow ray writes byte 4 * n + item

@@ -16,9 +16,10 @@
 //   for i = 0 .. iters:
 //     k_trace2(i)    closest hits of P(i)  +  any hits of S(i-1)         (one launch, mixed lanes)
 //     k_resmiss2(i)  over P(i-1): NEE result of iteration i-1, (result, throughput) stack, path end, frame write;
-//                    then, for the items k_shade2(i-1) queued into P(i) (P(i) is a subset of P(i-1)), the sky
-//                    radiance of this iteration's misses (i = 0: k_miss2 over P(0))
-//     k_shade2(i)    hit attributes, NEE set-up -> S(i), BRDF sample or path-2 start -> P(i+1)
+//                    with the extensions (or a debug render mode), then, for the items k_shade2(i-1) queued into
+//                    P(i) (a subset of P(i-1)), this iteration's misses (i = 0: k_miss2 over P(0))
+//     k_shade2(i)    the sky radiance of the misses (no extensions), hit attributes, NEE set-up -> S(i), BRDF
+//                    sample or path-2 start -> P(i+1)
 //
 // Hazards (all kernels on one stream): P(i+1) reuses P(i-1)'s buffer after k_resmiss2(i) read it;
 // S(i) reuses S(i-1)'s buffer after k_trace2(i) read it; k_resmiss2(i) reads ne/nb/nf/vis/R/T of an item for
@@ -67,11 +68,13 @@ __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, T
   }
 }
 
-// ---- a shadow-queue record -> its world ray: (I, light << 29 | index) rebuilt by light_ray exactly as the shading
-// kernel's NEE built it; the area light's rays (EXT, light kLightArea, index = item) are stored whole in ao / ad
+// ---- a shadow-queue entry (light << 29 | index) -> its world ray: rebuilt by light_ray from the item's hit point
+// (hp, one per item for its up to four light-class rays) exactly as the shading kernel's NEE built it; the area
+// light's rays (EXT, light kLightArea, index = item) are stored whole in ao / ad
 constexpr uint32_t kShIndexMask = (1u << 29) - 1u;
-__device__ __forceinline__ void shadow_of(const SceneDev& S, const WaveBufs& B, float4 e, V3& O, V3& D, float& tmax) {
-  const uint32_t code = __float_as_uint(e.w), light = code >> 29;
+__device__ __forceinline__ void shadow_of(const SceneDev& S, const WaveBufs& B, uint32_t code, V3& O, V3& D,
+                                          float& tmax) {
+  const uint32_t light = code >> 29;
   if (light == kLightArea) {
     const float4 o = B.ao[code & kShIndexMask], d = B.ad[code & kShIndexMask];
     O = v3(o.x, o.y, o.z);
@@ -79,16 +82,16 @@ __device__ __forceinline__ void shadow_of(const SceneDev& S, const WaveBufs& B, 
     tmax = o.w;
     return;
   }
+  const float4 I = B.hp[(code & kShIndexMask) >> 2];
   Ray r;
   V3 L;
   float dl;
-  light_ray(S, light, v3(e.x, e.y, e.z), r, tmax, L, dl);
+  light_ray(S, light, v3(I.x, I.y, I.z), r, tmax, L, dl);
   O = r.O;
   D = r.D;
 }
-// the visibility byte of a shadow-queue record: 4 x item + k, or 4n + item for the area light's ray
-__device__ __forceinline__ uint32_t shadow_vis(const WaveBufs& B, float4 e) {
-  const uint32_t code = __float_as_uint(e.w);
+// the visibility byte of a shadow-queue entry: 4 x item + k, or 4n + item for the area light's ray
+__device__ __forceinline__ uint32_t shadow_vis(const WaveBufs& B, uint32_t code) {
   return (code >> 29) == kLightArea ? 4u * B.n + (code & kShIndexMask) : (code & kShIndexMask);
 }
 
@@ -137,7 +140,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
         } else {
           h = map_slot(prefS, g - nP, B.scap);
           any = true;
-          shadow_of(S, B, B.sho[h], O, D, tmax);
+          shadow_of(S, B, B.shq[h], O, D, tmax);
           return h;
         }
         O = v3(o.x, o.y, o.z);
@@ -147,7 +150,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
       [&](uint32_t h, bool any, V3& O, V3& D) {
         if (any) {
           float tmax;
-          shadow_of(S, B, B.sho[h], O, D, tmax);
+          shadow_of(S, B, B.shq[h], O, D, tmax);
           return;
         }
         const float4 o = B.ro[h], d = B.rd[h];
@@ -156,7 +159,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
       },
       [&](uint32_t h, const Hit& hit, bool any, bool occluded) {
         if (any) {
-          if (!occluded) vis8[shadow_vis(B, B.sho[h])] = 1;
+          if (!occluded) vis8[shadow_vis(B, B.shq[h])] = 1;
         } else {
           B.hit[h] = make_float4(hit.t, hit.u, hit.v, __uint_as_float(pack_hit(S, hit.prim, hit.inst)));
         }
@@ -164,6 +167,17 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
       [&]() -> bool { return __hip_atomic_load(dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u; },
       B.coop_tail ? tail_lds : nullptr, tl ? tl + 3 : nullptr);
   if (tl && threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
+}
+
+// the skybox lookup out of line: its correctly rounded double atan2 / acos would otherwise raise the register
+// budget of the shading kernel, which looks up the sky for its misses itself
+// (the three fields it reads passed by value: a SceneDev& of a kernel argument would copy the struct to scratch)
+__device__ __noinline__ V3 sample_sky_call(const float* sky, int32_t w, int32_t h, V3 D) {
+  SceneDev S{};
+  S.sky = sky;
+  S.skyw = w;
+  S.skyh = h;
+  return sample_sky(S, D);
 }
 
 // ---- misses of P(iter) (:159): sky radiance (or 0) into ne, before k_shade2 replaces the ray.  EXT: a ray
@@ -190,7 +204,7 @@ __device__ __forceinline__ void miss_item(const SceneDev& S, const TraceArgs& A,
   V3 L = v3(0.0f, 0.0f, 0.0f);
   if (A.flags & kSkybox) {
     const float4 d = B.rd[item];
-    L = sample_sky(S, v3(d.x, d.y, d.z));
+    L = sample_sky_call(S.sky, S.skyw, S.skyh, v3(d.x, d.y, d.z));
   }
   B.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
 }
@@ -263,7 +277,7 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
   const uint32_t sub = blockIdx.x % kNSub;
   uint32_t* shcnt = qcounter(B.ctr, iter, 1, sub);
   uint32_t* ncnt = qcounter(B.ctr, iter + 1, 0, sub);
-  float4* sho = B.sho + (size_t)sub * B.scap;
+  uint32_t* shq = B.shq + (size_t)sub * B.scap;
   const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
   const uint32_t fl = A.flags;
   // software pipeline over the grid-stride chunks: the next chunk's item, info, hit and seed are loaded while this
@@ -297,6 +311,14 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
       item = item_n; info = info_n; hh = hh_n;
       const uint32_t sd = seed_n;
       if ((info & 0x1FFu) == 0) Bc.s1[item].w = hh.x;                                        // r1.hit.t
+      if (!EXT && hh.x >= kFar) {  // a miss (:159): the sky radiance (or 0) ends the path (EXT: k_miss2 / k_resmiss2)
+        V3 L = v3(0.0f, 0.0f, 0.0f);
+        if (fl & kSkybox) {
+          const float4 d = Bc.rd[item];
+          L = sample_sky_call(Sc.sky, Sc.skyw, Sc.skyh, v3(d.x, d.y, d.z));
+        }
+        Bc.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
+      }
       if (hh.x < kFar) {
         seed = sd;
         kind = nee_kind(fl, seed);                                                           // :198-214
@@ -318,10 +340,12 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
       const HitAttr ha = hit_attributes(Sc, hit_inst(Sc, pk), hit_prim(Sc, pk), hh.y, hh.z, (fl & kNormalMap) != 0);
       const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
       Bc.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
-      // a shadow ray is queued as (I, light, visibility index): the traversal kernel rebuilds it (shadow_of)
+      // a shadow ray is queued as (light, visibility index) with the item's hit point I stored once: the traversal
+      // kernel rebuilds it (shadow_of)
+      Bc.hp[item] = make_float4(I.x, I.y, I.z, 0.0f);
       const V3 brdf = nee_lights(Sc, fl, kind, I, V, ha.N, ha.m, seed,
                                  [&](int k, uint32_t light, const Ray&, float, V3 fk) {
-        sho[s0 + k] = make_float4(I.x, I.y, I.z, __uint_as_float((light << 29) | (4u * item + (uint32_t)k)));
+        shq[s0 + k] = (light << 29) | (4u * item + (uint32_t)k);
         Bc.nf[4 * (size_t)item + k] = make_float4(fk.x, fk.y, fk.z, 0.0f);
       });
       Bc.nb[item] = make_float4(brdf.x, brdf.y, brdf.z, 0.0f);
@@ -378,7 +402,7 @@ __global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, Tile
     }
     if constexpr (EXT) {  // the area-light shadow rays of the block, one more append
       const uint32_t a0 = block_append(shcnt, area_ray ? 1u : 0u, sm);
-      if (area_ray) sho[a0] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((kLightArea << 29) | item));
+      if (area_ray) shq[a0] = (kLightArea << 29) | item;
     }
     if (active) {
       if (status != kStNeeCont) {
@@ -510,7 +534,7 @@ __device__ __forceinline__ void resolve_item(const SceneDev& S, const TraceArgs&
 // separate kernels
 template <bool EXT>
 __global__ void __launch_bounds__(kBlock) k_resmiss2(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter,
-                                                     uint32_t iters, float4* __restrict__ out) {
+                                                     uint32_t iters, uint32_t misses, float4* __restrict__ out) {
   __shared__ uint32_t pref[kNSub + 1];
   const uint32_t* q = ((iter - 1) & 1) ? B.q1 : B.q0;
   const uint32_t total = load_prefix(B.ctr, iter - 1, 0, pref);
@@ -534,7 +558,7 @@ __global__ void __launch_bounds__(kBlock) k_resmiss2(SceneDev S, TraceArgs A, Wa
     prefetch(c + gridDim.x);
     if (g >= total) continue;
     resolve_item<EXT>(S, A, B, item, ri, ne, out);
-    if (iter < iters && (ri & kRiQueued)) miss_item<EXT>(S, A, B, item);
+    if (misses && iter < iters && (ri & kRiQueued)) miss_item<EXT>(S, A, B, item);
   }
 }
 
@@ -588,10 +612,15 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
   launch_trace2(c, S, B, it, iters);
   if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
   const bool ext = (S.area || S.has_diel) && A.mode == 0;
-  if (it > 0) {  // resolve of P(it - 1) + misses of P(it), one pass
-    if (ext) hipLaunchKernelGGL(k_resmiss2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it, iters, out);
-    else hipLaunchKernelGGL(k_resmiss2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it, iters, out);
-  } else {
+  // the misses' sky radiance: by k_shade2<false> itself, or (extensions: the area light can turn a hit into a miss
+  // first; debug render modes) by k_miss2 / k_resmiss2 before the shading
+  const uint32_t sep_miss = (ext || A.mode != 0) ? 1u : 0u;
+  if (it > 0) {  // resolve of P(it - 1) (+ misses of P(it)), one pass
+    if (ext) hipLaunchKernelGGL(k_resmiss2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it, iters, sep_miss,
+                                out);
+    else hipLaunchKernelGGL(k_resmiss2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it, iters, sep_miss,
+                            out);
+  } else if (sep_miss) {
     if (ext) hipLaunchKernelGGL(k_miss2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
     else hipLaunchKernelGGL(k_miss2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
   }
