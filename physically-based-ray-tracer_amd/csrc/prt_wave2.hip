@@ -263,8 +263,11 @@ struct Shade2Args {
   uint32_t iter;
 };
 typedef const __attribute__((address_space(4))) Shade2Args* Shade2ArgsPtr;
+// EXT (area light, dielectrics): held to 3 waves/SIMD (167 VGPRs, no spills; unbounded it takes 175 and runs 2
+// waves: C5 frame 135.7 -> 132.4 ms).  The plain form runs 4 waves at its natural 119 VGPRs (forcing 5 spilled
+// and was 2 % slower).
 template <bool EXT>
-__global__ void __launch_bounds__(kBlock) k_shade2(SceneDev S, TraceArgs A, TileMap M, WaveBufs B, uint32_t iter) {
+__global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, TraceArgs A, TileMap M, WaveBufs B, uint32_t iter) {
   const Shade2ArgsPtr args = (Shade2ArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
   if (args->iter != iter || args->B.n != B.n) {  // the layout above does not match this compiler's: fail the call
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(S.diag + 1, 1u);
