@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PRT_ABI_VERSION 5
+#define PRT_ABI_VERSION 6
 
 typedef enum {
     PRT_OK = 0,
@@ -216,6 +216,19 @@ int prt_render(prt_ctx* ctx, const prt_render_params* params, float* avg_rgba, u
 /* Reset the accumulation state: memset of the accumulator (Core/Renderer.cpp:147) and, with
  * full != 0, also samplesPerPixel/distances (fresh Renderer). */
 int prt_reset_accumulation(prt_ctx* ctx, int32_t full);
+
+/* ---- checkpoint / resume of the progressive accumulation (the reference keeps it in memory only) ----
+ * The accumulation state Renderer holds between Ticks (Core/Renderer.h:61-63: accumulator, samplesPerPixel,
+ * distances) as one opaque blob with a header recording the image and shard geometry it belongs to.
+ * prt_accumulation_bytes: the blob size (0 before the first render).  prt_save_accumulation: copies the state
+ * out (waits for the frames queued on the context's stream).  prt_load_accumulation: restores it into a context
+ * of the same shard geometry; the next prt_render with the same image size continues bit-identically (the caller
+ * restores its frame_index too: the RNG stream is keyed by it).  A mismatched or truncated blob:
+ * PRT_ERR_INVALID_ARGUMENT; a local group (prt_create_group): PRT_ERR_UNSUPPORTED (one blob per rank's context
+ * with RCCL). */
+int prt_accumulation_bytes(prt_ctx* ctx, uint64_t* bytes);
+int prt_save_accumulation(prt_ctx* ctx, void* blob, uint64_t bytes);
+int prt_load_accumulation(prt_ctx* ctx, const void* blob, uint64_t bytes);
 
 /* ---- multi-GPU inside the boundary ----
  * A sharded context renders only its rank's pixel tiles (tile_size x tile_size, numbered row-major, dealt

@@ -240,6 +240,21 @@ class Renderer {
     check(prt_reset_accumulation(ctx_, 0));
   }
 
+  // checkpoint of a long progressive render: the accumulation blob (prt_save_accumulation) and the frame counter
+  // the RNG stream continues from; Resume(blob, frame) before the next Tick continues bit for bit
+  std::vector<uint8_t> Checkpoint(uint32_t* frame) const {
+    uint64_t n = 0;
+    check(prt_accumulation_bytes(ctx_, &n));
+    std::vector<uint8_t> blob(n);
+    if (n) check(prt_save_accumulation(ctx_, blob.data(), n));
+    if (frame) *frame = frame_;
+    return blob;
+  }
+  void Resume(const std::vector<uint8_t>& blob, uint32_t frame) {
+    check(prt_load_accumulation(ctx_, blob.data(), blob.size()));
+    frame_ = frame;
+  }
+
   uint32_t Flags() const {
     return (AA ? PRT_FLAG_AA : 0u) | (accumulates ? PRT_FLAG_ACCUMULATE : 0u) | (GAMMACORRECTED ? PRT_FLAG_GAMMA : 0u) |
            (NORMALMAPPED ? PRT_FLAG_NORMALMAP : 0u) | (SKYBOX ? PRT_FLAG_SKYBOX : 0u) | (LIGHTED ? PRT_FLAG_LIGHTED : 0u) |

@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+LIB = os.environ.get("PRT_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")  # override: sanitizer builds
 REFLIB = os.path.join(HERE, "_ref", "libref_tinybvh.so")
 
 AA, ACCUMULATE, GAMMA, NORMALMAP, SKYBOX, LIGHTED, STOCHASTIC = (1 << i for i in range(7))

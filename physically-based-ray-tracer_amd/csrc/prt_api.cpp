@@ -1190,6 +1190,78 @@ int prt_reset_accumulation(prt_ctx* c, int32_t full) {
   return PRT_OK;
 }
 
+// ---- checkpoint / resume of the accumulation state (include/prt.h): header + accumulator (float4) + samples
+// (int32) + distances (float), n = accW * accH entries each
+namespace {
+struct AccHeader {
+  char magic[8];
+  uint32_t version, header_bytes;
+  int32_t w, h, sh_rank, sh_world, sh_tile, sh_kind;
+  uint64_t n;
+};
+constexpr char kAccMagic[8] = {'P', 'R', 'T', 'A', 'C', 'C', 'U', 'M'};
+constexpr uint32_t kAccVersion = 1;
+uint64_t acc_blob_bytes(uint64_t n) { return sizeof(AccHeader) + n * (16 + 4 + 4); }
+}  // namespace
+
+int prt_accumulation_bytes(prt_ctx* c, uint64_t* bytes) {
+  if (!c || !bytes) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/bytes is NULL");
+  if (!c->members.empty()) return fail(PRT_ERR_UNSUPPORTED, "accumulation checkpoints of a local group");
+  *bytes = c->acc.p ? acc_blob_bytes((uint64_t)c->accW * c->accH) : 0;
+  return PRT_OK;
+}
+
+int prt_save_accumulation(prt_ctx* c, void* blob, uint64_t bytes) {
+  if (!c || !blob) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/blob is NULL");
+  if (!c->members.empty()) return fail(PRT_ERR_UNSUPPORTED, "accumulation checkpoints of a local group");
+  if (!c->acc.p) return fail(PRT_ERR_NOT_READY, "nothing accumulated yet");
+  const uint64_t n = (uint64_t)c->accW * c->accH;
+  if (bytes < acc_blob_bytes(n)) return fail(PRT_ERR_INVALID_ARGUMENT, "blob smaller than prt_accumulation_bytes");
+  AccHeader hd{};
+  std::memcpy(hd.magic, kAccMagic, 8);
+  hd.version = kAccVersion;
+  hd.header_bytes = sizeof(AccHeader);
+  hd.w = c->accW;
+  hd.h = c->accH;
+  hd.sh_rank = c->sh_rank;
+  hd.sh_world = c->sh_world;
+  hd.sh_tile = c->sh_tile;
+  hd.sh_kind = c->sh_kind;
+  hd.n = n;
+  char* b = static_cast<char*>(blob);
+  std::memcpy(b, &hd, sizeof(hd));
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(b + sizeof(hd), c->acc.p, 16 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(b + sizeof(hd) + 16 * n, c->nsamp.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(b + sizeof(hd) + 20 * n, c->dist.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return PRT_OK;
+}
+
+int prt_load_accumulation(prt_ctx* c, const void* blob, uint64_t bytes) {
+  if (!c || !blob) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/blob is NULL");
+  if (!c->members.empty()) return fail(PRT_ERR_UNSUPPORTED, "accumulation checkpoints of a local group");
+  AccHeader hd{};
+  if (bytes < sizeof(hd)) return fail(PRT_ERR_INVALID_ARGUMENT, "truncated accumulation blob");
+  std::memcpy(&hd, blob, sizeof(hd));
+  if (std::memcmp(hd.magic, kAccMagic, 8) != 0 || hd.version != kAccVersion || hd.header_bytes != sizeof(hd))
+    return fail(PRT_ERR_INVALID_ARGUMENT, "not an accumulation blob of this ABI");
+  if (hd.w <= 0 || hd.h <= 0 || hd.n != (uint64_t)hd.w * (uint64_t)hd.h || bytes != acc_blob_bytes(hd.n))
+    return fail(PRT_ERR_INVALID_ARGUMENT, "accumulation blob size does not match its header");
+  if (hd.sh_rank != c->sh_rank || hd.sh_world != c->sh_world || hd.sh_tile != c->sh_tile || hd.sh_kind != c->sh_kind)
+    return fail(PRT_ERR_INVALID_ARGUMENT, "accumulation blob of another shard geometry");
+  HIP_TRY(hipSetDevice(c->device));
+  const int rc = ensure_state(c, hd.w, hd.h);
+  if (rc) return rc;
+  const char* b = static_cast<const char*>(blob);
+  const uint64_t n = hd.n;
+  HIP_TRY(hipMemcpyAsync(c->acc.p, b + sizeof(hd), 16 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->nsamp.p, b + sizeof(hd) + 16 * n, 4 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->dist.p, b + sizeof(hd) + 20 * n, 4 * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return PRT_OK;
+}
+
 int prt_render(prt_ctx* c, const prt_render_params* p, float* avg_rgba, uint32_t* rgb8, uint32_t out_flags,
                prt_stats* stats) {
   if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");

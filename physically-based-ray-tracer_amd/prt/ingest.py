@@ -35,7 +35,8 @@ def _ingest_lib():
     import ctypes as C
     global _INGEST_LIB
     if _INGEST_LIB is None:
-        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprt_ingest.so")
+        path = (os.environ.get("PRT_INGEST_LIB")  # override: sanitizer builds (tests/test_sanitizers.py)
+                or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprt_ingest.so"))
         if not os.path.exists(path):
             raise RuntimeError(f"{path} missing: build with make -C physically-based-ray-tracer_amd/csrc")
         L = C.CDLL(path)

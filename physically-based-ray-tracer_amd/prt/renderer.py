@@ -277,6 +277,21 @@ class Context:
     def reset_accumulation(self, full=True):
         check(self.L.prt_reset_accumulation(self.h, 1 if full else 0))
 
+    def save_accumulation(self) -> bytes:
+        """The accumulation state (accumulator, samplesPerPixel, distances) as an opaque blob
+        (prt_save_accumulation); b"" before the first render."""
+        n = C.c_uint64()
+        check(self.L.prt_accumulation_bytes(self.h, C.byref(n)))
+        if n.value == 0:
+            return b""
+        buf = (C.c_uint8 * n.value)()
+        check(self.L.prt_save_accumulation(self.h, buf, n.value))
+        return bytes(buf)
+
+    def load_accumulation(self, blob: bytes):
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        check(self.L.prt_load_accumulation(self.h, buf, len(blob)))
+
     def trace_primary(self, width, height):
         hits = np.zeros(width * height, dtype=[("t", F32), ("u", F32), ("v", F32), ("prim", np.uint32),
                                                ("inst", np.uint32)])
@@ -377,6 +392,21 @@ class Renderer:
         """Renderer::Capture (Core/Renderer.cpp:437-465): the screen as a PNG (the reference names it by time)."""
         from .ingest import capture_png
         capture_png(path, self.screen, self.width, self.height)
+
+    def SaveCheckpoint(self, path):
+        """Checkpoint of a long progressive render: the accumulation state plus the frame counter and
+        seed the RNG stream continues from, as an .npz of plain arrays (load with allow_pickle=False)."""
+        blob = np.frombuffer(self.ctx.save_accumulation(), np.uint8)
+        np.savez(path, accumulation=blob, frame=np.int64(self.frame), seed=np.int64(self.seed),
+                 size=np.array([self.width, self.height], np.int64))
+
+    def LoadCheckpoint(self, path):
+        """Resume from SaveCheckpoint: the next Tick continues the same frame sequence bit for bit."""
+        z = np.load(path, allow_pickle=False)
+        if tuple(int(v) for v in z["size"]) != (self.width, self.height):
+            raise ValueError("checkpoint of another image size")
+        self.ctx.load_accumulation(z["accumulation"].tobytes())
+        self.frame, self.seed = int(z["frame"]), int(z["seed"])
 
     def CameraMoved(self):
         """Camera::HandleInput returned true: memset of the accumulator only (Core/Renderer.cpp:147)."""
