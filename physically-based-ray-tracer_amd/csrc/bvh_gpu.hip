@@ -238,7 +238,12 @@ __global__ void __launch_bounds__(kB) k_boxes(const float4* __restrict__ tri, co
 // Internal nodes take ids n-2, n-3, ... as they are created, so the root (created last) is node 0 and the
 // LBVH node numbering (leaves n-1+i) and the collapse below apply unchanged; the collapse table of a node is
 // filled when it is created, from its children's (created in earlier launches).
-constexpr int kPlocR = 16;
+// search radius: 64 places (C4 rate on the resulting tree 3,327 / 3,428 / 3,534 / 3,492 / 3,466 Mrays/s at radius
+// 16 / 32 / 64 / 128 / 256, build 51-59 ms throughout; scripts/gpu_ploc_ab.sh)
+#ifndef PRT_PLOC_R
+#define PRT_PLOC_R 64
+#endif
+constexpr int kPlocR = PRT_PLOC_R;
 
 __global__ void __launch_bounds__(kB) k_ploc_leaves(const float4* __restrict__ tri,
                                                     const unsigned long long* __restrict__ keys, int n, float* box,

@@ -30,6 +30,8 @@ for name, b, col in (("host SAH", _lib.BUILDER_HOST_SAH, None), ("host SBVH", _l
                      ("GPU LBVH + optimal collapse", _lib.BUILDER_GPU_LBVH, None),
                      ("GPU PLOC + optimal collapse", _lib.BUILDER_GPU_PLOC, None),
                      ("GPU LBVH + greedy collapse", _lib.BUILDER_GPU_LBVH, "greedy")):
+    if "only-ploc" in sys.argv and "PLOC" not in name:  # A/B of PLOC variants (library builds)
+        continue
     if col:
         os.environ["PRT_COLLAPSE"] = col
     else:
