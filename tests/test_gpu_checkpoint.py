@@ -26,11 +26,14 @@ def test_resume_is_bit_identical(gpu_ctx, post):
     sd = scenes.multi_instance(scenes.config_small(40, 30))
     W, H = 96, 64
     pf = prt.postfx_preset(0, color_grading=(1.0, 0.9, 1.1, 1.0)) if post else None
-    gpu_scene(gpu_ctx, sd, W, H)
-    ref = _frames(gpu_ctx, W, H, [0, 1, 2, 3], pf)
-    gpu_scene(gpu_ctx, sd, W, H)
-    _frames(gpu_ctx, W, H, [0, 1], pf)
-    blob = gpu_ctx.save_accumulation()
+    try:
+        gpu_scene(gpu_ctx, sd, W, H)
+        ref = _frames(gpu_ctx, W, H, [0, 1, 2, 3], pf)
+        gpu_scene(gpu_ctx, sd, W, H)
+        _frames(gpu_ctx, W, H, [0, 1], pf)
+        blob = gpu_ctx.save_accumulation()
+    finally:
+        gpu_ctx.set_postfx(None)  # the session context's later users expect no screen pass (Panini moves rays)
     assert len(blob) == 48 + W * H * 24
     c2 = prt.Context(0)
     try:
@@ -50,16 +53,22 @@ def test_renderer_checkpoint_files(tmp_path):
     W, H = 64, 48
     cam = prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H))
     r1 = prt.Renderer(prt.Scene.from_data(sd), cam, W, H)
-    r1.Tick()
-    r1.Tick()
-    path = str(tmp_path / "ckpt.npz")
-    r1.SaveCheckpoint(path)
-    r1.Tick()
-    r2 = prt.Renderer(prt.Scene.from_data(sd), cam, W, H)
-    r2.LoadCheckpoint(path)
-    r2.Tick()
-    assert r2.frame == r1.frame == 3
-    assert np.array_equal(r2.average, r1.average) and np.array_equal(r2.screen, r1.screen)
+    r2 = None
+    try:
+        r1.Tick()
+        r1.Tick()
+        path = str(tmp_path / "ckpt.npz")
+        r1.SaveCheckpoint(path)
+        r1.Tick()
+        r2 = prt.Renderer(prt.Scene.from_data(sd), cam, W, H)
+        r2.LoadCheckpoint(path)
+        r2.Tick()
+        assert r2.frame == r1.frame == 3
+        assert np.array_equal(r2.average, r1.average) and np.array_equal(r2.screen, r1.screen)
+    finally:
+        r1.ctx.close()
+        if r2 is not None:
+            r2.ctx.close()
 
 
 def test_checkpoint_refusals(gpu_ctx):
