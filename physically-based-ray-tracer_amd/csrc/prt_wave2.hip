@@ -618,10 +618,15 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
   // the misses' sky radiance: by k_shade2<false> itself, or (extensions: the area light can turn a hit into a miss
   // first; debug render modes) by k_miss2 / k_resmiss2 before the shading
   const uint32_t sep_miss = (ext || A.mode != 0) ? 1u : 0u;
+#ifndef PRT_RES_GRID
+  const unsigned gres = gprod;
+#else
+  const unsigned gres = PRT_RES_GRID;  // A/B
+#endif
   if (it > 0) {  // resolve of P(it - 1) (+ misses of P(it)), one pass
-    if (ext) hipLaunchKernelGGL(k_resmiss2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it, iters, sep_miss,
+    if (ext) hipLaunchKernelGGL(k_resmiss2<true>, dim3(gres), dim3(kBlock), 0, c.stream, S, A, B, it, iters, sep_miss,
                                 out);
-    else hipLaunchKernelGGL(k_resmiss2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it, iters, sep_miss,
+    else hipLaunchKernelGGL(k_resmiss2<false>, dim3(gres), dim3(kBlock), 0, c.stream, S, A, B, it, iters, sep_miss,
                             out);
   } else if (sep_miss) {
     if (ext) hipLaunchKernelGGL(k_miss2<true>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
