@@ -245,13 +245,13 @@ def test_c3_full_size_matches_oracle(gpu_ctx):
     assert (s_g.segments, s_g.shadow_rays) == (s_o.segments, s_o.shadow_rays)
 
 
-def test_c5_quarter_matches_oracle(gpu_ctx):
-    """Config C5 (C4 + the quad area light with MIS, 16 spp, depth 8) at a quarter of its pixels (1920x1080, the
-    bench's CPU-baseline sample) against the oracle's extension restatement: RMSE <= 1e-4, >= 99.9 % identical
+def test_c5_full_size_matches_oracle(gpu_ctx):
+    """Config C5 (C4 + the quad area light with MIS, 16 spp, depth 8) at its own 3840x2160 (592M rays; the
+    bench's --scene c5 frame) against the oracle's extension restatement: RMSE <= 1e-4, >= 99.9 % identical
     pixels, identical ray counts."""
     import os
     sd = scenes.config_c5()
-    W, H = 1920, 1080
+    W, H = 3840, 2160
     gpu_scene(gpu_ctx, sd, W, H)
     a_g, r_g, s_g = gpu_ctx.render(W, H, 16, 8)
     osc = oracle.OracleScene(sd, W, H)
