@@ -16,6 +16,7 @@
 //      PRT_COLLAPSE=greedy instead opens the largest-area child with more than max_leaf triangles until 8.
 //      Nodes are quantised and laid out exactly as the host builder's Node8 (bvh_build.h): interior
 //      children contiguous (one atomic per node), leaf triangles contiguous (one atomic per node)
+//   (LBVH and PLOC trees can be refined by treelet restructuring before step 5, PRT_TRBVH: see k_trbvh)
 // The result is a different tree from the host's SAH build, so traversal cost differs; hits do not (the
 // hit rule is BVH-independent), which is what the GPU tests check.
 #include <hip/hip_runtime.h>
@@ -346,6 +347,201 @@ __device__ __forceinline__ uint8_t grid_exp(double ext, double qmax) {  // grid_
   return (uint8_t)min(254, max(1, e + 127));
 }
 
+// ---- treelet restructuring of the binary tree before the collapse (Karras, Aila 2013, "Fast Parallel
+// Construction of High-Quality Bounding Volume Hierarchies"), PRT_TRBVH passes (0 = off): one thread per leaf
+// walks towards the root; the second child to arrive at a node (agent atomic, as k_boxes) forms the treelet of up
+// to kTreeletLeaves subtrees below it (opening the largest-area treelet leaf until full), finds the binary
+// topology over them with the least SAH cost by dynamic programming over the subsets, and rewires the treelet's
+// internal nodes when that is cheaper.  Subtrees below a node are final when it is processed, nodes above it
+// untouched, so treelets of different threads never overlap.  Boxes, counts, costs and links move between threads
+// with sc1 loads / stores after the arrival atomic (per-XCD L2s, MI355X_MICROARCH.md).  The restructured tree's
+// subtrees are no longer Morton key ranges: the collapse walks them, and the collapse table is rebuilt.
+constexpr int kTreeletLeaves = 7;
+constexpr float kTrNode = 1.0f, kTrTri = 1.0f;  // binary SAH weights, as kDpNode / kDpTri
+
+__device__ __forceinline__ int ld_sc1_i(const int* p) {
+  return (int)__hip_atomic_load(reinterpret_cast<uint32_t*>(const_cast<int*>(p)), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_i(int* p, int v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(p), (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1_u(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_u(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float area_of(const float* lo, const float* hi) {
+  const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+
+// parent links of a tree given by left / right (PLOC builds none)
+__global__ void __launch_bounds__(kB) k_parents(const int* __restrict__ left, const int* __restrict__ right, int n,
+                                                int* parent) {
+  const int p = (int)(blockIdx.x * kB + threadIdx.x);
+  if (p == 0) parent[0] = -1;
+  if (p >= n - 1) return;
+  const int nn = 2 * n - 1, l = left[p], r = right[p];
+  if (l > 0 && l < nn) parent[l] = p;
+  if (r > 0 && r < nn) parent[r] = p;
+}
+
+__global__ void __launch_bounds__(kB) k_trbvh(int n, int* left, int* right, int* parent, float* box, uint32_t* count,
+                                              float* cost, uint32_t* flag, uint32_t* err) {
+  const int i = (int)(blockIdx.x * kB + threadIdx.x);
+  if (i >= n) return;
+  const int nn = 2 * n - 1;
+  int node = n - 1 + i;
+  {
+    const float* b = box + 6 * (size_t)node;
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; k++) { lo[k] = ld_sc1(b + k); hi[k] = ld_sc1(b + 3 + k); }
+    st_sc1(cost + node, kTrTri * area_of(lo, hi));
+  }
+  while (node != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this subtree's records are out before the arrival
+    const int p = ld_sc1_i(parent + node);
+    if (p < 0 || p >= n - 1) { atomicOr(err, 1u); return; }
+    if (atomicAdd(flag + p, 1u) == 0u) return;  // the sibling's thread finishes p
+    node = p;
+    // the treelet below p: internal nodes I (p first), leaves L (subtree roots)
+    int L[kTreeletLeaves], I[kTreeletLeaves - 1];
+    float lbx[kTreeletLeaves][6];
+    int nl = 0, ni = 0;
+    I[ni++] = p;
+    L[nl++] = ld_sc1_i(left + p);
+    L[nl++] = ld_sc1_i(right + p);
+    bool bad = false;
+    for (int j = 0; j < 2; j++) bad |= L[j] < 0 || L[j] >= nn;
+    if (bad) { atomicOr(err, 2u); return; }
+    for (int j = 0; j < 2; j++)
+      for (int k = 0; k < 6; k++) lbx[j][k] = ld_sc1(box + 6 * (size_t)L[j] + k);
+    while (nl < kTreeletLeaves) {  // open the largest-area interior treelet leaf
+      int bj = -1;
+      float ba = -1.0f;
+      for (int j = 0; j < nl; j++)
+        if (L[j] < n - 1) {
+          const float a = area_of(lbx[j], lbx[j] + 3);
+          if (a > ba) { ba = a; bj = j; }
+        }
+      if (bj < 0) break;
+      const int v = L[bj];
+      const int lv = ld_sc1_i(left + v), rv = ld_sc1_i(right + v);
+      if (lv < 0 || lv >= nn || rv < 0 || rv >= nn) { atomicOr(err, 4u); return; }
+      I[ni++] = v;
+      L[bj] = lv;
+      L[nl] = rv;
+      for (int k = 0; k < 6; k++) { lbx[bj][k] = ld_sc1(box + 6 * (size_t)lv + k); lbx[nl][k] = ld_sc1(box + 6 * (size_t)rv + k); }
+      nl++;
+    }
+    float lcost[kTreeletLeaves];
+    for (int j = 0; j < nl; j++) lcost[j] = ld_sc1(cost + L[j]);
+    float pb[6];
+    for (int k = 0; k < 3; k++) { pb[k] = 3.4e38f; pb[3 + k] = -3.4e38f; }
+    for (int j = 0; j < nl; j++)
+      for (int k = 0; k < 3; k++) { pb[k] = fminf(pb[k], lbx[j][k]); pb[3 + k] = fmaxf(pb[3 + k], lbx[j][3 + k]); }
+    // current cost of the treelet: rebuilt bottom-up over its internal nodes (I is in pre-order: reverse it)
+    const int full = (1 << nl) - 1;
+    float ca[1 << kTreeletLeaves], cs[1 << kTreeletLeaves];
+    uint8_t part[1 << kTreeletLeaves];
+    for (int S = 1; S <= full; S++) {
+      float lo[3] = {3.4e38f, 3.4e38f, 3.4e38f}, hi[3] = {-3.4e38f, -3.4e38f, -3.4e38f};
+      for (int j = 0; j < nl; j++)
+        if ((S >> j) & 1)
+          for (int k = 0; k < 3; k++) { lo[k] = fminf(lo[k], lbx[j][k]); hi[k] = fmaxf(hi[k], lbx[j][3 + k]); }
+      ca[S] = area_of(lo, hi);
+    }
+    for (int S = 1; S <= full; S++) {  // subsets of S are numerically smaller: already solved
+      if ((S & (S - 1)) == 0) {
+        cs[S] = lcost[__builtin_ctz(S)];
+        part[S] = 0;
+        continue;
+      }
+      const int low = S & -S;
+      float best = 3.4e38f;
+      int bp = low;
+      for (int P = (S - 1) & S; P; P = (P - 1) & S)
+        if (P & low) {
+          const float c = cs[P] + cs[S ^ P];
+          if (c < best) { best = c; bp = P; }
+        }
+      cs[S] = kTrNode * ca[S] + best;
+      part[S] = (uint8_t)bp;
+    }
+    const float old = kTrNode * area_of(pb, pb + 3) + ld_sc1(cost + ld_sc1_i(left + p)) + ld_sc1(cost + ld_sc1_i(right + p));
+    if (nl >= 3 && cs[full] < old * 0.9999f) {
+      // rewire: pre-order over the chosen partitions, internal nodes taken from I in order
+      int stS[kTreeletLeaves], stN[kTreeletLeaves], sp = 0, used = 1;
+      int oN[kTreeletLeaves - 1], oL[kTreeletLeaves - 1], oR[kTreeletLeaves - 1], no = 0;
+      stS[sp] = full; stN[sp++] = p;
+      while (sp > 0 && !bad) {
+        const int S = stS[--sp], id = stN[sp];
+        const int P = part[S], Q = S ^ P;
+        int ch[2];
+        const int sub[2] = {P, Q};
+        for (int h = 0; h < 2; h++) {
+          const int X = sub[h];
+          if ((X & (X - 1)) == 0) {
+            ch[h] = L[__builtin_ctz(X)];
+          } else {
+            if (used >= ni || sp >= kTreeletLeaves) { bad = true; break; }
+            ch[h] = I[used++];
+            stS[sp] = X; stN[sp++] = ch[h];
+          }
+        }
+        if (bad || no >= kTreeletLeaves - 1) { bad = true; break; }
+        oN[no] = id; oL[no] = ch[0]; oR[no] = ch[1]; no++;
+      }
+      if (bad || used != ni) { atomicOr(err, 8u); return; }
+      // links, then boxes / counts / costs children first (reverse pre-order)
+      for (int j = 0; j < no; j++) {
+        st_sc1_i(left + oN[j], oL[j]);
+        st_sc1_i(right + oN[j], oR[j]);
+        st_sc1_i(parent + oL[j], oN[j]);
+        st_sc1_i(parent + oR[j], oN[j]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int j = no - 1; j >= 0; j--) {
+        const int id = oN[j], l = oL[j], r = oR[j];
+        float lo[3], hi[3];
+        for (int k = 0; k < 3; k++) {
+          lo[k] = fminf(ld_sc1(box + 6 * (size_t)l + k), ld_sc1(box + 6 * (size_t)r + k));
+          hi[k] = fmaxf(ld_sc1(box + 6 * (size_t)l + 3 + k), ld_sc1(box + 6 * (size_t)r + 3 + k));
+        }
+        for (int k = 0; k < 3; k++) { st_sc1(box + 6 * (size_t)id + k, lo[k]); st_sc1(box + 6 * (size_t)id + 3 + k, hi[k]); }
+        st_sc1_u(count + id, ld_sc1_u(count + l) + ld_sc1_u(count + r));
+        st_sc1(cost + id, kTrNode * area_of(lo, hi) + ld_sc1(cost + l) + ld_sc1(cost + r));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // read back by the next (parent) record
+      }
+    } else {
+      st_sc1(cost + p, old);
+    }
+  }
+}
+
+// the collapse table over the restructured tree (boxes final): the dp_node pass of k_boxes, bottom-up
+__global__ void __launch_bounds__(kB) k_dp_rebuild(int n, const int* __restrict__ left, const int* __restrict__ right,
+                                                   const int* __restrict__ parent, const float* __restrict__ box,
+                                                   const uint32_t* __restrict__ count, uint32_t* flag, DpTab dp,
+                                                   int max_leaf, uint32_t* err) {
+  const int i = (int)(blockIdx.x * kB + threadIdx.x);
+  if (i >= n) return;
+  int node = n - 1 + i;
+  while (node != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int p = parent[node];
+    if (p < 0 || p >= n - 1) { atomicOr(err, 16u); return; }
+    if (atomicAdd(flag + p, 1u) == 0u) return;
+    const int lc = left[p], rc = right[p];
+    float pb[6], lb[6], rb[6];
+    for (int k = 0; k < 6; k++) { lb[k] = box[6 * (size_t)lc + k]; rb[k] = box[6 * (size_t)rc + k]; pb[k] = box[6 * (size_t)p + k]; }
+    dp_node(dp, p, lc, rc, pb, lb, rb, (int)count[p], n, max_leaf);
+    node = p;
+  }
+}
+
 struct Task {
   int n2;       // binary node
   uint32_t n8;  // wide node slot
@@ -637,6 +833,39 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
     if ((err = hipMemsetAsync(flag, 0, 4 * nn, s))) return fail(err);
     hipLaunchKernelGGL(k_boxes, dim3(grid_of(n)), dim3(kB), 0, s, tri, keys2, n, left, right, parent, box, flag, first,
                        count, dp, max_leaf);
+  }
+  // treelet restructuring passes (PRT_TRBVH; default 2 on the LBVH tree, 0 on PLOC's), then the collapse table over
+  // the new topology.  Measured (scripts/gpu_trbvh.sh; C4 / Spaceship rate on the tree, build time):
+  //   LBVH  0 / 1 / 2 / 3 passes: 2,997 / 3,364 / 3,529 / 3,537 Mrays/s (60 / 77 / 106 / 131 ms); ship 4,071 -> 4,372
+  //   PLOC  0 / 1 / 2 / 3 passes: 3,514 / 3,532 / 3,525 / 3,533 Mrays/s (55 / 78 / 112 / 128 ms); ship 4,172 -> 4,402
+  const char* tre = std::getenv("PRT_TRBVH");
+  const int tr_passes = tre ? std::atoi(tre) : (ploc ? 0 : 2);
+  if (tr_passes > 0 && n >= 3) {
+    float* tcost = nullptr;
+    uint32_t* terr = nullptr;
+    if ((err = hipMalloc(&tcost, 4 * nn)) || (err = hipMalloc(&terr, 4))) {
+      (void)hipFree(tcost);
+      return fail(err);
+    }
+    auto tfree = [&]() { (void)hipFree(tcost); (void)hipFree(terr); };
+    if ((err = hipMemsetAsync(terr, 0, 4, s))) { tfree(); return fail(err); }
+    if (ploc) hipLaunchKernelGGL(k_parents, dim3(grid_of(n)), dim3(kB), 0, s, left, right, n, parent);
+    for (int pass = 0; pass < tr_passes && !err; pass++) {
+      if ((err = hipMemsetAsync(flag, 0, 4 * nn, s))) break;
+      hipLaunchKernelGGL(k_trbvh, dim3(grid_of(n)), dim3(kB), 0, s, n, left, right, parent, box, count, tcost, flag,
+                         terr);
+    }
+    if (!err && dp.C && !(err = hipMemsetAsync(flag, 0, 4 * nn, s)))
+      hipLaunchKernelGGL(k_dp_rebuild, dim3(grid_of(n)), dim3(kB), 0, s, n, left, right, parent, box, count, flag, dp,
+                         max_leaf, terr);
+    uint32_t te = 0;
+    if (!err && !(err = hipMemcpyAsync(&te, terr, 4, hipMemcpyDeviceToHost, s)) && !(err = hipStreamSynchronize(s)) &&
+        te != 0u)
+      err = hipErrorInvalidValue;  // malformed tree
+    tfree();
+    if (err) return fail(err);
+    (void)hipFree(first);
+    first = nullptr;  // subtrees are no longer key ranges: the collapse walks them
   }
   // collapse, level by level from the binary root (node 0; the single leaf when n == 1)
   const Task t0{0, 0u};  // binary root: internal node 0, or the single leaf (node n - 1 = 0) when n == 1

@@ -32,6 +32,8 @@ for name, b, col in (("host SAH", _lib.BUILDER_HOST_SAH, None), ("host SBVH", _l
                      ("GPU LBVH + greedy collapse", _lib.BUILDER_GPU_LBVH, "greedy")):
     if "only-ploc" in sys.argv and "PLOC" not in name:  # A/B of PLOC variants (library builds)
         continue
+    if "only-gpu" in sys.argv and ("GPU" not in name or "greedy" in name):  # the device builders (PRT_TRBVH A/B)
+        continue
     if col:
         os.environ["PRT_COLLAPSE"] = col
     else:
