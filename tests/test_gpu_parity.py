@@ -321,6 +321,29 @@ def test_gpu_builder_renders_identical(gpu_ctx, which):
         assert out[0][3].segments == out[b][3].segments and out[0][3].shadow_rays == out[b][3].shadow_rays
 
 
+@pytest.mark.parametrize("passes", ["0", "1", "3"])
+def test_treelet_restructuring_renders_identical(gpu_ctx, monkeypatch, passes):
+    """Treelet restructuring of the device builders' trees (bvh_gpu.hip k_trbvh, PRT_TRBVH passes; default 2 on
+    LBVH, 0 on PLOC) changes the topology, never a hit: LBVH and PLOC trees at 0 / 1 / 3 passes render the host SAH
+    build's frame bit for bit."""
+    from prt import _lib
+    sd = scenes.multi_instance(scenes.config_small(60, 40))
+    W, H = 128, 80
+    gpu_ctx.set_bvh_builder(_lib.BUILDER_HOST_SAH)
+    gpu_scene(gpu_ctx, sd, W, H)
+    a0, r0, s0 = gpu_ctx.render(W, H, 4, 3)
+    monkeypatch.setenv("PRT_TRBVH", passes)
+    try:
+        for b in (_lib.BUILDER_GPU_LBVH, _lib.BUILDER_GPU_PLOC):
+            gpu_ctx.set_bvh_builder(b)
+            gpu_scene(gpu_ctx, sd, W, H)
+            a, r, st = gpu_ctx.render(W, H, 4, 3)
+            assert np.array_equal(a, a0) and np.array_equal(r, r0), (b, passes)
+            assert (st.segments, st.shadow_rays) == (s0.segments, s0.shadow_rays)
+    finally:
+        gpu_ctx.set_bvh_builder(_lib.BUILDER_HOST_SAH)
+
+
 def test_gpu_builders_release_device_memory(gpu_ctx):
     """Rebuilding the scene with the device builders (their per-mesh build buffers are scratch) and the host SBVH
     keeps the device's free memory flat: a 200k-triangle mesh set 4 more times after 2 warm-up builds loses
