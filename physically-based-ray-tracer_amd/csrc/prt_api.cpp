@@ -172,6 +172,14 @@ int drain(prt_ctx* c) {
   return PRT_OK;
 }
 
+// triangles per leaf slot the builders may form (binary SAH leaves and the collapse's leaf slots); PRT_MAX_LEAF
+// overrides (A/B)
+int max_leaf_tris() {
+  const char* e = std::getenv("PRT_MAX_LEAF");
+  const int v = e ? std::atoi(e) : 3;
+  return v < 1 ? 1 : (v > 4 ? 4 : v);
+}
+
 // waves/SIMD of the persistent traversal kernels: the LDS stack (8 / 9 / 11 / 14 / 18 groups at 8 / 7 / 6 / 5 / 4
 // waves) must hold max_depth - 1 groups; deeper BVHs (depth_ok caps them at kMaxBvhDepth = 64 levels) run the
 // 4-wave form with HBM spill columns (ensure_spill)
@@ -933,7 +941,7 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
       HIP_TRY(upload(fat, M.triangles, 48ull * (size_t)M.tri_count));
       HIP_TRY(g.nodes.ensure(sizeof(Node8) * (size_t)M.tri_count));
       HIP_TRY(g.tris.ensure(sizeof(TriMT) * (size_t)M.tri_count));
-      HIP_TRY(gpu_build_blas8(c->stream, fat.as<float>(), M.tri_count, 3, g.nodes.as<Node8>(), g.tris.as<TriMT>(), &g.gi,
+      HIP_TRY(gpu_build_blas8(c->stream, fat.as<float>(), M.tri_count, max_leaf_tris(), g.nodes.as<Node8>(), g.tris.as<TriMT>(), &g.gi,
                               builder == PRT_BUILDER_GPU_PLOC));
       fat.release();
       if ((uint64_t)gpu_nodes + g.gi.nodes >= (1ull << 32) || (uint64_t)gpu_tris + g.gi.tris >= (1ull << 32))
@@ -964,7 +972,8 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
         depth = built.depth; nnodes = (int64_t)built.nodes.size(); nleaves = built.leaves;
         return true;
       };
-      const bool ok = append(build_blas8(M.triangles, M.tri_count, 3, builder == PRT_BUILDER_HOST_SBVH), nodes8);
+      const bool ok = append(build_blas8(M.triangles, M.tri_count, max_leaf_tris(), builder == PRT_BUILDER_HOST_SBVH),
+                             nodes8);
       if (!ok) return fail(PRT_ERR_UNSUPPORTED, "too many triangles");
     }
     mh[i].prim_base = (uint32_t)stri.size();
