@@ -567,14 +567,17 @@ __global__ void __launch_bounds__(kBlock) k_resmiss2(SceneDev S, TraceArgs A, Wa
 
 // LDS per wave (one block): 2 x STACK x 256 B of stack + 264 B of prefix tables + the tail slots, within
 // 160 KB / (4 x WAVES) blocks per CU
+#ifndef PRT_REFILL
+#define PRT_REFILL 32  // idle lanes before a wave refills from the queue (A/B builds: -DPRT_REFILL=16 ...)
+#endif
 template <int STACK, int WAVES, int TAILN>
 void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
   static_assert(2 * STACK * 256 + 264 + 4 * 3 * TAILN <= 163840 / (4 * WAVES), "LDS over the occupancy budget");
   if (S.tlas)
-    hipLaunchKernelGGL((k_trace2<32, STACK, WAVES, TAILN, true>), dim3(256u * 4u * WAVES), dim3(64), 0, c.stream, S, B,
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, true>), dim3(256u * 4u * WAVES), dim3(64), 0, c.stream, S, B,
                        it, iters);
   else
-    hipLaunchKernelGGL((k_trace2<32, STACK, WAVES, TAILN, false>), dim3(256u * 4u * WAVES), dim3(64), 0, c.stream, S,
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, false>), dim3(256u * 4u * WAVES), dim3(64), 0, c.stream, S,
                        B, it, iters);
 }
 // persistent traversal occupancy (waves/SIMD) -> LDS stack groups per lane; a BVH deeper than the 18 LDS
