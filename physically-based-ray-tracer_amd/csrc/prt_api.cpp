@@ -409,7 +409,7 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces, bool ext) {
   const size_t o_seed = take(4ull * n), o_info = take(4ull * n), o_rinfo = take(4ull * n), o_ro = take(16ull * n), o_rd = take(16ull * n),
                o_R = take(16ull * n * levels), o_T = take(16ull * n * levels), o_s1 = take(16ull * n),
                o_jit = take(8ull * n), o_hit = take(16ull * n), o_ne = take(16ull * n), o_nb = take(16ull * n),
-               o_nf = take(64ull * n), o_vis = take(5ull * n), o_q0 = take(4 * qn), o_q1 = take(4 * qn),
+               o_nk = take(16ull * n), o_vis = take(5ull * n), o_q0 = take(4 * qn), o_q1 = take(4 * qn),
                o_shq = take(4 * sn), o_hp = take(16ull * n), o_ctr = take(4 * kCtrWords);
   const size_t o_na = ext ? take(16ull * n) : 0, o_dst = ext ? take(4ull * n) : 0,
                o_dro = ext ? take(16ull * n * levels) : 0, o_drd = ext ? take(16ull * n * levels) : 0,
@@ -424,7 +424,7 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces, bool ext) {
   W.seed = (uint32_t*)(b + o_seed); W.info = (uint32_t*)(b + o_info); W.rinfo = (uint32_t*)(b + o_rinfo);
   W.ro = (float4*)(b + o_ro); W.rd = (float4*)(b + o_rd); W.R = (float4*)(b + o_R); W.T = (float4*)(b + o_T);
   W.s1 = (float4*)(b + o_s1); W.jit = (float2*)(b + o_jit); W.hit = (float4*)(b + o_hit);
-  W.ne = (float4*)(b + o_ne); W.nb = (float4*)(b + o_nb); W.nf = (float4*)(b + o_nf); W.vis = (uint32_t*)(b + o_vis);
+  W.ne = (float4*)(b + o_ne); W.nb = (float4*)(b + o_nb); W.nk = (float4*)(b + o_nk); W.vis = (uint32_t*)(b + o_vis);
   W.q0 = (uint32_t*)(b + o_q0); W.q1 = (uint32_t*)(b + o_q1); W.shq = (uint32_t*)(b + o_shq); W.hp = (float4*)(b + o_hp);
   W.ctr = (uint32_t*)(b + o_ctr);
   W.na = ext ? (float4*)(b + o_na) : nullptr; W.dst = ext ? (uint32_t*)(b + o_dst) : nullptr;

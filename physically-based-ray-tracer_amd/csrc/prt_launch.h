@@ -40,7 +40,7 @@ struct WaveBufs {
   float4* hit;      // t, u, v, bits(prim | inst << 26)
   float4* ne;       // emissive (or the path's end value)
   float4* nb;       // NEE BRDF value
-  float4* nf;       // 4 x n NEE contributions per shadow ray
+  float4* nk;       // NEE factors the shadow rays' contributions are rebuilt from (prt_path.h nee_lights)
   uint32_t* vis;    // 4 visibility bytes per item
   uint32_t* q0;
   uint32_t* q1;

@@ -86,17 +86,20 @@ __device__ __forceinline__ void light_ray(const SceneDev& S, uint32_t light, V3 
   tmax = distance - kEpsilon;
 }
 
-// Builds the shadow rays of `kind` (emit(k, light, ray, tmax, f_k) per ray, in order, with f_k the ray's
-// unoccluded contribution before the pick-probability division) and returns the BRDF value the reference
-// evaluates for this light class (0 when !LIGHTED).  Draws whichLight for point lights: the reference
-// draws it after tracing the four shadow rays (:267), which consume no random numbers, so drawing it
-// first keeps the stream and lets only the chosen light direction stay live.
+// Picks the shadow rays of `kind` (emit(k, light) per ray, in order; the traversal kernel rebuilds each ray with
+// light_ray) and returns the BRDF value the reference evaluates for this light class (0 when !LIGHTED).  nk gets
+// the factors each ray's unoccluded contribution f_k is a product of: f_k = colour * factor, rebuilt by
+// nee_contrib with the same multiplies in the same order, so one float4 per item stands for up to four stored
+// contributions.  Draws whichLight for point lights: the reference draws it after tracing the four shadow rays
+// (:267), which consume no random numbers, so drawing it first keeps the stream and lets only the chosen light
+// direction stay live.
 template <class Emit>
 __device__ __forceinline__ V3 nee_lights(const SceneDev& S, uint32_t fl, int kind, V3 I, V3 V, V3 N, const Material& m,
-                                         uint32_t& seed, Emit&& emit) {
+                                         uint32_t& seed, float4& nk, Emit&& emit) {
   if (kind == 0) {                                                                          // :216-269
     const int wl = (int)(random_float(seed) * 10) % 4;                                     // :267
     V3 Lw = v3(0.0f, 0.0f, 0.0f);
+    float kf[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       Ray r;
@@ -106,43 +109,52 @@ __device__ __forceinline__ V3 nee_lights(const SceneDev& S, uint32_t fl, int kin
       const float invD = 1.0f / sqrtf(dsq);  // the same exact reciprocal light_ray scaled L by
       float cosa = (N.x * L.x + N.y * L.y) + N.z * L.z;
       cosa = (cosa > 0.0f) ? cosa : 0.0f;  // _mm_max_ps(cosa, 0)
-      const float k = invD * cosa;
+      kf[i] = invD * cosa;                 // f_i = colour_i * kf[i]
       if (i == wl) Lw = L;
-      emit(i, (uint32_t)i, r, tmax, v3(S.pcol[3 * i] * k, S.pcol[3 * i + 1] * k, S.pcol[3 * i + 2] * k));
+      emit(i, (uint32_t)i);
     }
+    nk = make_float4(kf[0], kf[1], kf[2], kf[3]);
     if (!(fl & kLighted)) return v3(0.0f, 0.0f, 0.0f);
     return eval_combined_brdf(N, Lw, V, m);
   }
-  const float* lc = (kind == 2) ? S.scol : S.dcol;                                          // :270-326
-  const uint32_t light = (kind == 2) ? kLightSpot : kLightDir;
+  const uint32_t light = (kind == 2) ? kLightSpot : kLightDir;                              // :270-326
   Ray r;
   float tmax, distance;
   V3 L;
   light_ray(S, light, I, r, tmax, L, distance);
   const float cosa = smax(0.0f, dot(N, L));
-  V3 f0;
-  if (kind == 2) {
+  if (kind == 2) {  // f_0 = (colour * (1 / d^2)) * cos inside the cone (factor > 0.9), else 0
     const float factor = dot(L, v3(S.srot[0], S.srot[1], S.srot[2]));
-    f0 = ((double)factor > 0.9) ? v3(lc[0], lc[1], lc[2]) * (1 / (distance * distance)) * cosa
-                                : v3(0.0f, 0.0f, 0.0f);
-  } else {
-    f0 = v3(lc[0], lc[1], lc[2]) * cosa;
+    nk = make_float4(cosa, 1 / (distance * distance), ((double)factor > 0.9) ? 1.0f : 0.0f, 0.0f);
+  } else {          // f_0 = colour * cos
+    nk = make_float4(cosa, 0.0f, 0.0f, 0.0f);
   }
-  emit(0, light, r, tmax, f0);
+  emit(0, light);
   return (fl & kLighted) ? eval_combined_brdf(N, L, V, m) : v3(0.0f, 0.0f, 0.0f);
+}
+
+// shadow ray k's unoccluded contribution from nee_lights' factors (Core/Renderer.cpp:257-263,283-288,309-316)
+__device__ __forceinline__ V3 nee_contrib(const SceneDev& S, int kind, int k, float4 nk) {
+  if (kind == 0) {
+    const float f = k == 0 ? nk.x : (k == 1 ? nk.y : (k == 2 ? nk.z : nk.w));
+    return v3(S.pcol[3 * k] * f, S.pcol[3 * k + 1] * f, S.pcol[3 * k + 2] * f);
+  }
+  if (kind == 2) return (nk.z != 0.0f) ? v3(S.scol[0], S.scol[1], S.scol[2]) * nk.y * nk.x : v3(0.0f, 0.0f, 0.0f);
+  return v3(S.dcol[0], S.dcol[1], S.dcol[2]) * nk.x;
 }
 
 // result after NEE: emissive + throughput(=1) * (BRDF * contribution), the reference's float order.
 // vis bit i = shadow ray i unoccluded.
-__device__ __forceinline__ V3 nee_resolve(int kind, uint32_t vis, V3 e, V3 brdf, const V3* f, uint32_t fl) {
+__device__ __forceinline__ V3 nee_resolve(const SceneDev& S, int kind, uint32_t vis, V3 e, V3 brdf, float4 nk,
+                                          uint32_t fl) {
   V3 c = v3(0.0f, 0.0f, 0.0f);
   if (kind == 0) {
 #pragma unroll
     for (int i = 0; i < 4; i++)
-      if (vis & (1u << i)) c = c + f[i];
+      if (vis & (1u << i)) c = c + nee_contrib(S, 0, i, nk);
     c = c / 0.3f;
   } else {
-    if (vis & 1u) c = f[0];
+    if (vis & 1u) c = nee_contrib(S, kind, 0, nk);
     if (kind == 1) c = c / 0.5f;
     else if (kind == 2) c = c / 0.2f;
   }

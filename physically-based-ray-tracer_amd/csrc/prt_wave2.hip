@@ -22,7 +22,7 @@
 //                    sample or path-2 start -> P(i+1)
 //
 // Hazards (all kernels on one stream): P(i+1) reuses P(i-1)'s buffer after k_resmiss2(i) read it;
-// S(i) reuses S(i-1)'s buffer after k_trace2(i) read it; k_resmiss2(i) reads ne/nb/nf/vis/R/T of an item for
+// S(i) reuses S(i-1)'s buffer after k_trace2(i) read it; k_resmiss2(i) reads ne/nb/nk/vis/R/T of an item for
 // iteration i-1 before it (misses) or k_shade2(i) (hits) overwrites them; rinfo keeps iteration i-1's status
 // (and whether the item was queued) while info already holds the state of the queued next ray.
 #include "prt_launch.h"
@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
     prefetch(c + gridDim.x);
     const uint32_t s0 = block_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic
     const uint32_t depth = info & 0xFFu, path = (info >> 8) & 1u;
-    uint32_t status = kStMiss;
+    uint32_t status = kStMiss, emissive = 0;
     bool next = false;
     bool area_ray = false;
     if (nr) {
@@ -341,17 +341,20 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
       const V3 I = v3(o.x, o.y, o.z) + hh.x * D;                                             // tiny_bvh.h:586
       const V3 V = -D;
       const HitAttr ha = hit_attributes(Sc, hit_inst(Sc, pk), hit_prim(Sc, pk), hh.y, hh.z, (fl & kNormalMap) != 0);
-      const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
-      Bc.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
       // a shadow ray is queued as (light, visibility index) with the item's hit point I stored once: the traversal
       // kernel rebuilds it (shadow_of)
       Bc.hp[item] = make_float4(I.x, I.y, I.z, 0.0f);
-      const V3 brdf = nee_lights(Sc, fl, kind, I, V, ha.N, ha.m, seed,
-                                 [&](int k, uint32_t light, const Ray&, float, V3 fk) {
+      float4 nk;
+      const V3 brdf = nee_lights(Sc, fl, kind, I, V, ha.N, ha.m, seed, nk, [&](int k, uint32_t light) {
         shq[s0 + k] = (light << 29) | (4u * item + (uint32_t)k);
-        Bc.nf[4 * (size_t)item + k] = make_float4(fk.x, fk.y, fk.z, 0.0f);
       });
+      const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
+      if (e.x != 0.0f || e.y != 0.0f || e.z != 0.0f) {  // otherwise e is +0 and the resolve rebuilds it
+        Bc.ne[item] = make_float4(e.x, e.y, e.z, 0.0f);
+        emissive = kRiEmissive;
+      }
       Bc.nb[item] = make_float4(brdf.x, brdf.y, brdf.z, 0.0f);
+      Bc.nk[item] = nk;
       Bc.vis[item] = 0u;
       status = kStNeeEnd;
       if constexpr (EXT) {
@@ -412,7 +415,7 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
         if (EXT && Sc.has_diel) next = diel_next(Bc, item, depth, path);
         if (!next) next = start_path2(Sc, A, M, Bc, item, path);
       }
-      Bc.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20) | (next ? kRiQueued : 0u);
+      Bc.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20) | (next ? kRiQueued : 0u) | emissive;
     }
     const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
     if (next) qn[sub * Bc.qcap + slot] = item;
@@ -455,26 +458,19 @@ __global__ void __launch_bounds__(kBlock) k_shade2_debug(SceneDev S, TraceArgs A
 // ---- NEE resolve of P(iter) (after k_trace2(iter + 1) traced S(iter)), stack, path end, frame write
 template <bool EXT>
 __device__ __forceinline__ void resolve_item(const SceneDev& S, const TraceArgs& A, const WaveBufs& B, uint32_t item,
-                                             uint32_t ri, float4 ne, float4* __restrict__ out) {
+                                             uint32_t ri, float4* __restrict__ out) {
   const uint32_t fl = A.flags;
   const uint32_t depth = ri & 0xFFu, path = (ri >> 8) & 1u, status = (ri >> 16) & 3u, kind = (ri >> 20) & 3u;
+  // ne: the end value (miss, debug mode) or a hit's emissive term, stored only when nonzero (kRiEmissive)
+  const bool nee = status == kStNeeEnd || status == kStNeeCont;
+  const float4 ne = (!nee || (ri & kRiEmissive)) ? B.ne[item] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   V3 L = v3(ne.x, ne.y, ne.z);
-  if (status == kStNeeEnd || status == kStNeeCont) {
-    const float4 nb = B.nb[item];
+  if (nee) {
+    const float4 nb = B.nb[item], nk = B.nk[item];
     const uint32_t vw = B.vis[item];
     const uint32_t vis = ((vw & 0xFFu) ? 1u : 0u) | ((vw & 0xFF00u) ? 2u : 0u) | ((vw & 0xFF0000u) ? 4u : 0u) |
                          ((vw & 0xFF000000u) ? 8u : 0u);
-    V3 f[4];
-    const uint32_t nr = kind == 0 ? 4u : 1u;
-    for (uint32_t k = 0; k < 4; k++) {
-      if (k < nr) {
-        const float4 fk = B.nf[4 * (size_t)item + k];
-        f[k] = v3(fk.x, fk.y, fk.z);
-      } else {
-        f[k] = v3(0.0f, 0.0f, 0.0f);
-      }
-    }
-    V3 result = nee_resolve((int)kind, vis, L, v3(nb.x, nb.y, nb.z), f, fl);
+    V3 result = nee_resolve(S, (int)kind, vis, L, v3(nb.x, nb.y, nb.z), nk, fl);
     if constexpr (EXT) {
       if (reinterpret_cast<const uint8_t*>(B.vis)[4 * (size_t)B.n + item]) {  // area light unoccluded
         const float4 a = B.na[item];
@@ -541,26 +537,23 @@ __global__ void __launch_bounds__(kBlock) k_resmiss2(SceneDev S, TraceArgs A, Wa
   __shared__ uint32_t pref[kNSub + 1];
   const uint32_t* q = ((iter - 1) & 1) ? B.q1 : B.q0;
   const uint32_t total = load_prefix(B.ctr, iter - 1, 0, pref);
-  // software pipeline over the grid-stride chunks: the next chunk's item, rinfo and ne are loaded while this
+  // software pipeline over the grid-stride chunks: the next chunk's item and rinfo are loaded while this
   // chunk's item is resolved
   uint32_t item_n = 0, ri_n = 0;
-  float4 ne_n = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   auto prefetch = [&](uint32_t cc) {
     const uint32_t gg = cc * kBlock + threadIdx.x;
     if (gg < total) {
       item_n = q[map_slot(pref, gg, B.qcap)];
       ri_n = B.rinfo[item_n];
-      ne_n = B.ne[item_n];
     }
   };
   prefetch(blockIdx.x);
   for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
     const uint32_t g = c * kBlock + threadIdx.x;
     const uint32_t item = item_n, ri = ri_n;
-    const float4 ne = ne_n;
     prefetch(c + gridDim.x);
     if (g >= total) continue;
-    resolve_item<EXT>(S, A, B, item, ri, ne, out);
+    resolve_item<EXT>(S, A, B, item, ri, out);
     if (misses && iter < iters && (ri & kRiQueued)) miss_item<EXT>(S, A, B, item);
   }
 }
