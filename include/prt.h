@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PRT_ABI_VERSION 6
+#define PRT_ABI_VERSION 7
 
 typedef enum {
     PRT_OK = 0,
@@ -216,6 +216,12 @@ int prt_render(prt_ctx* ctx, const prt_render_params* params, float* avg_rgba, u
 /* Reset the accumulation state: memset of the accumulator (Core/Renderer.cpp:147) and, with
  * full != 0, also samplesPerPixel/distances (fresh Renderer). */
 int prt_reset_accumulation(prt_ctx* ctx, int32_t full);
+/* Running ray totals (ABI 7): closest-hit segments and shadow rays of every render since the context was created
+ * or last reset, counted on the device at the end of each render (the figure behind the reference's ImGui ray
+ * counter, Core/Renderer.cpp:467-474) so a frame loop need not pass prt_stats, which waits for each frame.  Waits for
+ * the frames queued on the context's stream (a local group: on every member's, summed); reset != 0 zeroes the totals
+ * after reading them. */
+int prt_ray_totals(prt_ctx* ctx, uint64_t* segments, uint64_t* shadow_rays, int32_t reset);
 
 /* ---- checkpoint / resume of the progressive accumulation (the reference keeps it in memory only) ----
  * The accumulation state Renderer holds between Ticks (Core/Renderer.h:61-63: accumulator, samplesPerPixel,

@@ -255,6 +255,11 @@ class Renderer {
     frame_ = frame;
   }
 
+  // rays traced since construction (or the last reset): the reference's ImGui ray counter (Core/Renderer.cpp:467-474)
+  void RayTotals(uint64_t* segments, uint64_t* shadow_rays, bool reset = false) const {
+    check(prt_ray_totals(ctx_, segments, shadow_rays, reset ? 1 : 0));
+  }
+
   uint32_t Flags() const {
     return (AA ? PRT_FLAG_AA : 0u) | (accumulates ? PRT_FLAG_ACCUMULATE : 0u) | (GAMMACORRECTED ? PRT_FLAG_GAMMA : 0u) |
            (NORMALMAPPED ? PRT_FLAG_NORMALMAP : 0u) | (SKYBOX ? PRT_FLAG_SKYBOX : 0u) | (LIGHTED ? PRT_FLAG_LIGHTED : 0u) |

@@ -436,6 +436,9 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces, bool ext) {
   return PRT_OK;
 }
 
+// the context's running ray totals (prt_ray_totals): bytes 16-31 of the diag buffer, zeroed at prt_create
+Counters* ray_totals_dev(prt_ctx* c) { return reinterpret_cast<Counters*>(c->diag.as<char>() + 16); }
+
 // the shared trace + accumulate sequence for prt_render / prt_render_tiles
 // enqueues the render on the context stream; want_stats: per-launch timers + read_stats() afterwards
 int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4* avg_dev, uint32_t* rgb8_dev,
@@ -524,7 +527,8 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
       if (c->pfx.aberration != 0) { HIP_TRY(c->accprev.ensure(np * 16)); acc_prev = c->accprev.as<float4>(); }
     }
     HIP_TRY(launch_accumulate(L, M, Fb, p->flags, frames, c->acc.as<float4>(), c->nsamp.as<int32_t>(),
-                              c->dist.as<float>(), avg_dev, post ? nullptr : rgb8_dev, tiles_dev, acc_prev));
+                              c->dist.as<float>(), avg_dev, post ? nullptr : rgb8_dev, tiles_dev, acc_prev,
+                              c->wb.ctr, iters, ray_totals_dev(c)));
     if (post && last) {
       // with !accumulates the accumulator held this frame's value until the end-of-frame memset
       const float4* acc_new = (p->flags & PRT_FLAG_ACCUMULATE) ? c->acc.as<float4>() : avg_dev;
@@ -1212,6 +1216,26 @@ constexpr char kAccMagic[8] = {'P', 'R', 'T', 'A', 'C', 'C', 'U', 'M'};
 constexpr uint32_t kAccVersion = 1;
 uint64_t acc_blob_bytes(uint64_t n) { return sizeof(AccHeader) + n * (16 + 4 + 4); }
 }  // namespace
+
+int prt_ray_totals(prt_ctx* c, uint64_t* segments, uint64_t* shadow_rays, int32_t reset) {
+  if (!c || !segments || !shadow_rays) return fail(PRT_ERR_INVALID_ARGUMENT, "bad ray totals arguments");
+  std::vector<prt_ctx*> all{c};
+  all.insert(all.end(), c->members.begin(), c->members.end());
+  uint64_t seg = 0, sh = 0;
+  for (prt_ctx* m : all) {
+    HIP_TRY(hipSetDevice(m->device));
+    Counters h{};
+    HIP_TRY(hipMemcpyAsync(&h, ray_totals_dev(m), sizeof(h), hipMemcpyDeviceToHost, m->stream));
+    if (reset) HIP_TRY(hipMemsetAsync(ray_totals_dev(m), 0, sizeof(Counters), m->stream));
+    HIP_TRY(hipStreamSynchronize(m->stream));
+    seg += h.segments;
+    sh += h.shadow;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  *segments = seg;
+  *shadow_rays = sh;
+  return PRT_OK;
+}
 
 int prt_accumulation_bytes(prt_ctx* c, uint64_t* bytes) {
   if (!c || !bytes) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/bytes is NULL");

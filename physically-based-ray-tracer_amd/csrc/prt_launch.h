@@ -81,10 +81,11 @@ hipError_t launch_wave_init(const LaunchCfg& c, const SceneDev& S, const TraceAr
 // P(it) closest + S(it-1) any-hit, then resolve / miss / shade
 hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                              const WaveBufs& B, float4* out, WaveTimers* tm, uint32_t it);
-// acc_prev (nullable): the accumulator state before the last frame of the call (screen-pass input)
+// acc_prev (nullable): the accumulator state before the last frame of the call (screen-pass input);
+// totals (nullable): running ray totals, incremented by the queue counters ctr of the pass's `iters` iterations
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,
                              float4* acc, int32_t* nsamp, float* dist, float4* avg, uint32_t* rgb8, float4* tiles,
-                             float4* acc_prev);
+                             float4* acc_prev, const uint32_t* ctr, uint32_t iters, Counters* totals);
 // post-processed RGB8 of the whole image (Core/Renderer.cpp:107-133)
 hipError_t launch_postfx(const LaunchCfg& c, const PostDev& P, const float4* acc_new, const float4* acc_old,
                          const int32_t* nsamp, const float4* avg, uint32_t* rgb8);

@@ -21,11 +21,32 @@ __device__ __forceinline__ void wave_count(Counters* c, uint32_t seg, uint32_t s
 }
 
 // Core/Renderer.cpp:81-104,137.  tiles_out != null: write the average in item (tile-compact) order.
+// totals != null: the first wave also adds this pass's ray counts (the closest / shadow queue counters of its
+// `iters` wavefront iterations) to the context's running totals (prt_ray_totals), so a caller can count rays
+// without a host sync per frame
 __global__ void __launch_bounds__(kBlock) k_accumulate(TileMap M, int32_t frames, uint32_t flags,
                                                        const float4* __restrict__ fr, float4* __restrict__ acc,
                                                        int32_t* __restrict__ nsamp, float* __restrict__ dist,
                                                        float4* __restrict__ avg_out, uint32_t* __restrict__ rgb8_out,
-                                                       float4* __restrict__ tiles_out, float4* __restrict__ acc_prev) {
+                                                       float4* __restrict__ tiles_out, float4* __restrict__ acc_prev,
+                                                       const uint32_t* __restrict__ ctr, uint32_t iters,
+                                                       Counters* __restrict__ totals) {
+  if (totals && blockIdx.x == 0 && threadIdx.x < 64) {
+    unsigned long long seg = 0, sh = 0;
+    for (uint32_t j = threadIdx.x; j < iters * kNSub; j += 64) {
+      const uint32_t k = j / kNSub, s = j % kNSub;
+      seg += ctr[((k * 2u + 0u) * kNSub + s) * kCtrStride];
+      sh += ctr[((k * 2u + 1u) * kNSub + s) * kCtrStride];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      seg += __shfl_xor(seg, off, 64);
+      sh += __shfl_xor(sh, off, 64);
+    }
+    if (threadIdx.x == 0) {
+      atomicAdd(&totals->segments, seg);
+      atomicAdd(&totals->shadow, sh);
+    }
+  }
   const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
   if (r >= M.items) return;
   int32_t x, y;
@@ -173,10 +194,10 @@ static inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlock - 1) 
 
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,
                              float4* acc, int32_t* nsamp, float* dist, float4* avg, uint32_t* rgb8, float4* tiles,
-                             float4* acc_prev) {
+                             float4* acc_prev, const uint32_t* ctr, uint32_t iters, Counters* totals) {
   if (M.items == 0) return hipSuccess;
   hipLaunchKernelGGL(k_accumulate, dim3(grid_of(M.items)), dim3(kBlock), 0, c.stream, M, frames, flags, fr, acc, nsamp,
-                     dist, avg, rgb8, tiles, acc_prev);
+                     dist, avg, rgb8, tiles, acc_prev, ctr, iters, totals);
   return hipGetLastError();
 }
 

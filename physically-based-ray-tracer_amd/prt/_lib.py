@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIBPATH = os.path.join(HERE, "libprt.so")
 
 PRT_OK = 0
-ABI_VERSION = 6  # PRT_ABI_VERSION of the include/prt.h these structs mirror
+ABI_VERSION = 7  # PRT_ABI_VERSION of the include/prt.h these structs mirror
 FLAG_AA, FLAG_ACCUMULATE, FLAG_GAMMA, FLAG_NORMALMAP, FLAG_SKYBOX, FLAG_LIGHTED, FLAG_STOCHASTIC = (1 << i for i in range(7))
 FLAGS_DEFAULT = 0x7F
 OUT_DEVICE = 1
@@ -27,7 +27,7 @@ EXPORTS = [
     "prt_untile", "prt_trace_primary", "prt_intersect", "prt_occluded", "prt_get_scene_info", "prt_set_bvh_builder",
     "prt_set_instance_materials", "prt_set_area_lights", "prt_shard_unique_id", "prt_shard_init_rccl",
     "prt_shard_attach_rccl", "prt_create_group", "prt_get_shard_info", "prt_accumulation_bytes",
-    "prt_save_accumulation", "prt_load_accumulation",
+    "prt_save_accumulation", "prt_load_accumulation", "prt_ray_totals",
 ]
 SHARD_ID_BYTES = 128
 SHARD_NONE, SHARD_RCCL, SHARD_GROUP = 0, 1, 2  # prt_shard_info.transport
@@ -143,6 +143,7 @@ def load():
         "prt_accumulation_bytes": ([vp, C.POINTER(C.c_uint64)], C.c_int),
         "prt_save_accumulation": ([vp, vp, C.c_uint64], C.c_int),
         "prt_load_accumulation": ([vp, vp, C.c_uint64], C.c_int),
+        "prt_ray_totals": ([vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int32], C.c_int),
         "prt_tile_buffer_pixels": ([i32, i32, i32, i32, C.POINTER(C.c_int64)], C.c_int),
         "prt_tile_pixel_map": ([i32, i32, i32, i32, i32, C.c_void_p], C.c_int),
         "prt_render_tiles": ([vp, C.POINTER(RenderParams), i32, i32, i32, vp, C.POINTER(Stats)], C.c_int),

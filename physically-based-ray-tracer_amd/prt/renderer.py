@@ -277,6 +277,13 @@ class Context:
     def reset_accumulation(self, full=True):
         check(self.L.prt_reset_accumulation(self.h, 1 if full else 0))
 
+    def ray_totals(self, reset=False):
+        """(segments, shadow_rays) of every render since creation or the last reset, counted on the device
+        (prt_ray_totals): a frame loop can count rays without stats=True, which waits for each frame."""
+        seg, sh = C.c_uint64(), C.c_uint64()
+        check(self.L.prt_ray_totals(self.h, C.byref(seg), C.byref(sh), 1 if reset else 0))
+        return int(seg.value), int(sh.value)
+
     def save_accumulation(self) -> bytes:
         """The accumulation state (accumulator, samplesPerPixel, distances) as an opaque blob
         (prt_save_accumulation); b"" before the first render."""

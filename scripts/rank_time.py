@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-rank frame time of the pixel-tile sharding on ONE GPU: rank 0's share of the C4 frame for
 world = 1, 2, 4, 8 (what each GPU of an N-GPU node renders), to estimate strong scaling without a node.
-`rank_time.py [c5] [worlds...]`: c5 = 3840x2160, 16 spp, depth 8 with the area light (bench.py --scene c5)."""
+`rank_time.py [c5] [worlds...]`: c5 = 3840x2160, 16 spp, depth 8 with the area light (bench.py --scene c5).
+The timed frames run without stats, as bench.py's do (no host wait per frame; rays from prt_ray_totals)."""
 import os
 import sys
 import time
@@ -31,13 +32,15 @@ for world in WORLDS:
     tiles = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
     for i in range(1 if C5 else 2):
         ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i)
+    ctx.ray_totals(reset=True)
     torch.cuda.synchronize()
     n = 2 if C5 else 5
     t0 = time.perf_counter()
     for i in range(n):
-        st = ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i, stats=True)
+        ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / n
+    seg, sh = ctx.ray_totals(reset=True)
     base = base or ms * world
-    print(f"world {world}: rank-0 frame {ms:.3f} ms  rays {st.segments + st.shadow_rays}  "
+    print(f"world {world}: rank-0 frame {ms:.3f} ms  rays {(seg + sh) // n}  "
           f"ideal {base / world:.3f} ms  efficiency {base / world / ms:.2f}", flush=True)

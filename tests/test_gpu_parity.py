@@ -128,6 +128,41 @@ def test_progressive_accumulation(gpu_ctx):
     assert np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)) > 0.999
 
 
+def test_ray_totals_match_stats(gpu_ctx, monkeypatch):
+    """prt_ray_totals (the device-side running count behind bench.py's rays) equals the per-call prt_stats
+    counts summed, for calls with and without stats, a multi-pass call (PRT_MAX_ITEMS) and a tile render;
+    reset zeroes it."""
+    import torch
+    import prt
+    sd = scenes.config_small(40, 30)
+    W, H = 48, 32
+    gpu_scene(gpu_ctx, sd, W, H)
+    gpu_ctx.ray_totals(reset=True)
+    assert gpu_ctx.ray_totals() == (0, 0)
+    seg = sh = 0
+    for f in range(3):
+        _, _, st = gpu_ctx.render(W, H, 2, 3, frame_index=f, stats=True)
+        seg += st.segments
+        sh += st.shadow_rays
+    assert gpu_ctx.ray_totals() == (seg, sh) and seg > 0 and sh > 0
+    gpu_ctx.render(W, H, 2, 3, frame_index=3)  # no stats: still counted
+    _, _, st = gpu_ctx.render(W, H, 2, 3, frame_index=3, stats=True)
+    assert gpu_ctx.ray_totals(reset=True) == (seg + 2 * st.segments, sh + 2 * st.shadow_rays)
+    monkeypatch.setenv("PRT_MAX_ITEMS", str(W * H))  # one reference frame per pass: 4 passes
+    _, _, st = gpu_ctx.render(W, H, 8, 3, frame_index=4, stats=True)
+    monkeypatch.delenv("PRT_MAX_ITEMS")
+    assert gpu_ctx.ray_totals(reset=True) == (st.segments, st.shadow_rays)
+    gpu_ctx.reset_accumulation(True)
+    c = prt.Context(0)  # a tile render on a context of its own (the session context keeps its geometry)
+    gpu_scene(c, sd, W, H)
+    per = c.tile_buffer_pixels(W, H, 16, 2)
+    tiles = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
+    c.render_tiles(W, H, 2, 3, 16, 1, 2, tiles.data_ptr(), frame_index=0)
+    st = c.render_tiles(W, H, 2, 3, 16, 1, 2, tiles.data_ptr(), frame_index=0, stats=True)
+    assert c.ray_totals() == (2 * st.segments, 2 * st.shadow_rays) and st.segments > 0
+    c.close()
+
+
 @pytest.mark.parametrize("post", [False, True])
 def test_tiles_match_full_frame(gpu_ctx, post):
     """Pixel-tile sharding (config C4's decomposition) on one GPU: world ranks rendered by separate
