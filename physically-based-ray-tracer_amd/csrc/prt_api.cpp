@@ -477,7 +477,8 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   if (iters > (uint32_t)kMaxIters)
     return fail(PRT_ERR_UNSUPPORTED, S.has_diel ? "dielectric path trees exceed the wavefront iteration limit (lower bounces)"
                                                 : "too many wavefront iterations");
-  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  // the call's own events (prt_stats ms / ms_trace) only with stats: each record is a gap between kernels
+  if (want_stats) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   rc = ensure_wave(c, (uint32_t)(per * (uint64_t)F0), p->bounces, ext);
   if (rc) return rc;
   // PRT_TAIL=0 switches the cooperative traversal tail off (prt_persist.h; A/B runs only)
@@ -517,7 +518,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     HIP_TRY(launch_wave_init(L, S, A, M, c->wb, frames));
     for (uint32_t it = 0; it <= iters; it++)
       HIP_TRY(launch_wave2_iter(L, S, A, M, c->wb, frames, timers ? &c->wt : nullptr, it));
-    if (last) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    if (last && want_stats) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     // post-processing (single-GPU image): the screen pass needs the average and, for the aberration, the
     // accumulator before the last frame
     float4* acc_prev = nullptr;
@@ -546,7 +547,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
         }
     }
   }
-  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  if (want_stats) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   c->last_iters = iters;
   c->last_timers = timers;
   c->last_paths = tile_image_pixels(M) * (uint64_t)F * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
