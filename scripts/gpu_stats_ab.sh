@@ -1,4 +1,5 @@
 # A/B: rank-0 shares with a stats read (host sync) after every frame vs none (PRT_RANK_NOSTATS=1), timers off
+# (historical: the no-stats frame loop it measured is now rank_time.py's default and PRT_RANK_NOSTATS is gone; record in profiles/r03_sync_ab.txt)
 set -o pipefail
 mkdir -p gpurun_out
 out=gpurun_out/stats_ab.log
