@@ -510,8 +510,7 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
       const size_t qw = (size_t)(iters + 2) * 2 * kNSub * kCtrStride;
       const size_t fbase = (size_t)(kMaxIters + 2) * 2 * kNSub * kCtrStride;
       const size_t fw = (size_t)(iters + 2) * 2 * kParts * kCtrStride;
-      HIP_TRY(hipMemsetAsync(c->wb.ctr, 0, 4 * qw, c->stream));
-      HIP_TRY(hipMemsetAsync(c->wb.ctr + fbase, 0, 4 * fw, c->stream));
+      HIP_TRY(launch_clear2(L, c->wb.ctr, (uint32_t)qw, c->wb.ctr + fbase, (uint32_t)fw));
     }
     if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(c->wb.dst, 0, 4ull * c->wb.n, c->stream));
     float4* frames = c->frames.as<float4>();

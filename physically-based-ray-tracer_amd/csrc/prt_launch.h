@@ -81,6 +81,8 @@ hipError_t launch_wave_init(const LaunchCfg& c, const SceneDev& S, const TraceAr
 // P(it) closest + S(it-1) any-hit, then resolve / miss / shade
 hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                              const WaveBufs& B, float4* out, WaveTimers* tm, uint32_t it);
+// zero na words at a and nb words at b (one dispatch)
+hipError_t launch_clear2(const LaunchCfg& c, uint32_t* a, uint32_t na, uint32_t* b, uint32_t nb);
 // acc_prev (nullable): the accumulator state before the last frame of the call (screen-pass input);
 // totals (nullable): running ray totals, incremented by the queue counters ctr of the pass's `iters` iterations
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,

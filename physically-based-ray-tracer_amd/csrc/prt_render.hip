@@ -189,8 +189,24 @@ __global__ void __launch_bounds__(kBlock) k_occluded(SceneDev S, int32_t n, cons
   out[i] = scene_anyhit8<kQueryStack, kBlock>(S, r, tmax[i], stk) ? 1 : 0;
 }
 
+// zero two word ranges in one launch (a call's queue counters and fetch counters: one dispatch instead of two fills)
+__global__ void __launch_bounds__(kBlock) k_clear2(uint32_t* __restrict__ a, uint32_t na, uint32_t* __restrict__ b,
+                                                  uint32_t nb) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < na + nb; i += gridDim.x * kBlock) {
+    if (i < na) a[i] = 0u;
+    else b[i - na] = 0u;
+  }
+}
+
 // ---- launchers (host)
 static inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+hipError_t launch_clear2(const LaunchCfg& c, uint32_t* a, uint32_t na, uint32_t* b, uint32_t nb) {
+  const uint64_t n = (uint64_t)na + nb;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_clear2, dim3((unsigned)std::min<uint64_t>(grid_of(n), 256)), dim3(kBlock), 0, c.stream, a, na, b, nb);
+  return hipGetLastError();
+}
 
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,
                              float4* acc, int32_t* nsamp, float* dist, float4* avg, uint32_t* rgb8, float4* tiles,
