@@ -87,22 +87,11 @@ def fresh(d, live_hash):
     return bool(d) and live_hash is not None and d.get("code_hash") == live_hash
 
 
-def measured_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (profiles/traffic_current.json;
-    FETCH_SIZE x2 gfx950 correction of MI355X_MICROARCH.md, checked for this kernel's gathers by
-    profiles/fetch_calibration.json)."""
-    d, name = _pmc_kernel(os.path.join(ROOT, "profiles", "traffic_current.json"), kernel)
-    if d and "hbm_bytes_per_launch" in d:
-        return int(d["hbm_bytes_per_launch"]), name
-    return None, name
-
-
-def measured_valu(kernel):
-    """VALU wave-instructions per launch of `kernel` (SQ_INSTS_VALU, profiles/valu_current.json)."""
-    d, name = _pmc_kernel(os.path.join(ROOT, "profiles", "valu_current.json"), kernel)
-    if d and "SQ_INSTS_VALU" in d:
-        return d, name
-    return None, name
+def profile_record(scene, kernel):
+    """Per-launch record of `kernel` in profiles/current_<scene>.json (scripts/gpu_prof.sh + summarize_session.py:
+    rocprofv3 --stats, FETCH_SIZE / WRITE_SIZE, VALU-issue and stall --pmc passes of `bench.py --scene <scene>`,
+    stamped with the code hash of the kernels they measured)."""
+    return _pmc_kernel(os.path.join(ROOT, "profiles", f"current_{scene}.json"), kernel)
 
 
 def host_cpu():
@@ -315,20 +304,18 @@ def main():
         launches = max(1, iters)
         kern_ms = max(float(np.mean(ms_closest)) / launches, 1e-9)  # PRT_LAUNCH_TIMERS=0: no per-launch times
         seg_f, sh_f = seg_local / args.steps, shadow_local / args.steps  # rank 0's rays: its launches
-        c4 = args.scene == "c4" and W == 1920 and H == 1080 and world == 1  # the PMC passes are of this config
-        valu, valu_src = measured_valu(TRACE_KERNEL) if c4 else (None, None)
-        traffic, traffic_src = measured_traffic(TRACE_KERNEL) if c4 else (None, None)
+        # the PMC passes are of each scene's default configuration at N = 1 (scripts/gpu_prof.sh)
+        default_cfg = {"c3": (1920, 1080, 4, 4), "c4": (1920, 1080, 4, 4), "c5": (3840, 2160, 16, 8)}[args.scene]
+        priced = (W, H, args.spp, args.bounces) == default_cfg and world == 1
+        rec, rec_src = profile_record(args.scene, TRACE_KERNEL) if priced else (None, None)
         # the committed counters count only if they were taken on this very k_trace2 (code-object hash):
         # otherwise frac is withheld and the line says the profile is stale
         live_hash = current_code_hash(TRACE_KERNEL)
-        tr_rec, _ = _pmc_kernel(os.path.join(ROOT, "profiles", "traffic_current.json"), TRACE_KERNEL) if c4 else (None, None)
-        stale = {"valu": bool(valu) and not fresh(valu, live_hash),
-                 "traffic": bool(traffic) and not fresh(tr_rec, live_hash)}
-        valu_stale_rec = valu if stale["valu"] else None
-        if stale["valu"]:
-            valu = None
-        if stale["traffic"]:
-            traffic = None
+        stale = bool(rec) and not fresh(rec, live_hash)
+        ok = bool(rec) and not stale
+        valu = rec if ok and "SQ_INSTS_VALU" in rec else None
+        traffic = int(rec["hbm_bytes_per_launch"]) if ok and "hbm_bytes_per_launch" in rec else None
+        stall = rec.get("stall") if ok else None
         valu_rate = valu["SQ_INSTS_VALU"] / (kern_ms / 1e3) / 1e9 if valu else None
         hbm_rate = traffic / (kern_ms / 1e3) / 1e9 if traffic else None
         bpr = algorithmic_bytes_per_ray()
@@ -337,11 +324,17 @@ def main():
         own_bytes = (seg_f * own["closest"] + sh_f * own["anyhit"]) / launches if own else None
         hbm = {"achieved": round(hbm_rate, 1) if hbm_rate else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": round(hbm_rate / HBM_PEAK_GBS, 4) if hbm_rate else None, "traffic": traffic,
-               "source": traffic_src, "stale_profile": stale["traffic"]}
+               "source": rec_src}
+        # what bounds the kernel, from its stall counters: waves parked on s_waitcnt (dependent loads) most of
+        # their cycles = latency; otherwise the VALU issue rate (or, with no VALU pass, HBM bandwidth)
+        if stall and stall["wait"] > stall["issuing"] + stall["issue_stall"]:
+            bound = "latency"
+        else:
+            bound = "valu" if valu else "hbm"
         if valu_rate is not None:
-            roof = {"bound": "valu", "achieved": round(valu_rate, 1), "peak": VALU_PEAK_GINST,
+            roof = {"bound": bound, "achieved": round(valu_rate, 1), "peak": VALU_PEAK_GINST,
                     "unit": "G VALU wave-instructions/s", "frac": round(valu_rate / VALU_PEAK_GINST, 4),
-                    "traffic": traffic, "valu_insts_per_launch": int(valu["SQ_INSTS_VALU"]), "source": valu_src,
+                    "traffic": traffic, "valu_insts_per_launch": int(valu["SQ_INSTS_VALU"]), "source": rec_src,
                     # the single-wave issue rate (4 cycles per wave64 instruction, MI355X_MICROARCH.md
                     # constants table) bounds a SIMD holding one wave; k_trace2 holds 7, so frac uses 2 cycles
                     "frac_vs_single_wave_issue": round(2 * valu_rate / VALU_PEAK_GINST, 4)}
@@ -352,12 +345,14 @@ def main():
                 roof["pmc_clock_ghz"] = round(valu["clock_ghz"], 3)
                 roof["frac_at_pmc_clock"] = round(valu_rate / (VALU_PEAK_GINST * valu["clock_ghz"] / 2.4), 4)
         else:  # no fresh VALU pass for this config: price the measured HBM bytes (or nothing)
-            roof = {"bound": "valu" if valu_stale_rec else "hbm",
-                    "achieved": None if valu_stale_rec else hbm["achieved"],
-                    "peak": VALU_PEAK_GINST if valu_stale_rec else HBM_PEAK_GBS,
-                    "unit": "G VALU wave-instructions/s" if valu_stale_rec else "GB/s",
-                    "frac": None if valu_stale_rec else hbm["frac"], "traffic": traffic}
-        roof["stale_profile"] = stale["valu"] or stale["traffic"]
+            roof = {"bound": bound, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm["frac"], "traffic": traffic}
+        if stall:
+            roof["stall"] = {k: round(v, 4) for k, v in stall.items()}
+            roof["bound_basis"] = ("stall = fractions of SQ_WAVE_CYCLES: wait = parked on s_waitcnt (SQ_WAIT_ANY), "
+                                   "issue_stall = SQ_WAIT_INST_ANY, issuing = SQ_ACTIVE_INST_ANY; bound = latency "
+                                   "when wait > issuing + issue_stall")
+        roof["stale_profile"] = stale
         roof["code_hash"] = live_hash[:16] if live_hash else None
         roof.update({
             "kernel": TRACE_KERNEL, "per": f"launch (avg of {launches} launches per frame)",

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PRT_ABI_VERSION 7
+#define PRT_ABI_VERSION 8
 
 typedef enum {
     PRT_OK = 0,
@@ -313,6 +313,8 @@ typedef struct {
     double  build_ms;       /* wall time of the last prt_set_meshes (BLAS builds + uploads) */
     int32_t builder;        /* PRT_BUILDER_* used by the last prt_set_meshes */
     int32_t tlas_depth;     /* levels of the instance BVH the rays walk (0: instances tested as a linear list) */
+    int32_t tlas_rebuilds;  /* (ABI 8) device rebuilds of the instance BVH since the instance count last changed */
+    int32_t tlas_refits;    /* (ABI 8) device refits of it since then (prt_set_instances with the same count) */
 } prt_scene_info;
 int prt_get_scene_info(prt_ctx* ctx, prt_scene_info* info);
 

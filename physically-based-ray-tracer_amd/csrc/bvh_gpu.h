@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "prt_scene.h"
 
 namespace prt {
@@ -16,9 +18,11 @@ struct GpuBlasInfo {
 
 // tri_dev: fat triangles float4 x 3T in device memory.  nodes_out: room for T Node8; tris_out: T TriMT.
 // Synchronises on stream s once per tree level.  Child / triangle offsets are relative to the mesh.
-// ploc: PLOC clustering (bvh_gpu.hip) instead of the LBVH radix tree for the binary tree
+// ploc: PLOC clustering (bvh_gpu.hip) instead of the LBVH radix tree for the binary tree.  level_ends (optional):
+// the wide tree is emitted level by level, so level d's nodes are [level_ends[d-1], level_ends[d]) (level 0: [0, 1))
 hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, int max_leaf, Node8* nodes_out,
-                           TriMT* tris_out, GpuBlasInfo* info, bool ploc = false);
+                           TriMT* tris_out, GpuBlasInfo* info, bool ploc = false,
+                           std::vector<uint32_t>* level_ends = nullptr);
 // rebase a mesh's nodes into the concatenated arrays (in place) and record ShadeTri.pad[0] for its primitives
 hipError_t gpu_blas_finish(hipStream_t s, Node8* nodes, uint32_t n_nodes, uint32_t node_base, const TriMT* tris,
                            uint32_t n_tris, uint32_t tri_base, ShadeTri* stri, uint32_t prim_base);

@@ -745,7 +745,7 @@ __global__ void __launch_bounds__(kB) k_rebase(Node8* nodes, uint32_t n, uint32_
   } while (0)
 
 hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, int max_leaf, Node8* nodes_out,
-                           TriMT* tris_out, GpuBlasInfo* info, bool ploc) {
+                           TriMT* tris_out, GpuBlasInfo* info, bool ploc, std::vector<uint32_t>* level_ends) {
   const int n = n_tris;
   if (n <= 0) return hipErrorInvalidValue;
   const size_t nn = 2 * (size_t)n - 1;
@@ -874,6 +874,7 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
       (err = hipMemcpyAsync(ctr, c0, 16, hipMemcpyHostToDevice, s)))
     return fail(err);
   uint32_t ntasks = 1, depth = 0;
+  if (level_ends) level_ends->assign(1, 1u);  // level 0: the root (node 0)
   while (ntasks) {
     depth++;
     const uint32_t zero = 0;
@@ -886,6 +887,7 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
       return fail(err);
     if (c[3] & 0x80000000u) return fail(hipErrorInvalidValue);  // malformed tree (bounds checks above)
     ntasks = c[2];
+    if (level_ends && ntasks) level_ends->push_back(c[0]);  // the nodes this level allocated: the next level
     std::swap(ta, tb);
     info->nodes = c[0];
     info->tris = c[1];

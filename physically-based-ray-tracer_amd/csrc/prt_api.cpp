@@ -76,6 +76,20 @@ hipError_t upload(DevBuf& b, const void* src, size_t n) {
 }
 
 
+// wavefront state of one item group: the context's own (prt_ctx::ws), or of a concurrent group (prt_ctx::grp)
+struct WaveState {
+  DevBuf wave;
+  WaveBufs wb = {};
+  uint32_t n = 0, levels = 0;
+  bool ext = false;
+};
+// a concurrent item group beyond the first: its own stream, wavefront state and join event
+struct ItemGroup {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  WaveState ws;
+};
+
 struct MeshHost {
   float bmin[3], bmax[3];
   int depth;
@@ -113,6 +127,15 @@ struct prt_ctx {
   TlasTopo tlas_topo;    // its nodes by depth, deepest first (prt_tlas.h)
   int32_t tlas_n = -1;   // instance count of that build (-1: none)
   DevBuf tlas8, tlas_slot, tlas_order, tlas_aabb;
+  // device rebuild of the instance BVH when refitting has degraded it (ensure_instances): build scratch, the tree's
+  // SAH cost after every refit (device -> pinned host copy, read back without a host wait once its event is done)
+  DevBuf tlas_fat, tlas_tris, tlas_cost_dev;
+  double* tlas_cost_h = nullptr;  // pinned: [0] cost right after the last build, [1] after the latest refit
+  hipEvent_t tlas_cost_ev[2] = {nullptr, nullptr};
+  bool tlas_cost_pending[2] = {false, false};
+  double tlas_base_cost = 0.0;    // [0] once read
+  uint32_t tlas_nodes = 0;
+  int32_t tlas_rebuilds = 0, tlas_refits = 0;  // since the instance count last changed (diagnostics)
   DevBuf spill;  // traversal stack levels beyond the LDS ones (BVHs deeper than 17 levels)
   DevBuf diag;   // SceneDev::diag device counters ([0] traversal stack overflows, cumulative per context)
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
@@ -134,12 +157,13 @@ struct prt_ctx {
   int32_t accW = 0, accH = 0;
   DevBuf frames, avg, rgb8, counters, hits, tl;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  // wavefront state of the merged pipeline
-  DevBuf wave;
-  WaveBufs wb = {};
-  uint32_t wave_n = 0, wave_levels = 0;
-  bool wave_ext = false;
+  // wavefront state of the merged pipeline (the call's first item group)
+  WaveState ws;
   WaveTimers wt = {};
+  // concurrent item groups 1..G-1 of small calls (groups_for), created on first use
+  std::vector<ItemGroup> grp;
+  hipEvent_t fork = nullptr;
+  uint32_t last_groups = 1;
   // the last enqueued render, for its stats (read_stats)
   uint32_t last_iters = 0;
   bool last_timers = false;
@@ -153,6 +177,7 @@ struct prt_ctx {
   std::vector<prt_ctx*> members;  // local group: members 1..world-1, owned by member 0
   DevBuf shtiles, gathered;       // this rank's tile buffer; rank 0: [world][tile buffer] gathered
   hipEvent_t sh_ev = nullptr;     // member: tiles handed to member 0; member 0: untile done
+  bool layout_checked = false;    // check_layout_once done
 };
 
 namespace {
@@ -226,13 +251,94 @@ int ensure_instances(prt_ctx* c) {
   // BLASInstances every frame as the reference does (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770)
   const char* te = std::getenv("PRT_TLAS");
   c->use_tlas = n > kLinearInstances || (te && std::atoi(te) == 1);
-  // the instance BVH: built by the host SAH builder when the set of instances changes (its count; or every call with
-  // PRT_TLAS_HOST=1, the A/B form), otherwise refitted on the device behind k_refit (prt_tlas.hip): the reference
-  // rebuilds it every frame (Core/Renderer.cpp:33-41); a per-frame update costs no host BVH work and no sync
+  // The instance BVH.  The reference rebuilds it every frame (Core/Renderer.cpp:33-41).  Here the host SAH builder
+  // builds it when the set of instances changes (its count; or every call with PRT_TLAS_HOST=1, the A/B form);
+  // otherwise it is refitted on the device behind k_refit (prt_tlas.hip), and rebuilt on the device (PLOC +
+  // SAH-optimal collapse over the current boxes, gpu_build_tlas8) once refitting has raised the tree's SAH cost
+  // above PRT_TLAS_REBUILD (default 1.2) times its cost right after the last build (0: refit only).  The cost is
+  // measured on the device after every refit and read back without a host wait (a pinned copy behind an event):
+  // a frame decides on the latest cost already available.  No host BVH work and no host wait per frame.
   const char* th = std::getenv("PRT_TLAS_HOST");
-  if (c->use_tlas && c->tlas_n == n && !(th && std::atoi(th) == 1)) {
+  const char* tr = std::getenv("PRT_TLAS_REBUILD");
+  const double rebuild_ratio = tr ? std::atof(tr) : 1.2;
+  auto upload_order = [&]() -> int {
+    const size_t ob = 4 * c->tlas_topo.order.size(), ab = 24 * std::max<size_t>(c->tlas_nodes, 1);
+    if (c->tlas_order.bytes < ob || c->tlas_aabb.bytes < ab) {
+      const int rc = drain(c);
+      if (rc) return rc;
+      HIP_TRY(c->tlas_order.ensure(ob));
+      HIP_TRY(c->tlas_aabb.ensure(ab));
+    }
+    HIP_TRY(hipMemcpyAsync(c->tlas_order.p, c->tlas_topo.order.data(), ob, hipMemcpyHostToDevice, c->stream));
+    return PRT_OK;
+  };
+  // the tree's cost over its current boxes into pinned slot k (0: right after a build, 1: after a refit)
+  auto measure_cost = [&](int k) -> int {
+    if (rebuild_ratio <= 0) return PRT_OK;
+    if (!c->tlas_cost_h) {
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->tlas_cost_h), 2 * sizeof(double), hipHostMallocDefault));
+      for (auto& e : c->tlas_cost_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      HIP_TRY(c->tlas_cost_dev.ensure(2 * sizeof(double)));
+    }
+    HIP_TRY(launch_tlas_cost(c->stream, c->tlas8.as<Node8>(), c->tlas_nodes, c->tlas_aabb.as<float>(),
+                             c->inst.as<InstDev>(), c->tlas_slot.as<uint32_t>(), c->tlas_cost_dev.as<double>() + k));
+    HIP_TRY(hipMemcpyAsync(c->tlas_cost_h + k, c->tlas_cost_dev.as<double>() + k, sizeof(double),
+                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipEventRecord(c->tlas_cost_ev[k], c->stream));
+    c->tlas_cost_pending[k] = true;
+    return PRT_OK;
+  };
+  auto refit_tree = [&]() -> int {
     HIP_TRY(launch_tlas_refit(c->stream, c->inst.as<InstDev>(), c->tlas_topo, c->tlas_order.as<uint32_t>(),
                               c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(), c->tlas_aabb.as<float>()));
+    return PRT_OK;
+  };
+  if (c->use_tlas && c->tlas_n == n && !(th && std::atoi(th) == 1)) {
+    bool rebuild = false;
+    if (rebuild_ratio > 0) {
+      for (int k = 0; k < 2; k++)  // costs whose copies have landed (never waits)
+        if (c->tlas_cost_pending[k] && hipEventQuery(c->tlas_cost_ev[k]) == hipSuccess) {
+          c->tlas_cost_pending[k] = false;
+          if (k == 0) c->tlas_base_cost = c->tlas_cost_h[0];
+          else if (c->tlas_base_cost > 0 && c->tlas_cost_h[1] > rebuild_ratio * c->tlas_base_cost) rebuild = true;
+        }
+      (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady is not an error here
+    }
+    if (rebuild) {
+      // the device build writes the tree in place: frames queued before it keep stream order
+      if (c->tlas_fat.bytes < 48ull * n || c->tlas_tris.bytes < sizeof(TriMT) * (size_t)n ||
+          c->tlas8.bytes < sizeof(Node8) * (size_t)n || c->tlas_slot.bytes < 32ull * n) {
+        const int rc = drain(c);
+        if (rc) return rc;
+        HIP_TRY(c->tlas_fat.ensure(48ull * n));
+        HIP_TRY(c->tlas_tris.ensure(sizeof(TriMT) * (size_t)n));
+        HIP_TRY(c->tlas8.ensure(sizeof(Node8) * (size_t)n));
+        HIP_TRY(c->tlas_slot.ensure(32ull * n));
+      }
+      int depth = 0;
+      uint32_t nn = 0;
+      HIP_TRY(gpu_build_tlas8(c->stream, c->inst.as<InstDev>(), n, c->tlas_fat.as<float>(), c->tlas_tris.as<TriMT>(),
+                              c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(), &c->tlas_topo, &depth, &nn));
+      c->tlas_depth = depth;
+      c->tlas_nodes = nn;
+      int rc = upload_order();
+      if (rc) return rc;
+      rc = refit_tree();  // the refit's boxes (aabb) for the cost
+      if (rc) return rc;
+      c->tlas_base_cost = 0;
+      c->tlas_cost_pending[1] = false;
+      rc = measure_cost(0);
+      if (rc) return rc;
+      c->tlas_rebuilds++;
+    } else {
+      int rc = refit_tree();
+      if (rc) return rc;
+      c->tlas_refits++;
+      if (!c->tlas_cost_pending[1]) {  // at most one refit cost in flight
+        rc = measure_cost(1);
+        if (rc) return rc;
+      }
+    }
   } else if (c->use_tlas) {
     std::vector<float> boxes(6 * (size_t)n);
     for (int32_t i = 0; i < n; i++) {
@@ -243,6 +349,7 @@ int ensure_instances(prt_ctx* c) {
     }
     c->tlas_host = build_tlas8(boxes.data(), n);
     c->tlas_depth = c->tlas_host.depth;
+    c->tlas_nodes = (uint32_t)c->tlas_host.nodes.size();
     const size_t nb = c->tlas_host.nodes.size() * sizeof(Node8), sb = c->tlas_host.slot.size() * 4;
     if (c->tlas8.bytes < nb || c->tlas_slot.bytes < sb) {
       const int rc = drain(c);
@@ -251,17 +358,20 @@ int ensure_instances(prt_ctx* c) {
       HIP_TRY(c->tlas_slot.ensure(sb));
     }
     c->tlas_topo = tlas_topology(c->tlas_host.nodes);
-    const size_t ob = 4 * c->tlas_topo.order.size(), ab = 24 * c->tlas_host.nodes.size();
-    if (c->tlas_order.bytes < ob || c->tlas_aabb.bytes < ab) {
-      const int rc = drain(c);
-      if (rc) return rc;
-      HIP_TRY(c->tlas_order.ensure(ob));
-      HIP_TRY(c->tlas_aabb.ensure(ab));
-    }
     HIP_TRY(hipMemcpyAsync(c->tlas8.p, c->tlas_host.nodes.data(), nb, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->tlas_slot.p, c->tlas_host.slot.data(), sb, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->tlas_order.p, c->tlas_topo.order.data(), ob, hipMemcpyHostToDevice, c->stream));
+    int rc = upload_order();
+    if (rc) return rc;
+    if (c->tlas_n != n) c->tlas_rebuilds = c->tlas_refits = 0;
     c->tlas_n = n;
+    if (rebuild_ratio > 0 && !(th && std::atoi(th) == 1)) {  // the cost right after the build (its refit's boxes)
+      rc = refit_tree();
+      if (rc) return rc;
+      c->tlas_base_cost = 0;
+      c->tlas_cost_pending[1] = false;
+      rc = measure_cost(0);
+      if (rc) return rc;
+    }
   } else {
     c->tlas_depth = 0;
     c->tlas_n = -1;
@@ -393,14 +503,14 @@ int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
 // wavefront buffers sized for n items and (bounces-1) (result, throughput) stack levels
 // queue counters [iter][path|shadow][kNSub] + traversal fetch counters [iter][path|shadow][8 parts]
 constexpr size_t kCtrWords = (size_t)(kMaxIters + 2) * 2 * (kNSub + 8) * kCtrStride;
-int ensure_wave(prt_ctx* c, uint32_t n, int bounces, bool ext) {
+int ensure_wave(WaveState& ws, uint32_t n, int bounces, bool ext) {
   const uint32_t levels = (uint32_t)std::max(1, bounces - 1);
   // sub-queue t receives the 256-entry chunks c == t (mod kNSub): at most ceil(ceil(n/256)/kNSub) of them
   const uint32_t qcap = 256u * (((n + 255u) / 256u + kNSub - 1) / kNSub);
-  if (c->wave_n >= n && c->wave_levels >= levels && (c->wave_ext || !ext) && c->wave.p) {
-    c->wb.n = n;  // capacity stays; the SoA strides (R/T: depth * n + item) follow the current n
-    c->wb.qcap = qcap;
-    c->wb.scap = 5u * qcap;
+  if (ws.n >= n && ws.levels >= levels && (ws.ext || !ext) && ws.wave.p) {
+    ws.wb.n = n;  // capacity stays; the SoA strides (R/T: depth * n + item) follow the current n
+    ws.wb.qcap = qcap;
+    ws.wb.scap = 5u * qcap;
     return PRT_OK;
   }
   const size_t qn = (size_t)kNSub * qcap, sn = 5 * qn;  // <= 4 light-class + 1 area-light shadow rays per item
@@ -414,9 +524,9 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces, bool ext) {
   const size_t o_na = ext ? take(16ull * n) : 0, o_dst = ext ? take(4ull * n) : 0,
                o_dro = ext ? take(16ull * n * levels) : 0, o_drd = ext ? take(16ull * n * levels) : 0,
                o_ao = ext ? take(16ull * n) : 0, o_ad = ext ? take(16ull * n) : 0;
-  HIP_TRY(c->wave.ensure(off));
-  char* b = c->wave.as<char>();
-  WaveBufs& W = c->wb;
+  HIP_TRY(ws.wave.ensure(off));
+  char* b = ws.wave.as<char>();
+  WaveBufs& W = ws.wb;
   W.n = n;
   W.base = 0;
   W.qcap = qcap;
@@ -430,70 +540,156 @@ int ensure_wave(prt_ctx* c, uint32_t n, int bounces, bool ext) {
   W.na = ext ? (float4*)(b + o_na) : nullptr; W.dst = ext ? (uint32_t*)(b + o_dst) : nullptr;
   W.dro = ext ? (float4*)(b + o_dro) : nullptr; W.drd = ext ? (float4*)(b + o_drd) : nullptr;
   W.ao = ext ? (float4*)(b + o_ao) : nullptr; W.ad = ext ? (float4*)(b + o_ad) : nullptr;
-  c->wave_n = n;
-  c->wave_levels = levels;
-  c->wave_ext = ext;
+  ws.n = n;
+  ws.levels = levels;
+  ws.ext = ext;
   return PRT_OK;
 }
 
 // the context's running ray totals (prt_ray_totals): bytes 16-31 of the diag buffer, zeroed at prt_create
 Counters* ray_totals_dev(prt_ctx* c) { return reinterpret_cast<Counters*>(c->diag.as<char>() + 16); }
 
-// the shared trace + accumulate sequence for prt_render / prt_render_tiles
-// enqueues the render on the context stream; want_stats: per-launch timers + read_stats() afterwards
-int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4* avg_dev, uint32_t* rgb8_dev,
-               float4* tiles_dev, bool want_stats) {
+// k_shade2 reads its arguments through the kernarg segment (prt_wave2.hip Shade2Args) and flags diag[1] when the
+// layout it assumes is not the compiler's (it then shades nothing).  Checked once per context, after its first
+// render (one host wait), so stats-less frame loops fail loudly too; prt_ray_totals re-checks it
+int check_layout_once(prt_ctx* c) {
+  if (c->layout_checked) return PRT_OK;
+  uint32_t v[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(v, c->diag.p, 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (v[1] != 0) return fail(PRT_ERR_HIP, "k_shade2: kernel-argument layout check failed (Shade2Args)");
+  c->layout_checked = true;
+  return PRT_OK;
+}
+
+// fault injection (tests of the sharded error paths): PRT_FAIL_RENDER=<rank> makes that shard's render fail in
+// prepare_render, before anything is enqueued ("all": every context)
+int injected_failure(int32_t rank) {
+  const char* e = std::getenv("PRT_FAIL_RENDER");
+  if (!e || !*e) return PRT_OK;
+  if (std::strcmp(e, "all") == 0 || std::atoi(e) == rank)
+    return fail(PRT_ERR_HIP, "injected render failure (PRT_FAIL_RENDER) on shard " + std::to_string(rank));
+  return PRT_OK;
+}
+
+// A call's work items (pixels x reference frames) index the shadow-queue entries as 4 x item + k in 29 bits
+// (prt_wave2.hip kShIndexMask; the light class takes the top 3), so one pass holds at most 2^27 items
+constexpr uint64_t kMaxPassItems = 1ull << 27;
+
+// everything a render needs that can fail: validation and every allocation.  prepare_render enqueues no
+// rendering work (ensure_state's first-use clears aside), so a failure leaves the accumulation state as it was
+// and a sharded frame can still post its gather (render_sharded)
+struct RenderPlan {
   SceneDev S;
-  int rc = scene_ready(c, S);
+  TraceArgs A;
+  int32_t F = 0, fmax = 1, npass = 1, F0 = 0;
+  uint64_t per = 0;
+  bool ext = false;
+  uint32_t iters = 0;
+  uint32_t groups = 1;
+};
+
+// Concurrent item groups.  A call small enough that its traversal launches are bound by their
+// slowest rays (world-8 shares) can cut its items into G contiguous ranges, each with its own queues, stream and
+// launch chain, every grid 1/G of the resident blocks so the G chains co-reside and one chain's launch tail
+// overlaps another's busy phase.  PRT_GROUPS=1/2/4 (one-pass calls without HBM stack spill; default 1).
+uint32_t groups_for(const SceneDev& S, uint64_t items, int32_t npass) {
+  const char* e = std::getenv("PRT_GROUPS");
+  uint32_t g = e ? (uint32_t)std::max(1, std::atoi(e)) : 1u;
+  g = g >= 4 ? 4u : (g >= 2 ? 2u : 1u);
+  if (npass > 1 || S.spill || items < 256ull * g) g = 1;  // the spill columns are indexed by launch thread
+  return g;
+}
+
+int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int32_t rank, RenderPlan& R) {
+  SceneDev& S = R.S;
+  int rc = injected_failure(rank);
+  if (rc) return rc;
+  rc = scene_ready(c, S);
   if (rc) return rc;
   if (!c->have_camera) return fail(PRT_ERR_NOT_READY, "no camera: call prt_set_camera");
   if (!c->have_lights) return fail(PRT_ERR_NOT_READY, "no lights: call prt_set_lights");
   if (!depth_ok(c)) return fail(PRT_ERR_UNSUPPORTED, "BVH deeper than 64 levels");
+  // work items are pixels x reference frames (≈ 390 B of wavefront state each); a call holding more than 2^27 of
+  // them (≈ 52 GB of state) runs its frames in passes of up to 2^27 items (at least one frame), each folded into
+  // the accumulation state in order (the reference's frame sequence).  PRT_MAX_ITEMS sets a smaller pass size
+  // (tests run the multi-pass path at small sizes); a frame is never split, so one frame (of this shard) may
+  // hold at most 2^27 pixels
+  const uint64_t per = (uint64_t)M.items;
+  if (per > kMaxPassItems) return fail(PRT_ERR_UNSUPPORTED, "more than 2^27 pixels in one frame of one shard");
   rc = ensure_spill(c, S, 0);
   if (rc) return rc;
   rc = ensure_state(c, p->width, p->height);
   if (rc) return rc;
   const int32_t F = frames_of(p);
-  // work items are pixels x reference frames (≈ 390 B of wavefront state each); a call holding more than 2^27 of
-  // them (≈ 52 GB of state) runs its frames in passes of up to 2^27 items (at least one frame), each folded into
-  // the accumulation state in order (the reference's frame sequence).  PRT_MAX_ITEMS sets the pass size (tests
-  // run the multi-pass path at small sizes)
-  const uint64_t per = (uint64_t)M.items;
-  if (per >= (1ull << 30)) return fail(PRT_ERR_UNSUPPORTED, "more than 2^30 pixels in one frame");
   const char* emi = std::getenv("PRT_MAX_ITEMS");
-  const uint64_t max_items = emi ? std::min<uint64_t>(std::max<uint64_t>(std::strtoull(emi, nullptr, 10), 1), 1ull << 30)
-                                 : (1ull << 27);
-  const int32_t fmax = (int32_t)std::max<uint64_t>(1, (max_items - 1) / std::max<uint64_t>(per, 1));
+  const uint64_t max_items = emi ? std::min<uint64_t>(std::max<uint64_t>(std::strtoull(emi, nullptr, 10), 1), kMaxPassItems)
+                                 : kMaxPassItems;
+  const int32_t fmax = (int32_t)std::max<uint64_t>(1, max_items / std::max<uint64_t>(per, 1));
   const int32_t npass = F > fmax ? (F + fmax - 1) / fmax : 1;
   const int32_t F0 = std::min(F, fmax);
   HIP_TRY(c->frames.ensure(sizeof(float4) * (size_t)std::max<uint64_t>(per * (uint64_t)F0, 1)));
-  TraceArgs A;
+  TraceArgs& A = R.A;
   A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
   A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F0;
-  LaunchCfg L{c->stream, occ_for(c)};
   // extensions (area light, dielectric instances) take the EXT instantiations of the shading kernels
   const bool ext = (S.area || S.has_diel) && p->render_mode == 0;
   const uint32_t iters = wave_iters(S.has_diel != 0, p->bounces, p->flags);
   if (iters > (uint32_t)kMaxIters)
     return fail(PRT_ERR_UNSUPPORTED, S.has_diel ? "dielectric path trees exceed the wavefront iteration limit (lower bounces)"
                                                 : "too many wavefront iterations");
+  // sized for the first (largest) pass; later passes hold no more items
+  const uint64_t n0 = per * (uint64_t)F0;
+  const uint32_t G = groups_for(S, n0, npass);
+  for (uint32_t g = 0; g < G; g++) {
+    if (g > 0 && c->grp.size() < g) {  // a concurrent group's stream and join event (created once)
+      ItemGroup ig;
+      HIP_TRY(hipStreamCreateWithFlags(&ig.stream, hipStreamNonBlocking));
+      if (hipEventCreateWithFlags(&ig.done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipStreamDestroy(ig.stream);
+        return fail(PRT_ERR_HIP, "hipEventCreate failed");
+      }
+      c->grp.push_back(std::move(ig));
+    }
+    if (g > 0 && !c->fork) HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
+    WaveState& w = g == 0 ? c->ws : c->grp[g - 1].ws;
+    rc = ensure_wave(w, (uint32_t)(n0 * (g + 1) / G - n0 * g / G), p->bounces, ext);
+    if (rc) return rc;
+  }
+  R.F = F; R.fmax = fmax; R.npass = npass; R.F0 = F0; R.per = per; R.ext = ext; R.iters = iters; R.groups = G;
+  return PRT_OK;
+}
+
+// the shared trace + accumulate sequence for prt_render / prt_render_tiles, after prepare_render: enqueues the
+// render on the context stream; want_stats: per-launch timers + read_stats() afterwards
+int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, RenderPlan& R, float4* avg_dev,
+                   uint32_t* rgb8_dev, float4* tiles_dev, bool want_stats) {
+  SceneDev& S = R.S;
+  TraceArgs& A = R.A;
+  const int32_t F = R.F, fmax = R.fmax, npass = R.npass;
+  const uint64_t per = R.per;
+  const bool ext = R.ext;
+  const uint32_t iters = R.iters;
+  int rc = PRT_OK;
+  const uint32_t G = R.groups;
+  LaunchCfg L{c->stream, occ_for(c), 1};
+  auto gws = [&](uint32_t g) -> WaveState& { return g == 0 ? c->ws : c->grp[g - 1].ws; };
+  auto gcfg = [&](uint32_t g) { return LaunchCfg{g == 0 ? c->stream : c->grp[g - 1].stream, L.occ, G}; };
   // the call's own events (prt_stats ms / ms_trace) only with stats: each record is a gap between kernels
   if (want_stats) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-  rc = ensure_wave(c, (uint32_t)(per * (uint64_t)F0), p->bounces, ext);
-  if (rc) return rc;
   // PRT_TAIL=0 switches the cooperative traversal tail off (prt_persist.h; A/B runs only)
   const char* et = std::getenv("PRT_TAIL");
-  c->wb.coop_tail = (et && std::atoi(et) == 0) ? 0 : 1;
-  c->wb.tl = nullptr;
+  const int32_t coop = (et && std::atoi(et) == 0) ? 0 : 1;
   // per-launch traversal timers (HIP events around every k_trace launch) with stats, unless
-  // PRT_LAUNCH_TIMERS=0: each event record costs a few us between kernels (one-pass calls only)
+  // PRT_LAUNCH_TIMERS=0: each event record costs a few us between kernels (one-pass, one-group calls only)
   const char* elt = std::getenv("PRT_LAUNCH_TIMERS");
-  const bool timers = want_stats && npass == 1 && !(elt && std::strcmp(elt, "0") == 0);
+  const bool timers = want_stats && npass == 1 && G == 1 && !(elt && std::strcmp(elt, "0") == 0);
+  unsigned long long* tl = nullptr;
   if (want_stats && std::getenv("PRT_DEBUG_QUEUES")) {
     const size_t tlb = 32ull * kTlWaves * (kMaxIters + 2);
     HIP_TRY(c->tl.ensure(tlb));
     HIP_TRY(hipMemsetAsync(c->tl.p, 0, tlb, c->stream));
-    c->wb.tl = c->tl.as<unsigned long long>();
+    tl = c->tl.as<unsigned long long>();
   }
   c->carry_segments = c->carry_shadow = 0;
   const bool post = c->pfx.enabled && !tiles_dev && rgb8_dev && F > 0;
@@ -502,21 +698,37 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     const bool last = pass == npass - 1;
     A.frame_index = p->frame_index + f0;
     A.frames = Fb;
-    if (npass > 1) {
-      rc = ensure_wave(c, (uint32_t)(per * (uint64_t)Fb), p->bounces, ext);
-      if (rc) return rc;
-    }
-    {  // the queue counters and the fetch counters of the iterations this call uses (kMaxIters is the capacity)
-      const size_t qw = (size_t)(iters + 2) * 2 * kNSub * kCtrStride;
-      const size_t fbase = (size_t)(kMaxIters + 2) * 2 * kNSub * kCtrStride;
-      const size_t fw = (size_t)(iters + 2) * 2 * kParts * kCtrStride;
-      HIP_TRY(launch_clear2(L, c->wb.ctr, (uint32_t)qw, c->wb.ctr + fbase, (uint32_t)fw));
-    }
-    if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(c->wb.dst, 0, 4ull * c->wb.n, c->stream));
+    const uint64_t nb = per * (uint64_t)Fb;  // this pass's items, cut into G contiguous ranges
     float4* frames = c->frames.as<float4>();
-    HIP_TRY(launch_wave_init(L, S, A, M, c->wb, frames));
+    if (G > 1) {  // the groups' streams start after everything already on the context stream
+      HIP_TRY(hipEventRecord(c->fork, c->stream));
+      for (uint32_t g = 1; g < G; g++) HIP_TRY(hipStreamWaitEvent(gcfg(g).stream, c->fork, 0));
+    }
+    for (uint32_t g = 0; g < G; g++) {
+      WaveState& w = gws(g);
+      const LaunchCfg Lg = gcfg(g);
+      const uint32_t b0 = (uint32_t)(nb * g / G), b1 = (uint32_t)(nb * (g + 1) / G);
+      rc = ensure_wave(w, b1 - b0, p->bounces, ext);  // no allocation: prepare_render sized it for pass 0
+      if (rc) return rc;
+      w.wb.base = b0;
+      w.wb.coop_tail = coop;
+      w.wb.tl = g == 0 ? tl : nullptr;
+      {  // the queue counters and the fetch counters of the iterations this call uses (kMaxIters is the capacity)
+        const size_t qw = (size_t)(iters + 2) * 2 * kNSub * kCtrStride;
+        const size_t fbase = (size_t)(kMaxIters + 2) * 2 * kNSub * kCtrStride;
+        const size_t fw = (size_t)(iters + 2) * 2 * kParts * kCtrStride;
+        HIP_TRY(launch_clear2(Lg, w.wb.ctr, (uint32_t)qw, w.wb.ctr + fbase, (uint32_t)fw));
+      }
+      if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(w.wb.dst, 0, 4ull * w.wb.n, Lg.stream));
+      HIP_TRY(launch_wave_init(Lg, S, A, M, w.wb, frames + b0));
+    }
     for (uint32_t it = 0; it <= iters; it++)
-      HIP_TRY(launch_wave2_iter(L, S, A, M, c->wb, frames, timers ? &c->wt : nullptr, it));
+      for (uint32_t g = 0; g < G; g++)
+        HIP_TRY(launch_wave2_iter(gcfg(g), S, A, M, gws(g).wb, frames + gws(g).wb.base, timers ? &c->wt : nullptr, it));
+    for (uint32_t g = 1; g < G; g++) {  // join: the accumulation reads every group's frame values
+      HIP_TRY(hipEventRecord(c->grp[g - 1].done, gcfg(g).stream));
+      HIP_TRY(hipStreamWaitEvent(c->stream, c->grp[g - 1].done, 0));
+    }
     if (last && want_stats) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     // post-processing (single-GPU image): the screen pass needs the average and, for the aberration, the
     // accumulator before the last frame
@@ -528,16 +740,17 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
     }
     HIP_TRY(launch_accumulate(L, M, Fb, p->flags, frames, c->acc.as<float4>(), c->nsamp.as<int32_t>(),
                               c->dist.as<float>(), avg_dev, post ? nullptr : rgb8_dev, tiles_dev, acc_prev,
-                              c->wb.ctr, iters, ray_totals_dev(c)));
+                              c->ws.wb.ctr, iters, ray_totals_dev(c)));
+    for (uint32_t g = 1; g < G; g++) HIP_TRY(launch_add_totals(L, gws(g).wb.ctr, iters, ray_totals_dev(c)));
     if (post && last) {
       // with !accumulates the accumulator held this frame's value until the end-of-frame memset
       const float4* acc_new = (p->flags & PRT_FLAG_ACCUMULATE) ? c->acc.as<float4>() : avg_dev;
       HIP_TRY(launch_postfx(L, post_params(c, p->width, p->height), acc_new, acc_prev, c->nsamp.as<int32_t>(),
                             avg_dev, rgb8_dev));
     }
-    if (want_stats && !last) {  // this pass's ray counts, before the next pass clears the counters
+    if (want_stats && !last) {  // this pass's ray counts, before the next pass clears the counters (G == 1)
       std::vector<uint32_t> ctr((size_t)(iters + 2) * 2 * kNSub * kCtrStride);
-      HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipMemcpyAsync(ctr.data(), c->ws.wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
       for (uint32_t k = 0; k < iters; k++)
         for (uint32_t s2 = 0; s2 < kNSub; s2++) {
@@ -549,8 +762,17 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
   if (want_stats) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   c->last_iters = iters;
   c->last_timers = timers;
+  c->last_groups = G;
   c->last_paths = tile_image_pixels(M) * (uint64_t)F * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
-  return PRT_OK;
+  return check_layout_once(c);
+}
+
+int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4* avg_dev, uint32_t* rgb8_dev,
+               float4* tiles_dev, bool want_stats, int32_t rank = 0) {
+  RenderPlan R;
+  const int rc = prepare_render(c, p, M, rank, R);
+  if (rc) return rc;
+  return enqueue_render(c, p, M, R, avg_dev, rgb8_dev, tiles_dev, want_stats);
 }
 
 // the context's traversal stack overflow count (SceneDev::diag[0]); waits for the context stream.  diag[1] != 0:
@@ -566,6 +788,10 @@ uint64_t diag_overflows(prt_ctx* c, bool* layout_ok = nullptr) {
 
 // waits for the last render of run_render(..., want_stats = true) and fills its stats
 int read_stats(prt_ctx* c, prt_stats* stats) {
+#ifdef PRT_LANE_STATS
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  lane_stats_dump();
+#endif
   const uint32_t iters = c->last_iters;
   const bool timers = c->last_timers;
   {
@@ -574,7 +800,14 @@ int read_stats(prt_ctx* c, prt_stats* stats) {
     const bool dump = std::getenv("PRT_DEBUG_QUEUES") != nullptr;
     // the queue counters of the iterations this render used (the whole array with the queue dump)
     std::vector<uint32_t> ctr(dump ? kCtrWords : (size_t)(iters + 2) * 2 * kNSub * kCtrStride);
-    HIP_TRY(hipMemcpyAsync(ctr.data(), c->wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(ctr.data(), c->ws.wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
+    // concurrent item groups: their queue counters add up (the render joined them into the context stream)
+    std::vector<uint32_t> gctr(ctr.size());
+    for (uint32_t g = 1; g < c->last_groups && g <= c->grp.size(); g++) {
+      HIP_TRY(hipMemcpyAsync(gctr.data(), c->grp[g - 1].ws.wb.ctr, 4 * gctr.size(), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      for (size_t i = 0; i < ctr.size(); i++) ctr[i] += gctr[i];
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     const WaveTimers& wt = c->wt;
     for (uint32_t k = 0; k <= iters; k++) {
@@ -592,7 +825,7 @@ int read_stats(prt_ctx* c, prt_stats* stats) {
         std::fprintf(stderr, "prt: iteration %u: %llu closest rays, %llu shadow rays; trace launch %.3f ms\n", k,
                      (unsigned long long)qs, (unsigned long long)qa, a);
     }
-    if (dump && c->wb.tl) {  // launch timeline: start -> queue drained -> last wave out (us)
+    if (dump && c->ws.wb.tl) {  // launch timeline: start -> queue drained -> last wave out (us)
       std::vector<unsigned long long> t(4ull * kTlWaves * (kMaxIters + 2));
       HIP_TRY(hipMemcpy(t.data(), c->tl.p, 8 * t.size(), hipMemcpyDeviceToHost));
       for (uint32_t k = 0; k <= iters; k++) {
@@ -664,6 +897,41 @@ int read_stats(prt_ctx* c, prt_stats* stats) {
   return PRT_OK;
 }
 
+// A rank whose part of a frame failed still posts its part of the frame's ncclGather (zeros), so its peers are
+// never left blocked in the collective.  The send buffer is the tile buffer, or (if that could not be allocated)
+// any context buffer large enough; root's receive buffer likewise.  With no such buffer the rank aborts its
+// communicator: the peers' collective then fails through RCCL instead of completing.
+void post_zero_gather(prt_ctx* c, size_t per) {
+  const std::string why = g_err;  // the error being reported
+  const Rccl* R = rccl(nullptr);
+  if (!R || !c->comm) { g_err = why; return; }
+  (void)hipSetDevice(c->device);
+  (void)hipGetLastError();
+  const bool root = c->sh_rank == 0;
+  const size_t sb = per * sizeof(float4), rb = (size_t)c->sh_world * sb;
+  auto pick = [&](DevBuf& pref, size_t bytes, DevBuf* avoid) -> void* {
+    if (pref.bytes >= bytes || pref.ensure(bytes) == hipSuccess) return pref.p;
+    for (DevBuf* b : {&c->ws.wave, &c->frames, &c->shtiles, &c->gathered, &c->avg})
+      if (b != avoid && b->bytes >= bytes) return b->p;
+    return nullptr;
+  };
+  void* send = pick(c->shtiles, sb, nullptr);
+  void* recv = nullptr;
+  if (root && send) {
+    DevBuf* sendb = nullptr;
+    for (DevBuf* b : {&c->shtiles, &c->ws.wave, &c->frames, &c->gathered, &c->avg})
+      if (b->p == send) sendb = b;
+    recv = pick(c->gathered, rb, sendb);
+  }
+  if (send && (!root || recv) && hipMemsetAsync(send, 0, sb, c->stream) == hipSuccess) {
+    (void)R->Gather(send, recv, per * 4, ncclFloat32, 0, c->comm, c->stream);
+  } else if (R->CommAbort) {
+    (void)R->CommAbort(c->comm);
+    c->comm = nullptr;  // unusable from here on: later sharded frames fail up front
+  }
+  g_err = why;
+}
+
 // Sharded frame: every rank renders its tiles into shtiles, rank 0 gathers [world][per] and untiles.
 // RCCL: one ncclGather per frame on this rank's stream.  Local group: each member renders on its own stream
 // and copies its tile buffer into member 0's gathered buffer (peer copy over xGMI across devices); member 0
@@ -677,38 +945,55 @@ int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint
   std::vector<prt_ctx*> all{c};
   all.insert(all.end(), c->members.begin(), c->members.end());
   const bool root = c->sh_rank == 0;
-  for (size_t k = 0; k < all.size(); k++) {
-    prt_ctx* m = all[k];
-    const int32_t rank = c->sh_kind == 2 ? (int32_t)k : c->sh_rank;
-    HIP_TRY(hipSetDevice(m->device));
-    HIP_TRY(m->shtiles.ensure(per * sizeof(float4)));
-    const TileMap M = make_tilemap(W, H, ts, rank, world);
-    if (per > M.items)  // the tail of a shorter rank's buffer
-      HIP_TRY(hipMemsetAsync(m->shtiles.as<float4>() + M.items, 0, sizeof(float4) * (per - M.items), m->stream));
-    int rc = run_render(m, p, M, nullptr, nullptr, m->shtiles.as<float4>(), stats != nullptr);
-    if (rc) {
-      // RCCL: the other ranks are already (or soon) inside this frame's ncclGather; post this rank's part
-      // (zeros) anyway so they complete, then report the local error
-      if (c->sh_kind == 1) {
-        const std::string why = g_err;
-        const Rccl* R = rccl(nullptr);
-        if (R && hipMemsetAsync(c->shtiles.p, 0, per * sizeof(float4), c->stream) == hipSuccess) {
-          float4* g = nullptr;
-          if (root && c->gathered.ensure((size_t)world * per * sizeof(float4)) == hipSuccess) g = c->gathered.as<float4>();
-          if (!root || g) (void)R->Gather(c->shtiles.p, g, per * 4, ncclFloat32, 0, c->comm, c->stream);
-        }
-        g_err = why;
-      }
-      return rc;
+  const bool coll = c->sh_kind == 1;  // RCCL: the peers of this rank meet it in this frame's ncclGather
+  if (coll && !c->comm) return fail(PRT_ERR_HIP, "the RCCL communicator was aborted by an earlier failed frame");
+  const Rccl* R = coll ? rccl(nullptr) : nullptr;
+  // 1. everything that can fail, on every member, before any render work is enqueued: a failure leaves every
+  //    member's accumulation state as it was (the next frame is the one the failed call would have been)
+  std::vector<RenderPlan> plans(all.size());
+  auto prepare_all = [&]() -> int {
+    for (size_t k = 0; k < all.size(); k++) {
+      prt_ctx* m = all[k];
+      const int32_t rank = c->sh_kind == 2 ? (int32_t)k : c->sh_rank;
+      HIP_TRY(hipSetDevice(m->device));
+      HIP_TRY(m->shtiles.ensure(per * sizeof(float4)));
+      const int rc = prepare_render(m, p, make_tilemap(W, H, ts, rank, world), rank, plans[k]);
+      if (rc) return rc;
     }
+    HIP_TRY(hipSetDevice(c->device));
+    if (root) HIP_TRY(c->gathered.ensure((size_t)world * per * sizeof(float4)));
+    if (coll && !R) {
+      const char* why = "RCCL not loaded";
+      (void)rccl(&why);
+      return fail(PRT_ERR_UNSUPPORTED, why);
+    }
+    return PRT_OK;
+  };
+  // 2. the renders
+  auto enqueue_all = [&]() -> int {
+    for (size_t k = 0; k < all.size(); k++) {
+      prt_ctx* m = all[k];
+      const int32_t rank = c->sh_kind == 2 ? (int32_t)k : c->sh_rank;
+      HIP_TRY(hipSetDevice(m->device));
+      const TileMap M = make_tilemap(W, H, ts, rank, world);
+      if (per > M.items)  // the tail of a shorter rank's buffer
+        HIP_TRY(hipMemsetAsync(m->shtiles.as<float4>() + M.items, 0, sizeof(float4) * (per - M.items), m->stream));
+      const int rc = enqueue_render(m, p, M, plans[k], nullptr, nullptr, m->shtiles.as<float4>(), stats != nullptr);
+      if (rc) return rc;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    return PRT_OK;
+  };
+  int rc = prepare_all();
+  if (!rc) rc = enqueue_all();
+  if (rc) {
+    // RCCL: the other ranks are already (or soon) inside this frame's ncclGather; post this rank's part (zeros)
+    // so they complete, then report the local error
+    if (coll) post_zero_gather(c, per);
+    return rc;
   }
-  HIP_TRY(hipSetDevice(c->device));
-  if (root) HIP_TRY(c->gathered.ensure((size_t)world * per * sizeof(float4)));
   float4* g = root ? c->gathered.as<float4>() : nullptr;
-  if (c->sh_kind == 1) {
-    const char* why = nullptr;
-    const Rccl* R = rccl(&why);
-    if (!R) return fail(PRT_ERR_UNSUPPORTED, why);
+  if (coll) {
     const ncclResult_t r = R->Gather(c->shtiles.p, g, per * 4, ncclFloat32, 0, c->comm, c->stream);
     if (r != ncclSuccess) return fail(PRT_ERR_HIP, std::string("ncclGather: ") + R->GetErrorString(r));
   } else {
@@ -748,6 +1033,8 @@ int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint
         sum.ms = std::max(sum.ms, st.ms);
         sum.ms_trace = std::max(sum.ms_trace, st.ms_trace);
         sum.ms_closest += st.ms_closest;
+        sum.stack_overflows = (sum.stack_overflows == ~0ull || st.stack_overflows == ~0ull)
+                                  ? ~0ull : sum.stack_overflows + st.stack_overflows;  // ~0: unreadable
       }
     }
     sum.ranks = (int32_t)all.size();
@@ -856,6 +1143,16 @@ int prt_destroy(prt_ctx* c) {
   }
   c->comm = nullptr;
   if (c->sh_ev) (void)hipEventDestroy(c->sh_ev);
+  for (ItemGroup& g : c->grp) {
+    if (g.stream) (void)hipStreamSynchronize(g.stream);
+    if (g.done) (void)hipEventDestroy(g.done);
+    if (g.stream) (void)hipStreamDestroy(g.stream);
+  }
+  c->grp.clear();
+  if (c->fork) (void)hipEventDestroy(c->fork);
+  for (auto e : c->tlas_cost_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->tlas_cost_h) (void)hipHostFree(c->tlas_cost_h);
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto e : c->wt.ev)
@@ -1225,9 +1522,12 @@ int prt_ray_totals(prt_ctx* c, uint64_t* segments, uint64_t* shadow_rays, int32_
   for (prt_ctx* m : all) {
     HIP_TRY(hipSetDevice(m->device));
     Counters h{};
+    uint32_t dg[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(&h, ray_totals_dev(m), sizeof(h), hipMemcpyDeviceToHost, m->stream));
+    HIP_TRY(hipMemcpyAsync(dg, m->diag.p, 8, hipMemcpyDeviceToHost, m->stream));
     if (reset) HIP_TRY(hipMemsetAsync(ray_totals_dev(m), 0, sizeof(Counters), m->stream));
     HIP_TRY(hipStreamSynchronize(m->stream));
+    if (dg[1] != 0) return fail(PRT_ERR_HIP, "k_shade2: kernel-argument layout check failed (Shade2Args)");
     seg += h.segments;
     sh += h.shadow;
   }
@@ -1364,7 +1664,7 @@ int prt_render_tiles(prt_ctx* c, const prt_render_params* p, int32_t ts, int32_t
   if (M0.items > M.items)  // pad the tail of the (equal-size) per-rank buffer
     HIP_TRY(hipMemsetAsync(reinterpret_cast<float4*>(tiles_dev) + M.items, 0, sizeof(float4) * (M0.items - M.items),
                            c->stream));
-  rc = run_render(c, p, M, nullptr, nullptr, reinterpret_cast<float4*>(tiles_dev), stats != nullptr);
+  rc = run_render(c, p, M, nullptr, nullptr, reinterpret_cast<float4*>(tiles_dev), stats != nullptr, rank);
   if (!rc && stats) rc = read_stats(c, stats);
   return rc;
 }
@@ -1573,6 +1873,8 @@ int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
   }
   info->max_depth = c->max_depth;
   info->tlas_depth = c->use_tlas ? c->tlas_depth : 0;
+  info->tlas_rebuilds = c->tlas_rebuilds;
+  info->tlas_refits = c->tlas_refits;
   info->build_ms = c->build_ms;
   info->builder = c->built_with;
   info->device_bytes = (int64_t)(c->nodes8.bytes + c->tris.bytes + c->stri.bytes + c->texels.bytes + c->sky.bytes +

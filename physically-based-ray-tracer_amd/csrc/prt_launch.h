@@ -18,6 +18,8 @@ struct HitOut {
 struct LaunchCfg {
   hipStream_t stream;
   int occ;     // persistent traversal waves/SIMD: 8 / 7 / 6 / 5 / 4 (8 / 9 / 11 / 14 / 18 LDS stack groups)
+  uint32_t groups = 1;  // concurrent item groups of the call: every wavefront grid is 1/groups of the resident
+                        // blocks, so the groups' launch chains co-reside on the SIMDs (prt_api.cpp)
 };
 
 // wavefront pipeline buffers (SoA over n work items; R/T hold (bounces-1) x n entries)
@@ -62,6 +64,9 @@ struct WaveBufs {
 };
 constexpr uint32_t kParts = 8;  // XCD parts of a traversal launch's live range, one fetch counter each (prt_queue.h)
 constexpr int kMaxIters = 128;  // wavefront iterations per call: bounces <= 64 (AA) / 6 with dielectrics (AA)
+#ifdef PRT_LANE_STATS
+void lane_stats_dump();  // diagnostic build: prints and clears the traversal lane counters (prt_wave2.hip)
+#endif
 // wavefront iterations of one call: one per path segment, paths x bounces; with dielectric instances a path
 // is a binary tree walked depth first (one segment per iteration), at most 2^bounces - 1 segments per path
 inline uint32_t wave_iters(bool dielectric, int bounces, uint32_t flags) {
@@ -83,6 +88,8 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
                              const WaveBufs& B, float4* out, WaveTimers* tm, uint32_t it);
 // zero na words at a and nb words at b (one dispatch)
 hipError_t launch_clear2(const LaunchCfg& c, uint32_t* a, uint32_t na, uint32_t* b, uint32_t nb);
+// one concurrent item group's ray counts (queue counters ctr of `iters` iterations) added to totals
+hipError_t launch_add_totals(const LaunchCfg& c, const uint32_t* ctr, uint32_t iters, Counters* totals);
 // acc_prev (nullable): the accumulator state before the last frame of the call (screen-pass input);
 // totals (nullable): running ray totals, incremented by the queue counters ctr of the pass's `iters` iterations
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,

@@ -250,6 +250,11 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
 #ifdef PRT_DRAIN_POLL
   uint32_t iter_no = 0;
 #endif
+#ifdef PRT_LANE_STATS  // diagnostic build: per-wave counters of how the lanes of each loop iteration are used,
+                       // added to dbg[0..31] when the wave leaves (k_trace2: one 32-counter row per launch)
+  uint32_t lst[32] = {};
+  lst[31] = 1;
+#endif
   while (true) {
     // ---- refill idle lanes from the queue
     const uint64_t idle = __ballot(!active);
@@ -283,6 +288,17 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       continue;
     }
     if (tail && drained && __popcll(act) <= (uint32_t)TAILN) break;  // cooperative tail below
+#ifdef PRT_LANE_STATS
+    {
+      const uint32_t nn = (uint32_t)__popcll(__ballot(active && node != kNoNode && lhit == 0));
+      const uint32_t nt = (uint32_t)__popcll(__ballot(active && (lhit | tcnt)));
+      const uint32_t nd = (uint32_t)__popcll(__ballot(active && node == kNoNode && lhit == 0 && tcnt == 0));
+      lst[0]++; lst[1] += (uint32_t)__popcll(act); lst[2] += nn; lst[3] += nt;
+      lst[4] += nn ? 1u : 0u; lst[5] += nt ? 1u : 0u; lst[6] += (nn && nt) ? 1u : 0u; lst[7] += nd ? 1u : 0u;
+      lst[8 + (nn + 7) / 8]++;
+      lst[17 + (nt + 7) / 8]++;
+    }
+#endif
     // ---- BLAS done: next instance, or the ray is finished
     if (active && node == kNoNode && lhit == 0 && tcnt == 0) {
       bool more = false;
@@ -310,7 +326,16 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       }
     }
   }
+#ifdef PRT_LANE_STATS
+  auto flush_stats = [&]() {
+    if (dbg && lane == 0)
+      for (int k = 0; k < 32; k++)
+        if (lst[k]) atomicAdd(dbg + k, (unsigned long long)lst[k]);
+  };
+  if (__ballot(active) == 0) { flush_stats(); return; }
+#else
   if (__ballot(active) == 0) return;
+#endif
 
   if (tail) {
     // ---------------------------------------------------------------- cooperative tail
@@ -450,6 +475,13 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
         const unsigned long long k = tkey[slot];
         if (k != ~0ull) tlim = fminf(tlim, __uint_as_float((uint32_t)(k >> 32)));
       }
+#ifdef PRT_LANE_STATS
+      {
+        const uint32_t nn = (uint32_t)__popcll(__ballot(busy && node != kNoNode && lhit == 0 && tcnt == 0));
+        const uint32_t nt = (uint32_t)__popcll(__ballot(busy && (lhit | tcnt)));
+        lst[26]++; lst[27] += nn; lst[28] += nt; lst[29] += nn ? 1u : 0u; lst[30] += nt ? 1u : 0u;
+      }
+#endif
       if (busy && node != kNoNode && lhit == 0 && tcnt == 0) node_step(tlim);
       if (busy && (lhit | tcnt)) {
         const float t0 = h.t;
@@ -465,6 +497,9 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
              ((unsigned long long)(uint32_t)ts_t0 << 32);
 #endif
   }
+#ifdef PRT_LANE_STATS
+  flush_stats();
+#endif
 }
 
 template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, bool SPILL = false, class Fetch,

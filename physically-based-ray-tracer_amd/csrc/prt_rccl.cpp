@@ -37,6 +37,7 @@ void load() {
     g_why = "librccl.so.1 lacks a required entry point (ncclGather needs RCCL >= 2.18)";
     return;
   }
+  r.CommAbort = reinterpret_cast<ncclResult_t (*)(ncclComm_t)>(dlsym(h, "ncclCommAbort"));
   g_ok = &g_rccl;
 }
 

@@ -18,6 +18,7 @@ struct Rccl {
   ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*);
   ncclResult_t (*Gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
   const char* (*GetErrorString)(ncclResult_t);
+  ncclResult_t (*CommAbort)(ncclComm_t);  // optional (nullptr when the library lacks it)
 };
 
 // nullptr when RCCL cannot be loaded (the message is in *why)

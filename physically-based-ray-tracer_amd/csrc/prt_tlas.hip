@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "bvh_build.h"
+#include "bvh_gpu.h"
 #include "prt_tlas.h"
 
 namespace prt {
@@ -89,7 +90,95 @@ __global__ void k_tlas_refit(const InstDev* __restrict__ inst, const uint32_t* _
   for (int a = 0; a < 3; a++) { b[a] = nlo[a]; b[3 + a] = nhi[a]; }
 }
 
+// ---- device rebuild of the topology: the instances' current world boxes through the device BLAS
+// builder (bvh_gpu.hip: PLOC + SAH-optimal 8-wide collapse, one instance per leaf slot), converted to the
+// instance-BVH form exactly as the host's build_tlas8 converts its BLAS-form tree
+
+// instance i's inflated world box as the degenerate "triangle" {lo, hi, lo} (bvh_build.cpp build_tlas8)
+__global__ void k_inst_fat(const InstDev* __restrict__ inst, int32_t n, float4* __restrict__ fat) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const InstDev& I = inst[i];
+  const float4 lo = make_float4(I.bmin[0], I.bmin[1], I.bmin[2], 0.0f), hi = make_float4(I.bmax[0], I.bmax[1], I.bmax[2], 0.0f);
+  fat[3 * (size_t)i] = lo;
+  fat[3 * (size_t)i + 1] = hi;
+  fat[3 * (size_t)i + 2] = lo;
+}
+
+// leaf slot s of node j -> the instance it holds (slot[8j + s]); tri_base = 8j (build_tlas8's conversion)
+__global__ void k_tlas_slots(Node8* __restrict__ nodes, uint32_t n_nodes, const TriMT* __restrict__ tris,
+                             uint32_t* __restrict__ slot) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_nodes) return;
+  Node8& nd = nodes[j];
+  for (uint32_t s = 0; s < 8; s++)
+    slot[8 * (size_t)j + s] = (!((nd.imask >> s) & 1u) && nd.meta[s]) ? tris[nd.tri_base + (nd.meta[s] >> 3)].prim
+                                                                        : 0xFFFFFFFFu;
+  nd.tri_base = 8u * j;
+}
+
+__device__ __forceinline__ double box_area(const float* lo, const float* hi) {
+  const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+  return (dx < 0 || dy < 0 || dz < 0) ? 0.0 : 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+// the tree's SAH cost (node-visit + instance-test cost per unit root area) over the boxes the last refit left in
+// aabb and the instances' current boxes: one block
+__global__ void __launch_bounds__(1024) k_tlas_cost(const Node8* __restrict__ nodes, uint32_t n_nodes,
+                                                    const float* __restrict__ aabb, const InstDev* __restrict__ inst,
+                                                    const uint32_t* __restrict__ slot, double* __restrict__ out) {
+  __shared__ double red[1024];
+  double acc = 0.0;
+  for (uint32_t j = threadIdx.x; j < n_nodes; j += blockDim.x) {
+    const float* b = aabb + 6 * (size_t)j;
+    acc += box_area(b, b + 3);
+    for (uint32_t s = 0; s < 8; s++) {
+      const uint32_t id = slot[8 * (size_t)j + s];
+      if (id != 0xFFFFFFFFu) acc += box_area(inst[id].bmin, inst[id].bmax);
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (uint32_t w = blockDim.x / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double root = box_area(aabb, aabb + 3);
+    out[0] = root > 0 ? red[0] / root : 0.0;
+  }
+}
+
 }  // namespace
+
+hipError_t gpu_build_tlas8(hipStream_t s, const InstDev* inst, int32_t n, float* fat, TriMT* tris, Node8* nodes,
+                           uint32_t* slot, TlasTopo* T, int* depth, uint32_t* n_nodes) {
+  if (n <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_inst_fat, dim3((n + 255) / 256), dim3(256), 0, s, inst, n, reinterpret_cast<float4*>(fat));
+  GpuBlasInfo gi{};
+  std::vector<uint32_t> ends;
+  hipError_t e = gpu_build_blas8(s, fat, n, 1, nodes, tris, &gi, true, &ends);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_tlas_slots, dim3((gi.nodes + 255) / 256), dim3(256), 0, s, nodes, gi.nodes, tris, slot);
+  // the collapse emits level by level: the refit order is the identity, levels deepest first
+  T->order.resize(gi.nodes);
+  for (uint32_t i = 0; i < gi.nodes; i++) T->order[i] = i;
+  T->level_off.clear();
+  T->level_cnt.clear();
+  for (size_t l = ends.size(); l-- > 0;) {
+    const uint32_t b = l == 0 ? 0u : ends[l - 1];
+    T->level_off.push_back(b);
+    T->level_cnt.push_back(ends[l] - b);
+  }
+  *depth = gi.depth;
+  *n_nodes = gi.nodes;
+  return hipGetLastError();
+}
+
+hipError_t launch_tlas_cost(hipStream_t s, const Node8* nodes, uint32_t n_nodes, const float* aabb,
+                            const InstDev* inst, const uint32_t* slot, double* out) {
+  hipLaunchKernelGGL(k_tlas_cost, dim3(1), dim3(1024), 0, s, nodes, n_nodes, aabb, inst, slot, out);
+  return hipGetLastError();
+}
 
 TlasTopo tlas_topology(const std::vector<Node8>& nodes) {
   // depth of every node from the root (node 0): interior children sit at child_base + rank among the interior slots

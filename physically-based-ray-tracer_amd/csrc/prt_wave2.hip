@@ -25,12 +25,31 @@
 // S(i) reuses S(i-1)'s buffer after k_trace2(i) read it; k_resmiss2(i) reads ne/nb/nk/vis/R/T of an item for
 // iteration i-1 before it (misses) or k_shade2(i) (hits) overwrites them; rinfo keeps iteration i-1's status
 // (and whether the item was queued) while info already holds the state of the queued next ray.
+#include <cstdio>
+
 #include "prt_launch.h"
 #include "prt_path.h"
 #include "prt_persist.h"
 #include "prt_queue.h"
 
 namespace prt {
+
+#ifdef PRT_LANE_STATS  // diagnostic build: prt_persist.h lane counters, one 32-counter row per traversal launch
+__device__ unsigned long long g_lane_stats[(kMaxIters + 2) * 32];
+void lane_stats_dump() {
+  static unsigned long long h[(kMaxIters + 2) * 32];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_lane_stats), sizeof(h)) != hipSuccess) return;
+  for (int i = 0; i < kMaxIters + 2; i++) {
+    const unsigned long long* r = h + 32 * i;
+    if (!r[31]) continue;
+    std::fprintf(stderr, "prt: lanestats %d", i);
+    for (int k = 0; k < 32; k++) std::fprintf(stderr, " %llu", r[k]);
+    std::fprintf(stderr, "\n");
+  }
+  static const unsigned long long z[(kMaxIters + 2) * 32] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lane_stats), z, sizeof(z));
+}
+#endif
 
 // ---- init: items -> primary rays, appended to queue 0 (sub-queue = block % kNSub)
 __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, TileMap M, WaveBufs B,
@@ -165,7 +184,11 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
         }
       },
       [&]() -> bool { return __hip_atomic_load(dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u; },
+#ifdef PRT_LANE_STATS
+      B.coop_tail ? tail_lds : nullptr, g_lane_stats + 32 * iter);
+#else
       B.coop_tail ? tail_lds : nullptr, tl ? tl + 3 : nullptr);
+#endif
   if (tl && threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -567,22 +590,22 @@ template <int STACK, int WAVES, int TAILN>
 void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
   static_assert(2 * STACK * 256 + 264 + 4 * 3 * TAILN <= 163840 / (4 * WAVES), "LDS over the occupancy budget");
   if (S.tlas)
-    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, true>), dim3(256u * 4u * WAVES), dim3(64), 0, c.stream, S, B,
-                       it, iters);
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, true>), dim3(256u * 4u * WAVES / c.groups), dim3(64), 0,
+                       c.stream, S, B, it, iters);
   else
-    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, false>), dim3(256u * 4u * WAVES), dim3(64), 0, c.stream, S,
-                       B, it, iters);
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, false>), dim3(256u * 4u * WAVES / c.groups), dim3(64), 0,
+                       c.stream, S, B, it, iters);
 }
 // persistent traversal occupancy (waves/SIMD) -> LDS stack groups per lane; a BVH deeper than the 18 LDS
 // groups at 4 waves/SIMD hold runs the 4-wave form with the HBM spill columns (S.spill)
 static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
   if (S.spill) {
     if (S.tlas)
-      hipLaunchKernelGGL((k_trace2<32, 18, 4, 32, true, true>), dim3(kSpillTraceBlocks), dim3(64), 0, c.stream, S, B,
-                         it, iters);
+      hipLaunchKernelGGL((k_trace2<32, 18, 4, 32, true, true>), dim3(kSpillTraceBlocks / c.groups), dim3(64), 0,
+                         c.stream, S, B, it, iters);
     else
-      hipLaunchKernelGGL((k_trace2<32, 18, 4, 32, false, true>), dim3(kSpillTraceBlocks), dim3(64), 0, c.stream, S,
-                         B, it, iters);
+      hipLaunchKernelGGL((k_trace2<32, 18, 4, 32, false, true>), dim3(kSpillTraceBlocks / c.groups), dim3(64), 0,
+                         c.stream, S, B, it, iters);
   } else if (c.occ == 8) launch_t2<8, 8, 32>(c, S, B, it, iters);
   else if (c.occ == 7) launch_t2<9, 7, 64>(c, S, B, it, iters);
   else if (c.occ == 6) launch_t2<11, 6, 64>(c, S, B, it, iters);
@@ -594,7 +617,7 @@ static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs&
 hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                              const WaveBufs& B, float4* out, WaveTimers* tm, uint32_t it) {
   if (B.n == 0) return hipSuccess;
-  const unsigned gprod = 256u * 4u;  // producer blocks (multiple of kNSub)
+  const unsigned gprod = 256u * 4u / c.groups;  // producer blocks (multiple of kNSub for groups <= 32)
   // k_shade2 over 4x the resident blocks when a call holds >= 2^21 items: the extra blocks queue behind the
   // resident ones and even out the kernel's end (C4 frame -1 to -2 %); below that the extra launch width costs
   // more than it evens out (world-8 shares). PRT_SHADE_GRID overrides (A/B runs).
@@ -639,7 +662,7 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
 
 hipError_t launch_wave_init(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                             const WaveBufs& B, float4* out) {
-  hipLaunchKernelGGL(k_wave_init, dim3(256u * 4u), dim3(kBlock), 0, c.stream, S, A, M, B, out);
+  hipLaunchKernelGGL(k_wave_init, dim3(256u * 4u / c.groups), dim3(kBlock), 0, c.stream, S, A, M, B, out);
   return hipGetLastError();
 }
 

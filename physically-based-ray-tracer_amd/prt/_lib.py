@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIBPATH = os.path.join(HERE, "libprt.so")
 
 PRT_OK = 0
-ABI_VERSION = 7  # PRT_ABI_VERSION of the include/prt.h these structs mirror
+ABI_VERSION = 8  # PRT_ABI_VERSION of the include/prt.h these structs mirror
 FLAG_AA, FLAG_ACCUMULATE, FLAG_GAMMA, FLAG_NORMALMAP, FLAG_SKYBOX, FLAG_LIGHTED, FLAG_STOCHASTIC = (1 << i for i in range(7))
 FLAGS_DEFAULT = 0x7F
 OUT_DEVICE = 1
@@ -101,7 +101,7 @@ class ShardInfo(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("blas_nodes", C.c_int64), ("blas_leaves", C.c_int64), ("device_bytes", C.c_int64),
                 ("max_depth", C.c_int32), ("triangles", C.c_int32), ("build_ms", C.c_double), ("builder", C.c_int32),
-                ("tlas_depth", C.c_int32)]
+                ("tlas_depth", C.c_int32), ("tlas_rebuilds", C.c_int32), ("tlas_refits", C.c_int32)]
 
 
 _lib = None

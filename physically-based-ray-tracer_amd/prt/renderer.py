@@ -404,12 +404,16 @@ class Renderer:
         """Checkpoint of a long progressive render: the accumulation state plus the frame counter and
         seed the RNG stream continues from, as an .npz of plain arrays (load with allow_pickle=False)."""
         blob = np.frombuffer(self.ctx.save_accumulation(), np.uint8)
-        np.savez(path, accumulation=blob, frame=np.int64(self.frame), seed=np.int64(self.seed),
-                 size=np.array([self.width, self.height], np.int64))
+        # through a file handle: np.savez(<str>) would append ".npz" to a path without it, and LoadCheckpoint(path)
+        # would then look for a file that does not exist
+        with open(path, "wb") as f:
+            np.savez(f, accumulation=blob, frame=np.int64(self.frame), seed=np.int64(self.seed),
+                     size=np.array([self.width, self.height], np.int64))
 
     def LoadCheckpoint(self, path):
         """Resume from SaveCheckpoint: the next Tick continues the same frame sequence bit for bit."""
-        z = np.load(path, allow_pickle=False)
+        with open(path, "rb") as f:
+            z = dict(np.load(f, allow_pickle=False))
         if tuple(int(v) for v in z["size"]) != (self.width, self.height):
             raise ValueError("checkpoint of another image size")
         self.ctx.load_accumulation(z["accumulation"].tobytes())

@@ -57,7 +57,7 @@ def test_renderer_checkpoint_files(tmp_path):
     try:
         r1.Tick()
         r1.Tick()
-        path = str(tmp_path / "ckpt.npz")
+        path = str(tmp_path / "ckpt")  # no .npz suffix: SaveCheckpoint / LoadCheckpoint use the path as given
         r1.SaveCheckpoint(path)
         r1.Tick()
         r2 = prt.Renderer(prt.Scene.from_data(sd), cam, W, H)

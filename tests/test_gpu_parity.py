@@ -512,3 +512,109 @@ def test_device_tlas_moving_instances(gpu_ctx, monkeypatch, n):
     gpu_ctx.set_instances(frames[-1].instances)
     a_h, r_h, _ = gpu_ctx.render(W, H, 2, 3, flags)
     assert np.array_equal(a_h, out[-1].cpu().numpy())
+
+
+def test_device_tlas_rebuild_long_motion(gpu_ctx, monkeypatch):
+    """1,000 tori drift across the field for 120 frames (every instance moves before every frame, the
+    frames queued back to back with device outputs and no host wait).  The refitted instance BVH degrades; once its
+    SAH cost (measured on the device after every refit, read back without a wait) exceeds 1.2x its cost after the
+    last build, the topology is rebuilt on the device (gpu_build_tlas8: PLOC + SAH-optimal collapse).  Every 10th
+    frame equals the oracle's render of that frame's transforms, and at least one device rebuild happened."""
+    import dataclasses
+    import torch
+    import prt
+    monkeypatch.delenv("PRT_TLAS_HOST", raising=False)
+    monkeypatch.delenv("PRT_TLAS_REBUILD", raising=False)
+    n, nframes = 1000, 120
+    sd0 = scenes.instance_field(n, seed=17)
+    W, H = 64, 48
+    flags = oracle.DEFAULT_FLAGS & ~oracle.ACCUMULATE
+    rng = np.random.default_rng(3)
+    vel = rng.uniform(-0.08, 0.08, (len(sd0.instances), 2)).astype(np.float32)
+    inst = [(m, np.array(T, np.float32)) for m, T in sd0.instances]
+    frames = []
+    for f in range(nframes):
+        moved = []
+        for i, (m, T) in enumerate(inst):
+            T = T.copy()
+            if m == 1:  # the tori drift (wrapping inside the field); the heightfield stays
+                for k, a in ((0, 0), (1, 2)):
+                    x = T[a, 3] + vel[i, k]
+                    T[a, 3] = np.float32(x - 9.0 if x > 4.5 else (x + 9.0 if x < -4.5 else x))
+            moved.append((m, T))
+        inst = moved
+        frames.append(dataclasses.replace(sd0, instances=list(inst)))
+    c = prt.Context(0)
+    try:
+        gpu_scene(c, sd0, W, H)
+        out = {}
+        rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        scratch = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+        for f, sd in enumerate(frames):
+            c.set_instances(sd.instances)
+            o = scratch
+            if f % 10 == 9:
+                o = out[f] = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+            c.render(W, H, 2, 3, flags, avg=o.data_ptr(), rgb8=rgb.data_ptr(), device_out=True, stats=False)
+        torch.cuda.synchronize()
+        si = c.scene_info()
+        assert si.tlas_rebuilds >= 1 and si.tlas_depth > 0, (si.tlas_rebuilds, si.tlas_refits)
+        for f, o in out.items():
+            a_o, _, _, _ = oracle.OracleScene(frames[f], W, H).render(W, H, spp=2, bounces=3, flags=flags)
+            assert np.array_equal(o.cpu().numpy(), a_o), f
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("groups", ["2", "4"])
+def test_item_groups_match_one_chain(gpu_ctx, monkeypatch, groups):
+    """Concurrent item groups (PRT_GROUPS, prt_api.cpp groups_for): the call's items cut into 2 / 4 contiguous
+    ranges, each with its own queues and launch chain on its own stream, grids 1/G of the resident blocks --
+    accumulating frames, ray counts (stats and the device totals) and a debug mode bit-identical to one chain."""
+    import prt
+    sd = scenes.multi_instance(scenes.config_small(60, 40))
+    W, H = 100, 70
+    monkeypatch.delenv("PRT_GROUPS", raising=False)
+    gpu_scene(gpu_ctx, sd, W, H)
+    ref = [gpu_ctx.render(W, H, 4, 3, frame_index=2 * i) for i in range(2)]
+    ref_dbg = gpu_ctx.render(W, H, 2, 2, mode=2)
+    c = prt.Context(0)
+    try:
+        monkeypatch.setenv("PRT_GROUPS", groups)
+        gpu_scene(c, sd, W, H)
+        c.ray_totals(reset=True)
+        for i, (ea, er, es) in enumerate(ref):
+            a, r, st = c.render(W, H, 4, 3, frame_index=2 * i)
+            assert np.array_equal(a, ea) and np.array_equal(r, er)
+            assert (st.segments, st.shadow_rays, st.paths) == (es.segments, es.shadow_rays, es.paths)
+        assert c.ray_totals() == (sum(e[2].segments for e in ref), sum(e[2].shadow_rays for e in ref))
+        a, r, _ = c.render(W, H, 2, 2, mode=2)
+        assert np.array_equal(a, ref_dbg[0]) and np.array_equal(r, ref_dbg[1])
+    finally:
+        c.close()
+
+
+def test_item_groups_world8_share_c4(gpu_ctx, monkeypatch):
+    """The world-8 share of the bench frame (C4 rank 0's 32x32 tiles, 4 spp, depth 4) with 2 and 4 concurrent item
+    groups equals the one-chain share bit for bit, with the same ray counts."""
+    import torch
+    import prt
+    sd = scenes.config_c4()
+    W, H, ts, world = 1920, 1080, 32, 8
+    monkeypatch.delenv("PRT_GROUPS", raising=False)
+    c = prt.Context(0)
+    try:
+        gpu_scene(c, sd, W, H)
+        per = c.tile_buffer_pixels(W, H, ts, world)
+        ref = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
+        s0 = c.render_tiles(W, H, 4, 4, ts, 0, world, ref.data_ptr(), stats=True)
+        for groups in ("2", "4"):
+            monkeypatch.setenv("PRT_GROUPS", groups)
+            c.reset_accumulation(full=True)
+            t = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
+            st = c.render_tiles(W, H, 4, 4, ts, 0, world, t.data_ptr(), stats=True)
+            torch.cuda.synchronize()
+            assert torch.equal(t, ref)
+            assert (st.segments, st.shadow_rays) == (s0.segments, s0.shadow_rays)
+    finally:
+        c.close()

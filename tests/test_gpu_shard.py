@@ -218,3 +218,66 @@ def test_rccl_world2_matches_single(gpu_ctx, tmp_path):
     z = np.load(out)
     assert np.array_equal(z["avg"], a_full) and np.array_equal(z["rgb"], r_full)
     assert tuple(int(x) for x in z["rays"]) == (s_full.segments, s_full.shadow_rays)
+
+
+def test_failed_group_frame_returns_error_and_next_frame_exact(gpu_ctx, monkeypatch):
+    """A member's render fails (PRT_FAIL_RENDER=<member>, raised in prepare_render before any render work is
+    enqueued): the group call returns the error, no member's accumulation advanced, and the next frames equal the
+    single-context frames of the same sequence without the failed call."""
+    import prt
+    sd = scenes.multi_instance(scenes.config_small(60, 40))
+    W, H, ts = 100, 70, 16
+    gpu_scene(gpu_ctx, sd, W, H)
+    a1, r1, _ = gpu_ctx.render(W, H, 4, 3)
+    a2, r2, _ = gpu_ctx.render(W, H, 4, 3, frame_index=2)  # accumulating
+    g = prt.Context(group=[0] * 3, tile=ts)
+    try:
+        gpu_scene(g, sd, W, H)
+        a, r, _ = g.render(W, H, 4, 3)
+        assert np.array_equal(a, a1) and np.array_equal(r, r1)
+        monkeypatch.setenv("PRT_FAIL_RENDER", "2")
+        with pytest.raises(prt.PrtError, match="injected"):
+            g.render(W, H, 4, 3, frame_index=2)
+        monkeypatch.delenv("PRT_FAIL_RENDER")
+        a, r, _ = g.render(W, H, 4, 3, frame_index=2)
+        assert np.array_equal(a, a2) and np.array_equal(r, r2)
+    finally:
+        g.close()
+
+
+def test_failed_rccl_frame_posts_gather_and_next_frame_exact(gpu_ctx, monkeypatch):
+    """RCCL world 1: the failing rank still posts its (zero) part of the frame's ncclGather (post_zero_gather,
+    so peers never block), returns the error, and the next frame is exact."""
+    import prt
+    sd = scenes.multi_instance(scenes.config_small(50, 40))
+    W, H = 90, 60
+    gpu_scene(gpu_ctx, sd, W, H)
+    a1, r1, _ = gpu_ctx.render(W, H, 4, 3)
+    a2, r2, _ = gpu_ctx.render(W, H, 4, 3, frame_index=2)
+    c = prt.Context(0)
+    try:
+        c.shard_rccl(prt.Context.shard_unique_id(), 0, 1, 32)
+        gpu_scene(c, sd, W, H)
+        a, r, _ = c.render(W, H, 4, 3)
+        assert np.array_equal(a, a1) and np.array_equal(r, r1)
+        monkeypatch.setenv("PRT_FAIL_RENDER", "0")
+        with pytest.raises(prt.PrtError, match="injected"):
+            c.render(W, H, 4, 3, frame_index=2)
+        monkeypatch.delenv("PRT_FAIL_RENDER")
+        a, r, st = c.render(W, H, 4, 3, frame_index=2)  # the zero gather completed: the stream is not stuck
+        assert np.array_equal(a, a2) and np.array_equal(r, r2)
+        assert st.stack_overflows == 0
+    finally:
+        c.close()
+
+
+def test_frame_above_pass_limit_refused(gpu_ctx):
+    """A frame (of one shard) above 2^27 pixels would overflow the 29-bit item field of the shadow-queue entries
+    (prt_wave2.hip kShIndexMask): refused with PRT_ERR_UNSUPPORTED before any allocation."""
+    import prt
+    sd = scenes.config_small(20, 20)
+    gpu_scene(gpu_ctx, sd, 64, 48)
+    with pytest.raises(prt.PrtError, match="2\\^27"):
+        gpu_ctx.render(16384, 16384, 2, 1, device_out=True, stats=False)  # no output buffers
+    a, _, _ = gpu_ctx.render(64, 48, 2, 2)  # the context is still usable
+    assert np.isfinite(a).all()
