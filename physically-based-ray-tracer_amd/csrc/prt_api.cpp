@@ -260,7 +260,8 @@ int ensure_instances(prt_ctx* c) {
   // a frame decides on the latest cost already available.  No host BVH work and no host wait per frame.
   const char* th = std::getenv("PRT_TLAS_HOST");
   const char* tr = std::getenv("PRT_TLAS_REBUILD");
-  const double rebuild_ratio = tr ? std::atof(tr) : 1.2;
+  const bool rebuild_always = tr && std::strcmp(tr, "always") == 0;  // A/B: a device rebuild for every update
+  const double rebuild_ratio = rebuild_always ? 0.0 : (tr ? std::atof(tr) : 1.2);
   auto upload_order = [&]() -> int {
     const size_t ob = 4 * c->tlas_topo.order.size(), ab = 24 * std::max<size_t>(c->tlas_nodes, 1);
     if (c->tlas_order.bytes < ob || c->tlas_aabb.bytes < ab) {
@@ -294,7 +295,7 @@ int ensure_instances(prt_ctx* c) {
     return PRT_OK;
   };
   if (c->use_tlas && c->tlas_n == n && !(th && std::atoi(th) == 1)) {
-    bool rebuild = false;
+    bool rebuild = rebuild_always;
     if (rebuild_ratio > 0) {
       for (int k = 0; k < 2; k++)  // costs whose copies have landed (never waits)
         if (c->tlas_cost_pending[k] && hipEventQuery(c->tlas_cost_ev[k]) == hipSuccess) {

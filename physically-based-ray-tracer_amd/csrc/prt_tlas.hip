@@ -121,21 +121,21 @@ __device__ __forceinline__ double box_area(const float* lo, const float* hi) {
   const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
   return (dx < 0 || dy < 0 || dz < 0) ? 0.0 : 2.0 * (dx * dy + dy * dz + dz * dx);
 }
-// the tree's SAH cost (node-visit + instance-test cost per unit root area) over the boxes the last refit left in
-// aabb and the instances' current boxes: one block
+// the tree's node-visit SAH cost (the sum of its nodes' areas per unit root area) over the boxes the last refit left
+// in aabb: one block
 __global__ void __launch_bounds__(1024) k_tlas_cost(const Node8* __restrict__ nodes, uint32_t n_nodes,
                                                     const float* __restrict__ aabb, const InstDev* __restrict__ inst,
                                                     const uint32_t* __restrict__ slot, double* __restrict__ out) {
   __shared__ double red[1024];
+  // the interior nodes' areas only: the leaf term (the instances' own boxes) does not change as instances move, so
+  // it would dilute the growth the refit causes
   double acc = 0.0;
   for (uint32_t j = threadIdx.x; j < n_nodes; j += blockDim.x) {
     const float* b = aabb + 6 * (size_t)j;
     acc += box_area(b, b + 3);
-    for (uint32_t s = 0; s < 8; s++) {
-      const uint32_t id = slot[8 * (size_t)j + s];
-      if (id != 0xFFFFFFFFu) acc += box_area(inst[id].bmin, inst[id].bmax);
-    }
   }
+  (void)inst;
+  (void)slot;
   red[threadIdx.x] = acc;
   __syncthreads();
   for (uint32_t w = blockDim.x / 2; w > 0; w >>= 1) {

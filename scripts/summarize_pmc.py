@@ -2,8 +2,7 @@
 """Summaries of the rocprofv3 --pmc passes behind bench.py's roofline (MI355X_MICROARCH.md, HBM / rocprofv3).
 
   valu <name> [dir]         gpurun_out/pmc_valu/run_counter_collection.csv (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU,
-                            SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, SQ_WAVES, GRBM_GUI_ACTIVE) -> profiles/<name>.json and
-                            profiles/valu_current.json: per-launch means per kernel, plus
+                            SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, SQ_WAVES, GRBM_GUI_ACTIVE) -> profiles/<name>.json: per-launch means per kernel, plus
                               valu_busy = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
                               (SQ_ACTIVE_INST_VALU counts quad-cycles; GRBM_GUI_ACTIVE is summed over the 8 XCDs)
   calib <name> [dir]        scripts/bin/fetch_calibration under FETCH_SIZE / WRITE_SIZE passes
@@ -68,7 +67,7 @@ def valu(name, src):
                 rec["clock_source"] = ns_src
         out["kernels"][k] = rec
     stamp(out, src)
-    for fn in (f"{name}.json", "valu_current.json"):
+    for fn in (f"{name}.json",):  # bench.py prices profiles/current_<scene>.json (scripts/summarize_session.py)
         with open(os.path.join(ROOT, "profiles", fn), "w") as f:
             json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))

@@ -6,7 +6,9 @@ HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZ
 FETCH_SIZE reports 1/2 of the bytes of 128-B requests (TCC_EA0_RDREQ x 64 B), so read bytes = 2 x 1024 x
 FETCH_SIZE; WRITE_SIZE is taken as 1024 x WRITE_SIZE.  Infinity-Cache hits are counted as fabric reads.
 
-usage: scripts/summarize_prof.py <name> [gpurun_out] [frames_in_pmc_pass]
+usage: scripts/summarize_prof.py <name> [gpurun_out]
+(Round 4: superseded by scripts/gpu_prof.sh + scripts/summarize_session.py, whose profiles/current_<scene>.json
+bench.py prices; this summariser is kept for the older gpu_check.sh 'prof' layout.)
 """
 import csv
 import json
@@ -43,7 +45,6 @@ def short(name):
 def main():
     name = sys.argv[1]
     src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out")
-    frames = int(sys.argv[3]) if len(sys.argv) > 3 else 3  # bench.py --steps 2 --warmup 1 in the PMC passes
     out = {"name": name, "kernels": {}}
     stats = os.path.join(src, "prof_stats", "run_kernel_stats.csv")
     for r in csv.DictReader(open(stats)):
@@ -61,12 +62,17 @@ def main():
             k = short(r["Kernel_Name"])
             agg.setdefault(k, {}).setdefault(r["Dispatch_Id"], 0.0)
             agg[k][r["Dispatch_Id"]] += float(r["Counter_Value"])
+        # frames in the pass = dispatches of k_wave_init (once per frame): a kernel's launches per frame are its
+        # dispatches over that count (round 3 divided by a fixed 3 and overstated k_trace2's bytes per frame 1.5x)
+        frames = next((len(v) for k2, v in agg.items() if k2.endswith("k_wave_init")), None)
         for k, per in agg.items():
             vals = list(per.values())
             d = out["kernels"].setdefault(k, {})
             d[f"{counter}_raw_kib_per_launch"] = sum(vals) / len(vals)
             d[f"hbm_{kind}_bytes_per_launch"] = sum(vals) / len(vals) * scale
-            d[f"hbm_{kind}_bytes_per_frame"] = sum(vals) * scale / frames
+            if frames:
+                d["launches_per_frame"] = len(vals) / frames
+                d[f"hbm_{kind}_bytes_per_frame"] = sum(vals) * scale / frames
     for k, d in out["kernels"].items():
         if "hbm_fetch_bytes_per_launch" in d or "hbm_write_bytes_per_launch" in d:
             d["hbm_bytes_per_launch"] = d.get("hbm_fetch_bytes_per_launch", 0) + d.get("hbm_write_bytes_per_launch", 0)
@@ -76,8 +82,6 @@ def main():
     with open(os.path.join(ROOT, "profiles", f"{name}.json"), "w") as f:
         json.dump(out, f, indent=1)
     shutil.copy(stats, os.path.join(ROOT, "profiles", f"{name}_kernel_stats.csv"))
-    with open(os.path.join(ROOT, "profiles", "traffic_current.json"), "w") as f:
-        json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 
 

@@ -63,7 +63,7 @@ def test_bench_withholds_frac_on_a_stale_profile():
 
 
 def test_committed_profiles_are_stamped():
-    for f in ("traffic_current.json", "valu_current.json"):
+    for f in ("current_c4.json", "current_c5.json"):  # what bench.py prices (scripts/summarize_session.py)
         d = json.load(open(os.path.join(ROOT, "profiles", f)))
         rec = [v for k, v in d["kernels"].items() if codeobj.profile_kernel_base(k) == "k_trace2"]
         assert rec and len(rec[0].get("code_hash", "")) == 64, f
