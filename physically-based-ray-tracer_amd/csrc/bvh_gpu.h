@@ -22,7 +22,8 @@ struct GpuBlasInfo {
 // the wide tree is emitted level by level, so level d's nodes are [level_ends[d-1], level_ends[d]) (level 0: [0, 1))
 hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, int max_leaf, Node8* nodes_out,
                            TriMT* tris_out, GpuBlasInfo* info, bool ploc = false,
-                           std::vector<uint32_t>* level_ends = nullptr);
+                           std::vector<uint32_t>* level_ends = nullptr, int trbvh = -1,  // trbvh < 0: PRT_TRBVH / default
+                           int ploc_radius = 64);  // PLOC search radius: 64 (PRT_PLOC_R) or 512
 // rebase a mesh's nodes into the concatenated arrays (in place) and record ShadeTri.pad[0] for its primitives
 hipError_t gpu_blas_finish(hipStream_t s, Node8* nodes, uint32_t n_nodes, uint32_t node_base, const TriMT* tris,
                            uint32_t n_tris, uint32_t tri_base, ShadeTri* stri, uint32_t prim_base);

@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(kB) k_boxes(const float4* __restrict__ tri, co
 #ifndef PRT_PLOC_R
 #define PRT_PLOC_R 64
 #endif
-constexpr int kPlocR = PRT_PLOC_R;
+constexpr int kPlocDefaultR = PRT_PLOC_R;
 
 __global__ void __launch_bounds__(kB) k_ploc_leaves(const float4* __restrict__ tri,
                                                     const unsigned long long* __restrict__ keys, int n, float* box,
@@ -262,6 +262,7 @@ __global__ void __launch_bounds__(kB) k_ploc_leaves(const float4* __restrict__ t
 
 // nearest neighbour of every cluster (by merged surface area) within kPlocR places; the block's boxes (plus the
 // kPlocR on either side) staged in LDS
+template <int kPlocR>
 __global__ void __launch_bounds__(kB) k_ploc_nn(const int* __restrict__ clus, int m, const float* __restrict__ box,
                                                 int* nn) {
   __shared__ float sb[6 * (kB + 2 * kPlocR)];
@@ -738,6 +739,12 @@ __global__ void __launch_bounds__(kB) k_rebase(Node8* nodes, uint32_t n, uint32_
 
 }  // namespace
 
+// the build's scratch is stream-ordered (hipMallocAsync / hipFreeAsync on the build stream): no device-wide
+// synchronisation, so a build on a side stream (the instance BVH's rebuild, prt_api.cpp) overlaps queued frames
+inline void afree(void* p, hipStream_t s) {
+  if (p) (void)hipFreeAsync(p, s);
+}
+
 #define GB_TRY(x)                          \
   do {                                     \
     const hipError_t e_ = (x);             \
@@ -745,7 +752,8 @@ __global__ void __launch_bounds__(kB) k_rebase(Node8* nodes, uint32_t n, uint32_
   } while (0)
 
 hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, int max_leaf, Node8* nodes_out,
-                           TriMT* tris_out, GpuBlasInfo* info, bool ploc, std::vector<uint32_t>* level_ends) {
+                           TriMT* tris_out, GpuBlasInfo* info, bool ploc, std::vector<uint32_t>* level_ends,
+                           int trbvh, int ploc_radius) {
   const int n = n_tris;
   if (n <= 0) return hipErrorInvalidValue;
   const size_t nn = 2 * (size_t)n - 1;
@@ -760,23 +768,23 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
   size_t tmp_bytes = 0;
   hipError_t err = hipSuccess;
   auto fail = [&](hipError_t e) {
-    (void)hipFree(keys); (void)hipFree(keys2); (void)hipFree(left); (void)hipFree(right); (void)hipFree(parent);
-    (void)hipFree(first); (void)hipFree(count); (void)hipFree(flag); (void)hipFree(ctr); (void)hipFree(cb);
-    (void)hipFree(box); (void)hipFree(ta); (void)hipFree(tb); (void)hipFree(tmp);
-    (void)hipFree(dp.C); (void)hipFree(dp.dec);
+    afree(keys, s); afree(keys2, s); afree(left, s); afree(right, s); afree(parent, s);
+    afree(first, s); afree(count, s); afree(flag, s); afree(ctr, s); afree(cb, s);
+    afree(box, s); afree(ta, s); afree(tb, s); afree(tmp, s);
+    afree(dp.C, s); afree(dp.dec, s);
     return e;
   };
   const float4* tri = reinterpret_cast<const float4*>(tri_dev);
-  if ((err = hipMalloc(&keys, 8 * (size_t)n)) || (err = hipMalloc(&keys2, 8 * (size_t)n)) ||
-      (err = hipMalloc(&left, 4 * nn)) || (err = hipMalloc(&right, 4 * nn)) || (err = hipMalloc(&parent, 4 * nn)) ||
-      (err = hipMalloc(&first, 4 * nn)) || (err = hipMalloc(&count, 4 * nn)) || (err = hipMalloc(&flag, 4 * nn)) ||
-      (err = hipMalloc(&box, 24 * nn)) || (err = hipMalloc(&ta, sizeof(Task) * (size_t)n)) ||
-      (err = hipMalloc(&tb, sizeof(Task) * (size_t)n)) || (err = hipMalloc(&ctr, 16)) || (err = hipMalloc(&cb, 24)))
+  if ((err = hipMallocAsync(reinterpret_cast<void**>(&keys), 8 * (size_t)n, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&keys2), 8 * (size_t)n, s)) ||
+      (err = hipMallocAsync(reinterpret_cast<void**>(&left), 4 * nn, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&right), 4 * nn, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&parent), 4 * nn, s)) ||
+      (err = hipMallocAsync(reinterpret_cast<void**>(&first), 4 * nn, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&count), 4 * nn, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&flag), 4 * nn, s)) ||
+      (err = hipMallocAsync(reinterpret_cast<void**>(&box), 24 * nn, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&ta), sizeof(Task) * (size_t)n, s)) ||
+      (err = hipMallocAsync(reinterpret_cast<void**>(&tb), sizeof(Task) * (size_t)n, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&ctr), 16, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&cb), 24, s)))
     return fail(err);
   const char* ce = std::getenv("PRT_COLLAPSE");
   if (!(ce && std::strcmp(ce, "greedy") == 0) && n > 1) {
-    if ((err = hipMalloc(&dp.C, 8 * sizeof(double) * (size_t)(n - 1))) ||
-        (err = hipMalloc(&dp.dec, sizeof(uint32_t) * (size_t)(n - 1))))
+    if ((err = hipMallocAsync(reinterpret_cast<void**>(&dp.C), 8 * sizeof(double) * (size_t)(n - 1), s)) ||
+        (err = hipMallocAsync(reinterpret_cast<void**>(&dp.dec), sizeof(uint32_t) * (size_t)(n - 1), s)))
       return fail(err);
   }
   const uint32_t init_cb[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
@@ -784,7 +792,7 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
   hipLaunchKernelGGL(k_centroid_bounds, dim3(grid_of(n)), dim3(kB), 0, s, tri, (uint32_t)n, cb);
   hipLaunchKernelGGL(k_morton, dim3(grid_of(n)), dim3(kB), 0, s, tri, (uint32_t)n, cb, keys);
   if ((err = hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, keys, keys2, n, 0, 64, s))) return fail(err);
-  if ((err = hipMalloc(&tmp, tmp_bytes))) return fail(err);
+  if ((err = hipMallocAsync(reinterpret_cast<void**>(&tmp), tmp_bytes, s))) return fail(err);
   if ((err = hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, keys, keys2, n, 0, 64, s))) return fail(err);
   if (ploc) {
     // clusters: the Morton-ordered leaves; iterate nearest-neighbour / merge / compact down to the root
@@ -792,14 +800,14 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
     void* stmp = nullptr;
     size_t stmp_bytes = 0;
     auto pfree = [&]() {
-      (void)hipFree(clus); (void)hipFree(clus2); (void)hipFree(nnb); (void)hipFree(keep); (void)hipFree(nsel);
-      (void)hipFree(stmp);
+      afree(clus, s); afree(clus2, s); afree(nnb, s); afree(keep, s); afree(nsel, s);
+      afree(stmp, s);
     };
-    if ((err = hipMalloc(&clus, 4 * (size_t)n)) || (err = hipMalloc(&clus2, 4 * (size_t)n)) ||
-        (err = hipMalloc(&nnb, 4 * (size_t)n)) || (err = hipMalloc(&keep, 4 * (size_t)n)) ||
-        (err = hipMalloc(&nsel, 4)) ||
+    if ((err = hipMallocAsync(reinterpret_cast<void**>(&clus), 4 * (size_t)n, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&clus2), 4 * (size_t)n, s)) ||
+        (err = hipMallocAsync(reinterpret_cast<void**>(&nnb), 4 * (size_t)n, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&keep), 4 * (size_t)n, s)) ||
+        (err = hipMallocAsync(reinterpret_cast<void**>(&nsel), 4, s)) ||
         (err = hipcub::DeviceSelect::Flagged(nullptr, stmp_bytes, clus2, keep, clus, nsel, n, s)) ||
-        (err = hipMalloc(&stmp, stmp_bytes))) {
+        (err = hipMallocAsync(reinterpret_cast<void**>(&stmp), stmp_bytes, s))) {
       pfree();
       return fail(err);
     }
@@ -808,7 +816,8 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
     hipLaunchKernelGGL(k_ploc_leaves, dim3(grid_of(n)), dim3(kB), 0, s, tri, keys2, n, box, count, clus);
     int m = n;
     while (m > 1 && !err) {
-      hipLaunchKernelGGL(k_ploc_nn, dim3(grid_of(m)), dim3(kB), 0, s, clus, m, box, nnb);
+      if (ploc_radius >= 512) hipLaunchKernelGGL(k_ploc_nn<512>, dim3(grid_of(m)), dim3(kB), 0, s, clus, m, box, nnb);
+      else hipLaunchKernelGGL(k_ploc_nn<kPlocDefaultR>, dim3(grid_of(m)), dim3(kB), 0, s, clus, m, box, nnb);
       hipLaunchKernelGGL(k_ploc_merge, dim3(grid_of(m)), dim3(kB), 0, s, clus, m, nnb, box, left, right, count, clus2,
                          keep, ctr, dp, n, max_leaf);
       if ((err = hipcub::DeviceSelect::Flagged(stmp, stmp_bytes, clus2, keep, clus, nsel, m, s))) break;
@@ -823,7 +832,7 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
       err = hipErrorInvalidValue;  // not exactly n - 1 internal nodes
     pfree();
     if (err) return fail(err);
-    (void)hipFree(first);
+    afree(first, s);
     first = nullptr;  // PLOC subtrees are not key ranges: the collapse walks them
   } else {
     if ((err = hipMemsetAsync(parent, 0xFF, 4 * nn, s))) return fail(err);
@@ -839,15 +848,15 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
   //   LBVH  0 / 1 / 2 / 3 passes: 2,997 / 3,364 / 3,529 / 3,537 Mrays/s (60 / 77 / 106 / 131 ms); ship 4,071 -> 4,372
   //   PLOC  0 / 1 / 2 / 3 passes: 3,514 / 3,532 / 3,525 / 3,533 Mrays/s (55 / 78 / 112 / 128 ms); ship 4,172 -> 4,402
   const char* tre = std::getenv("PRT_TRBVH");
-  const int tr_passes = tre ? std::atoi(tre) : (ploc ? 0 : 2);
+  const int tr_passes = trbvh >= 0 ? trbvh : (tre ? std::atoi(tre) : (ploc ? 0 : 2));
   if (tr_passes > 0 && n >= 3) {
     float* tcost = nullptr;
     uint32_t* terr = nullptr;
-    if ((err = hipMalloc(&tcost, 4 * nn)) || (err = hipMalloc(&terr, 4))) {
-      (void)hipFree(tcost);
+    if ((err = hipMallocAsync(reinterpret_cast<void**>(&tcost), 4 * nn, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&terr), 4, s))) {
+      afree(tcost, s);
       return fail(err);
     }
-    auto tfree = [&]() { (void)hipFree(tcost); (void)hipFree(terr); };
+    auto tfree = [&]() { afree(tcost, s); afree(terr, s); };
     if ((err = hipMemsetAsync(terr, 0, 4, s))) { tfree(); return fail(err); }
     if (ploc) hipLaunchKernelGGL(k_parents, dim3(grid_of(n)), dim3(kB), 0, s, left, right, n, parent);
     for (int pass = 0; pass < tr_passes && !err; pass++) {
@@ -864,7 +873,7 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
       err = hipErrorInvalidValue;  // malformed tree
     tfree();
     if (err) return fail(err);
-    (void)hipFree(first);
+    afree(first, s);
     first = nullptr;  // subtrees are no longer key ranges: the collapse walks them
   }
   // collapse, level by level from the binary root (node 0; the single leaf when n == 1)

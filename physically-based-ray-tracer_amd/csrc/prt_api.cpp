@@ -129,7 +129,14 @@ struct prt_ctx {
   DevBuf tlas8, tlas_slot, tlas_order, tlas_aabb;
   // device rebuild of the instance BVH when refitting has degraded it (ensure_instances): build scratch, the tree's
   // SAH cost after every refit (device -> pinned host copy, read back without a host wait once its event is done)
-  DevBuf tlas_fat, tlas_tris, tlas_cost_dev;
+  DevBuf tlas_fat, tlas_tris, tlas_cost_dev, tlas_boxes;
+  // the rebuild runs on its own stream into back buffers while queued frames keep the current tree; the buffers
+  // swap behind an event (tlas_built) and the back buffers are written again only after the frames queued before
+  // the swap (tlas_back_free)
+  DevBuf tlas8_b, tlas_slot_b, tlas_order_b, tlas_aabb_b;
+  hipStream_t tlas_stream = nullptr;
+  hipEvent_t tlas_built = nullptr, tlas_back_free = nullptr;
+  bool tlas_back_busy = false;
   double* tlas_cost_h = nullptr;  // pinned: [0] cost right after the last build, [1] after the latest refit
   hipEvent_t tlas_cost_ev[2] = {nullptr, nullptr};
   bool tlas_cost_pending[2] = {false, false};
@@ -306,25 +313,57 @@ int ensure_instances(prt_ctx* c) {
       (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady is not an error here
     }
     if (rebuild) {
-      // the device build writes the tree in place: frames queued before it keep stream order
+      // boxes of the instances' current transforms (the same refit_instance as k_refit), built on the side stream
+      // into the back buffers: the frames already queued keep walking the current tree, the host waits only for
+      // the build's own steps
+      if (!c->tlas_stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->tlas_stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&c->tlas_built, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&c->tlas_back_free, hipEventDisableTiming));
+      }
+      std::vector<float> boxes(6 * (size_t)n);
+      for (int32_t i = 0; i < n; i++) {
+        InstDev I;
+        refit_instance(src[i], I);
+        std::memcpy(&boxes[6 * (size_t)i], I.bmin, 12);
+        std::memcpy(&boxes[6 * (size_t)i + 3], I.bmax, 12);
+      }
+      if (c->tlas_back_busy) HIP_TRY(hipStreamWaitEvent(c->tlas_stream, c->tlas_back_free, 0));
       if (c->tlas_fat.bytes < 48ull * n || c->tlas_tris.bytes < sizeof(TriMT) * (size_t)n ||
-          c->tlas8.bytes < sizeof(Node8) * (size_t)n || c->tlas_slot.bytes < 32ull * n) {
-        const int rc = drain(c);
-        if (rc) return rc;
+          c->tlas8_b.bytes < sizeof(Node8) * (size_t)n || c->tlas_slot_b.bytes < 32ull * n ||
+          c->tlas_boxes.bytes < 24ull * n || c->tlas_order_b.bytes < 4ull * n || c->tlas_aabb_b.bytes < 24ull * n) {
+        HIP_TRY(hipStreamSynchronize(c->tlas_stream));  // the back buffers are free (tlas_back_free) before realloc
         HIP_TRY(c->tlas_fat.ensure(48ull * n));
         HIP_TRY(c->tlas_tris.ensure(sizeof(TriMT) * (size_t)n));
-        HIP_TRY(c->tlas8.ensure(sizeof(Node8) * (size_t)n));
-        HIP_TRY(c->tlas_slot.ensure(32ull * n));
+        HIP_TRY(c->tlas8_b.ensure(sizeof(Node8) * (size_t)n));
+        HIP_TRY(c->tlas_slot_b.ensure(32ull * n));
+        HIP_TRY(c->tlas_boxes.ensure(24ull * n));
+        HIP_TRY(c->tlas_order_b.ensure(4ull * n));
+        HIP_TRY(c->tlas_aabb_b.ensure(24ull * n));
       }
+      HIP_TRY(hipMemcpyAsync(c->tlas_boxes.p, boxes.data(), 24ull * n, hipMemcpyHostToDevice, c->tlas_stream));
+      TlasTopo topo;
       int depth = 0;
       uint32_t nn = 0;
-      HIP_TRY(gpu_build_tlas8(c->stream, c->inst.as<InstDev>(), n, c->tlas_fat.as<float>(), c->tlas_tris.as<TriMT>(),
-                              c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(), &c->tlas_topo, &depth, &nn));
+      HIP_TRY(gpu_build_tlas8(c->tlas_stream, c->tlas_boxes.as<float>(), n, c->tlas_fat.as<float>(),
+                              c->tlas_tris.as<TriMT>(), c->tlas8_b.as<Node8>(), c->tlas_slot_b.as<uint32_t>(), &topo,
+                              &depth, &nn));
+      HIP_TRY(hipMemcpyAsync(c->tlas_order_b.p, topo.order.data(), 4 * topo.order.size(), hipMemcpyHostToDevice,
+                             c->tlas_stream));
+      HIP_TRY(hipEventRecord(c->tlas_built, c->tlas_stream));
+      // swap: frames queued from here on walk the new tree (after the build, in stream order); the old one becomes
+      // the back buffer once the frames queued before this point are done
+      HIP_TRY(hipStreamWaitEvent(c->stream, c->tlas_built, 0));
+      HIP_TRY(hipEventRecord(c->tlas_back_free, c->stream));
+      c->tlas_back_busy = true;
+      std::swap(c->tlas8, c->tlas8_b);
+      std::swap(c->tlas_slot, c->tlas_slot_b);
+      std::swap(c->tlas_order, c->tlas_order_b);
+      std::swap(c->tlas_aabb, c->tlas_aabb_b);
+      c->tlas_topo = std::move(topo);
       c->tlas_depth = depth;
       c->tlas_nodes = nn;
-      int rc = upload_order();
-      if (rc) return rc;
-      rc = refit_tree();  // the refit's boxes (aabb) for the cost
+      int rc = refit_tree();  // the new tree re-quantised over this frame's boxes (k_refit above); its aabb for the cost
       if (rc) return rc;
       c->tlas_base_cost = 0;
       c->tlas_cost_pending[1] = false;
@@ -452,6 +491,7 @@ int scene_ready(prt_ctx* c, SceneDev& S) {
   std::memcpy(S.al, c->al, sizeof(S.al));
   S.area = c->area;
   S.area_two_sided = c->area_two_sided;
+  S.pool_ok = c->tris.bytes / sizeof(TriMT) < (1ull << 26) ? 1 : 0;
   S.has_diel = 0;
   for (size_t i = 0; i < c->inst_mesh.size() && i < c->inst_kind.size(); i++)
     if (c->inst_kind[i] == kMatDielectric) S.has_diel = 1;
@@ -1153,6 +1193,10 @@ int prt_destroy(prt_ctx* c) {
   if (c->fork) (void)hipEventDestroy(c->fork);
   for (auto e : c->tlas_cost_ev)
     if (e) (void)hipEventDestroy(e);
+  if (c->tlas_stream) (void)hipStreamSynchronize(c->tlas_stream);
+  if (c->tlas_built) (void)hipEventDestroy(c->tlas_built);
+  if (c->tlas_back_free) (void)hipEventDestroy(c->tlas_back_free);
+  if (c->tlas_stream) (void)hipStreamDestroy(c->tlas_stream);
   if (c->tlas_cost_h) (void)hipHostFree(c->tlas_cost_h);
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);

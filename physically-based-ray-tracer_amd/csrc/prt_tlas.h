@@ -17,12 +17,13 @@ struct TlasTopo {
 TlasTopo tlas_topology(const std::vector<Node8>& nodes);
 // queue the refit on stream s over the refit instance records `inst` (their inflated world boxes): one launch per
 // level; order_dev = T.order on the device; aabb: 6 floats per node of scratch; nothing is synchronised
-// rebuild the instance BVH's topology on the device over the instances' current (refit) boxes: bvh_gpu.hip's PLOC +
-// SAH-optimal collapse with one instance per leaf slot, converted to the instance form (slot[8j + s], tri_base 8j).
-// Scratch: fat 12 n floats, tris n TriMT; nodes: room for n Node8, slot 8 n.  Fills the refit order T (level by
-// level, as the collapse emits), the depth and the node count.  Synchronises on s once per builder level.
+// rebuild the instance BVH's topology on the device over the instances' inflated world boxes (boxes: 6 floats per
+// instance, device): bvh_gpu.hip's PLOC + treelet restructuring + SAH-optimal collapse with one instance per leaf
+// slot, converted to the instance form (slot[8j + s], tri_base 8j).  Scratch: fat 12 n floats, tris n TriMT; nodes:
+// room for n Node8, slot 8 n.  Fills the refit order T (level by level, as the collapse emits), the depth and the
+// node count.  Synchronises on s (only) once per builder level; its scratch is stream-ordered.
 struct TriMT;
-hipError_t gpu_build_tlas8(hipStream_t s, const InstDev* inst, int32_t n, float* fat, TriMT* tris, Node8* nodes,
+hipError_t gpu_build_tlas8(hipStream_t s, const float* boxes, int32_t n, float* fat, TriMT* tris, Node8* nodes,
                            uint32_t* slot, TlasTopo* T, int* depth, uint32_t* n_nodes);
 // the tree's SAH cost over its current boxes (after a refit) into *out (device), one block
 hipError_t launch_tlas_cost(hipStream_t s, const Node8* nodes, uint32_t n_nodes, const float* aabb,

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "bvh_build.h"
@@ -94,12 +95,12 @@ __global__ void k_tlas_refit(const InstDev* __restrict__ inst, const uint32_t* _
 // builder (bvh_gpu.hip: PLOC + SAH-optimal 8-wide collapse, one instance per leaf slot), converted to the
 // instance-BVH form exactly as the host's build_tlas8 converts its BLAS-form tree
 
-// instance i's inflated world box as the degenerate "triangle" {lo, hi, lo} (bvh_build.cpp build_tlas8)
-__global__ void k_inst_fat(const InstDev* __restrict__ inst, int32_t n, float4* __restrict__ fat) {
+// instance i's inflated world box (6 floats) as the degenerate "triangle" {lo, hi, lo} (bvh_build.cpp build_tlas8)
+__global__ void k_inst_fat(const float* __restrict__ boxes, int32_t n, float4* __restrict__ fat) {
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const InstDev& I = inst[i];
-  const float4 lo = make_float4(I.bmin[0], I.bmin[1], I.bmin[2], 0.0f), hi = make_float4(I.bmax[0], I.bmax[1], I.bmax[2], 0.0f);
+  const float* b = boxes + 6 * (size_t)i;
+  const float4 lo = make_float4(b[0], b[1], b[2], 0.0f), hi = make_float4(b[3], b[4], b[5], 0.0f);
   fat[3 * (size_t)i] = lo;
   fat[3 * (size_t)i + 1] = hi;
   fat[3 * (size_t)i + 2] = lo;
@@ -150,13 +151,19 @@ __global__ void __launch_bounds__(1024) k_tlas_cost(const Node8* __restrict__ no
 
 }  // namespace
 
-hipError_t gpu_build_tlas8(hipStream_t s, const InstDev* inst, int32_t n, float* fat, TriMT* tris, Node8* nodes,
+hipError_t gpu_build_tlas8(hipStream_t s, const float* boxes, int32_t n, float* fat, TriMT* tris, Node8* nodes,
                            uint32_t* slot, TlasTopo* T, int* depth, uint32_t* n_nodes) {
   if (n <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_inst_fat, dim3((n + 255) / 256), dim3(256), 0, s, inst, n, reinterpret_cast<float4*>(fat));
+  hipLaunchKernelGGL(k_inst_fat, dim3((n + 255) / 256), dim3(256), 0, s, boxes, n, reinterpret_cast<float4*>(fat));
   GpuBlasInfo gi{};
   std::vector<uint32_t> ends;
-  hipError_t e = gpu_build_blas8(s, fat, n, 1, nodes, tris, &gi, true, &ends);
+  // PLOC search radius (PRT_TLAS_PLOC_R: 64 or 512, default 512) and treelet restructuring passes over its tree
+  // (PRT_TLAS_TRBVH, default 0).  Measured on the 1,000-instance drift (scripts/tlas_drift.py): radius 64 without
+  // restructuring renders 3-4 % behind a fresh host SAH tree, one pass 1-5 % behind at ~4 ms more per build
+  const char* te = std::getenv("PRT_TLAS_TRBVH");
+  const char* tr = std::getenv("PRT_TLAS_PLOC_R");
+  hipError_t e = gpu_build_blas8(s, fat, n, 1, nodes, tris, &gi, true, &ends, te ? std::max(0, std::atoi(te)) : 0,
+                                 tr ? std::atoi(tr) : 512);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_tlas_slots, dim3((gi.nodes + 255) / 256), dim3(256), 0, s, nodes, gi.nodes, tris, slot);
   // the collapse emits level by level: the refit order is the identity, levels deepest first

@@ -115,11 +115,11 @@ __device__ __forceinline__ uint32_t shadow_vis(const WaveBufs& B, uint32_t code)
 }
 
 // ---- one traversal launch: closest hits of P(iter) (iter < iters) + any hits of S(iter - 1) (iter > 0)
-template <int REFILL, int STACK, int WAVES, int TAILN, bool TLAS, bool SPILL = false>
+template <int REFILL, int STACK, int WAVES, int TAILN, bool TLAS, bool SPILL = false, int POOL = 0>
 __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, uint32_t iter, uint32_t iters) {
   __shared__ uint32_t lds_stack[2 * STACK * 64];
   __shared__ uint32_t prefP[kNSub + 1], prefS[kNSub + 1];
-  __shared__ uint32_t tail_lds[tail_lds_words(TAILN)];
+  __shared__ __attribute__((aligned(8))) uint32_t tail_lds[tail_pool_words(TAILN, POOL)];
   uint8_t* vis8 = reinterpret_cast<uint8_t*>(B.vis);
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
   const uint32_t nP = iter < iters ? load_prefix(B.ctr, iter, 0, prefP) : 0u;
@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   unsigned long long* tl = B.tl ? B.tl + ((size_t)iter * kTlWaves + blockIdx.x) * 4 : nullptr;
   bool seen_drain = false;
   if (tl && threadIdx.x == 0) tl[0] = __builtin_amdgcn_s_memrealtime();
-  trav8_persistent<2, STACK, REFILL, TAILN, TLAS, SPILL>(
+  trav8_persistent<2, STACK, REFILL, TAILN, TLAS, SPILL, POOL>(
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) {
         const uint32_t got = fetch_some(fctr, total, part, base, want);
@@ -185,9 +185,9 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
       },
       [&]() -> bool { return __hip_atomic_load(dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u; },
 #ifdef PRT_LANE_STATS
-      B.coop_tail ? tail_lds : nullptr, g_lane_stats + 32 * iter);
+      B.coop_tail ? tail_lds : nullptr, g_lane_stats + 32 * iter, tail_lds);
 #else
-      B.coop_tail ? tail_lds : nullptr, tl ? tl + 3 : nullptr);
+      B.coop_tail ? tail_lds : nullptr, tl ? tl + 3 : nullptr, tail_lds);
 #endif
   if (tl && threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
@@ -586,15 +586,20 @@ __global__ void __launch_bounds__(kBlock) k_resmiss2(SceneDev S, TraceArgs A, Wa
 #ifndef PRT_REFILL
 #define PRT_REFILL 32  // idle lanes before a wave refills from the queue (A/B builds: -DPRT_REFILL=16 ...)
 #endif
-template <int STACK, int WAVES, int TAILN>
+// PRT_POOL: triangle-pool entries of the 7-wave traversal (prt_persist.h; 0 = one triangle per lane per iteration)
+#ifndef PRT_POOL
+#define PRT_POOL 0
+#endif
+template <int STACK, int WAVES, int TAILN, int POOL = 0>
 void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
-  static_assert(2 * STACK * 256 + 264 + 4 * 3 * TAILN <= 163840 / (4 * WAVES), "LDS over the occupancy budget");
+  static_assert(2 * STACK * 256 + 264 + 4 * tail_pool_words(TAILN, POOL) <= 163840 / (4 * WAVES),
+                "LDS over the occupancy budget");
   if (S.tlas)
-    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, true>), dim3(256u * 4u * WAVES / c.groups), dim3(64), 0,
-                       c.stream, S, B, it, iters);
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, true, false, POOL>), dim3(256u * 4u * WAVES / c.groups),
+                       dim3(64), 0, c.stream, S, B, it, iters);
   else
-    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, false>), dim3(256u * 4u * WAVES / c.groups), dim3(64), 0,
-                       c.stream, S, B, it, iters);
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, false, false, POOL>), dim3(256u * 4u * WAVES / c.groups),
+                       dim3(64), 0, c.stream, S, B, it, iters);
 }
 // persistent traversal occupancy (waves/SIMD) -> LDS stack groups per lane; a BVH deeper than the 18 LDS
 // groups at 4 waves/SIMD hold runs the 4-wave form with the HBM spill columns (S.spill)
@@ -607,6 +612,7 @@ static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs&
       hipLaunchKernelGGL((k_trace2<32, 18, 4, 32, false, true>), dim3(kSpillTraceBlocks / c.groups), dim3(64), 0,
                          c.stream, S, B, it, iters);
   } else if (c.occ == 8) launch_t2<8, 8, 32>(c, S, B, it, iters);
+  else if (c.occ == 7 && PRT_POOL > 0 && S.pool_ok) launch_t2<9, 7, 64, PRT_POOL>(c, S, B, it, iters);
   else if (c.occ == 7) launch_t2<9, 7, 64>(c, S, B, it, iters);
   else if (c.occ == 6) launch_t2<11, 6, 64>(c, S, B, it, iters);
   else if (c.occ == 5) launch_t2<14, 5, 32>(c, S, B, it, iters);

@@ -47,8 +47,20 @@ def timed(ctx, avg, rgb, n, inst=None):
     return (time.perf_counter() - t0) * 1e3 / n, inst
 
 
-MODES = [("refit only", "0"), ("device rebuild", None), ("device rebuild every frame", "always")]
-for mode, env in MODES + MODES:
+MODES = [("refit only", "0", None), ("device rebuild", None, None), ("device rebuild every frame", "always", None)]
+if os.environ.get("TLAS_MODES") == "trbvh":  # A/B of the device tree's treelet-restructuring passes
+    MODES = [(f"device rebuild every frame, {k} TRBVH passes", "always", k) for k in ("0", "1", "2", "3")]
+if os.environ.get("TLAS_MODES") == "radius":  # A/B of the device tree's PLOC radius (0 / 1 TRBVH passes)
+    MODES = [(f"device rebuild every frame, PLOC radius {r}, {k} TRBVH passes", "always", k + ":" + r)
+             for r, k in (("64", "0"), ("512", "0"), ("512", "1"))]
+for mode, env, trbvh in MODES + MODES:
+    if trbvh is None:
+        os.environ.pop("PRT_TLAS_TRBVH", None)
+        os.environ.pop("PRT_TLAS_PLOC_R", None)
+    else:
+        os.environ["PRT_TLAS_TRBVH"] = trbvh.split(":")[0]
+        if ":" in trbvh:
+            os.environ["PRT_TLAS_PLOC_R"] = trbvh.split(":")[1]
     os.environ.pop("PRT_TLAS_HOST", None)
     if env is None:
         os.environ.pop("PRT_TLAS_REBUILD", None)
