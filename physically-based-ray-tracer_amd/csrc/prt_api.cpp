@@ -81,7 +81,7 @@ struct WaveState {
   DevBuf wave;
   WaveBufs wb = {};
   uint32_t n = 0, levels = 0;
-  bool ext = false;
+  bool ext = false, merge = false;
 };
 // a concurrent item group beyond the first: its own stream, wavefront state and join event
 struct ItemGroup {
@@ -261,14 +261,14 @@ int ensure_instances(prt_ctx* c) {
   // The instance BVH.  The reference rebuilds it every frame (Core/Renderer.cpp:33-41).  Here the host SAH builder
   // builds it when the set of instances changes (its count; or every call with PRT_TLAS_HOST=1, the A/B form);
   // otherwise it is refitted on the device behind k_refit (prt_tlas.hip), and rebuilt on the device (PLOC +
-  // SAH-optimal collapse over the current boxes, gpu_build_tlas8) once refitting has raised the tree's SAH cost
-  // above PRT_TLAS_REBUILD (default 1.2) times its cost right after the last build (0: refit only).  The cost is
+  // SAH-optimal collapse over the current boxes, gpu_build_tlas8) once refitting has raised the tree's node-area
+  // cost above PRT_TLAS_REBUILD (default 1.1) times its cost right after the last build (0: refit only).  The cost is
   // measured on the device after every refit and read back without a host wait (a pinned copy behind an event):
   // a frame decides on the latest cost already available.  No host BVH work and no host wait per frame.
   const char* th = std::getenv("PRT_TLAS_HOST");
   const char* tr = std::getenv("PRT_TLAS_REBUILD");
   const bool rebuild_always = tr && std::strcmp(tr, "always") == 0;  // A/B: a device rebuild for every update
-  const double rebuild_ratio = rebuild_always ? 0.0 : (tr ? std::atof(tr) : 1.2);
+  const double rebuild_ratio = rebuild_always ? 0.0 : (tr ? std::atof(tr) : 1.1);
   auto upload_order = [&]() -> int {
     const size_t ob = 4 * c->tlas_topo.order.size(), ab = 24 * std::max<size_t>(c->tlas_nodes, 1);
     if (c->tlas_order.bytes < ob || c->tlas_aabb.bytes < ab) {
@@ -491,7 +491,6 @@ int scene_ready(prt_ctx* c, SceneDev& S) {
   std::memcpy(S.al, c->al, sizeof(S.al));
   S.area = c->area;
   S.area_two_sided = c->area_two_sided;
-  S.pool_ok = c->tris.bytes / sizeof(TriMT) < (1ull << 26) ? 1 : 0;
   S.has_diel = 0;
   for (size_t i = 0; i < c->inst_mesh.size() && i < c->inst_kind.size(); i++)
     if (c->inst_kind[i] == kMatDielectric) S.has_diel = 1;
@@ -544,24 +543,30 @@ int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
 // wavefront buffers sized for n items and (bounces-1) (result, throughput) stack levels
 // queue counters [iter][path|shadow][kNSub] + traversal fetch counters [iter][path|shadow][8 parts]
 constexpr size_t kCtrWords = (size_t)(kMaxIters + 2) * 2 * (kNSub + 8) * kCtrStride;
-int ensure_wave(WaveState& ws, uint32_t n, int bounces, bool ext) {
+int ensure_wave(WaveState& ws, uint32_t n, int bounces, bool ext, bool merge) {
   const uint32_t levels = (uint32_t)std::max(1, bounces - 1);
   // sub-queue t receives the 256-entry chunks c == t (mod kNSub): at most ceil(ceil(n/256)/kNSub) of them
   const uint32_t qcap = 256u * (((n + 255u) / 256u + kNSub - 1) / kNSub);
-  if (ws.n >= n && ws.levels >= levels && (ws.ext || !ext) && ws.wave.p) {
+  if (ws.n >= n && ws.levels >= levels && (ws.ext || !ext) && (ws.merge || !merge) && ws.wave.p) {
     ws.wb.n = n;  // capacity stays; the SoA strides (R/T: depth * n + item) follow the current n
     ws.wb.qcap = qcap;
     ws.wb.scap = 5u * qcap;
+    ws.wb.merge = merge ? 1 : 0;
     return PRT_OK;
   }
+  // merge: two record slots (path 1, path 2) per item for the NEE record, hit point, status and stack
+  const size_t ns = merge ? 2ull * n : (size_t)n;
   const size_t qn = (size_t)kNSub * qcap, sn = 5 * qn;  // <= 4 light-class + 1 area-light shadow rays per item
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
-  const size_t o_seed = take(4ull * n), o_info = take(4ull * n), o_rinfo = take(4ull * n), o_ro = take(16ull * n), o_rd = take(16ull * n),
-               o_R = take(16ull * n * levels), o_T = take(16ull * n * levels), o_s1 = take(16ull * n),
-               o_jit = take(8ull * n), o_hit = take(16ull * n), o_ne = take(16ull * n), o_nb = take(16ull * n),
-               o_nk = take(16ull * n), o_vis = take(5ull * n), o_q0 = take(4 * qn), o_q1 = take(4 * qn),
-               o_shq = take(4 * sn), o_hp = take(16ull * n), o_ctr = take(4 * kCtrWords);
+  const size_t o_seed = take(4ull * n), o_info = take(4ull * n), o_rinfo = take(4ull * ns), o_ro = take(16ull * n),
+               o_rd = take(16ull * n), o_R = take(16ull * ns * levels), o_T = take(16ull * ns * levels),
+               o_s1 = take(16ull * n), o_jit = take(8ull * n), o_hit = take(16ull * n), o_ne = take(16ull * ns),
+               o_nb = take(16ull * ns), o_nk = take(16ull * ns), o_vis = take(merge ? 8ull * n : 5ull * n),
+               o_q0 = take(4 * qn), o_q1 = take(4 * qn), o_shq = take(4 * sn), o_hp = take(16ull * ns),
+               o_ctr = take(4 * kCtrWords);
+  const size_t o_ro2 = merge ? take(16ull * n) : 0, o_rd2 = merge ? take(16ull * n) : 0,
+               o_hit2 = merge ? take(16ull * n) : 0;
   const size_t o_na = ext ? take(16ull * n) : 0, o_dst = ext ? take(4ull * n) : 0,
                o_dro = ext ? take(16ull * n * levels) : 0, o_drd = ext ? take(16ull * n * levels) : 0,
                o_ao = ext ? take(16ull * n) : 0, o_ad = ext ? take(16ull * n) : 0;
@@ -581,9 +586,13 @@ int ensure_wave(WaveState& ws, uint32_t n, int bounces, bool ext) {
   W.na = ext ? (float4*)(b + o_na) : nullptr; W.dst = ext ? (uint32_t*)(b + o_dst) : nullptr;
   W.dro = ext ? (float4*)(b + o_dro) : nullptr; W.drd = ext ? (float4*)(b + o_drd) : nullptr;
   W.ao = ext ? (float4*)(b + o_ao) : nullptr; W.ad = ext ? (float4*)(b + o_ad) : nullptr;
+  W.ro2 = merge ? (float4*)(b + o_ro2) : nullptr; W.rd2 = merge ? (float4*)(b + o_rd2) : nullptr;
+  W.hit2 = merge ? (float4*)(b + o_hit2) : nullptr;
+  W.merge = merge ? 1 : 0;
   ws.n = n;
   ws.levels = levels;
   ws.ext = ext;
+  ws.merge = merge;
   return PRT_OK;
 }
 
@@ -625,10 +634,19 @@ struct RenderPlan {
   TraceArgs A;
   int32_t F = 0, fmax = 1, npass = 1, F0 = 0;
   uint64_t per = 0;
-  bool ext = false;
+  bool ext = false, merge = false;
   uint32_t iters = 0;
   uint32_t groups = 1;
 };
+
+// the merged pipeline (prt_wave2.hip k_shade2m): AA frames of render mode 0 without extensions; PRT_MERGE=0 turns it
+// off (A/B).  Its shadow-queue entries index 4 x (slot x n + item) + k in 29 bits: at most 2^26 items per pass
+constexpr uint64_t kMaxMergedPassItems = 1ull << 26;
+bool merge_for(const prt_render_params* p, bool ext, uint64_t per) {
+  const char* e = std::getenv("PRT_MERGE");
+  if (e && std::atoi(e) == 0) return false;
+  return !ext && p->render_mode == 0 && (p->flags & PRT_FLAG_AA) && p->bounces > 0 && per <= kMaxMergedPassItems;
+}
 
 // Concurrent item groups.  A call small enough that its traversal launches are bound by their
 // slowest rays (world-8 shares) can cut its items into G contiguous ranges, each with its own queues, stream and
@@ -663,9 +681,13 @@ int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int
   rc = ensure_state(c, p->width, p->height);
   if (rc) return rc;
   const int32_t F = frames_of(p);
+  // extensions (area light, dielectric instances) take the EXT instantiations of the shading kernels
+  const bool ext = (S.area || S.has_diel) && p->render_mode == 0;
+  const bool merge = merge_for(p, ext, per);
+  const uint64_t pass_cap = merge ? kMaxMergedPassItems : kMaxPassItems;
   const char* emi = std::getenv("PRT_MAX_ITEMS");
-  const uint64_t max_items = emi ? std::min<uint64_t>(std::max<uint64_t>(std::strtoull(emi, nullptr, 10), 1), kMaxPassItems)
-                                 : kMaxPassItems;
+  const uint64_t max_items = emi ? std::min<uint64_t>(std::max<uint64_t>(std::strtoull(emi, nullptr, 10), 1), pass_cap)
+                                 : pass_cap;
   const int32_t fmax = (int32_t)std::max<uint64_t>(1, max_items / std::max<uint64_t>(per, 1));
   const int32_t npass = F > fmax ? (F + fmax - 1) / fmax : 1;
   const int32_t F0 = std::min(F, fmax);
@@ -673,9 +695,7 @@ int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int
   TraceArgs& A = R.A;
   A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
   A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F0;
-  // extensions (area light, dielectric instances) take the EXT instantiations of the shading kernels
-  const bool ext = (S.area || S.has_diel) && p->render_mode == 0;
-  const uint32_t iters = wave_iters(S.has_diel != 0, p->bounces, p->flags);
+  const uint32_t iters = wave_iters(S.has_diel != 0, p->bounces, p->flags, merge);
   if (iters > (uint32_t)kMaxIters)
     return fail(PRT_ERR_UNSUPPORTED, S.has_diel ? "dielectric path trees exceed the wavefront iteration limit (lower bounces)"
                                                 : "too many wavefront iterations");
@@ -694,10 +714,11 @@ int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int
     }
     if (g > 0 && !c->fork) HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
     WaveState& w = g == 0 ? c->ws : c->grp[g - 1].ws;
-    rc = ensure_wave(w, (uint32_t)(n0 * (g + 1) / G - n0 * g / G), p->bounces, ext);
+    rc = ensure_wave(w, (uint32_t)(n0 * (g + 1) / G - n0 * g / G), p->bounces, ext, merge);
     if (rc) return rc;
   }
-  R.F = F; R.fmax = fmax; R.npass = npass; R.F0 = F0; R.per = per; R.ext = ext; R.iters = iters; R.groups = G;
+  R.F = F; R.fmax = fmax; R.npass = npass; R.F0 = F0; R.per = per; R.ext = ext; R.merge = merge; R.iters = iters;
+  R.groups = G;
   return PRT_OK;
 }
 
@@ -749,7 +770,7 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
       WaveState& w = gws(g);
       const LaunchCfg Lg = gcfg(g);
       const uint32_t b0 = (uint32_t)(nb * g / G), b1 = (uint32_t)(nb * (g + 1) / G);
-      rc = ensure_wave(w, b1 - b0, p->bounces, ext);  // no allocation: prepare_render sized it for pass 0
+      rc = ensure_wave(w, b1 - b0, p->bounces, ext, R.merge);  // no allocation: prepare_render sized it for pass 0
       if (rc) return rc;
       w.wb.base = b0;
       w.wb.coop_tail = coop;
@@ -793,7 +814,7 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
       std::vector<uint32_t> ctr((size_t)(iters + 2) * 2 * kNSub * kCtrStride);
       HIP_TRY(hipMemcpyAsync(ctr.data(), c->ws.wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
-      for (uint32_t k = 0; k < iters; k++)
+      for (uint32_t k = 0; k < iters + 2; k++)  // (+2: the merged path-2 primaries are counted at iters + 1)
         for (uint32_t s2 = 0; s2 < kNSub; s2++) {
           c->carry_segments += ctr[((k * 2 + 0) * kNSub + s2) * kCtrStride];
           c->carry_shadow += ctr[((k * 2 + 1) * kNSub + s2) * kCtrStride];
@@ -851,16 +872,16 @@ int read_stats(prt_ctx* c, prt_stats* stats) {
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     const WaveTimers& wt = c->wt;
-    for (uint32_t k = 0; k <= iters; k++) {
+    for (uint32_t k = 0; k <= iters + 1; k++) {  // iteration iters + 1: the merged path-2 primaries (Q2)
       uint64_t qs = 0, qa = 0;
-      for (uint32_t s = 0; s < kNSub && k < iters; s++) {
+      for (uint32_t s = 0; s < kNSub; s++) {
         qs += ctr[((k * 2 + 0) * kNSub + s) * kCtrStride];
         qa += ctr[((k * 2 + 1) * kNSub + s) * kCtrStride];
       }
       stats->segments += qs;
       stats->shadow_rays += qa;
       float a = 0;
-      if (timers) HIP_TRY(hipEventElapsedTime(&a, wt.ev[4 * k + 0], wt.ev[4 * k + 1]));
+      if (timers && k <= iters) HIP_TRY(hipEventElapsedTime(&a, wt.ev[4 * k + 0], wt.ev[4 * k + 1]));
       stats->ms_closest += a;  // one merged trace launch per iteration plus the final shadow-only one
       if (dump && k < iters)
         std::fprintf(stderr, "prt: iteration %u: %llu closest rays, %llu shadow rays; trace launch %.3f ms\n", k,

@@ -60,7 +60,11 @@ struct WaveBufs {
   float4* ad;       // ... direction
   unsigned long long* tl;  // PRT_DEBUG_QUEUES: [launch][wave] {start, first empty fetch, exit, -}
   int32_t coop_tail;       // cooperative traversal tail (prt_persist.h)
-  int32_t pad;
+  int32_t merge;           // path-2 merge (prt_wave2.hip): the AA path-2 primaries traced with path 1's, and
+                           // each path's NEE record / (result, throughput) stack in its own slot (slot p at p * n)
+  float4* ro2;             // merge: the path-2 primary ray (k_wave_init), traced by k_trace2(0) ...
+  float4* rd2;
+  float4* hit2;            // ... into hit2; shaded by k_shade2 right after path 1 ends
 };
 constexpr uint32_t kParts = 8;  // XCD parts of a traversal launch's live range, one fetch counter each (prt_queue.h)
 constexpr int kMaxIters = 128;  // wavefront iterations per call: bounces <= 64 (AA) / 6 with dielectrics (AA)
@@ -69,8 +73,10 @@ void lane_stats_dump();  // diagnostic build: prints and clears the traversal la
 #endif
 // wavefront iterations of one call: one per path segment, paths x bounces; with dielectric instances a path
 // is a binary tree walked depth first (one segment per iteration), at most 2^bounces - 1 segments per path
-inline uint32_t wave_iters(bool dielectric, int bounces, uint32_t flags) {
+inline uint32_t wave_iters(bool dielectric, int bounces, uint32_t flags, bool merge = false) {
   const uint32_t paths = (flags & 1u) ? 2u : 1u;  // PRT_FLAG_AA: two camera paths per reference frame
+  // merged: path 2's first segment is shaded in the iteration path 1 ends in (its primary hit traced up front)
+  if (merge && paths == 2 && bounces > 0) return 2u * (uint32_t)bounces - 1u;
   if (!dielectric) return paths * (uint32_t)bounces;
   return bounces > 8 ? 0xFFFFFFFFu : paths * ((1u << bounces) - 1u);  // dst holds 4 bits per level for 8 levels
 }

@@ -35,13 +35,6 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 constexpr uint32_t kInstGroup = 0x100u;  // gimask flag: the group's children are instances (TLAS walk)
 // a drained wave with at most TAILN rays turns cooperative; its LDS: TAILN x {count | found << 16, key lo, key hi}
 constexpr uint32_t tail_lds_words(int tailn) { return 3u * (uint32_t)tailn; }
-// LDS words of the tail region when the triangle pool (POOL entries + 64 two-word keys) shares it
-constexpr uint32_t tail_pool_words(int tailn, int pool) {
-  return tail_lds_words(tailn) > (uint32_t)pool + 128u ? tail_lds_words(tailn) : (uint32_t)pool + 128u;
-}
-#ifndef PRT_POOL_PASS_LANES
-#define PRT_POOL_PASS_LANES 32  // a pool pass also runs when at most this many lanes have node work
-#endif
 
 // index of the n-th (0-based) set bit of m; n < popcount(m)
 __device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
@@ -67,13 +60,12 @@ __device__ __forceinline__ uint32_t nth_set(uint64_t m, uint32_t n) {
 // tail: tail_lds_words(TAILN) words of LDS for the cooperative tail, or nullptr (no tail mode).
 // The world ray is not kept in registers (reloaded per extra instance) so the loop state fits the
 // register budget of 6-8 waves/SIMD.
-template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, bool SPILL = false, int POOL = 0,
-          class Fetch, class Load, class Reload, class Finish, class Tick, class Drained>
+template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, bool SPILL = false, class Fetch,
+          class Load, class Reload, class Finish, class Tick, class Drained>
 __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                    Load load, Reload reload, Finish finish, Tick tick,
                                                    Drained drained_elsewhere, uint32_t* __restrict__ tail = nullptr,
-                                                   unsigned long long* __restrict__ dbg = nullptr,
-                                                   uint32_t* __restrict__ pool = nullptr) {
+                                                   unsigned long long* __restrict__ dbg = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lanes_below = (1ull << lane) - 1ull;
   bool active = false, drained = false;
@@ -263,22 +255,9 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   uint32_t lst[32] = {};
   lst[31] = 1;
 #endif
-  // ---- triangle pool (POOL > 0; the LDS of the cooperative tail, free until the tail): a lane's node visit puts
-  // the triangles of its hit leaf children into a wave-shared ring of POOL entries (TriMT index << 6 | lane) and
-  // goes on visiting nodes; once 64 entries wait (or few lanes have node work) one pass tests 64 of them, one per
-  // lane, on their owners' rays (read across lanes), and each owner takes its best candidate through a 64-bit LDS
-  // key per lane (t, ~prim: the hit rule's order within one instance).  The tri branch thus runs at full width
-  // instead of with the ~10 of 64 lanes the one-triangle-per-lane step had (profiles/r04_lane_stats.json); the
-  // hit rule is order-independent, so testing a leaf later (with a larger cull distance meanwhile) cannot change
-  // a hit.  A lane waits for its entries before it finishes or changes instance (the pass reads its current ray),
-  // and is not refilled while any of its entries is in the ring.
-  uint32_t phead = 0, ptail = 0, phm = 0, ptm = 0;  // wave-uniform: ring sequence numbers and their positions mod POOL
-  uint32_t plast = 0;                                // this lane's entries: sequence numbers below plast
-  unsigned long long* pkey = reinterpret_cast<unsigned long long*>(pool + POOL);
-  if constexpr (POOL > 0) pkey[lane] = ~0ull;
   while (true) {
     // ---- refill idle lanes from the queue
-    const uint64_t idle = __ballot(!active && (POOL == 0 || plast <= phead));
+    const uint64_t idle = __ballot(!active);
     tick((uint32_t)__popcll(idle), drained);
 #ifdef PRT_DRAIN_POLL  // A/B: learn of the empty queue from other waves (measured slower: DESIGN.md 6)
     if (tail && !drained && idle != 0 && (++iter_no & 3u) == 0 && drained_elsewhere()) drained = true;
@@ -304,11 +283,11 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       }
     }
     const uint64_t act = __ballot(active);
-    if (act == 0 && (POOL == 0 || phead == ptail)) {
+    if (act == 0) {
       if (drained) break;
       continue;
     }
-    if (tail && drained && __popcll(act) <= (uint32_t)TAILN && (POOL == 0 || phead == ptail)) break;  // cooperative tail
+    if (tail && drained && __popcll(act) <= (uint32_t)TAILN) break;  // cooperative tail below
 #ifdef PRT_LANE_STATS
     {
       const uint32_t nn = (uint32_t)__popcll(__ballot(active && node != kNoNode && lhit == 0));
@@ -320,8 +299,8 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
       lst[17 + (nt + 7) / 8]++;
     }
 #endif
-    // ---- BLAS done (and, with the pool, its triangles tested): next instance, or the ray is finished
-    if (active && node == kNoNode && lhit == 0 && tcnt == 0 && (POOL == 0 || plast <= phead)) {
+    // ---- BLAS done: next instance, or the ray is finished
+    if (active && node == kNoNode && lhit == 0 && tcnt == 0) {
       bool more = false;
       if constexpr (TLAS) {
         if (inst >= 0) more = leave_blas();
@@ -339,110 +318,11 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
     // the current leaf (tcur, tcnt) are tested alongside the next node visits (order-independent hit rule;
     // measured 1.5-2.5 % faster per launch on C4 than waiting for the leaf to finish)
     if (active && node != kNoNode && lhit == 0) node_step(h.t);
-    if constexpr (POOL == 0) {
-      // ---- one triangle test for lanes with pending leaf triangles
-      if (active && (lhit | tcnt)) {
-        if (tri_step()) {
-          finish(handle, h, true, true);
-          active = false;
-        }
-      }
-    } else {
-      // ---- the hit leaf children's triangles into the ring (lanes in order while they fit; the rest next time)
-      uint32_t n = 0;
-      if (active && lhit) {
-        for (uint32_t m = lhit; m; m &= m - 1u) {
-          const uint32_t k = __builtin_ctz(m);
-          n += (((k < 4 ? lmeta0 : lmeta1) >> (8 * (k & 3))) & 7u);
-        }
-      }
-      const uint64_t b1 = __ballot(n & 1u), b2 = __ballot(n & 2u), b4 = __ballot(n & 4u), b8 = __ballot(n & 8u),
-                     b16 = __ballot(n & 16u);
-      if (b1 | b2 | b4 | b8 | b16) {
-        const uint32_t before = (uint32_t)__popcll(b1 & lanes_below) + 2u * (uint32_t)__popcll(b2 & lanes_below) +
-                                4u * (uint32_t)__popcll(b4 & lanes_below) + 8u * (uint32_t)__popcll(b8 & lanes_below) +
-                                16u * (uint32_t)__popcll(b16 & lanes_below);
-        const uint32_t room = (uint32_t)POOL - (ptail - phead);
-        const bool fits = n != 0 && before + n <= room;
-        if (fits) {
-          uint32_t pos = ptm + before;
-          if (pos >= (uint32_t)POOL) pos -= (uint32_t)POOL;
-          for (uint32_t m = lhit; m; m &= m - 1u) {
-            const uint32_t k = __builtin_ctz(m);
-            const uint32_t meta = ((k < 4 ? lmeta0 : lmeta1) >> (8 * (k & 3))) & 0xFFu;
-            const uint32_t first = ltri + (meta >> 3);
-            for (uint32_t i = 0; i < (meta & 7u); i++) {
-              pool[pos] = ((first + i) << 6) | lane;
-              if (++pos == (uint32_t)POOL) pos = 0;
-            }
-          }
-          plast = ptail + before + n;
-          lhit = 0;
-        }
-        // entries pushed: up to the first lane (with triangles) that did not fit
-        const uint64_t over = __ballot(n != 0 && !fits);
-        uint32_t pushed;
-        if (over) {
-          pushed = (uint32_t)__shfl((int)before, (int)__builtin_ctzll(over));
-        } else {
-          pushed = (uint32_t)__popcll(b1) + 2u * (uint32_t)__popcll(b2) + 4u * (uint32_t)__popcll(b4) +
-                   8u * (uint32_t)__popcll(b8) + 16u * (uint32_t)__popcll(b16);
-        }
-        ptail += pushed;
-        ptm += pushed;
-        if (ptm >= (uint32_t)POOL) ptm -= (uint32_t)POOL;
-      }
-      // ---- a pass over the oldest (up to) 64 entries: when 64 wait, when few lanes have node work, or to empty
-      // the ring before the cooperative tail
-      const uint32_t cnt = ptail - phead;
-      const uint32_t prog = (uint32_t)__popcll(__ballot(active && node != kNoNode && lhit == 0));
-      if (cnt >= 64u || (cnt != 0u && (prog <= (uint32_t)PRT_POOL_PASS_LANES || drained))) {
-        const uint32_t m = cnt < 64u ? cnt : 64u;
-        const bool mine = lane < m;
-        uint32_t e = phm + lane;
-        if (e >= (uint32_t)POOL) e -= (uint32_t)POOL;
-        const uint32_t w = mine ? pool[e] : 0u;
-        const int src = (int)(w & 63u);
-        const float ox = __shfl(O.x, src), oy = __shfl(O.y, src), oz = __shfl(O.z, src);
-        const float dx = __shfl(D.x, src), dy = __shfl(D.y, src), dz = __shfl(D.z, src);
-        const float oht = __shfl(h.t, src);
-        const bool oany = MODE == 1 || (MODE == 2 && __shfl((int)any, src) != 0);
-        float t = 0.0f, u = 0.0f, v = 0.0f;
-        uint32_t prim = 0;
-        bool cand = false;
-        if (mine) {
-          const bool hit = mt_test(S.tris + (w >> 6), v3(ox, oy, oz), v3(dx, dy, dz), t, u, v, prim);
-          cand = hit && (oany ? t < oht : t <= oht);  // tiny_bvh.h:6594 / the closest rule's t bound
-        }
-        const unsigned long long key = oany ? 0ull : (((unsigned long long)__float_as_uint(t) << 32) | (~prim & 0xFFFFFFFFull));
-        if (cand) atomicMin(&pkey[src], key);
-        __syncthreads();  // one wave per block: orders the wave's LDS operations
-        const unsigned long long best = pkey[lane];           // this lane's best candidate of the pass
-        const unsigned long long srcbest = pkey[src];
-        __syncthreads();
-        if (cand && !oany && key == srcbest)  // the winner publishes (u, v) (a duplicated triangle: same values)
-          pkey[src] = ((unsigned long long)__float_as_uint(u) << 32) | __float_as_uint(v);
-        __syncthreads();
-        const unsigned long long uv = pkey[lane];
-        pkey[lane] = ~0ull;
-        if (active && best != ~0ull) {
-          if (any) {  // occluded
-            finish(handle, h, true, true);
-            active = false;
-            node = kNoNode; lhit = 0; tcnt = 0;
-          } else {
-            const float bt = __uint_as_float((uint32_t)(best >> 32));
-            const uint32_t bp = ~(uint32_t)best;
-            if (bt < h.t || (bt == h.t && ((uint32_t)inst < h.inst || ((uint32_t)inst == h.inst && bp > h.prim)))) {
-              h.t = bt; h.prim = bp; h.inst = (uint32_t)inst;
-              h.u = __uint_as_float((uint32_t)(uv >> 32));
-              h.v = __uint_as_float((uint32_t)uv);
-            }
-          }
-        }
-        phead += m;
-        phm += m;
-        if (phm >= (uint32_t)POOL) phm -= (uint32_t)POOL;
+    // ---- one triangle test for lanes with pending leaf triangles
+    if (active && (lhit | tcnt)) {
+      if (tri_step()) {
+        finish(handle, h, true, true);
+        active = false;
       }
     }
   }
@@ -622,16 +502,14 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
 #endif
 }
 
-template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, bool SPILL = false, int POOL = 0,
-          class Fetch, class Load, class Reload, class Finish, class Drained>
+template <int MODE, int STACK, int REFILL, int TAILN = 32, bool TLAS = false, bool SPILL = false, class Fetch,
+          class Load, class Reload, class Finish, class Drained>
 __device__ __forceinline__ void trav8_persistent(const SceneDev& S, uint32_t* __restrict__ stk, Fetch fetch,
                                                  Load load, Reload reload, Finish finish, Drained drained_elsewhere,
                                                  uint32_t* __restrict__ tail = nullptr,
-                                                 unsigned long long* __restrict__ dbg = nullptr,
-                                                 uint32_t* __restrict__ pool = nullptr) {
-  trav8_persistent_t<MODE, STACK, REFILL, TAILN, TLAS, SPILL, POOL>(S, stk, fetch, load, reload, finish,
-                                                                   [](uint32_t, bool) {}, drained_elsewhere, tail, dbg,
-                                                                   pool);
+                                                 unsigned long long* __restrict__ dbg = nullptr) {
+  trav8_persistent_t<MODE, STACK, REFILL, TAILN, TLAS, SPILL>(S, stk, fetch, load, reload, finish, [](uint32_t, bool) {},
+                                                        drained_elsewhere, tail, dbg);
 }
 
 }  // namespace prt

@@ -8,6 +8,7 @@ namespace prt {
 enum : uint32_t { kStEndValue = 0, kStNeeEnd = 1, kStNeeCont = 2, kStMiss = 3 };
 constexpr uint32_t kRiQueued = 1u << 24;  // rinfo: the shading kernel queued the item's next ray
 constexpr uint32_t kRiEmissive = 1u << 25;  // rinfo: a hit's emissive term is nonzero (stored in ne; else +0)
+constexpr uint32_t kRiFresh = 1u << 26;     // rinfo (merged pipeline): this slot was shaded in the last iteration
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 __device__ __forceinline__ uint32_t* qcounter(uint32_t* ctr, uint32_t iter, uint32_t which, uint32_t s) {

@@ -25,7 +25,7 @@ __device__ __forceinline__ void wave_count(Counters* c, uint32_t seg, uint32_t s
 __global__ void __launch_bounds__(64) k_add_totals(const uint32_t* __restrict__ ctr, uint32_t iters,
                                                    Counters* __restrict__ totals) {
   unsigned long long seg = 0, sh = 0;
-  for (uint32_t j = threadIdx.x; j < iters * kNSub; j += 64) {
+  for (uint32_t j = threadIdx.x; j < (iters + 2u) * kNSub; j += 64) {  // (+2: P(iters + 1) holds the merged path-2 primaries)
     const uint32_t k = j / kNSub, s = j % kNSub;
     seg += ctr[((k * 2u + 0u) * kNSub + s) * kCtrStride];
     sh += ctr[((k * 2u + 1u) * kNSub + s) * kCtrStride];
@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(kBlock) k_accumulate(TileMap M, int32_t frames
                                                        Counters* __restrict__ totals) {
   if (totals && blockIdx.x == 0 && threadIdx.x < 64) {
     unsigned long long seg = 0, sh = 0;
-    for (uint32_t j = threadIdx.x; j < iters * kNSub; j += 64) {
+    for (uint32_t j = threadIdx.x; j < (iters + 2u) * kNSub; j += 64) {  // (+2: P(iters + 1) holds the merged path-2 primaries)
       const uint32_t k = j / kNSub, s = j % kNSub;
       seg += ctr[((k * 2u + 0u) * kNSub + s) * kCtrStride];
       sh += ctr[((k * 2u + 1u) * kNSub + s) * kCtrStride];

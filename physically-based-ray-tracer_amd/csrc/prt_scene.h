@@ -82,7 +82,7 @@ struct SceneDev {
   float basis[9];  // right, up, ahead (Core/Camera.h:17)
   float pan_b, pan_d;
   int32_t panini;
-  int32_t pool_ok;  // TriMT indices fit the traversal's 26-bit triangle-pool entries (prt_persist.h POOL)
+  int32_t pad1;
   // extensions beyond the reference's Trace: one area light, dielectric instances
   float al[16];     // p0, eu, ev, n = normalize(cross(eu, ev)), Le, area
   int32_t area;     // 1 = the area light is set

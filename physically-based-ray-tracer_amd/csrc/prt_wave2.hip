@@ -51,12 +51,17 @@ void lane_stats_dump() {
 }
 #endif
 
-// ---- init: items -> primary rays, appended to queue 0 (sub-queue = block % kNSub)
+// the merged pipeline's queue of path-2 primaries: the counters of iteration iters + 1 (kind 0), never a path queue
+__device__ __forceinline__ uint32_t q2_iter(const TraceArgs& A) { return 2u * (uint32_t)A.bounces; }
+
+// ---- init: items -> primary rays, appended to queue 0 (sub-queue = block % kNSub).  Merged pipeline (B.merge):
+// the AA path-2 primary ray too (its jitter is drawn here, :61), into ro2 / rd2 and the path-2 queue Q2 (shq)
 __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, TileMap M, WaveBufs B,
                                                       float4* __restrict__ out) {
   __shared__ uint32_t sm[8];
   const uint32_t sub = blockIdx.x % kNSub;
   uint32_t* cnt = qcounter(B.ctr, 0, 0, sub);
+  uint32_t* cnt2 = qcounter(B.ctr, q2_iter(A), 0, sub);
   for (uint32_t c = blockIdx.x; c * kBlock < B.n; c += gridDim.x) {
     const uint32_t i = c * kBlock + threadIdx.x;
     bool enq = false;
@@ -77,13 +82,28 @@ __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, T
         B.rd[i] = make_float4(r1.D.x, r1.D.y, r1.D.z, 0.0f);
         B.info[i] = 0u;
         B.s1[i] = make_float4(0.0f, 0.0f, 0.0f, kFar);
+        if (B.merge) {
+          const Ray r2 = primary_ray(S, (float)x + jx, (float)y + jy, A.W, A.H);
+          B.ro2[i] = make_float4(r2.O.x, r2.O.y, r2.O.z, 0.0f);
+          B.rd2[i] = make_float4(r2.D.x, r2.D.y, r2.D.z, 0.0f);
+          B.rinfo[i] = 0u;
+          B.rinfo[B.n + i] = 0u;
+        }
         enq = true;
       } else {
         out[i] = make_float4(0.0f, 0.0f, 0.0f, kFar);  // bounces == 0: Trace returns 0, t1 stays BVH_FAR
+        if (B.merge) {
+          B.rinfo[i] = 0u;
+          B.rinfo[B.n + i] = 0u;
+        }
       }
     }
     const uint32_t slot = block_append(cnt, enq ? 1u : 0u, sm);
     if (enq) B.q0[sub * B.qcap + slot] = i;
+    if (B.merge) {
+      const uint32_t s2 = block_append(cnt2, enq ? 1u : 0u, sm);
+      if (enq) B.shq[sub * B.scap + s2] = i;
+    }
   }
 }
 
@@ -115,15 +135,18 @@ __device__ __forceinline__ uint32_t shadow_vis(const WaveBufs& B, uint32_t code)
 }
 
 // ---- one traversal launch: closest hits of P(iter) (iter < iters) + any hits of S(iter - 1) (iter > 0)
-template <int REFILL, int STACK, int WAVES, int TAILN, bool TLAS, bool SPILL = false, int POOL = 0>
+template <int REFILL, int STACK, int WAVES, int TAILN, bool TLAS, bool SPILL = false>
 __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, uint32_t iter, uint32_t iters) {
   __shared__ uint32_t lds_stack[2 * STACK * 64];
   __shared__ uint32_t prefP[kNSub + 1], prefS[kNSub + 1];
-  __shared__ __attribute__((aligned(8))) uint32_t tail_lds[tail_pool_words(TAILN, POOL)];
+  __shared__ uint32_t tail_lds[tail_lds_words(TAILN)];
   uint8_t* vis8 = reinterpret_cast<uint8_t*>(B.vis);
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
   const uint32_t nP = iter < iters ? load_prefix(B.ctr, iter, 0, prefP) : 0u;
-  const uint32_t nS = iter > 0 ? load_prefix(B.ctr, iter - 1, 1, prefS) : 0u;
+  // merged pipeline, iteration 0: the second segment is the path-2 primaries (Q2, in shq; closest hits -> hit2)
+  const bool q2 = iter == 0 && B.merge;
+  const uint32_t nS = iter > 0 ? load_prefix(B.ctr, iter - 1, 1, prefS)
+                               : (q2 ? load_prefix(B.ctr, iters + 1, 0, prefS) : 0u);
   const uint32_t total = nP + nS;
   if (blockIdx.x * 64u >= total) return;
   uint32_t* fctr = fetch_counters(B.ctr, iter, 0);
@@ -133,7 +156,7 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
   unsigned long long* tl = B.tl ? B.tl + ((size_t)iter * kTlWaves + blockIdx.x) * 4 : nullptr;
   bool seen_drain = false;
   if (tl && threadIdx.x == 0) tl[0] = __builtin_amdgcn_s_memrealtime();
-  trav8_persistent<2, STACK, REFILL, TAILN, TLAS, SPILL, POOL>(
+  trav8_persistent<2, STACK, REFILL, TAILN, TLAS, SPILL>(
       S, lds_stack + threadIdx.x,
       [&](uint32_t* base, uint32_t want) {
         const uint32_t got = fetch_some(fctr, total, part, base, want);
@@ -156,6 +179,13 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
           d = B.rd[h];
           tmax = kFar;
           any = false;
+        } else if (q2) {  // a path-2 primary ray: handle = item | 1 << 31
+          h = B.shq[map_slot(prefS, g - nP, B.scap)];
+          o = B.ro2[h];
+          d = B.rd2[h];
+          tmax = kFar;
+          any = false;
+          h |= 0x80000000u;
         } else {
           h = map_slot(prefS, g - nP, B.scap);
           any = true;
@@ -172,7 +202,8 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
           shadow_of(S, B, B.shq[h], O, D, tmax);
           return;
         }
-        const float4 o = B.ro[h], d = B.rd[h];
+        const bool p2 = (h & 0x80000000u) != 0u;
+        const float4 o = p2 ? B.ro2[h & 0x7FFFFFFFu] : B.ro[h], d = p2 ? B.rd2[h & 0x7FFFFFFFu] : B.rd[h];
         O = v3(o.x, o.y, o.z);
         D = v3(d.x, d.y, d.z);
       },
@@ -180,14 +211,16 @@ __global__ void __launch_bounds__(64, WAVES) k_trace2(SceneDev S, WaveBufs B, ui
         if (any) {
           if (!occluded) vis8[shadow_vis(B, B.shq[h])] = 1;
         } else {
-          B.hit[h] = make_float4(hit.t, hit.u, hit.v, __uint_as_float(pack_hit(S, hit.prim, hit.inst)));
+          const float4 rec = make_float4(hit.t, hit.u, hit.v, __uint_as_float(pack_hit(S, hit.prim, hit.inst)));
+          if (h & 0x80000000u) B.hit2[h & 0x7FFFFFFFu] = rec;
+          else B.hit[h] = rec;
         }
       },
       [&]() -> bool { return __hip_atomic_load(dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u; },
 #ifdef PRT_LANE_STATS
-      B.coop_tail ? tail_lds : nullptr, g_lane_stats + 32 * iter, tail_lds);
+      B.coop_tail ? tail_lds : nullptr, g_lane_stats + 32 * iter);
 #else
-      B.coop_tail ? tail_lds : nullptr, tl ? tl + 3 : nullptr, tail_lds);
+      B.coop_tail ? tail_lds : nullptr, tl ? tl + 3 : nullptr);
 #endif
   if (tl && threadIdx.x == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
@@ -445,6 +478,124 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
   }
 }
 
+// ---- merged pipeline (B.merge: AA, render mode 0, no extensions).  Shading of P(iter) as k_shade2<false>, each
+// path's records (hit point, NEE record, status, (result, throughput) stack) in its own slot (slot = path, at
+// slot * n + item), and where path 1 ends its item shades path 2's first segment at once, from the primary hit
+// k_trace2(0) traced next to path 1's: the RNG stream continues from path 1's last draw exactly as if path 2's
+// primary ray had been traced after path 1 ended, so the result is the same bit for bit and
+// a frame needs one wavefront iteration (a traversal, a shading and a resolve launch) fewer.
+__global__ void __launch_bounds__(kBlock, 1) k_shade2m(SceneDev S, TraceArgs A, TileMap M, WaveBufs B, uint32_t iter) {
+  const Shade2ArgsPtr args = (Shade2ArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  if (args->iter != iter || args->B.n != B.n) {  // the Shade2Args layout does not match this compiler's: fail
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(S.diag + 1, 1u);
+    return;
+  }
+  __shared__ uint32_t pref[kNSub + 1];
+  __shared__ uint32_t sm[8];
+  const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
+  uint32_t* qn = (iter & 1) ? B.q0 : B.q1;
+  const uint32_t sub = blockIdx.x % kNSub;
+  uint32_t* shcnt = qcounter(B.ctr, iter, 1, sub);
+  uint32_t* ncnt = qcounter(B.ctr, iter + 1, 0, sub);
+  uint32_t* shq = B.shq + (size_t)sub * B.scap;
+  const uint32_t total = load_prefix(B.ctr, iter, 0, pref);
+  const uint32_t fl = A.flags;
+  const uint32_t levels = (uint32_t)max(1, A.bounces - 1);
+  uint32_t item_n = 0, info_n = 0, seed_n = 0;
+  float4 hh_n = make_float4(kFar, 0.0f, 0.0f, 0.0f);
+  auto prefetch = [&](uint32_t cc) {
+    const uint32_t gg = cc * kBlock + threadIdx.x;
+    if (gg < total) {
+      item_n = q[map_slot(pref, gg, B.qcap)];
+      info_n = B.info[item_n];
+      hh_n = B.hit[item_n];
+      seed_n = B.seed[item_n];
+    }
+  };
+  prefetch(blockIdx.x);
+  for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    Shade2ArgsPtr ka = args;  // descriptors from the kernarg segment per chunk (k_shade2)
+    asm volatile("" : "+s"(ka));
+    const SceneDev& Sc = *(const SceneDev*)&ka->S;
+    const WaveBufs& Bc = *(const WaveBufs*)&ka->B;
+    const uint32_t g = c * kBlock + threadIdx.x;
+    const bool active = g < total;
+    uint32_t item = 0, info = 0, seed = 0;
+    float4 hh = make_float4(kFar, 0.0f, 0.0f, 0.0f);
+    if (active) { item = item_n; info = info_n; hh = hh_n; seed = seed_n; }
+    prefetch(c + gridDim.x);
+    bool next = false, need2 = false;
+#pragma unroll 1
+    for (int pass = 0; pass < 2; pass++) {
+      const bool act = pass == 0 ? active : need2;
+      if (pass == 1 && act) { info = 1u << 8; hh = Bc.hit2[item]; }          // path 2, depth 0: its primary hit
+      const uint32_t depth = info & 0xFFu, path = (info >> 8) & 1u;
+      const size_t sn = (size_t)path * Bc.n + item;                         // this path's record slot
+      const float4* rop = pass ? Bc.ro2 : Bc.ro;
+      const float4* rdp = pass ? Bc.rd2 : Bc.rd;
+      int kind = 0;
+      uint32_t nr = 0;
+      if (act) {
+        if ((info & 0x1FFu) == 0) Bc.s1[item].w = hh.x;                                     // r1.hit.t
+        if (hh.x >= kFar) {  // a miss (:159): the sky radiance (or 0) ends the path
+          V3 L = v3(0.0f, 0.0f, 0.0f);
+          if (fl & kSkybox) {
+            const float4 d = rdp[item];
+            L = sample_sky_call(Sc.sky, Sc.skyw, Sc.skyh, v3(d.x, d.y, d.z));
+          }
+          Bc.ne[sn] = make_float4(L.x, L.y, L.z, 0.0f);
+        } else {
+          kind = nee_kind(fl, seed);                                                        // :198-214
+          nr = (uint32_t)nee_rays(kind);
+        }
+      }
+      const uint32_t s0 = block_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic per pass
+      uint32_t status = kStMiss, emissive = 0;
+      if (nr) {
+        const float4 o = rop[item], d = rdp[item];
+        const V3 D = v3(d.x, d.y, d.z);
+        const uint32_t pk = __float_as_uint(hh.w);
+        const V3 I = v3(o.x, o.y, o.z) + hh.x * D;                                           // tiny_bvh.h:586
+        const V3 V = -D;
+        const HitAttr ha = hit_attributes(Sc, hit_inst(Sc, pk), hit_prim(Sc, pk), hh.y, hh.z, (fl & kNormalMap) != 0);
+        Bc.hp[sn] = make_float4(I.x, I.y, I.z, 0.0f);
+        float4 nk;
+        const V3 brdf = nee_lights(Sc, fl, kind, I, V, ha.N, ha.m, seed, nk, [&](int k, uint32_t light) {
+          shq[s0 + k] = (light << 29) | (4u * (uint32_t)sn + (uint32_t)k);
+        });
+        const V3 e = v3(0.0f, 0.0f, 0.0f) + v3(1.0f, 1.0f, 1.0f) * ha.m.emis;                // :196
+        if (e.x != 0.0f || e.y != 0.0f || e.z != 0.0f) {
+          Bc.ne[sn] = make_float4(e.x, e.y, e.z, 0.0f);
+          emissive = kRiEmissive;
+        }
+        Bc.nb[sn] = make_float4(brdf.x, brdf.y, brdf.z, 0.0f);
+        Bc.nk[sn] = nk;
+        Bc.vis[sn] = 0u;
+        status = kStNeeEnd;
+        if ((int)depth != A.bounces - 1) {                                                   // :329
+          V3 dir, thr;
+          if (sample_bounce(ha.m, V, ha.N, seed, dir, thr)) {                               // :376-399
+            status = kStNeeCont;
+            Bc.T[((size_t)path * levels + depth) * Bc.n + item] = make_float4(thr.x, thr.y, thr.z, 0.0f);
+            const Ray nr2 = make_ray(I + dir * kEpsilon, dir);                               // :404
+            Bc.ro[item] = make_float4(nr2.O.x, nr2.O.y, nr2.O.z, 0.0f);
+            Bc.rd[item] = make_float4(nr2.D.x, nr2.D.y, nr2.D.z, 0.0f);
+            Bc.info[item] = (depth + 1u) | (path << 8);
+            next = true;
+          }
+        }
+        Bc.seed[item] = seed;
+      }
+      if (act) {
+        Bc.rinfo[sn] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20) | emissive | kRiFresh;
+        need2 = pass == 0 && path == 0 && status != kStNeeCont && (fl & kAA);
+      }
+    }
+    const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
+    if (next) qn[sub * Bc.qcap + slot] = item;
+  }
+}
+
 // ---- debug render modes (:170-194): the hit's debug colour (or the sky) ends the path
 __global__ void __launch_bounds__(kBlock) k_shade2_debug(SceneDev S, TraceArgs A, TileMap M, WaveBufs B,
                                                          uint32_t iter) {
@@ -581,25 +732,87 @@ __global__ void __launch_bounds__(kBlock) k_resmiss2(SceneDev S, TraceArgs A, Wa
   }
 }
 
+// ---- merged pipeline: the resolve of P(iter - 1) per record slot (path 1's, then path 2's), as resolve_item<false>
+__device__ __forceinline__ void resolve_slot(const SceneDev& S, const TraceArgs& A, const WaveBufs& B, uint32_t item,
+                                             uint32_t path, uint32_t ri, float4* __restrict__ out) {
+  const uint32_t fl = A.flags;
+  const uint32_t levels = (uint32_t)max(1, A.bounces - 1);
+  const size_t sn = (size_t)path * B.n + item;
+  const uint32_t depth = ri & 0xFFu, status = (ri >> 16) & 3u, kind = (ri >> 20) & 3u;
+  const bool nee = status == kStNeeEnd || status == kStNeeCont;
+  const float4 ne = (!nee || (ri & kRiEmissive)) ? B.ne[sn] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  V3 L = v3(ne.x, ne.y, ne.z);
+  if (nee) {
+    const float4 nb = B.nb[sn], nk = B.nk[sn];
+    const uint32_t vw = B.vis[sn];
+    const uint32_t vis = ((vw & 0xFFu) ? 1u : 0u) | ((vw & 0xFF00u) ? 2u : 0u) | ((vw & 0xFF0000u) ? 4u : 0u) |
+                         ((vw & 0xFF000000u) ? 8u : 0u);
+    const V3 result = nee_resolve(S, (int)kind, vis, L, v3(nb.x, nb.y, nb.z), nk, fl);
+    if (status == kStNeeCont) {  // the path goes on: result joins its stack
+      B.R[((size_t)path * levels + depth) * B.n + item] = make_float4(result.x, result.y, result.z, 0.0f);
+      return;
+    }
+    L = result;
+  }
+  for (int k = (int)depth - 1; k >= 0; k--) {                                              // result + Trace(..) * throughput
+    const size_t e = ((size_t)path * levels + (uint32_t)k) * B.n + item;
+    const float4 Rk = B.R[e], Tk = B.T[e];
+    L = v3(Rk.x, Rk.y, Rk.z) + L * v3(Tk.x, Tk.y, Tk.z);
+  }
+  const float4 s1 = B.s1[item];
+  if (path == 0 && (fl & kAA)) {  // path 2 follows (shaded in the same iteration); keep path 1's radiance
+    B.s1[item] = make_float4(L.x, L.y, L.z, s1.w);
+  } else {
+    V3 res = (fl & kAA) ? 0.5f * (v3(s1.x, s1.y, s1.z) + L) : L;                           // :65
+    if (fl & kGamma) res = v3(sqrtf(res.x), sqrtf(res.y), sqrtf(res.z));                  // :73-79
+    out[item] = make_float4(res.x, res.y, res.z, s1.w);
+  }
+}
+__global__ void __launch_bounds__(kBlock) k_resmiss2m(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter,
+                                                      float4* __restrict__ out) {
+  __shared__ uint32_t pref[kNSub + 1];
+  const uint32_t* q = ((iter - 1) & 1) ? B.q1 : B.q0;
+  const uint32_t total = load_prefix(B.ctr, iter - 1, 0, pref);
+  uint32_t item_n = 0, r0_n = 0, r1_n = 0;
+  auto prefetch = [&](uint32_t cc) {
+    const uint32_t gg = cc * kBlock + threadIdx.x;
+    if (gg < total) {
+      item_n = q[map_slot(pref, gg, B.qcap)];
+      r0_n = B.rinfo[item_n];
+      r1_n = B.rinfo[B.n + item_n];
+    }
+  };
+  prefetch(blockIdx.x);
+  for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    const uint32_t g = c * kBlock + threadIdx.x;
+    const uint32_t item = item_n, r0 = r0_n, r1 = r1_n;
+    prefetch(c + gridDim.x);
+    if (g >= total) continue;
+    if (r0 & kRiFresh) {
+      resolve_slot(S, A, B, item, 0u, r0, out);
+      B.rinfo[item] = r0 & ~kRiFresh;
+    }
+    if (r1 & kRiFresh) {
+      resolve_slot(S, A, B, item, 1u, r1, out);
+      B.rinfo[B.n + item] = r1 & ~kRiFresh;
+    }
+  }
+}
+
 // LDS per wave (one block): 2 x STACK x 256 B of stack + 264 B of prefix tables + the tail slots, within
 // 160 KB / (4 x WAVES) blocks per CU
 #ifndef PRT_REFILL
 #define PRT_REFILL 32  // idle lanes before a wave refills from the queue (A/B builds: -DPRT_REFILL=16 ...)
 #endif
-// PRT_POOL: triangle-pool entries of the 7-wave traversal (prt_persist.h; 0 = one triangle per lane per iteration)
-#ifndef PRT_POOL
-#define PRT_POOL 0
-#endif
-template <int STACK, int WAVES, int TAILN, int POOL = 0>
+template <int STACK, int WAVES, int TAILN>
 void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
-  static_assert(2 * STACK * 256 + 264 + 4 * tail_pool_words(TAILN, POOL) <= 163840 / (4 * WAVES),
-                "LDS over the occupancy budget");
+  static_assert(2 * STACK * 256 + 264 + 4 * 3 * TAILN <= 163840 / (4 * WAVES), "LDS over the occupancy budget");
   if (S.tlas)
-    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, true, false, POOL>), dim3(256u * 4u * WAVES / c.groups),
-                       dim3(64), 0, c.stream, S, B, it, iters);
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, true>), dim3(256u * 4u * WAVES / c.groups), dim3(64), 0,
+                       c.stream, S, B, it, iters);
   else
-    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, false, false, POOL>), dim3(256u * 4u * WAVES / c.groups),
-                       dim3(64), 0, c.stream, S, B, it, iters);
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, false>), dim3(256u * 4u * WAVES / c.groups), dim3(64), 0,
+                       c.stream, S, B, it, iters);
 }
 // persistent traversal occupancy (waves/SIMD) -> LDS stack groups per lane; a BVH deeper than the 18 LDS
 // groups at 4 waves/SIMD hold runs the 4-wave form with the HBM spill columns (S.spill)
@@ -612,7 +825,6 @@ static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs&
       hipLaunchKernelGGL((k_trace2<32, 18, 4, 32, false, true>), dim3(kSpillTraceBlocks / c.groups), dim3(64), 0,
                          c.stream, S, B, it, iters);
   } else if (c.occ == 8) launch_t2<8, 8, 32>(c, S, B, it, iters);
-  else if (c.occ == 7 && PRT_POOL > 0 && S.pool_ok) launch_t2<9, 7, 64, PRT_POOL>(c, S, B, it, iters);
   else if (c.occ == 7) launch_t2<9, 7, 64>(c, S, B, it, iters);
   else if (c.occ == 6) launch_t2<11, 6, 64>(c, S, B, it, iters);
   else if (c.occ == 5) launch_t2<14, 5, 32>(c, S, B, it, iters);
@@ -635,7 +847,7 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
   static_assert(PRT_SHADE_GRID % kNSub == 0, "PRT_SHADE_GRID must be a multiple of kNSub");
   const unsigned gshade = PRT_SHADE_GRID;
 #endif
-  const uint32_t iters = wave_iters(S.has_diel != 0, A.bounces, A.flags);
+  const uint32_t iters = wave_iters(S.has_diel != 0, A.bounces, A.flags, B.merge != 0);
   if (tm) (void)hipEventRecord(tm->ev[4 * it + 0], c.stream);
   launch_trace2(c, S, B, it, iters);
   if (tm) (void)hipEventRecord(tm->ev[4 * it + 1], c.stream);
@@ -648,7 +860,9 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
 #else
   const unsigned gres = PRT_RES_GRID;  // A/B
 #endif
-  if (it > 0) {  // resolve of P(it - 1) (+ misses of P(it)), one pass
+  if (it > 0 && B.merge) {
+    hipLaunchKernelGGL(k_resmiss2m, dim3(gres), dim3(kBlock), 0, c.stream, S, A, B, it, out);
+  } else if (it > 0) {  // resolve of P(it - 1) (+ misses of P(it)), one pass
     if (ext) hipLaunchKernelGGL(k_resmiss2<true>, dim3(gres), dim3(kBlock), 0, c.stream, S, A, B, it, iters, sep_miss,
                                 out);
     else hipLaunchKernelGGL(k_resmiss2<false>, dim3(gres), dim3(kBlock), 0, c.stream, S, A, B, it, iters, sep_miss,
@@ -658,7 +872,8 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
     else hipLaunchKernelGGL(k_miss2<false>, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, B, it);
   }
   if (it < iters) {
-    if (A.mode != 0) hipLaunchKernelGGL(k_shade2_debug, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
+    if (B.merge) hipLaunchKernelGGL(k_shade2m, dim3(gshade), dim3(kBlock), 0, c.stream, S, A, M, B, it);
+    else if (A.mode != 0) hipLaunchKernelGGL(k_shade2_debug, dim3(gprod), dim3(kBlock), 0, c.stream, S, A, M, B, it);
     else if (ext) hipLaunchKernelGGL(k_shade2<true>, dim3(gshade), dim3(kBlock), 0, c.stream, S, A, M, B, it);
     else hipLaunchKernelGGL(k_shade2<false>, dim3(gshade), dim3(kBlock), 0, c.stream, S, A, M, B, it);
   }

@@ -517,7 +517,7 @@ def test_device_tlas_moving_instances(gpu_ctx, monkeypatch, n):
 def test_device_tlas_rebuild_long_motion(gpu_ctx, monkeypatch):
     """1,000 tori drift across the field for 120 frames (every instance moves before every frame, the
     frames queued back to back with device outputs and no host wait).  The refitted instance BVH degrades; once its
-    SAH cost (measured on the device after every refit, read back without a wait) exceeds 1.2x its cost after the
+    node-area cost (measured on the device after every refit, read back without a wait) exceeds 1.1x its cost after the
     last build, the topology is rebuilt on the device (gpu_build_tlas8: PLOC + SAH-optimal collapse).  Every 10th
     frame equals the oracle's render of that frame's transforms, and at least one device rebuild happened."""
     import dataclasses
@@ -616,5 +616,40 @@ def test_item_groups_world8_share_c4(gpu_ctx, monkeypatch):
             torch.cuda.synchronize()
             assert torch.equal(t, ref)
             assert (st.segments, st.shadow_rays) == (s0.segments, s0.shadow_rays)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("spp,bounces", [(2, 1), (4, 2), (4, 4), (6, 3)])
+def test_merged_pipeline_matches_unmerged(gpu_ctx, monkeypatch, spp, bounces):
+    """The merged pipeline (default for AA frames of render mode 0 without extensions; prt_wave2.hip k_shade2m):
+    path 2's primary ray is traced in the first launch beside path 1's and its first segment is shaded in the
+    iteration path 1 ends in, on the same RNG stream -- frames (accumulating), ray counts and tiles bit-identical to
+    the unmerged pipeline (PRT_MERGE=0), which the oracle tests pin."""
+    import torch
+    import prt
+    sd = scenes.multi_instance(scenes.config_small(60, 40))
+    W, H = 100, 70
+    monkeypatch.setenv("PRT_MERGE", "0")
+    gpu_scene(gpu_ctx, sd, W, H)
+    ref = [gpu_ctx.render(W, H, spp, bounces, frame_index=spp * i) for i in range(2)]
+    per = gpu_ctx.tile_buffer_pixels(W, H, 16, 3)
+    t_ref = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
+    gpu_ctx.reset_accumulation(full=True)
+    gpu_ctx.render_tiles(W, H, spp, bounces, 16, 1, 3, t_ref.data_ptr())
+    monkeypatch.delenv("PRT_MERGE")
+    c = prt.Context(0)
+    try:
+        gpu_scene(c, sd, W, H)
+        for i, (ea, er, es) in enumerate(ref):
+            a, r, st = c.render(W, H, spp, bounces, frame_index=spp * i)
+            assert np.array_equal(a, ea) and np.array_equal(r, er), i
+            assert (st.segments, st.shadow_rays, st.paths) == (es.segments, es.shadow_rays, es.paths)
+            assert st.iterations == es.iterations - 1  # one traversal launch fewer
+        c.reset_accumulation(full=True)
+        t = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
+        c.render_tiles(W, H, spp, bounces, 16, 1, 3, t.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(t, t_ref)
     finally:
         c.close()
