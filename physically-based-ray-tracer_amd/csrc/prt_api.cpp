@@ -143,6 +143,7 @@ struct prt_ctx {
   double tlas_base_cost = 0.0;    // [0] once read
   uint32_t tlas_nodes = 0;
   int32_t tlas_rebuilds = 0, tlas_refits = 0;  // since the instance count last changed (diagnostics)
+  int32_t tlas_since_build = 0;                 // refits since the last build
   DevBuf spill;  // traversal stack levels beyond the LDS ones (BVHs deeper than 17 levels)
   DevBuf diag;   // SceneDev::diag device counters ([0] traversal stack overflows, cumulative per context)
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
@@ -262,13 +263,17 @@ int ensure_instances(prt_ctx* c) {
   // builds it when the set of instances changes (its count; or every call with PRT_TLAS_HOST=1, the A/B form);
   // otherwise it is refitted on the device behind k_refit (prt_tlas.hip), and rebuilt on the device (PLOC +
   // SAH-optimal collapse over the current boxes, gpu_build_tlas8) once refitting has raised the tree's node-area
-  // cost above PRT_TLAS_REBUILD (default 1.1) times its cost right after the last build (0: refit only).  The cost is
+  // cost above PRT_TLAS_REBUILD (default 1.05) times its cost right after the last build (0: refit only).  The cost is
   // measured on the device after every refit and read back without a host wait (a pinned copy behind an event):
   // a frame decides on the latest cost already available.  No host BVH work and no host wait per frame.
   const char* th = std::getenv("PRT_TLAS_HOST");
   const char* tr = std::getenv("PRT_TLAS_REBUILD");
   const bool rebuild_always = tr && std::strcmp(tr, "always") == 0;  // A/B: a device rebuild for every update
-  const double rebuild_ratio = rebuild_always ? 0.0 : (tr ? std::atof(tr) : 1.1);
+  const double rebuild_ratio = rebuild_always ? 0.0 : (tr ? std::atof(tr) : 1.05);
+  // and at the latest after PRT_TLAS_MAX_REFITS refits (default 8): the node-area cost understates what a node
+  // stretched across the scene costs the rays that must now open it
+  const char* tm = std::getenv("PRT_TLAS_MAX_REFITS");
+  const int32_t max_refits = tm ? std::atoi(tm) : 8;
   auto upload_order = [&]() -> int {
     const size_t ob = 4 * c->tlas_topo.order.size(), ab = 24 * std::max<size_t>(c->tlas_nodes, 1);
     if (c->tlas_order.bytes < ob || c->tlas_aabb.bytes < ab) {
@@ -302,7 +307,8 @@ int ensure_instances(prt_ctx* c) {
     return PRT_OK;
   };
   if (c->use_tlas && c->tlas_n == n && !(th && std::atoi(th) == 1)) {
-    bool rebuild = rebuild_always;
+    bool rebuild = rebuild_always ||
+                   (rebuild_ratio > 0 && max_refits > 0 && c->tlas_since_build >= max_refits);
     if (rebuild_ratio > 0) {
       for (int k = 0; k < 2; k++)  // costs whose copies have landed (never waits)
         if (c->tlas_cost_pending[k] && hipEventQuery(c->tlas_cost_ev[k]) == hipSuccess) {
@@ -317,7 +323,11 @@ int ensure_instances(prt_ctx* c) {
       // into the back buffers: the frames already queued keep walking the current tree, the host waits only for
       // the build's own steps
       if (!c->tlas_stream) {
-        HIP_TRY(hipStreamCreateWithFlags(&c->tlas_stream, hipStreamNonBlocking));
+        // the highest stream priority: the build's short dependent launches are dispatched ahead of the render
+        // stream's queued work as CUs free up, so the host's waits on the build stay short
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&c->tlas_stream, hipStreamNonBlocking, hi));
         HIP_TRY(hipEventCreateWithFlags(&c->tlas_built, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&c->tlas_back_free, hipEventDisableTiming));
       }
@@ -370,10 +380,12 @@ int ensure_instances(prt_ctx* c) {
       rc = measure_cost(0);
       if (rc) return rc;
       c->tlas_rebuilds++;
+      c->tlas_since_build = 0;
     } else {
       int rc = refit_tree();
       if (rc) return rc;
       c->tlas_refits++;
+      c->tlas_since_build++;
       if (!c->tlas_cost_pending[1]) {  // at most one refit cost in flight
         rc = measure_cost(1);
         if (rc) return rc;
@@ -403,6 +415,7 @@ int ensure_instances(prt_ctx* c) {
     int rc = upload_order();
     if (rc) return rc;
     if (c->tlas_n != n) c->tlas_rebuilds = c->tlas_refits = 0;
+    c->tlas_since_build = 0;
     c->tlas_n = n;
     if (rebuild_ratio > 0 && !(th && std::atoi(th) == 1)) {  // the cost right after the build (its refit's boxes)
       rc = refit_tree();
@@ -639,13 +652,20 @@ struct RenderPlan {
   uint32_t groups = 1;
 };
 
-// the merged pipeline (prt_wave2.hip k_shade2m): AA frames of render mode 0 without extensions; PRT_MERGE=0 turns it
-// off (A/B).  Its shadow-queue entries index 4 x (slot x n + item) + k in 29 bits: at most 2^26 items per pass
+// The merged pipeline (prt_wave2.hip k_shade2m): AA frames of render mode 0 without extensions, in calls small
+// enough that their traversal launches are bound by their slowest rays (one launch fewer per frame: world-8 share
+// of C4 1.83-1.87 -> 1.74-1.77 ms), not by throughput (the path-2 first segments shaded in partly filled waves
+// cost a full C4 frame 1.5 %).  PRT_MERGE=0 / 1 forces it off / on; PRT_MERGE_MAX_ITEMS sets the size limit
+// (default 2^21 items per call).  Its shadow-queue entries index 4 x (slot x n + item) + k in 29 bits: at most 2^26
+// items per pass.
 constexpr uint64_t kMaxMergedPassItems = 1ull << 26;
 bool merge_for(const prt_render_params* p, bool ext, uint64_t per) {
+  const bool ok = !ext && p->render_mode == 0 && (p->flags & PRT_FLAG_AA) && p->bounces > 0 && per <= kMaxMergedPassItems;
   const char* e = std::getenv("PRT_MERGE");
-  if (e && std::atoi(e) == 0) return false;
-  return !ext && p->render_mode == 0 && (p->flags & PRT_FLAG_AA) && p->bounces > 0 && per <= kMaxMergedPassItems;
+  if (e) return ok && std::atoi(e) != 0;
+  const char* m = std::getenv("PRT_MERGE_MAX_ITEMS");
+  const uint64_t cap = m ? std::strtoull(m, nullptr, 10) : (1ull << 21);
+  return ok && per * (uint64_t)frames_of(p) <= cap;
 }
 
 // Concurrent item groups.  A call small enough that its traversal launches are bound by their
