@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -548,15 +549,13 @@ struct Task {
   uint32_t n8;  // wide node slot
 };
 
-__global__ void __launch_bounds__(kB) k_collapse(const float4* __restrict__ tri, const unsigned long long* __restrict__ keys,
-                                                 int n, const int* __restrict__ left, const int* __restrict__ right,
-                                                 const float* __restrict__ box, const uint32_t* __restrict__ first,
-                                                 const uint32_t* __restrict__ count, int max_leaf,
-                                                 const Task* __restrict__ tasks, uint32_t ntasks, Task* next,
-                                                 uint32_t* ctr, Node8* nodes, TriMT* tris, DpTab dp) {
-  const uint32_t t = blockIdx.x * kB + threadIdx.x;
-  if (t >= ntasks) return;
-  const Task tk = tasks[t];
+// one wide node of the collapse: task tk (binary node -> wide node slot); the next level's tasks go to next
+__device__ __forceinline__ void collapse_task(const Task tk, const float4* __restrict__ tri,
+                                              const unsigned long long* __restrict__ keys, int n,
+                                              const int* __restrict__ left, const int* __restrict__ right,
+                                              const float* __restrict__ box, const uint32_t* __restrict__ first,
+                                              const uint32_t* __restrict__ count, int max_leaf, Task* next,
+                                              uint32_t* ctr, Node8* nodes, TriMT* tris, const DpTab& dp) {
   const int nn = 2 * n - 1;
   if (tk.n2 < 0 || tk.n2 >= nn || tk.n8 >= (uint32_t)n) { atomicOr(ctr + 3, 0x80000000u); return; }
   // a child slot's form: leaf (all its triangles) or a wide node of its own
@@ -719,6 +718,233 @@ __global__ void __launch_bounds__(kB) k_collapse(const float4* __restrict__ tri,
     }
   }
   nodes[tk.n8] = nd;
+}
+
+__global__ void __launch_bounds__(kB) k_collapse(const float4* __restrict__ tri, const unsigned long long* __restrict__ keys,
+                                                 int n, const int* __restrict__ left, const int* __restrict__ right,
+                                                 const float* __restrict__ box, const uint32_t* __restrict__ first,
+                                                 const uint32_t* __restrict__ count, int max_leaf,
+                                                 const Task* __restrict__ tasks, uint32_t ntasks, Task* next,
+                                                 uint32_t* ctr, Node8* nodes, TriMT* tris, DpTab dp) {
+  const uint32_t t = blockIdx.x * kB + threadIdx.x;
+  if (t >= ntasks) return;
+  collapse_task(tasks[t], tri, keys, n, left, right, box, first, count, max_leaf, next, ctr, nodes, tris, dp);
+}
+
+// ---- single-workgroup build for small inputs (the instance BVH's per-frame rebuild): the same steps in one launch,
+// with no host round trip -- Morton keys bitonic-sorted in LDS, PLOC over the clusters' boxes in LDS (iterations
+// separated by barriers instead of launches), the SAH-optimal collapse level by level behind barriers.  The
+// scratch arrays are the multi-launch builder's (global, touched by this one workgroup only: plain loads see the
+// workgroup's own stores after a barrier).
+constexpr int kSmallThreads = 1024;
+constexpr int kSmallR = 512;  // PLOC search radius (as the instance BVH's multi-launch build)
+struct SmallScratch {
+  unsigned long long* keys;  // n sorted keys
+  int *left, *right;         // 2n - 1
+  uint32_t* count;           // 2n - 1
+  float* box;                // 6 (2n - 1)
+  DpTab dp;                  // 8 (n - 1) doubles, n - 1 decisions
+  Task *ta, *tb;             // n each
+  uint32_t* ctr;             // 4
+};
+
+// exclusive prefix sum of one value per thread over the workgroup; *total = the sum
+__device__ __forceinline__ uint32_t small_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t x = v;
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+  for (uint32_t k = 0; k < kSmallThreads / 64; k++) {
+    before += k < w ? wsum[k] : 0u;
+    all += wsum[k];
+  }
+  __syncthreads();
+  *total = all;
+  return before + x - v;
+}
+
+__global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __restrict__ tri, int n, int max_leaf,
+                                                               SmallScratch sc, Node8* nodes, TriMT* tris,
+                                                               uint32_t* out, uint32_t* level_end, int max_levels) {
+  __shared__ union {
+    unsigned long long keys[kGpuSmallBuild];
+    float sbox[6 * kGpuSmallBuild];
+  } U;
+  __shared__ int sclus[kGpuSmallBuild];
+  __shared__ int snn[kGpuSmallBuild];
+  __shared__ uint32_t wsum[kSmallThreads / 64];
+  __shared__ uint32_t cb[6];
+  __shared__ int s_next;
+  __shared__ uint32_t s_err;
+  const int tid = (int)threadIdx.x;
+  if (tid < 3) { cb[tid] = 0xFFFFFFFFu; cb[3 + tid] = 0u; }
+  if (tid == 0) { s_err = 0u; s_next = n - 2; }
+  __syncthreads();
+  // 1. centroid bounds (k_centroid_bounds) and Morton keys (k_morton), padded to a power of two with ~0
+  for (int i = tid; i < n; i += kSmallThreads) {
+    const float4 a = tri[3 * i], b = tri[3 * i + 1], d = tri[3 * i + 2];
+    const float c[3] = {(a.x + b.x + d.x) * (1.0f / 3.0f), (a.y + b.y + d.y) * (1.0f / 3.0f),
+                        (a.z + b.z + d.z) * (1.0f / 3.0f)};
+    for (int k = 0; k < 3; k++) {
+      atomicMin(&cb[k], ord(c[k]));
+      atomicMax(&cb[3 + k], ord(c[k]));
+    }
+  }
+  __syncthreads();
+  int P = 2;
+  while (P < n) P <<= 1;
+  for (int i = tid; i < P; i += kSmallThreads) {
+    unsigned long long key = ~0ull;
+    if (i < n) {
+      const float4 a = tri[3 * i], b = tri[3 * i + 1], d = tri[3 * i + 2];
+      const float c[3] = {(a.x + b.x + d.x) * (1.0f / 3.0f), (a.y + b.y + d.y) * (1.0f / 3.0f),
+                          (a.z + b.z + d.z) * (1.0f / 3.0f)};
+      uint32_t q[3];
+      for (int k = 0; k < 3; k++) {
+        const float lo = unord(cb[k]), hi = unord(cb[3 + k]);
+        const float ext = hi - lo;
+        const float t = ext > 0.0f ? (c[k] - lo) / ext : 0.0f;
+        q[k] = (uint32_t)fminf(fmaxf(t * 1024.0f, 0.0f), 1023.0f);
+      }
+      const uint32_t code = (spread10(q[0]) << 2) | (spread10(q[1]) << 1) | spread10(q[2]);
+      key = ((unsigned long long)code << 32) | (uint32_t)i;
+    }
+    U.keys[i] = key;
+  }
+  __syncthreads();
+  // 2. bitonic sort (ascending; keys are unique)
+  for (int k = 2; k <= P; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P; i += kSmallThreads) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long a = U.keys[i], b = U.keys[ixj];
+          if ((a > b) == ((i & k) == 0)) { U.keys[i] = b; U.keys[ixj] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  // 3. leaves (k_ploc_leaves): binary leaf n - 1 + i = the i-th prim in key order
+  for (int i = tid; i < n; i += kSmallThreads) {
+    const unsigned long long key = U.keys[i];
+    sc.keys[i] = key;
+    const uint32_t prim = (uint32_t)key;
+    const float4 a = tri[3 * prim], b = tri[3 * prim + 1], c = tri[3 * prim + 2];
+    float* bx = sc.box + 6 * (size_t)(n - 1 + i);
+    bx[0] = fminf(fminf(a.x, b.x), c.x); bx[1] = fminf(fminf(a.y, b.y), c.y); bx[2] = fminf(fminf(a.z, b.z), c.z);
+    bx[3] = fmaxf(fmaxf(a.x, b.x), c.x); bx[4] = fmaxf(fmaxf(a.y, b.y), c.y); bx[5] = fmaxf(fmaxf(a.z, b.z), c.z);
+    sc.count[n - 1 + i] = 1u;
+    sclus[i] = n - 1 + i;
+  }
+  __syncthreads();  // the keys are read: U becomes the cluster boxes
+  for (int i = tid; i < n; i += kSmallThreads)
+    for (int k = 0; k < 6; k++) U.sbox[6 * i + k] = sc.box[6 * (size_t)(n - 1 + i) + k];
+  __syncthreads();
+  // 4. PLOC iterations (k_ploc_nn / k_ploc_merge / compaction), the cluster list and boxes in LDS
+  int m = n;
+  while (m > 1) {
+    for (int i = tid; i < m; i += kSmallThreads) {
+      const float* bi = U.sbox + 6 * i;
+      float best = 3.4e38f;
+      int bj = -1;
+      for (int j = max(0, i - kSmallR); j <= min(m - 1, i + kSmallR); j++) {
+        if (j == i) continue;
+        const float* b6 = U.sbox + 6 * j;
+        const float dx = fmaxf(bi[3], b6[3]) - fminf(bi[0], b6[0]);
+        const float dy = fmaxf(bi[4], b6[4]) - fminf(bi[1], b6[1]);
+        const float dz = fmaxf(bi[5], b6[5]) - fminf(bi[2], b6[2]);
+        const float a = dx * dy + dy * dz + dz * dx;
+        const bool better = a < best || (a == best && bj >= 0 && (min(i, j) < min(i, bj) ||
+                                                                  (min(i, j) == min(i, bj) && max(i, j) < max(i, bj))));
+        if (bj < 0 || better) { best = a; bj = j; }
+      }
+      snn[i] = bj;
+    }
+    __syncthreads();
+    // merge: thread t owns clusters 4t .. 4t + 3 (m <= 4 x 1024)
+    int nc[4];
+    float nb[4][6];
+    uint32_t keep = 0;
+    for (int e = 0; e < 4; e++) {
+      const int i = 4 * tid + e;
+      if (i >= m) continue;
+      const int j = snn[i];
+      const bool mutual = j >= 0 && snn[j] == i;
+      if (mutual && i > j) continue;  // merged into the cluster at j
+      keep |= 1u << e;
+      if (!mutual) {
+        nc[e] = sclus[i];
+        for (int k = 0; k < 6; k++) nb[e][k] = U.sbox[6 * i + k];
+        continue;
+      }
+      const int lc = sclus[i], rc = sclus[j];
+      const int p = atomicSub(&s_next, 1);
+      if (p < 0) { atomicOr(&s_err, 1u); nc[e] = lc; for (int k = 0; k < 6; k++) nb[e][k] = U.sbox[6 * i + k]; continue; }
+      float lb[6], rb[6];
+      for (int k = 0; k < 6; k++) { lb[k] = U.sbox[6 * i + k]; rb[k] = U.sbox[6 * j + k]; }
+      for (int k = 0; k < 3; k++) { nb[e][k] = fminf(lb[k], rb[k]); nb[e][3 + k] = fmaxf(lb[3 + k], rb[3 + k]); }
+      for (int k = 0; k < 6; k++) sc.box[6 * (size_t)p + k] = nb[e][k];
+      sc.left[p] = lc;
+      sc.right[p] = rc;
+      sc.count[p] = sc.count[lc] + sc.count[rc];
+      if (sc.dp.C) dp_node(sc.dp, p, lc, rc, nb[e], lb, rb, (int)sc.count[p], n, max_leaf);
+      nc[e] = p;
+    }
+    uint32_t total = 0;
+    uint32_t pos = small_scan((uint32_t)__popc(keep), wsum, &total);  // (its barriers order the reads above)
+    for (int e = 0; e < 4; e++) {
+      if (!((keep >> e) & 1u)) continue;
+      sclus[pos] = nc[e];
+      for (int k = 0; k < 6; k++) U.sbox[6 * pos + k] = nb[e][k];
+      pos++;
+    }
+    if (total >= (uint32_t)m) { if (tid == 0) s_err |= 2u; total = 1; }  // no merge: cannot happen
+    m = (int)total;
+    __syncthreads();
+  }
+  if (tid == 0 && s_next != -1 && n > 1) s_err |= 4u;  // not exactly n - 1 internal nodes
+  // 5. the collapse, one level per pass, behind barriers (k_collapse)
+  if (tid == 0) {
+    sc.ta[0] = Task{0, 0u};
+    sc.ctr[0] = 1u; sc.ctr[1] = 0u; sc.ctr[2] = 0u; sc.ctr[3] = 0u;
+    level_end[0] = 1u;
+  }
+  __syncthreads();
+  Task *ta = sc.ta, *tb = sc.tb;
+  uint32_t ntasks = s_err ? 0u : 1u;
+  int levels = 0;
+  while (ntasks) {
+    levels++;
+    for (uint32_t t = (uint32_t)tid; t < ntasks; t += kSmallThreads)
+      collapse_task(ta[t], tri, sc.keys, n, sc.left, sc.right, sc.box, nullptr, sc.count, max_leaf, tb, sc.ctr, nodes,
+                    tris, sc.dp);
+    __syncthreads();
+    ntasks = ld_sc1_u(sc.ctr + 2);
+    const uint32_t used = ld_sc1_u(sc.ctr + 0);
+    __syncthreads();
+    if (tid == 0) {
+      st_sc1_u(sc.ctr + 2, 0u);
+      if (ntasks && levels < max_levels) level_end[levels] = used;
+    }
+    if (levels >= max_levels && ntasks) {  // deeper than the caller's stacks hold
+      if (tid == 0) s_err |= 8u;
+      ntasks = 0;
+    }
+    __syncthreads();
+    Task* tt = ta; ta = tb; tb = tt;
+  }
+  if (tid == 0) {
+    const uint32_t c0 = ld_sc1_u(sc.ctr + 0), c1 = ld_sc1_u(sc.ctr + 1), c3 = ld_sc1_u(sc.ctr + 3);
+    out[0] = c0;
+    out[1] = c1;
+    out[2] = (uint32_t)levels;
+    out[3] = s_err | ((c3 & 0x80000000u) ? 16u : 0u) | (c1 != (uint32_t)n ? 32u : 0u);
+  }
 }
 
 // ShadeTri.pad[0] = the primitive's TriMT record (the cooperative traversal tail, prt_persist.h)
@@ -908,6 +1134,36 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
   if ((err = hipMemcpyAsync(rb, box, 24, hipMemcpyDeviceToHost, s)) || (err = hipStreamSynchronize(s))) return fail(err);
   for (int k = 0; k < 3; k++) { info->bmin[k] = rb[k]; info->bmax[k] = rb[3 + k]; }
   return fail(hipSuccess);
+}
+
+size_t gpu_small_scratch_bytes(int32_t n) {
+  const size_t nn = 2 * (size_t)std::max(n, 1) - 1, ni = (size_t)std::max(n - 1, 1);
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  return al(8 * (size_t)n) + 3 * al(4 * nn) + al(24 * nn) + al(64 * ni) + al(4 * ni) + 2 * al(sizeof(Task) * (size_t)n) +
+         al(16);
+}
+
+hipError_t gpu_build_blas8_small(hipStream_t s, const float* tri_dev, int32_t n, int max_leaf, Node8* nodes_out,
+                                 TriMT* tris_out, void* scratch, uint32_t* out, uint32_t* level_end, int max_levels) {
+  if (n <= 0 || n > kGpuSmallBuild) return hipErrorInvalidValue;
+  const size_t nn = 2 * (size_t)n - 1, ni = (size_t)std::max(n - 1, 1);
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  char* p = static_cast<char*>(scratch);
+  SmallScratch sc;
+  sc.keys = reinterpret_cast<unsigned long long*>(p); p += al(8 * (size_t)n);
+  sc.left = reinterpret_cast<int*>(p); p += al(4 * nn);
+  sc.right = reinterpret_cast<int*>(p); p += al(4 * nn);
+  sc.count = reinterpret_cast<uint32_t*>(p); p += al(4 * nn);
+  sc.box = reinterpret_cast<float*>(p); p += al(24 * nn);
+  sc.dp.C = reinterpret_cast<double*>(p); p += al(64 * ni);
+  sc.dp.dec = reinterpret_cast<uint32_t*>(p); p += al(4 * ni);
+  sc.ta = reinterpret_cast<Task*>(p); p += al(sizeof(Task) * (size_t)n);
+  sc.tb = reinterpret_cast<Task*>(p); p += al(sizeof(Task) * (size_t)n);
+  sc.ctr = reinterpret_cast<uint32_t*>(p);
+  if (n == 1) sc.dp = DpTab{nullptr, nullptr};  // the root is the single leaf
+  hipLaunchKernelGGL(k_build_small, dim3(1), dim3(kSmallThreads), 0, s, reinterpret_cast<const float4*>(tri_dev), n,
+                     max_leaf, sc, nodes_out, tris_out, out, level_end, max_levels);
+  return hipGetLastError();
 }
 
 hipError_t gpu_blas_finish(hipStream_t s, Node8* nodes, uint32_t n_nodes, uint32_t node_base, const TriMT* tris,

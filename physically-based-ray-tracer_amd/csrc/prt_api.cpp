@@ -134,6 +134,13 @@ struct prt_ctx {
   // swap behind an event (tlas_built) and the back buffers are written again only after the frames queued before
   // the swap (tlas_back_free)
   DevBuf tlas8_b, tlas_slot_b, tlas_order_b, tlas_aabb_b;
+  // up to kGpuSmallBuild instances (tlas_small): the tree is described on the device (TlasMeta: node count, refit
+  // levels), rebuilt by one workgroup from the side stream's own refit records (tlas_src -> tlas_inst) with no host
+  // round trip, and committed into the front buffers by a copy kernel on the render stream
+  bool tlas_small = false;
+  int tlas_depth_cap = 0;
+  TlasMeta tlas_meta_h{};  // host staging of the host build's meta (read by the async upload)
+  DevBuf tlas_meta, tlas_meta_b, tlas_small_scr, tlas_small_out, tlas_src, tlas_inst;
   hipStream_t tlas_stream = nullptr;
   hipEvent_t tlas_built = nullptr, tlas_back_free = nullptr;
   bool tlas_back_busy = false;
@@ -275,14 +282,16 @@ int ensure_instances(prt_ctx* c) {
   const char* tm = std::getenv("PRT_TLAS_MAX_REFITS");
   const int32_t max_refits = tm ? std::atoi(tm) : 8;
   auto upload_order = [&]() -> int {
-    const size_t ob = 4 * c->tlas_topo.order.size(), ab = 24 * std::max<size_t>(c->tlas_nodes, 1);
+    const size_t cap_nodes = std::max<size_t>(c->tlas_nodes, c->tlas_small ? (size_t)n : 1);
+    const size_t ob = 4 * std::max(c->tlas_topo.order.size(), cap_nodes), ab = 24 * cap_nodes;
     if (c->tlas_order.bytes < ob || c->tlas_aabb.bytes < ab) {
       const int rc = drain(c);
       if (rc) return rc;
       HIP_TRY(c->tlas_order.ensure(ob));
       HIP_TRY(c->tlas_aabb.ensure(ab));
     }
-    HIP_TRY(hipMemcpyAsync(c->tlas_order.p, c->tlas_topo.order.data(), ob, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->tlas_order.p, c->tlas_topo.order.data(), 4 * c->tlas_topo.order.size(),
+                           hipMemcpyHostToDevice, c->stream));
     return PRT_OK;
   };
   // the tree's cost over its current boxes into pinned slot k (0: right after a build, 1: after a refit)
@@ -294,7 +303,8 @@ int ensure_instances(prt_ctx* c) {
       HIP_TRY(c->tlas_cost_dev.ensure(2 * sizeof(double)));
     }
     HIP_TRY(launch_tlas_cost(c->stream, c->tlas8.as<Node8>(), c->tlas_nodes, c->tlas_aabb.as<float>(),
-                             c->inst.as<InstDev>(), c->tlas_slot.as<uint32_t>(), c->tlas_cost_dev.as<double>() + k));
+                             c->inst.as<InstDev>(), c->tlas_slot.as<uint32_t>(), c->tlas_cost_dev.as<double>() + k,
+                             c->tlas_small ? c->tlas_meta.as<TlasMeta>() : nullptr));
     HIP_TRY(hipMemcpyAsync(c->tlas_cost_h + k, c->tlas_cost_dev.as<double>() + k, sizeof(double),
                            hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipEventRecord(c->tlas_cost_ev[k], c->stream));
@@ -302,8 +312,13 @@ int ensure_instances(prt_ctx* c) {
     return PRT_OK;
   };
   auto refit_tree = [&]() -> int {
-    HIP_TRY(launch_tlas_refit(c->stream, c->inst.as<InstDev>(), c->tlas_topo, c->tlas_order.as<uint32_t>(),
-                              c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(), c->tlas_aabb.as<float>()));
+    if (c->tlas_small)
+      HIP_TRY(launch_tlas_refit_meta(c->stream, c->inst.as<InstDev>(), c->tlas_meta.as<TlasMeta>(),
+                                     c->tlas_order.as<uint32_t>(), c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(),
+                                     c->tlas_aabb.as<float>()));
+    else
+      HIP_TRY(launch_tlas_refit(c->stream, c->inst.as<InstDev>(), c->tlas_topo, c->tlas_order.as<uint32_t>(),
+                                c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(), c->tlas_aabb.as<float>()));
     return PRT_OK;
   };
   if (c->use_tlas && c->tlas_n == n && !(th && std::atoi(th) == 1)) {
@@ -318,7 +333,60 @@ int ensure_instances(prt_ctx* c) {
         }
       (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady is not an error here
     }
-    if (rebuild) {
+    if (rebuild && c->tlas_small) {
+      // sync-free: the side stream refits its own copy of the instance records, one workgroup builds the tree into
+      // the back buffers, and the render stream copies it over the front tree when it is valid (k_tlas_commit); the
+      // back buffers are written again only after that copy (tlas_back_free).  No host wait.
+      if (!c->tlas_stream) {
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&c->tlas_stream, hipStreamNonBlocking, hi));
+        HIP_TRY(hipEventCreateWithFlags(&c->tlas_built, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&c->tlas_back_free, hipEventDisableTiming));
+      }
+      if (c->tlas_back_busy) HIP_TRY(hipStreamWaitEvent(c->tlas_stream, c->tlas_back_free, 0));
+      const size_t scr = gpu_small_scratch_bytes(n);
+      if (c->tlas_fat.bytes < 48ull * n || c->tlas_tris.bytes < sizeof(TriMT) * (size_t)n ||
+          c->tlas8_b.bytes < sizeof(Node8) * (size_t)n || c->tlas_slot_b.bytes < 32ull * n ||
+          c->tlas_order_b.bytes < 4ull * n || c->tlas_meta_b.bytes < sizeof(TlasMeta) || c->tlas_small_scr.bytes < scr ||
+          c->tlas_small_out.bytes < 4ull * (4 + kTlasMaxLevels) || c->tlas_src.bytes < sizeof(InstSrc) * (size_t)n ||
+          c->tlas_inst.bytes < sizeof(InstDev) * (size_t)n) {
+        HIP_TRY(hipStreamSynchronize(c->tlas_stream));  // the back buffers are free (tlas_back_free) before realloc
+        HIP_TRY(c->tlas_fat.ensure(48ull * n));
+        HIP_TRY(c->tlas_tris.ensure(sizeof(TriMT) * (size_t)n));
+        HIP_TRY(c->tlas8_b.ensure(sizeof(Node8) * (size_t)n));
+        HIP_TRY(c->tlas_slot_b.ensure(32ull * n));
+        HIP_TRY(c->tlas_order_b.ensure(4ull * n));
+        HIP_TRY(c->tlas_meta_b.ensure(sizeof(TlasMeta)));
+        HIP_TRY(c->tlas_small_scr.ensure(scr));
+        HIP_TRY(c->tlas_small_out.ensure(4ull * (4 + kTlasMaxLevels)));
+        HIP_TRY(c->tlas_src.ensure(sizeof(InstSrc) * (size_t)n));
+        HIP_TRY(c->tlas_inst.ensure(sizeof(InstDev) * (size_t)n));
+      }
+      HIP_TRY(hipMemcpyAsync(c->tlas_src.p, src.data(), sizeof(InstSrc) * (size_t)n, hipMemcpyHostToDevice,
+                             c->tlas_stream));
+      HIP_TRY(launch_refit(c->tlas_stream, c->tlas_src.as<InstSrc>(), n, c->tlas_inst.as<InstDev>()));
+      HIP_TRY(gpu_rebuild_tlas_small(c->tlas_stream, c->tlas_inst.as<InstDev>(), n, c->tlas_fat.as<float>(),
+                                     c->tlas_tris.as<TriMT>(), c->tlas_small_scr.p, c->tlas_small_out.as<uint32_t>(),
+                                     c->tlas8_b.as<Node8>(), c->tlas_slot_b.as<uint32_t>(),
+                                     c->tlas_order_b.as<uint32_t>(), c->tlas_meta_b.as<TlasMeta>(), c->tlas_depth_cap));
+      HIP_TRY(hipEventRecord(c->tlas_built, c->tlas_stream));
+      HIP_TRY(hipStreamWaitEvent(c->stream, c->tlas_built, 0));
+      HIP_TRY(launch_tlas_commit(c->stream, c->tlas_meta_b.as<TlasMeta>(), c->tlas8_b.as<Node8>(),
+                                 c->tlas_slot_b.as<uint32_t>(), c->tlas_order_b.as<uint32_t>(),
+                                 c->tlas_meta.as<TlasMeta>(), c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(),
+                                 c->tlas_order.as<uint32_t>()));
+      HIP_TRY(hipEventRecord(c->tlas_back_free, c->stream));
+      c->tlas_back_busy = true;
+      int rc = refit_tree();  // over this frame's boxes (k_refit above); its aabb for the cost
+      if (rc) return rc;
+      c->tlas_base_cost = 0;
+      c->tlas_cost_pending[1] = false;
+      rc = measure_cost(0);
+      if (rc) return rc;
+      c->tlas_rebuilds++;
+      c->tlas_since_build = 0;
+    } else if (rebuild) {
       // boxes of the instances' current transforms (the same refit_instance as k_refit), built on the side stream
       // into the back buffers: the frames already queued keep walking the current tree, the host waits only for
       // the build's own steps
@@ -402,16 +470,31 @@ int ensure_instances(prt_ctx* c) {
     c->tlas_host = build_tlas8(boxes.data(), n);
     c->tlas_depth = c->tlas_host.depth;
     c->tlas_nodes = (uint32_t)c->tlas_host.nodes.size();
+    // the sync-free device rebuild (up to kGpuSmallBuild instances): the front buffers hold any tree of n instances,
+    // and the stacks are sized one level deeper than the host tree so a device tree of that depth is usable
+    c->tlas_small = n <= kGpuSmallBuild && !(th && std::atoi(th) == 1) && (rebuild_always || rebuild_ratio > 0);
+    if (c->tlas_small) {
+      c->tlas_depth_cap = c->tlas_depth + 1;
+      c->tlas_depth = c->tlas_depth_cap;
+    }
+    const size_t cap_nodes = c->tlas_small ? std::max<size_t>(c->tlas_host.nodes.size(), (size_t)n)
+                                           : c->tlas_host.nodes.size();
     const size_t nb = c->tlas_host.nodes.size() * sizeof(Node8), sb = c->tlas_host.slot.size() * 4;
-    if (c->tlas8.bytes < nb || c->tlas_slot.bytes < sb) {
+    if (c->tlas8.bytes < cap_nodes * sizeof(Node8) || c->tlas_slot.bytes < cap_nodes * 32 ||
+        (c->tlas_small && c->tlas_meta.bytes < sizeof(TlasMeta))) {
       const int rc = drain(c);
       if (rc) return rc;
-      HIP_TRY(c->tlas8.ensure(nb));
-      HIP_TRY(c->tlas_slot.ensure(sb));
+      HIP_TRY(c->tlas8.ensure(cap_nodes * sizeof(Node8)));
+      HIP_TRY(c->tlas_slot.ensure(cap_nodes * 32));
+      if (c->tlas_small) HIP_TRY(c->tlas_meta.ensure(sizeof(TlasMeta)));
     }
     c->tlas_topo = tlas_topology(c->tlas_host.nodes);
     HIP_TRY(hipMemcpyAsync(c->tlas8.p, c->tlas_host.nodes.data(), nb, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->tlas_slot.p, c->tlas_host.slot.data(), sb, hipMemcpyHostToDevice, c->stream));
+    if (c->tlas_small) {
+      c->tlas_meta_h = tlas_meta(c->tlas_topo, c->tlas_nodes);
+      HIP_TRY(hipMemcpyAsync(c->tlas_meta.p, &c->tlas_meta_h, sizeof(TlasMeta), hipMemcpyHostToDevice, c->stream));
+    }
     int rc = upload_order();
     if (rc) return rc;
     if (c->tlas_n != n) c->tlas_rebuilds = c->tlas_refits = 0;
@@ -428,6 +511,7 @@ int ensure_instances(prt_ctx* c) {
   } else {
     c->tlas_depth = 0;
     c->tlas_n = -1;
+    c->tlas_small = false;
   }
   c->inst_dirty = false;
   return PRT_OK;
@@ -1418,6 +1502,15 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
     HIP_TRY(upload(c->nodes8, nodes8.data(), nodes8.size() * sizeof(Node8)));
     HIP_TRY(upload(c->tris, tris.data(), tris.size() * sizeof(TriMT)));
     HIP_TRY(upload(c->stri, stri.data(), stri.size() * sizeof(ShadeTri)));
+  }
+  if (kBlasNodeStride != sizeof(Node8) && c->nodes8.bytes) {  // one node per kBlasNodeStride bytes (A/B build)
+    const size_t nn = c->nodes8.bytes / sizeof(Node8);
+    DevBuf wide;
+    HIP_TRY(wide.ensure(kBlasNodeStride * nn));
+    HIP_TRY(hipMemcpy2DAsync(wide.p, kBlasNodeStride, c->nodes8.p, sizeof(Node8), sizeof(Node8), nn,
+                             hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::swap(c->nodes8, wide);
   }
   c->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_build0).count();
   c->built_with = builder;

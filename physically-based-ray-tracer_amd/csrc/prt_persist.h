@@ -199,7 +199,7 @@ __device__ __forceinline__ void trav8_persistent_t(const SceneDev& S, uint32_t* 
   // one node visit (lanes without pending triangles)
   auto node_step = [&](float tlimit) {
     const bool top = TLAS && inst < 0;  // a node of the instance BVH
-    const uint4* np = reinterpret_cast<const uint4*>((top ? S.tlas8 : S.nodes8) + node);
+    const uint4* np = top ? reinterpret_cast<const uint4*>(S.tlas8 + node) : blas_node(S.nodes8, node);
     const uint4 a = np[0], b = np[1];
     const uint4 c = np[2], d = np[3], e = np[4];
     const uint32_t hits = node8_hits(a, c, d, e, O, rD, tlimit);

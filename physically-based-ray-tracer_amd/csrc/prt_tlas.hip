@@ -41,13 +41,9 @@ __device__ __forceinline__ uint32_t grid_exp(double ext) {
   return (uint32_t)min(254, max(1, e + 127));
 }
 
-// one level of the refit: the nodes order[0..count) (all at one depth); their interior children (one level deeper)
-// were refitted by the previous launch and left their boxes in aabb
-__global__ void k_tlas_refit(const InstDev* __restrict__ inst, const uint32_t* __restrict__ order, uint32_t count,
-                             Node8* __restrict__ nodes, const uint32_t* __restrict__ slot, float* __restrict__ aabb) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= count) return;
-  const uint32_t node = order[j];
+// refit of one node: its interior children (one level deeper) were refitted before and left their boxes in aabb
+__device__ __forceinline__ void refit_node(const InstDev* __restrict__ inst, uint32_t node, Node8* __restrict__ nodes,
+                                           const uint32_t* __restrict__ slot, float* __restrict__ aabb) {
   Node8 nd = nodes[node];
   float clo[8][3], chi[8][3];
   bool used[8];
@@ -91,6 +87,27 @@ __global__ void k_tlas_refit(const InstDev* __restrict__ inst, const uint32_t* _
   for (int a = 0; a < 3; a++) { b[a] = nlo[a]; b[3 + a] = nhi[a]; }
 }
 
+// one level of the refit: the nodes order[0..count) (all at one depth)
+__global__ void k_tlas_refit(const InstDev* __restrict__ inst, const uint32_t* __restrict__ order, uint32_t count,
+                             Node8* __restrict__ nodes, const uint32_t* __restrict__ slot, float* __restrict__ aabb) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= count) return;
+  refit_node(inst, order[j], nodes, slot, aabb);
+}
+
+// the whole refit in one workgroup, levels from the device-resident TlasMeta (deepest first) behind barriers
+__global__ void __launch_bounds__(1024) k_tlas_refit_meta(const InstDev* __restrict__ inst,
+                                                          const TlasMeta* __restrict__ meta,
+                                                          const uint32_t* __restrict__ order, Node8* __restrict__ nodes,
+                                                          const uint32_t* __restrict__ slot, float* __restrict__ aabb) {
+  const uint32_t nl = meta->nlevels;
+  for (uint32_t l = 0; l < nl && l < (uint32_t)kTlasMaxLevels; l++) {
+    const uint32_t off = meta->level_off[l], cnt = meta->level_cnt[l];
+    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) refit_node(inst, order[off + j], nodes, slot, aabb);
+    __syncthreads();
+  }
+}
+
 // ---- device rebuild of the topology: the instances' current world boxes through the device BLAS
 // builder (bvh_gpu.hip: PLOC + SAH-optimal 8-wide collapse, one instance per leaf slot), converted to the
 // instance-BVH form exactly as the host's build_tlas8 converts its BLAS-form tree
@@ -104,6 +121,68 @@ __global__ void k_inst_fat(const float* __restrict__ boxes, int32_t n, float4* _
   fat[3 * (size_t)i] = lo;
   fat[3 * (size_t)i + 1] = hi;
   fat[3 * (size_t)i + 2] = lo;
+}
+
+// the refit records' world boxes (InstDev bmin / bmax: refit_instance's inflated box, the boxes the host build reads)
+// as degenerate triangles
+__global__ void k_inst_fat_dev(const InstDev* __restrict__ inst, int32_t n, float4* __restrict__ fat) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const InstDev& I = inst[i];
+  const float4 lo = make_float4(I.bmin[0], I.bmin[1], I.bmin[2], 0.0f), hi = make_float4(I.bmax[0], I.bmax[1], I.bmax[2], 0.0f);
+  fat[3 * (size_t)i] = lo;
+  fat[3 * (size_t)i + 1] = hi;
+  fat[3 * (size_t)i + 2] = lo;
+}
+
+// after k_build_small: instance slots (as k_tlas_slots), identity refit order, and the TlasMeta (levels deepest
+// first); valid = 0 when the build failed or is deeper than the stacks the context sized for its instance BVH
+__global__ void __launch_bounds__(1024) k_tlas_small_finish(Node8* __restrict__ nodes, const TriMT* __restrict__ tris,
+                                                            uint32_t* __restrict__ slot, uint32_t* __restrict__ order,
+                                                            const uint32_t* __restrict__ out,
+                                                            const uint32_t* __restrict__ level_end,
+                                                            uint32_t depth_cap, TlasMeta* __restrict__ meta) {
+  const uint32_t nn = out[0], levels = out[2];
+  const bool valid = out[3] == 0u && nn > 0u && levels >= 1u && levels <= depth_cap;
+  if (valid)
+    for (uint32_t j = threadIdx.x; j < nn; j += blockDim.x) {
+      Node8& nd = nodes[j];
+      for (uint32_t s = 0; s < 8; s++)
+        slot[8 * (size_t)j + s] = (!((nd.imask >> s) & 1u) && nd.meta[s]) ? tris[nd.tri_base + (nd.meta[s] >> 3)].prim
+                                                                            : 0xFFFFFFFFu;
+      nd.tri_base = 8u * j;
+      order[j] = j;
+    }
+  if (threadIdx.x == 0) {
+    meta->n_nodes = valid ? nn : 0u;
+    meta->nlevels = valid ? levels : 0u;
+    meta->depth = valid ? levels : 0u;
+    meta->valid = valid ? 1u : 0u;
+    if (valid)
+      for (uint32_t l = levels, k = 0; l-- > 0; k++) {
+        const uint32_t b = l == 0 ? 0u : level_end[l - 1];
+        meta->level_off[k] = b;
+        meta->level_cnt[k] = level_end[l] - b;
+      }
+  }
+}
+
+// the render stream's side of a device rebuild: the back tree replaces the front one when it is valid (the front
+// tree is only ever written in render-stream order, so queued frames never see a half-written tree)
+__global__ void __launch_bounds__(1024) k_tlas_commit(const TlasMeta* __restrict__ mb, const Node8* __restrict__ nb,
+                                                      const uint32_t* __restrict__ sb, const uint32_t* __restrict__ ob,
+                                                      TlasMeta* __restrict__ mf, Node8* __restrict__ nf,
+                                                      uint32_t* __restrict__ sf, uint32_t* __restrict__ of) {
+  if (!mb->valid) return;
+  const uint32_t nn = mb->n_nodes;
+  const uint4* ns = reinterpret_cast<const uint4*>(nb);
+  uint4* nd = reinterpret_cast<uint4*>(nf);
+  for (uint32_t i = threadIdx.x; i < 5u * nn; i += blockDim.x) nd[i] = ns[i];
+  for (uint32_t i = threadIdx.x; i < 8u * nn; i += blockDim.x) sf[i] = sb[i];
+  for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) of[i] = ob[i];
+  const uint32_t* ms = reinterpret_cast<const uint32_t*>(mb);
+  uint32_t* md = reinterpret_cast<uint32_t*>(mf);
+  for (uint32_t i = threadIdx.x; i < sizeof(TlasMeta) / 4; i += blockDim.x) md[i] = ms[i];
 }
 
 // leaf slot s of node j -> the instance it holds (slot[8j + s]); tri_base = 8j (build_tlas8's conversion)
@@ -126,8 +205,10 @@ __device__ __forceinline__ double box_area(const float* lo, const float* hi) {
 // in aabb: one block
 __global__ void __launch_bounds__(1024) k_tlas_cost(const Node8* __restrict__ nodes, uint32_t n_nodes,
                                                     const float* __restrict__ aabb, const InstDev* __restrict__ inst,
-                                                    const uint32_t* __restrict__ slot, double* __restrict__ out) {
+                                                    const uint32_t* __restrict__ slot, double* __restrict__ out,
+                                                    const TlasMeta* __restrict__ meta) {
   __shared__ double red[1024];
+  if (meta) n_nodes = meta->n_nodes;
   // the interior nodes' areas only: the leaf term (the instances' own boxes) does not change as instances move, so
   // it would dilute the growth the refit causes
   double acc = 0.0;
@@ -182,9 +263,46 @@ hipError_t gpu_build_tlas8(hipStream_t s, const float* boxes, int32_t n, float* 
 }
 
 hipError_t launch_tlas_cost(hipStream_t s, const Node8* nodes, uint32_t n_nodes, const float* aabb,
-                            const InstDev* inst, const uint32_t* slot, double* out) {
-  hipLaunchKernelGGL(k_tlas_cost, dim3(1), dim3(1024), 0, s, nodes, n_nodes, aabb, inst, slot, out);
+                            const InstDev* inst, const uint32_t* slot, double* out, const TlasMeta* meta) {
+  hipLaunchKernelGGL(k_tlas_cost, dim3(1), dim3(1024), 0, s, nodes, n_nodes, aabb, inst, slot, out, meta);
   return hipGetLastError();
+}
+
+hipError_t gpu_rebuild_tlas_small(hipStream_t s, const InstDev* inst, int32_t n, float* fat, TriMT* tris,
+                                  void* scratch, uint32_t* out, Node8* nodes, uint32_t* slot, uint32_t* order,
+                                  TlasMeta* meta, int depth_cap) {
+  if (n <= 0 || n > kGpuSmallBuild) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_inst_fat_dev, dim3((n + 255) / 256), dim3(256), 0, s, inst, n, reinterpret_cast<float4*>(fat));
+  const hipError_t e = gpu_build_blas8_small(s, fat, n, 1, nodes, tris, scratch, out, out + 4, kTlasMaxLevels);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_tlas_small_finish, dim3(1), dim3(1024), 0, s, nodes, tris, slot, order, out, out + 4,
+                     (uint32_t)depth_cap, meta);
+  return hipGetLastError();
+}
+
+hipError_t launch_tlas_commit(hipStream_t s, const TlasMeta* mb, const Node8* nb, const uint32_t* sb,
+                              const uint32_t* ob, TlasMeta* mf, Node8* nf, uint32_t* sf, uint32_t* of) {
+  hipLaunchKernelGGL(k_tlas_commit, dim3(1), dim3(1024), 0, s, mb, nb, sb, ob, mf, nf, sf, of);
+  return hipGetLastError();
+}
+
+hipError_t launch_tlas_refit_meta(hipStream_t s, const InstDev* inst, const TlasMeta* meta, const uint32_t* order,
+                                  Node8* nodes, const uint32_t* slot, float* aabb) {
+  hipLaunchKernelGGL(k_tlas_refit_meta, dim3(1), dim3(1024), 0, s, inst, meta, order, nodes, slot, aabb);
+  return hipGetLastError();
+}
+
+TlasMeta tlas_meta(const TlasTopo& T, uint32_t n_nodes) {
+  TlasMeta m{};
+  m.n_nodes = n_nodes;
+  m.nlevels = (uint32_t)std::min<size_t>(T.level_cnt.size(), kTlasMaxLevels);
+  m.depth = m.nlevels;
+  m.valid = 1u;
+  for (uint32_t l = 0; l < m.nlevels; l++) {
+    m.level_off[l] = T.level_off[l];
+    m.level_cnt[l] = T.level_cnt[l];
+  }
+  return m;
 }
 
 TlasTopo tlas_topology(const std::vector<Node8>& nodes) {

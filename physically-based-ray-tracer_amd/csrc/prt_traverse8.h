@@ -115,7 +115,7 @@ __device__ __forceinline__ bool blas_traverse8(const Node8* __restrict__ nodes, 
   int sp = 0;
   while (true) {
     {
-      const uint4* np = reinterpret_cast<const uint4*>(nodes + node);
+      const uint4* np = blas_node(nodes, node);
       const uint4 a = np[0], b = np[1];
       const uint32_t imask = a.w >> 24;
       const uint32_t hits = node8_hits(a, np[2], np[3], np[4], O, rD, h.t);

@@ -15,14 +15,15 @@
 //   k_wave_init                                   P(0) = primary rays r1
 //   for i = 0 .. iters:
 //     k_trace2(i)    closest hits of P(i)  +  any hits of S(i-1)         (one launch, mixed lanes)
-//     k_resmiss2(i)  over P(i-1): NEE result of iteration i-1, (result, throughput) stack, path end, frame write;
-//                    with the extensions (or a debug render mode), then, for the items k_shade2(i-1) queued into
-//                    P(i) (a subset of P(i-1)), this iteration's misses (i = 0: k_miss2 over P(0))
+//     k_res2d(i)     the items of P(i-1) (rinfo kRiFresh), walked in index order: NEE result of iteration i-1,
+//                    (result, throughput) stack, path end, frame write.  With the extensions or a debug render mode
+//                    k_resmiss2(i) walks the queue P(i-1) instead and also shades, for the items k_shade2(i-1)
+//                    queued into P(i) (a subset of P(i-1)), this iteration's misses (i = 0: k_miss2 over P(0))
 //     k_shade2(i)    the sky radiance of the misses (no extensions), hit attributes, NEE set-up -> S(i), BRDF
 //                    sample or path-2 start -> P(i+1)
 //
-// Hazards (all kernels on one stream): P(i+1) reuses P(i-1)'s buffer after k_resmiss2(i) read it;
-// S(i) reuses S(i-1)'s buffer after k_trace2(i) read it; k_resmiss2(i) reads ne/nb/nk/vis/R/T of an item for
+// Hazards (all kernels on one stream): P(i+1) reuses P(i-1)'s buffer after the resolve (i) read it;
+// S(i) reuses S(i-1)'s buffer after k_trace2(i) read it; the resolve (i) reads ne/nb/nk/vis/R/T of an item for
 // iteration i-1 before it (misses) or k_shade2(i) (hits) overwrites them; rinfo keeps iteration i-1's status
 // (and whether the item was queued) while info already holds the state of the queued next ray.
 #include <cstdio>
@@ -49,6 +50,19 @@ void lane_stats_dump() {
   static const unsigned long long z[(kMaxIters + 2) * 32] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lane_stats), z, sizeof(z));
 }
+#endif
+
+// The resolve of the plain pipeline (no extensions, render mode 0) and of the merged one walks all items in index
+// order and takes those whose rinfo carries kRiFresh (set by the shading of the last iteration, cleared by the
+// resolve), so its record loads coalesce; with extensions or a debug render mode it walks the last iteration's queue
+// (k_resmiss2), which also shades that iteration's misses
+constexpr uint32_t kResFresh = kRiFresh;
+
+// the shading kernels' queue appends: per block (one atomic, three barriers) or, A/B -DPRT_WAVE_APPEND, per wave
+#ifdef PRT_WAVE_APPEND
+#define shade_append(counter, n, sm) wave_append(counter, n)
+#else
+#define shade_append(counter, n, sm) block_append(counter, n, sm)
 #endif
 
 // the merged pipeline's queue of path-2 primaries: the counters of iteration iters + 1 (kind 0), never a path queue
@@ -86,16 +100,14 @@ __global__ void __launch_bounds__(kBlock) k_wave_init(SceneDev S, TraceArgs A, T
           const Ray r2 = primary_ray(S, (float)x + jx, (float)y + jy, A.W, A.H);
           B.ro2[i] = make_float4(r2.O.x, r2.O.y, r2.O.z, 0.0f);
           B.rd2[i] = make_float4(r2.D.x, r2.D.y, r2.D.z, 0.0f);
-          B.rinfo[i] = 0u;
           B.rinfo[B.n + i] = 0u;
         }
+        B.rinfo[i] = 0u;
         enq = true;
       } else {
         out[i] = make_float4(0.0f, 0.0f, 0.0f, kFar);  // bounces == 0: Trace returns 0, t1 stays BVH_FAR
-        if (B.merge) {
-          B.rinfo[i] = 0u;
-          B.rinfo[B.n + i] = 0u;
-        }
+        if (B.merge) B.rinfo[B.n + i] = 0u;
+        B.rinfo[i] = 0u;
       }
     }
     const uint32_t slot = block_append(cnt, enq ? 1u : 0u, sm);
@@ -343,6 +355,7 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
   // chunk's item is shaded
   uint32_t item_n = 0, info_n = 0, seed_n = 0;
   float4 hh_n = make_float4(kFar, 0.0f, 0.0f, 0.0f);
+  float4 ro_n = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rd_n = ro_n;  // (plain form: the ray too)
   auto prefetch = [&](uint32_t cc) {
     const uint32_t gg = cc * kBlock + threadIdx.x;
     if (gg < total) {
@@ -350,10 +363,12 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
       info_n = B.info[item_n];
       hh_n = B.hit[item_n];
       seed_n = B.seed[item_n];
+      if (!EXT) { ro_n = B.ro[item_n]; rd_n = B.rd[item_n]; }
     }
   };
   prefetch(blockIdx.x);
   for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
+    const float4 ro_c = ro_n, rd_c = rd_n;
     // The scene and buffer descriptors are read from the kernarg segment inside each chunk (scalar loads, scalar
     // cache) instead of being held in SGPRs across the loop: their ~90 live words spilled to VGPR lanes (378
     // v_readlane in the loop) when hoisted.  The empty asm hides the pointer's loop invariance.
@@ -373,7 +388,7 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
       if (!EXT && hh.x >= kFar) {  // a miss (:159): the sky radiance (or 0) ends the path (EXT: k_miss2 / k_resmiss2)
         V3 L = v3(0.0f, 0.0f, 0.0f);
         if (fl & kSkybox) {
-          const float4 d = Bc.rd[item];
+          const float4 d = EXT ? Bc.rd[item] : rd_c;
           L = sample_sky_call(Sc.sky, Sc.skyw, Sc.skyh, v3(d.x, d.y, d.z));
         }
         Bc.ne[item] = make_float4(L.x, L.y, L.z, 0.0f);
@@ -385,13 +400,13 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
       }
     }
     prefetch(c + gridDim.x);
-    const uint32_t s0 = block_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic
+    const uint32_t s0 = shade_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic
     const uint32_t depth = info & 0xFFu, path = (info >> 8) & 1u;
     uint32_t status = kStMiss, emissive = 0;
     bool next = false;
     bool area_ray = false;
     if (nr) {
-      const float4 o = Bc.ro[item], d = Bc.rd[item];
+      const float4 o = EXT ? Bc.ro[item] : ro_c, d = EXT ? Bc.rd[item] : rd_c;
       const V3 D = v3(d.x, d.y, d.z);
       const uint32_t pk = __float_as_uint(hh.w);
       const V3 I = v3(o.x, o.y, o.z) + hh.x * D;                                             // tiny_bvh.h:586
@@ -463,7 +478,7 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
       Bc.seed[item] = seed;
     }
     if constexpr (EXT) {  // the area-light shadow rays of the block, one more append
-      const uint32_t a0 = block_append(shcnt, area_ray ? 1u : 0u, sm);
+      const uint32_t a0 = shade_append(shcnt, area_ray ? 1u : 0u, sm);
       if (area_ray) shq[a0] = (kLightArea << 29) | item;
     }
     if (active) {
@@ -471,9 +486,10 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
         if (EXT && Sc.has_diel) next = diel_next(Bc, item, depth, path);
         if (!next) next = start_path2(Sc, A, M, Bc, item, path);
       }
-      Bc.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20) | (next ? kRiQueued : 0u) | emissive;
+      Bc.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20) | (next ? kRiQueued : 0u) | emissive |
+                       (EXT ? 0u : kResFresh);
     }
-    const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
+    const uint32_t slot = shade_append(ncnt, next ? 1u : 0u, sm);
     if (next) qn[sub * Bc.qcap + slot] = item;
   }
 }
@@ -549,7 +565,7 @@ __global__ void __launch_bounds__(kBlock, 1) k_shade2m(SceneDev S, TraceArgs A, 
           nr = (uint32_t)nee_rays(kind);
         }
       }
-      const uint32_t s0 = block_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic per pass
+      const uint32_t s0 = shade_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic per pass
       uint32_t status = kStMiss, emissive = 0;
       if (nr) {
         const float4 o = rop[item], d = rdp[item];
@@ -591,7 +607,7 @@ __global__ void __launch_bounds__(kBlock, 1) k_shade2m(SceneDev S, TraceArgs A, 
         need2 = pass == 0 && path == 0 && status != kStNeeCont && (fl & kAA);
       }
     }
-    const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
+    const uint32_t slot = shade_append(ncnt, next ? 1u : 0u, sm);
     if (next) qn[sub * Bc.qcap + slot] = item;
   }
 }
@@ -732,6 +748,21 @@ __global__ void __launch_bounds__(kBlock) k_resmiss2(SceneDev S, TraceArgs A, Wa
   }
 }
 
+// dense resolve (plain pipeline, no extensions, render mode 0): every item in index order, the next item's rinfo
+// loaded while this one is resolved
+__global__ void __launch_bounds__(kBlock) k_res2d(SceneDev S, TraceArgs A, WaveBufs B, float4* __restrict__ out) {
+  const uint32_t stride = gridDim.x * kBlock;
+  uint32_t item = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t ri_n = item < B.n ? B.rinfo[item] : 0u;
+  for (; item < B.n; item += stride) {
+    const uint32_t ri = ri_n;
+    if (item + stride < B.n) ri_n = B.rinfo[item + stride];
+    if (!(ri & kRiFresh)) continue;
+    resolve_item<false>(S, A, B, item, ri, out);
+    B.rinfo[item] = ri & ~kRiFresh;
+  }
+}
+
 // ---- merged pipeline: the resolve of P(iter - 1) per record slot (path 1's, then path 2's), as resolve_item<false>
 __device__ __forceinline__ void resolve_slot(const SceneDev& S, const TraceArgs& A, const WaveBufs& B, uint32_t item,
                                              uint32_t path, uint32_t ri, float4* __restrict__ out) {
@@ -768,26 +799,14 @@ __device__ __forceinline__ void resolve_slot(const SceneDev& S, const TraceArgs&
     out[item] = make_float4(res.x, res.y, res.z, s1.w);
   }
 }
-__global__ void __launch_bounds__(kBlock) k_resmiss2m(SceneDev S, TraceArgs A, WaveBufs B, uint32_t iter,
-                                                      float4* __restrict__ out) {
-  __shared__ uint32_t pref[kNSub + 1];
-  const uint32_t* q = ((iter - 1) & 1) ? B.q1 : B.q0;
-  const uint32_t total = load_prefix(B.ctr, iter - 1, 0, pref);
-  uint32_t item_n = 0, r0_n = 0, r1_n = 0;
-  auto prefetch = [&](uint32_t cc) {
-    const uint32_t gg = cc * kBlock + threadIdx.x;
-    if (gg < total) {
-      item_n = q[map_slot(pref, gg, B.qcap)];
-      r0_n = B.rinfo[item_n];
-      r1_n = B.rinfo[B.n + item_n];
-    }
-  };
-  prefetch(blockIdx.x);
-  for (uint32_t c = blockIdx.x; c * kBlock < total; c += gridDim.x) {
-    const uint32_t g = c * kBlock + threadIdx.x;
-    const uint32_t item = item_n, r0 = r0_n, r1 = r1_n;
-    prefetch(c + gridDim.x);
-    if (g >= total) continue;
+__global__ void __launch_bounds__(kBlock) k_res2md(SceneDev S, TraceArgs A, WaveBufs B, float4* __restrict__ out) {
+  const uint32_t stride = gridDim.x * kBlock;
+  uint32_t item = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t r0_n = 0, r1_n = 0;
+  if (item < B.n) { r0_n = B.rinfo[item]; r1_n = B.rinfo[B.n + item]; }
+  for (; item < B.n; item += stride) {
+    const uint32_t r0 = r0_n, r1 = r1_n;
+    if (item + stride < B.n) { r0_n = B.rinfo[item + stride]; r1_n = B.rinfo[B.n + item + stride]; }
     if (r0 & kRiFresh) {
       resolve_slot(S, A, B, item, 0u, r0, out);
       B.rinfo[item] = r0 & ~kRiFresh;
@@ -860,8 +879,12 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
 #else
   const unsigned gres = PRT_RES_GRID;  // A/B
 #endif
+  // the dense resolves over 2x the resident producer blocks (8 waves/SIMD), at most one chunk per block
+  const unsigned gdense = std::min<unsigned>(2u * gprod, (B.n + kBlock - 1) / kBlock);
   if (it > 0 && B.merge) {
-    hipLaunchKernelGGL(k_resmiss2m, dim3(gres), dim3(kBlock), 0, c.stream, S, A, B, it, out);
+    hipLaunchKernelGGL(k_res2md, dim3(gdense), dim3(kBlock), 0, c.stream, S, A, B, out);
+  } else if (it > 0 && !ext && !sep_miss) {
+    hipLaunchKernelGGL(k_res2d, dim3(gdense), dim3(kBlock), 0, c.stream, S, A, B, out);
   } else if (it > 0) {  // resolve of P(it - 1) (+ misses of P(it)), one pass
     if (ext) hipLaunchKernelGGL(k_resmiss2<true>, dim3(gres), dim3(kBlock), 0, c.stream, S, A, B, it, iters, sep_miss,
                                 out);
