@@ -911,7 +911,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   // 5. the collapse, one level per pass, behind barriers (k_collapse)
   if (tid == 0) {
     sc.ta[0] = Task{0, 0u};
-    sc.ctr[0] = 1u; sc.ctr[1] = 0u; sc.ctr[2] = 0u; sc.ctr[3] = 0u;
+    st_sc1_u(sc.ctr + 0, 1u); st_sc1_u(sc.ctr + 1, 0u); st_sc1_u(sc.ctr + 2, 0u); st_sc1_u(sc.ctr + 3, 0u);
     level_end[0] = 1u;
   }
   __syncthreads();

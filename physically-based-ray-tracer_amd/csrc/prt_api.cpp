@@ -472,7 +472,10 @@ int ensure_instances(prt_ctx* c) {
     c->tlas_nodes = (uint32_t)c->tlas_host.nodes.size();
     // the sync-free device rebuild (up to kGpuSmallBuild instances): the front buffers hold any tree of n instances,
     // and the stacks are sized one level deeper than the host tree so a device tree of that depth is usable
-    c->tlas_small = n <= kGpuSmallBuild && !(th && std::atoi(th) == 1) && (rebuild_always || rebuild_ratio > 0);
+    // (PRT_TLAS_SMALL=1 opts in: the single-workgroup builder has not yet run on the GPU in this tree)
+    const char* ts = std::getenv("PRT_TLAS_SMALL");
+    c->tlas_small = ts && std::atoi(ts) == 1 && n <= kGpuSmallBuild && !(th && std::atoi(th) == 1) &&
+                    (rebuild_always || rebuild_ratio > 0);
     if (c->tlas_small) {
       c->tlas_depth_cap = c->tlas_depth + 1;
       c->tlas_depth = c->tlas_depth_cap;

@@ -514,18 +514,27 @@ def test_device_tlas_moving_instances(gpu_ctx, monkeypatch, n):
     assert np.array_equal(a_h, out[-1].cpu().numpy())
 
 
-def test_device_tlas_rebuild_long_motion(gpu_ctx, monkeypatch):
+@pytest.mark.parametrize("mode", ["default", "always", "large", "small", "small_always"])
+def test_device_tlas_rebuild_long_motion(gpu_ctx, monkeypatch, mode):
     """1,000 tori drift across the field for 120 frames (every instance moves before every frame, the
-    frames queued back to back with device outputs and no host wait).  The refitted instance BVH degrades; once its
-    node-area cost (measured on the device after every refit, read back without a wait) exceeds 1.05x its cost after the
-    last build, the topology is rebuilt on the device (gpu_build_tlas8: PLOC + SAH-optimal collapse).  Every 10th
-    frame equals the oracle's render of that frame's transforms, and at least one device rebuild happened."""
+    frames queued back to back with device outputs and no host wait).  The instance BVH is rebuilt on the device:
+    up to 4,096 instances by one workgroup in one launch on a side stream (k_build_small: PLOC + SAH-optimal
+    collapse), committed by a copy kernel on the render stream (PRT_TLAS_SMALL=1: "small", "small_always"), else
+    by the multi-launch builder ("default", "always"; "large": 5,000 instances, 40 frames) -- on the default trigger
+    (node-area cost 1.05x the last build's, or 8 refits) or for every frame (PRT_TLAS_REBUILD=always, as the
+    reference's per-frame BVH::Build).  Every 10th frame equals the oracle's render of that frame's transforms, and
+    the device rebuilds happened."""
     import dataclasses
     import torch
     import prt
     monkeypatch.delenv("PRT_TLAS_HOST", raising=False)
     monkeypatch.delenv("PRT_TLAS_REBUILD", raising=False)
-    n, nframes = 1000, 120
+    n, nframes = (5000, 40) if mode == "large" else (1000, 120)
+    monkeypatch.delenv("PRT_TLAS_SMALL", raising=False)
+    if mode.startswith("small"):
+        monkeypatch.setenv("PRT_TLAS_SMALL", "1")
+    if mode.endswith("always"):
+        monkeypatch.setenv("PRT_TLAS_REBUILD", "always")
     sd0 = scenes.instance_field(n, seed=17)
     W, H = 64, 48
     flags = oracle.DEFAULT_FLAGS & ~oracle.ACCUMULATE
@@ -559,6 +568,8 @@ def test_device_tlas_rebuild_long_motion(gpu_ctx, monkeypatch):
         torch.cuda.synchronize()
         si = c.scene_info()
         assert si.tlas_rebuilds >= 1 and si.tlas_depth > 0, (si.tlas_rebuilds, si.tlas_refits)
+        if mode.endswith("always"):
+            assert si.tlas_rebuilds == nframes - 1 and si.tlas_refits == 0, (si.tlas_rebuilds, si.tlas_refits)
         for f, o in out.items():
             a_o, _, _, _ = oracle.OracleScene(frames[f], W, H).render(W, H, spp=2, bounces=3, flags=flags)
             assert np.array_equal(o.cpu().numpy(), a_o), f
