@@ -53,7 +53,14 @@ if os.environ.get("TLAS_MODES") == "trbvh":  # A/B of the device tree's treelet-
 if os.environ.get("TLAS_MODES") == "radius":  # A/B of the device tree's PLOC radius (0 / 1 TRBVH passes)
     MODES = [(f"device rebuild every frame, PLOC radius {r}, {k} TRBVH passes", "always", k + ":" + r)
              for r, k in (("64", "0"), ("512", "0"), ("512", "1"))]
+if os.environ.get("TLAS_MODES") == "small":  # the single-workgroup sync-free builder (PRT_TLAS_SMALL=1)
+    MODES = [("refit only", "0", None), ("small builder, trigger", None, "S"),
+             ("small builder, every frame", "always", "S"), ("multi-launch builder, every frame", "always", None)]
 for mode, env, trbvh in MODES + MODES:
+    os.environ.pop("PRT_TLAS_SMALL", None)
+    if trbvh == "S":
+        os.environ["PRT_TLAS_SMALL"] = "1"
+        trbvh = None
     if trbvh is None:
         os.environ.pop("PRT_TLAS_TRBVH", None)
         os.environ.pop("PRT_TLAS_PLOC_R", None)
@@ -85,6 +92,7 @@ for mode, env, trbvh in MODES + MODES:
     ctx.set_instances(inst)  # a fresh host SAH tree over the final positions
     os.environ.pop("PRT_TLAS_HOST")
     os.environ["PRT_TLAS_REBUILD"] = "0"
+    os.environ.pop("PRT_TLAS_SMALL", None)
     t_fresh, _ = timed(ctx, avg, rgb, 20)
     hd = ctx.scene_info().tlas_depth
     print(f"{N} instances, {F} frames, {mode}: static frame at start {t_first:.3f} ms; drift ms/frame per 20 frames "

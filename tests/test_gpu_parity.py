@@ -2,6 +2,8 @@
 
 Bar: hit records bit-exact where the primitive agrees (>= 99.99 % agreement); images per-channel
 RMSE <= 1e-4 (BASELINE.json), and in practice bit-exact for all but a handful of pixels."""
+import os
+
 import numpy as np
 import pytest
 
@@ -532,6 +534,8 @@ def test_device_tlas_rebuild_long_motion(gpu_ctx, monkeypatch, mode):
     n, nframes = (5000, 40) if mode == "large" else (1000, 120)
     monkeypatch.delenv("PRT_TLAS_SMALL", raising=False)
     if mode.startswith("small"):
+        if os.environ.get("PRT_TEST_TLAS_SMALL") != "1":  # opt-in until the builder has run on the GPU
+            pytest.skip("single-workgroup instance-BVH builder: PRT_TEST_TLAS_SMALL=1 runs it")
         monkeypatch.setenv("PRT_TLAS_SMALL", "1")
     if mode.endswith("always"):
         monkeypatch.setenv("PRT_TLAS_REBUILD", "always")
