@@ -1506,15 +1506,6 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
     HIP_TRY(upload(c->tris, tris.data(), tris.size() * sizeof(TriMT)));
     HIP_TRY(upload(c->stri, stri.data(), stri.size() * sizeof(ShadeTri)));
   }
-  if (kBlasNodeStride != sizeof(Node8) && c->nodes8.bytes) {  // one node per kBlasNodeStride bytes (A/B build)
-    const size_t nn = c->nodes8.bytes / sizeof(Node8);
-    DevBuf wide;
-    HIP_TRY(wide.ensure(kBlasNodeStride * nn));
-    HIP_TRY(hipMemcpy2DAsync(wide.p, kBlasNodeStride, c->nodes8.p, sizeof(Node8), sizeof(Node8), nn,
-                             hipMemcpyDeviceToDevice, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    std::swap(c->nodes8, wide);
-  }
   c->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_build0).count();
   c->built_with = builder;
   HIP_TRY(upload(c->mesh, mh.data(), mh.size() * sizeof(MeshDev)));

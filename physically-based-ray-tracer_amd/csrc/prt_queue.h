@@ -91,17 +91,6 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, uint32_t n, 
   return off + before;
 }
 
-// the same append with one atomic per wave and no barrier (every lane of the wave calls it)
-__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, uint32_t n) {
-  const uint64_t b1 = __ballot(n & 1u), b2 = __ballot((n >> 1) & 1u), b4 = __ballot((n >> 2) & 1u);
-  const uint64_t lt = (1ull << lane_id()) - 1ull;
-  const uint32_t before = (uint32_t)__popcll(b1 & lt) + 2u * (uint32_t)__popcll(b2 & lt) + 4u * (uint32_t)__popcll(b4 & lt);
-  const uint32_t wtot = (uint32_t)__popcll(b1) + 2u * (uint32_t)__popcll(b2) + 4u * (uint32_t)__popcll(b4);
-  uint32_t base = 0;
-  if (lane_id() == 0 && wtot) base = atomicAdd(counter, wtot);
-  return (uint32_t)__shfl((int)base, 0) + before;
-}
-
 // hit record word: prim in the low S.pbits bits (enough for the largest mesh), instance above (prt_api.cpp
 // checks that both fit in 32 bits)
 __device__ __forceinline__ uint32_t pack_hit(const SceneDev& S, uint32_t prim, uint32_t inst) {

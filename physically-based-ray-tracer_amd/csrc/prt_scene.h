@@ -54,19 +54,14 @@ struct TexDev {
 constexpr int kLinearInstances = 64;
 constexpr int kMaxInstances = 1 << 24;
 
-// device stride of a BLAS node in nodes8: 80 B packed (a node straddles two 128-B lines about half the time), or
-// with -DPRT_NODE128 (A/B) one node per 128-B line
-#ifdef PRT_NODE128
-constexpr uint32_t kBlasNodeStride = 128;
-#else
-constexpr uint32_t kBlasNodeStride = 80;
-#endif
+// one BLAS node (80 B, 5 x 16-B loads).  A 128-B stride (one line per node) measured slower: the footprint grows
+// 1.6x and the L2 holds less of the tree
 __host__ __device__ inline const uint4* blas_node(const Node8* base, uint32_t node) {
-  return reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(base) + (size_t)node * kBlasNodeStride);
+  return reinterpret_cast<const uint4*>(base + node);
 }
 
 struct SceneDev {
-  const Node8* nodes8;    // all BLASes at kBlasNodeStride; MeshDev.root indexes it
+  const Node8* nodes8;    // all BLASes; MeshDev.root indexes it
   const TriMT* tris;
   const ShadeTri* stri;
   const uint32_t* texels;

@@ -58,13 +58,6 @@ void lane_stats_dump() {
 // (k_resmiss2), which also shades that iteration's misses
 constexpr uint32_t kResFresh = kRiFresh;
 
-// the shading kernels' queue appends: per block (one atomic, three barriers) or, A/B -DPRT_WAVE_APPEND, per wave
-#ifdef PRT_WAVE_APPEND
-#define shade_append(counter, n, sm) wave_append(counter, n)
-#else
-#define shade_append(counter, n, sm) block_append(counter, n, sm)
-#endif
-
 // the merged pipeline's queue of path-2 primaries: the counters of iteration iters + 1 (kind 0), never a path queue
 __device__ __forceinline__ uint32_t q2_iter(const TraceArgs& A) { return 2u * (uint32_t)A.bounces; }
 
@@ -400,7 +393,7 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
       }
     }
     prefetch(c + gridDim.x);
-    const uint32_t s0 = shade_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic
+    const uint32_t s0 = block_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic
     const uint32_t depth = info & 0xFFu, path = (info >> 8) & 1u;
     uint32_t status = kStMiss, emissive = 0;
     bool next = false;
@@ -478,7 +471,7 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
       Bc.seed[item] = seed;
     }
     if constexpr (EXT) {  // the area-light shadow rays of the block, one more append
-      const uint32_t a0 = shade_append(shcnt, area_ray ? 1u : 0u, sm);
+      const uint32_t a0 = block_append(shcnt, area_ray ? 1u : 0u, sm);
       if (area_ray) shq[a0] = (kLightArea << 29) | item;
     }
     if (active) {
@@ -489,7 +482,7 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
       Bc.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20) | (next ? kRiQueued : 0u) | emissive |
                        (EXT ? 0u : kResFresh);
     }
-    const uint32_t slot = shade_append(ncnt, next ? 1u : 0u, sm);
+    const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
     if (next) qn[sub * Bc.qcap + slot] = item;
   }
 }
@@ -565,7 +558,7 @@ __global__ void __launch_bounds__(kBlock, 1) k_shade2m(SceneDev S, TraceArgs A, 
           nr = (uint32_t)nee_rays(kind);
         }
       }
-      const uint32_t s0 = shade_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic per pass
+      const uint32_t s0 = block_append(shcnt, nr, sm);  // the block's shadow-ray slots, one atomic per pass
       uint32_t status = kStMiss, emissive = 0;
       if (nr) {
         const float4 o = rop[item], d = rdp[item];
@@ -607,7 +600,7 @@ __global__ void __launch_bounds__(kBlock, 1) k_shade2m(SceneDev S, TraceArgs A, 
         need2 = pass == 0 && path == 0 && status != kStNeeCont && (fl & kAA);
       }
     }
-    const uint32_t slot = shade_append(ncnt, next ? 1u : 0u, sm);
+    const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
     if (next) qn[sub * Bc.qcap + slot] = item;
   }
 }
