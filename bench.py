@@ -326,11 +326,13 @@ def main():
                "frac": round(hbm_rate / HBM_PEAK_GBS, 4) if hbm_rate else None, "traffic": traffic,
                "source": rec_src}
         # what bounds the kernel, from its stall counters: waves parked on s_waitcnt (dependent loads) most of
-        # their cycles = latency; otherwise the VALU issue rate (or, with no VALU pass, HBM bandwidth)
-        if stall and stall["wait"] > stall["issuing"] + stall["issue_stall"]:
+        # their cycles = latency, otherwise the VALU issue rate; with no fresh stall pass nothing is claimed
+        if not stall:
+            bound = None
+        elif stall["wait"] > stall["issuing"] + stall["issue_stall"]:
             bound = "latency"
         else:
-            bound = "valu" if valu else "hbm"
+            bound = "valu"
         if valu_rate is not None:
             roof = {"bound": bound, "achieved": round(valu_rate, 1), "peak": VALU_PEAK_GINST,
                     "unit": "G VALU wave-instructions/s", "frac": round(valu_rate / VALU_PEAK_GINST, 4),

@@ -156,7 +156,8 @@ struct prt_ctx {
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
   float al[16] = {};
   int32_t area = 0, area_two_sided = 0;
-  bool inst_dirty = true;
+  bool inst_dirty = true;  // the device instance records (k_refit) are out of date
+  bool tlas_dirty = true;  // transforms or meshes changed since the instance BVH was last built / refitted
   // sky, lights, camera
   DevBuf sky;
   int32_t skyw = 0, skyh = 0;
@@ -262,10 +263,17 @@ int ensure_instances(prt_ctx* c) {
   }
   HIP_TRY(hipMemcpyAsync(c->inst_src.p, src.data(), sizeof(InstSrc) * n, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(launch_refit(c->stream, c->inst_src.as<InstSrc>(), n, c->inst.as<InstDev>()));
+  const char* te = std::getenv("PRT_TLAS");
+  const bool use_tlas = n > kLinearInstances || (te && std::atoi(te) == 1);
+  // a materials-only update (prt_set_instance_materials) moves no box: the refit above rewrote the records' kinds
+  // over unchanged inverses and boxes, and the instance BVH is neither refitted, measured nor rebuilt
+  if (!c->tlas_dirty && use_tlas == c->use_tlas && (!use_tlas || c->tlas_n == n)) {
+    c->inst_dirty = false;
+    return PRT_OK;
+  }
   // instance BVH over the refit's world boxes (the same refit_instance on the host), BVH::Build over the
   // BLASInstances every frame as the reference does (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770)
-  const char* te = std::getenv("PRT_TLAS");
-  c->use_tlas = n > kLinearInstances || (te && std::atoi(te) == 1);
+  c->use_tlas = use_tlas;
   // The instance BVH.  The reference rebuilds it every frame (Core/Renderer.cpp:33-41).  Here the host SAH builder
   // builds it when the set of instances changes (its count; or every call with PRT_TLAS_HOST=1, the A/B form);
   // otherwise it is refitted on the device behind k_refit (prt_tlas.hip), and rebuilt on the device (PLOC +
@@ -325,13 +333,18 @@ int ensure_instances(prt_ctx* c) {
     bool rebuild = rebuild_always ||
                    (rebuild_ratio > 0 && max_refits > 0 && c->tlas_since_build >= max_refits);
     if (rebuild_ratio > 0) {
-      for (int k = 0; k < 2; k++)  // costs whose copies have landed (never waits)
-        if (c->tlas_cost_pending[k] && hipEventQuery(c->tlas_cost_ev[k]) == hipSuccess) {
-          c->tlas_cost_pending[k] = false;
-          if (k == 0) c->tlas_base_cost = c->tlas_cost_h[0];
-          else if (c->tlas_base_cost > 0 && c->tlas_cost_h[1] > rebuild_ratio * c->tlas_base_cost) rebuild = true;
+      for (int k = 0; k < 2; k++) {  // costs whose copies have landed (never waits)
+        if (!c->tlas_cost_pending[k]) continue;
+        const hipError_t q = hipEventQuery(c->tlas_cost_ev[k]);
+        if (q == hipErrorNotReady) {
+          (void)hipGetLastError();  // not an error here: the cost is read by a later update
+          continue;
         }
-      (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady is not an error here
+        HIP_TRY(q);
+        c->tlas_cost_pending[k] = false;
+        if (k == 0) c->tlas_base_cost = c->tlas_cost_h[0];
+        else if (c->tlas_base_cost > 0 && c->tlas_cost_h[1] > rebuild_ratio * c->tlas_base_cost) rebuild = true;
+      }
     }
     if (rebuild && c->tlas_small) {
       // sync-free: the side stream refits its own copy of the instance records, one workgroup builds the tree into
@@ -517,6 +530,7 @@ int ensure_instances(prt_ctx* c) {
     c->tlas_small = false;
   }
   c->inst_dirty = false;
+  c->tlas_dirty = false;
   return PRT_OK;
 }
 
@@ -643,6 +657,9 @@ int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
 // wavefront buffers sized for n items and (bounces-1) (result, throughput) stack levels
 // queue counters [iter][path|shadow][kNSub] + traversal fetch counters [iter][path|shadow][8 parts]
 constexpr size_t kCtrWords = (size_t)(kMaxIters + 2) * 2 * (kNSub + 8) * kCtrStride;
+// shadow-queue entries one shading launch may append per item: <= 4 light-class + 1 area-light ray; the merged
+// pipeline (no extensions) shades path 1's last segment and path 2's first in the same launch, 4 + 4
+constexpr uint32_t shadow_per_item(bool merge) { return merge ? 8u : 5u; }
 int ensure_wave(WaveState& ws, uint32_t n, int bounces, bool ext, bool merge) {
   const uint32_t levels = (uint32_t)std::max(1, bounces - 1);
   // sub-queue t receives the 256-entry chunks c == t (mod kNSub): at most ceil(ceil(n/256)/kNSub) of them
@@ -650,13 +667,13 @@ int ensure_wave(WaveState& ws, uint32_t n, int bounces, bool ext, bool merge) {
   if (ws.n >= n && ws.levels >= levels && (ws.ext || !ext) && (ws.merge || !merge) && ws.wave.p) {
     ws.wb.n = n;  // capacity stays; the SoA strides (R/T: depth * n + item) follow the current n
     ws.wb.qcap = qcap;
-    ws.wb.scap = 5u * qcap;
+    ws.wb.scap = shadow_per_item(merge) * qcap;
     ws.wb.merge = merge ? 1 : 0;
     return PRT_OK;
   }
   // merge: two record slots (path 1, path 2) per item for the NEE record, hit point, status and stack
   const size_t ns = merge ? 2ull * n : (size_t)n;
-  const size_t qn = (size_t)kNSub * qcap, sn = 5 * qn;  // <= 4 light-class + 1 area-light shadow rays per item
+  const size_t qn = (size_t)kNSub * qcap, sn = shadow_per_item(merge) * qn;
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
   const size_t o_seed = take(4ull * n), o_info = take(4ull * n), o_rinfo = take(4ull * ns), o_ro = take(16ull * n),
@@ -676,7 +693,7 @@ int ensure_wave(WaveState& ws, uint32_t n, int bounces, bool ext, bool merge) {
   W.n = n;
   W.base = 0;
   W.qcap = qcap;
-  W.scap = 5u * qcap;
+  W.scap = shadow_per_item(merge) * qcap;
   W.seed = (uint32_t*)(b + o_seed); W.info = (uint32_t*)(b + o_info); W.rinfo = (uint32_t*)(b + o_rinfo);
   W.ro = (float4*)(b + o_ro); W.rd = (float4*)(b + o_rd); W.R = (float4*)(b + o_R); W.T = (float4*)(b + o_T);
   W.s1 = (float4*)(b + o_s1); W.jit = (float2*)(b + o_jit); W.hit = (float4*)(b + o_hit);
@@ -1513,6 +1530,7 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
   c->mesh_info = info;
   c->max_depth = maxd;
   c->inst_dirty = true;
+  c->tlas_dirty = true;
   PRT_FOR_MEMBERS(prt_set_meshes(m, m_in, n));
   return PRT_OK;
 }
@@ -1532,6 +1550,7 @@ int prt_set_instances(prt_ctx* c, const float* xf, const uint32_t* mi, int32_t n
   if ((size_t)n != c->inst_mesh.size()) c->inst_kind.clear();  // materials survive transform updates only
   c->inst_mesh.assign(mi, mi + n);
   c->inst_dirty = true;
+  c->tlas_dirty = true;
   HIP_TRY(hipSetDevice(c->device));
   if (!c->mesh_host.empty()) {
     const int rc = ensure_instances(c);
