@@ -204,6 +204,9 @@ def main():
                     help="c4 = the metric's workload (default); c5 = C4 + a quad area light with MIS at 4K, 16 spp, depth 8")
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
+                    help="frames in flight (prt_set_frames_in_flight): 2 overlaps consecutive frames' wavefront "
+                         "chains, accumulation and gathers stay in call order")
     ap.add_argument("--host-out", action="store_true",
                     help="outputs (avg + rgb8) to host memory every step: the PCIe-inclusive rate (not the contract value)")
     args = ap.parse_args()
@@ -242,6 +245,7 @@ def main():
     ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
     info = ctx.scene_info()
     ranks_seen = 1
+    ctx.set_frames_in_flight(args.inflight)
     if world > 1:
         si = prt.tiles.join_rccl(ctx, dist, args.tile)
         one = torch.ones(1, dtype=torch.float32, device=dev)

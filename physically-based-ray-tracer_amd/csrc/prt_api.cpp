@@ -89,6 +89,16 @@ struct ItemGroup {
   hipEvent_t done = nullptr;
   WaveState ws;
 };
+// a frame in flight (prt_set_frames_in_flight): the wavefront chain of one call on its own stream.  Slot 0 uses the
+// context's own wavefront state and frame buffer, slot 1 its own; done = the call's last work (the accumulation,
+// and for a sharded frame its gather and untile), which the next call's accumulation waits for
+struct Flight {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  WaveState ws;
+  DevBuf frames;
+  bool pending = false;  // done is not yet in the context stream's order
+};
 
 struct MeshHost {
   float bmin[3], bmax[3];
@@ -194,6 +204,11 @@ struct prt_ctx {
   DevBuf shtiles, gathered;       // this rank's tile buffer; rank 0: [world][tile buffer] gathered
   hipEvent_t sh_ev = nullptr;     // member: tiles handed to member 0; member 0: untile done
   bool layout_checked = false;    // check_layout_once done
+  // frames in flight (prt_set_frames_in_flight): 1 = every call complete in the context stream's order
+  int32_t inflight = 1;
+  Flight fl[2];
+  int32_t next_fl = 0, last_fl = -1;  // the slot of the next call / of the last call still ordering accumulation
+  hipEvent_t fl_fork = nullptr;
 };
 
 namespace {
@@ -206,8 +221,25 @@ constexpr int kMaxBvhDepth = 64;
 int stack_depth(const prt_ctx* c) { return c->max_depth + (c->use_tlas ? c->tlas_depth : 0); }
 bool depth_ok(const prt_ctx* c) { return stack_depth(c) <= kMaxBvhDepth; }
 
-// finish the frames queued on the context stream before a setter overwrites (or frees) resident buffers
+// frames in flight: the context stream waits for every call still in flight.  Every entry point but an in-flight
+// prt_render starts with it, so its work (and the host waits of drain()) comes after those frames
+int join_flights(prt_ctx* c) {
+  if (c->last_fl < 0) return PRT_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  for (Flight& f : c->fl)
+    if (f.pending) {
+      HIP_TRY(hipStreamWaitEvent(c->stream, f.done, 0));
+      f.pending = false;
+    }
+  c->last_fl = -1;  // the next call's accumulation is ordered through the context stream again
+  return PRT_OK;
+}
+
+// finish the frames queued on the context stream (and the frames in flight) before a setter overwrites (or frees)
+// resident buffers
 int drain(prt_ctx* c) {
+  const int rc = join_flights(c);
+  if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return PRT_OK;
@@ -640,6 +672,10 @@ int32_t frames_of(const prt_render_params* p) {
 
 int ensure_state(prt_ctx* c, int32_t W, int32_t H) {
   if (c->accW == W && c->accH == H && c->acc.p) return PRT_OK;
+  if (c->acc.p) {  // a new image size: the frames still queued (or in flight) read the old state
+    const int rc = drain(c);
+    if (rc) return rc;
+  }
   const size_t n = (size_t)W * H;
   HIP_TRY(c->acc.ensure(n * 16));
   HIP_TRY(c->nsamp.ensure(n * 4));
@@ -719,11 +755,11 @@ Counters* ray_totals_dev(prt_ctx* c) { return reinterpret_cast<Counters*>(c->dia
 // k_shade2 reads its arguments through the kernarg segment (prt_wave2.hip Shade2Args) and flags diag[1] when the
 // layout it assumes is not the compiler's (it then shades nothing).  Checked once per context, after its first
 // render (one host wait), so stats-less frame loops fail loudly too; prt_ray_totals re-checks it
-int check_layout_once(prt_ctx* c) {
+int check_layout_once(prt_ctx* c, hipStream_t st) {
   if (c->layout_checked) return PRT_OK;
   uint32_t v[2] = {0, 0};
-  HIP_TRY(hipMemcpyAsync(v, c->diag.p, 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpyAsync(v, c->diag.p, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
   if (v[1] != 0) return fail(PRT_ERR_HIP, "k_shade2: kernel-argument layout check failed (Shade2Args)");
   c->layout_checked = true;
   return PRT_OK;
@@ -784,7 +820,8 @@ uint32_t groups_for(const SceneDev& S, uint64_t items, int32_t npass) {
   return g;
 }
 
-int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int32_t rank, RenderPlan& R) {
+int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int32_t rank, RenderPlan& R,
+                   Flight* fl = nullptr) {
   SceneDev& S = R.S;
   int rc = injected_failure(rank);
   if (rc) return rc;
@@ -815,7 +852,8 @@ int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int
   const int32_t fmax = (int32_t)std::max<uint64_t>(1, max_items / std::max<uint64_t>(per, 1));
   const int32_t npass = F > fmax ? (F + fmax - 1) / fmax : 1;
   const int32_t F0 = std::min(F, fmax);
-  HIP_TRY(c->frames.ensure(sizeof(float4) * (size_t)std::max<uint64_t>(per * (uint64_t)F0, 1)));
+  DevBuf& frames = fl ? fl->frames : c->frames;
+  HIP_TRY(frames.ensure(sizeof(float4) * (size_t)std::max<uint64_t>(per * (uint64_t)F0, 1)));
   TraceArgs& A = R.A;
   A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
   A.frame_index = p->frame_index; A.seed = p->seed; A.frames = F0;
@@ -825,7 +863,7 @@ int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int
                                                 : "too many wavefront iterations");
   // sized for the first (largest) pass; later passes hold no more items
   const uint64_t n0 = per * (uint64_t)F0;
-  const uint32_t G = groups_for(S, n0, npass);
+  const uint32_t G = fl ? 1u : groups_for(S, n0, npass);
   for (uint32_t g = 0; g < G; g++) {
     if (g > 0 && c->grp.size() < g) {  // a concurrent group's stream and join event (created once)
       ItemGroup ig;
@@ -837,7 +875,7 @@ int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int
       c->grp.push_back(std::move(ig));
     }
     if (g > 0 && !c->fork) HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
-    WaveState& w = g == 0 ? c->ws : c->grp[g - 1].ws;
+    WaveState& w = g == 0 ? (fl ? fl->ws : c->ws) : c->grp[g - 1].ws;
     rc = ensure_wave(w, (uint32_t)(n0 * (g + 1) / G - n0 * g / G), p->bounces, ext, merge);
     if (rc) return rc;
   }
@@ -848,8 +886,11 @@ int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int
 
 // the shared trace + accumulate sequence for prt_render / prt_render_tiles, after prepare_render: enqueues the
 // render on the context stream; want_stats: per-launch timers + read_stats() afterwards
+// fl: a frame in flight (its stream, wavefront state and frame buffer; the accumulation first waits for acc_after,
+// the previous call's last work), else the context stream and state
 int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, RenderPlan& R, float4* avg_dev,
-                   uint32_t* rgb8_dev, float4* tiles_dev, bool want_stats) {
+                   uint32_t* rgb8_dev, float4* tiles_dev, bool want_stats, Flight* fl = nullptr,
+                   hipEvent_t acc_after = nullptr) {
   SceneDev& S = R.S;
   TraceArgs& A = R.A;
   const int32_t F = R.F, fmax = R.fmax, npass = R.npass;
@@ -858,11 +899,13 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
   const uint32_t iters = R.iters;
   int rc = PRT_OK;
   const uint32_t G = R.groups;
-  LaunchCfg L{c->stream, occ_for(c), 1};
-  auto gws = [&](uint32_t g) -> WaveState& { return g == 0 ? c->ws : c->grp[g - 1].ws; };
-  auto gcfg = [&](uint32_t g) { return LaunchCfg{g == 0 ? c->stream : c->grp[g - 1].stream, L.occ, G}; };
+  const hipStream_t st = fl ? fl->stream : c->stream;
+  WaveState& ws0 = fl ? fl->ws : c->ws;
+  LaunchCfg L{st, occ_for(c), 1};
+  auto gws = [&](uint32_t g) -> WaveState& { return g == 0 ? ws0 : c->grp[g - 1].ws; };
+  auto gcfg = [&](uint32_t g) { return LaunchCfg{g == 0 ? st : c->grp[g - 1].stream, L.occ, G}; };
   // the call's own events (prt_stats ms / ms_trace) only with stats: each record is a gap between kernels
-  if (want_stats) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  if (want_stats) HIP_TRY(hipEventRecord(c->ev[0], st));
   // PRT_TAIL=0 switches the cooperative traversal tail off (prt_persist.h; A/B runs only)
   const char* et = std::getenv("PRT_TAIL");
   const int32_t coop = (et && std::atoi(et) == 0) ? 0 : 1;
@@ -874,7 +917,7 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
   if (want_stats && std::getenv("PRT_DEBUG_QUEUES")) {
     const size_t tlb = 32ull * kTlWaves * (kMaxIters + 2);
     HIP_TRY(c->tl.ensure(tlb));
-    HIP_TRY(hipMemsetAsync(c->tl.p, 0, tlb, c->stream));
+    HIP_TRY(hipMemsetAsync(c->tl.p, 0, tlb, st));
     tl = c->tl.as<unsigned long long>();
   }
   c->carry_segments = c->carry_shadow = 0;
@@ -885,9 +928,9 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
     A.frame_index = p->frame_index + f0;
     A.frames = Fb;
     const uint64_t nb = per * (uint64_t)Fb;  // this pass's items, cut into G contiguous ranges
-    float4* frames = c->frames.as<float4>();
+    float4* frames = (fl ? fl->frames : c->frames).as<float4>();
     if (G > 1) {  // the groups' streams start after everything already on the context stream
-      HIP_TRY(hipEventRecord(c->fork, c->stream));
+      HIP_TRY(hipEventRecord(c->fork, st));
       for (uint32_t g = 1; g < G; g++) HIP_TRY(hipStreamWaitEvent(gcfg(g).stream, c->fork, 0));
     }
     for (uint32_t g = 0; g < G; g++) {
@@ -913,9 +956,9 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
         HIP_TRY(launch_wave2_iter(gcfg(g), S, A, M, gws(g).wb, frames + gws(g).wb.base, timers ? &c->wt : nullptr, it));
     for (uint32_t g = 1; g < G; g++) {  // join: the accumulation reads every group's frame values
       HIP_TRY(hipEventRecord(c->grp[g - 1].done, gcfg(g).stream));
-      HIP_TRY(hipStreamWaitEvent(c->stream, c->grp[g - 1].done, 0));
+      HIP_TRY(hipStreamWaitEvent(st, c->grp[g - 1].done, 0));
     }
-    if (last && want_stats) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    if (last && want_stats) HIP_TRY(hipEventRecord(c->ev[1], st));
     // post-processing (single-GPU image): the screen pass needs the average and, for the aberration, the
     // accumulator before the last frame
     float4* acc_prev = nullptr;
@@ -924,9 +967,11 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
       if (!avg_dev) { HIP_TRY(c->avg.ensure(np * 16)); avg_dev = c->avg.as<float4>(); }
       if (c->pfx.aberration != 0) { HIP_TRY(c->accprev.ensure(np * 16)); acc_prev = c->accprev.as<float4>(); }
     }
+    // frames in flight: the accumulation state (and outputs, ray totals) are updated in call order
+    if (acc_after) HIP_TRY(hipStreamWaitEvent(st, acc_after, 0));
     HIP_TRY(launch_accumulate(L, M, Fb, p->flags, frames, c->acc.as<float4>(), c->nsamp.as<int32_t>(),
                               c->dist.as<float>(), avg_dev, post ? nullptr : rgb8_dev, tiles_dev, acc_prev,
-                              c->ws.wb.ctr, iters, ray_totals_dev(c)));
+                              ws0.wb.ctr, iters, ray_totals_dev(c)));
     for (uint32_t g = 1; g < G; g++) HIP_TRY(launch_add_totals(L, gws(g).wb.ctr, iters, ray_totals_dev(c)));
     if (post && last) {
       // with !accumulates the accumulator held this frame's value until the end-of-frame memset
@@ -936,8 +981,8 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
     }
     if (want_stats && !last) {  // this pass's ray counts, before the next pass clears the counters (G == 1)
       std::vector<uint32_t> ctr((size_t)(iters + 2) * 2 * kNSub * kCtrStride);
-      HIP_TRY(hipMemcpyAsync(ctr.data(), c->ws.wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(hipMemcpyAsync(ctr.data(), ws0.wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
       for (uint32_t k = 0; k < iters + 2; k++)  // (+2: the merged path-2 primaries are counted at iters + 1)
         for (uint32_t s2 = 0; s2 < kNSub; s2++) {
           c->carry_segments += ctr[((k * 2 + 0) * kNSub + s2) * kCtrStride];
@@ -945,20 +990,61 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
         }
     }
   }
-  if (want_stats) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  if (want_stats) HIP_TRY(hipEventRecord(c->ev[2], st));
   c->last_iters = iters;
   c->last_timers = timers;
   c->last_groups = G;
   c->last_paths = tile_image_pixels(M) * (uint64_t)F * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
-  return check_layout_once(c);
+  return check_layout_once(c, st);
 }
 
+// frames in flight: the slot the next call takes (calls with stats or host outputs run in the context stream's
+// order instead)
+Flight* flight_for(prt_ctx* c, bool sync) {
+  return (c->inflight > 1 && !sync && c->sh_kind != 2) ? &c->fl[c->next_fl] : nullptr;
+}
+// the call of slot f is enqueued: its stream forked from the context stream (fork_flight) before its first work;
+// here the previous call joins the context stream (its outputs are complete in the caller's order from now on)
+int fork_flight(prt_ctx* c, Flight& f) {
+  HIP_TRY(hipEventRecord(c->fl_fork, c->stream));
+  HIP_TRY(hipStreamWaitEvent(f.stream, c->fl_fork, 0));
+  return PRT_OK;
+}
+int land_flight(prt_ctx* c, Flight& f) {
+  HIP_TRY(hipEventRecord(f.done, f.stream));
+  const int32_t s = (int32_t)(&f - c->fl);
+  Flight& o = c->fl[s ^ 1];
+  if (o.pending) {
+    HIP_TRY(hipStreamWaitEvent(c->stream, o.done, 0));
+    o.pending = false;
+  }
+  f.pending = true;
+  c->last_fl = s;
+  c->next_fl = s ^ 1;
+  return PRT_OK;
+}
+// the event the next call's accumulation waits for: the last call still in flight (none: the context stream orders)
+hipEvent_t flight_after(const prt_ctx* c) { return c->last_fl >= 0 ? c->fl[c->last_fl].done : nullptr; }
+
 int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4* avg_dev, uint32_t* rgb8_dev,
-               float4* tiles_dev, bool want_stats, int32_t rank = 0) {
-  RenderPlan R;
-  const int rc = prepare_render(c, p, M, rank, R);
+               float4* tiles_dev, bool want_stats, int32_t rank = 0, bool sync = true) {
+  Flight* f = flight_for(c, want_stats || sync);
+  int rc = f ? PRT_OK : join_flights(c);
   if (rc) return rc;
-  return enqueue_render(c, p, M, R, avg_dev, rgb8_dev, tiles_dev, want_stats);
+  RenderPlan R;
+  rc = prepare_render(c, p, M, rank, R, f);
+  if (rc) return rc;
+  if (!f) return enqueue_render(c, p, M, R, avg_dev, rgb8_dev, tiles_dev, want_stats);
+  rc = fork_flight(c, *f);
+  if (rc) return rc;
+  rc = enqueue_render(c, p, M, R, avg_dev, rgb8_dev, tiles_dev, false, f, flight_after(c));
+  const int lrc = land_flight(c, *f);  // a failed call's partial work joins the context stream too
+  if (rc) {
+    const std::string why = g_err;
+    (void)join_flights(c);
+    return fail(rc, why);
+  }
+  return lrc;
 }
 
 // the context's traversal stack overflow count (SceneDev::diag[0]); waits for the context stream.  diag[1] != 0:
@@ -1122,7 +1208,8 @@ void post_zero_gather(prt_ctx* c, size_t per) {
 // RCCL: one ncclGather per frame on this rank's stream.  Local group: each member renders on its own stream
 // and copies its tile buffer into member 0's gathered buffer (peer copy over xGMI across devices); member 0
 // waits for those copies, and the members' next copies wait for member 0's untile.
-int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint32_t* rgb_dev, prt_stats* stats) {
+int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint32_t* rgb_dev, prt_stats* stats,
+                   bool sync) {
   const int32_t W = p->width, H = p->height, ts = c->sh_tile, world = c->sh_world;
   if (c->pfx.enabled && c->pfx.aberration != 0)
     return fail(PRT_ERR_UNSUPPORTED, "chromatic aberration needs the accumulators of neighbouring tiles");
@@ -1134,6 +1221,14 @@ int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint
   const bool coll = c->sh_kind == 1;  // RCCL: the peers of this rank meet it in this frame's ncclGather
   if (coll && !c->comm) return fail(PRT_ERR_HIP, "the RCCL communicator was aborted by an earlier failed frame");
   const Rccl* R = coll ? rccl(nullptr) : nullptr;
+  // frames in flight (RCCL shards): the frame's chain, gather and untile on the slot's stream; the accumulation
+  // waits for the previous call's untile, so the gathers stay in call order on every rank
+  Flight* f = coll ? flight_for(c, stats != nullptr || sync) : nullptr;
+  if (!f) {
+    const int jrc = join_flights(c);
+    if (jrc) return jrc;
+  }
+  const hipStream_t st = f ? f->stream : c->stream;
   // 1. everything that can fail, on every member, before any render work is enqueued: a failure leaves every
   //    member's accumulation state as it was (the next frame is the one the failed call would have been)
   std::vector<RenderPlan> plans(all.size());
@@ -1143,7 +1238,7 @@ int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint
       const int32_t rank = c->sh_kind == 2 ? (int32_t)k : c->sh_rank;
       HIP_TRY(hipSetDevice(m->device));
       HIP_TRY(m->shtiles.ensure(per * sizeof(float4)));
-      const int rc = prepare_render(m, p, make_tilemap(W, H, ts, rank, world), rank, plans[k]);
+      const int rc = prepare_render(m, p, make_tilemap(W, H, ts, rank, world), rank, plans[k], f);
       if (rc) return rc;
     }
     HIP_TRY(hipSetDevice(c->device));
@@ -1157,31 +1252,48 @@ int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint
   };
   // 2. the renders
   auto enqueue_all = [&]() -> int {
+    if (f) {
+      const int frc = fork_flight(c, *f);
+      if (frc) return frc;
+    }
     for (size_t k = 0; k < all.size(); k++) {
       prt_ctx* m = all[k];
       const int32_t rank = c->sh_kind == 2 ? (int32_t)k : c->sh_rank;
       HIP_TRY(hipSetDevice(m->device));
       const TileMap M = make_tilemap(W, H, ts, rank, world);
-      if (per > M.items)  // the tail of a shorter rank's buffer
-        HIP_TRY(hipMemsetAsync(m->shtiles.as<float4>() + M.items, 0, sizeof(float4) * (per - M.items), m->stream));
-      const int rc = enqueue_render(m, p, M, plans[k], nullptr, nullptr, m->shtiles.as<float4>(), stats != nullptr);
+      const hipStream_t ms = f ? st : m->stream;
+      if (per > M.items)  // the tail of a shorter rank's buffer (zeros over zeros while a previous gather reads it)
+        HIP_TRY(hipMemsetAsync(m->shtiles.as<float4>() + M.items, 0, sizeof(float4) * (per - M.items), ms));
+      const int rc = enqueue_render(m, p, M, plans[k], nullptr, nullptr, m->shtiles.as<float4>(), stats != nullptr,
+                                    f, f ? flight_after(c) : nullptr);
       if (rc) return rc;
     }
     HIP_TRY(hipSetDevice(c->device));
     return PRT_OK;
   };
   int rc = prepare_all();
-  if (!rc) rc = enqueue_all();
+  bool forked = false;
+  if (!rc) {
+    rc = enqueue_all();
+    forked = f != nullptr;
+  }
   if (rc) {
     // RCCL: the other ranks are already (or soon) inside this frame's ncclGather; post this rank's part (zeros)
-    // so they complete, then report the local error
+    // so they complete, then report the local error (frames in flight: after the earlier calls' gathers)
+    const std::string why = g_err;
+    if (forked) (void)land_flight(c, *f);
+    (void)join_flights(c);
+    g_err = why;
     if (coll) post_zero_gather(c, per);
     return rc;
   }
   float4* g = root ? c->gathered.as<float4>() : nullptr;
   if (coll) {
-    const ncclResult_t r = R->Gather(c->shtiles.p, g, per * 4, ncclFloat32, 0, c->comm, c->stream);
-    if (r != ncclSuccess) return fail(PRT_ERR_HIP, std::string("ncclGather: ") + R->GetErrorString(r));
+    const ncclResult_t r = R->Gather(c->shtiles.p, g, per * 4, ncclFloat32, 0, c->comm, st);
+    if (r != ncclSuccess) {
+      if (f) (void)land_flight(c, *f);
+      return fail(PRT_ERR_HIP, std::string("ncclGather: ") + R->GetErrorString(r));
+    }
   } else {
     HIP_TRY(hipMemcpyAsync(g, c->shtiles.p, per * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
     for (size_t k = 1; k < all.size(); k++) {
@@ -1199,10 +1311,11 @@ int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint
     for (size_t k = 1; k < all.size(); k++) HIP_TRY(hipStreamWaitEvent(c->stream, all[k]->sh_ev, 0));
   }
   if (root && (avg_dev || rgb_dev)) {
-    LaunchCfg L{c->stream, occ_for(c)};
+    LaunchCfg L{st, occ_for(c)};
     const PostDev P = post_params(c, W, H);
     HIP_TRY(launch_untile(L, W, H, ts, world, (uint32_t)per, g, avg_dev, rgb_dev, c->pfx.enabled ? &P : nullptr));
   }
+  if (f) return land_flight(c, *f);
   if (c->sh_ev) HIP_TRY(hipEventRecord(c->sh_ev, c->stream));
   if (stats) {
     prt_stats sum{};
@@ -1244,6 +1357,13 @@ int shard_setup(prt_ctx* c, int32_t tile) {
   if (!c->sh_ev) HIP_TRY(hipEventCreateWithFlags(&c->sh_ev, hipEventDisableTiming));
   return PRT_OK;
 }
+
+// every entry point but an in-flight prt_render first joins the frames in flight (join_flights)
+#define PRT_JOIN(ctx)                       \
+  do {                                      \
+    const int rcj_ = join_flights(ctx);     \
+    if (rcj_) return rcj_;                  \
+  } while (0)
 
 // a setter of a local group applies to every member (member 0 = the group context itself)
 #define PRT_FOR_MEMBERS(call)                 \
@@ -1322,7 +1442,14 @@ int prt_destroy(prt_ctx* c) {
   for (prt_ctx* m : c->members) (void)prt_destroy(m);
   c->members.clear();
   (void)hipSetDevice(c->device);
+  (void)join_flights(c);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (Flight& f : c->fl) {
+    if (f.stream) (void)hipStreamSynchronize(f.stream);
+    if (f.done) (void)hipEventDestroy(f.done);
+    if (f.stream) (void)hipStreamDestroy(f.stream);
+  }
+  if (c->fl_fork) (void)hipEventDestroy(c->fl_fork);
   if (c->comm && c->own_comm) {
     const Rccl* R = rccl(nullptr);
     if (R) (void)R->CommDestroy(c->comm);
@@ -1354,12 +1481,39 @@ int prt_destroy(prt_ctx* c) {
 
 int prt_set_stream(prt_ctx* c, void* s) {
   if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  const int rc = join_flights(c);  // the frames in flight complete in the old stream's order
+  if (rc) return rc;
   c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own_stream;
+  return PRT_OK;
+}
+
+int prt_set_frames_in_flight(prt_ctx* c, int32_t n) {
+  if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  if (n < 1 || n > 2) return fail(PRT_ERR_INVALID_ARGUMENT, "frames in flight must be 1 or 2");
+  if (n > 1 && c->sh_kind == 2) return fail(PRT_ERR_UNSUPPORTED, "frames in flight on a local shard group");
+  PRT_JOIN(c);
+  HIP_TRY(hipSetDevice(c->device));
+  if (n > 1 && !c->fl_fork) {
+    for (Flight& f : c->fl) {
+      if (!f.stream) HIP_TRY(hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking));
+      if (!f.done) HIP_TRY(hipEventCreateWithFlags(&f.done, hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventCreateWithFlags(&c->fl_fork, hipEventDisableTiming));
+  }
+  c->inflight = n;
+  c->next_fl = 0;
+  return PRT_OK;
+}
+
+int prt_finish(prt_ctx* c) {
+  if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  PRT_JOIN(c);
   return PRT_OK;
 }
 
 int prt_set_textures(prt_ctx* c, const prt_texture* t, int32_t n) {
   if (!c || (n > 0 && !t) || n < 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad textures");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   std::vector<uint32_t> all;
   std::vector<TexDev> host(n);
   for (int32_t i = 0; i < n; i++) {
@@ -1382,6 +1536,7 @@ int prt_set_textures(prt_ctx* c, const prt_texture* t, int32_t n) {
 int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
   const prt_mesh* m = m_in;
   if (!c || !m || n <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad meshes");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   int builder = c->builder;
   if (builder < 0) {
     const char* e = std::getenv("PRT_BUILDER");
@@ -1545,6 +1700,7 @@ int prt_set_bvh_builder(prt_ctx* c, int32_t builder) {
 
 int prt_set_instances(prt_ctx* c, const float* xf, const uint32_t* mi, int32_t n) {
   if (!c || !xf || !mi || n <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad instances");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   if (n > kMaxInstances) return fail(PRT_ERR_UNSUPPORTED, "more than 2^24 instances");
   c->inst_xf.assign(xf, xf + 16 * (size_t)n);
   if ((size_t)n != c->inst_mesh.size()) c->inst_kind.clear();  // materials survive transform updates only
@@ -1562,6 +1718,7 @@ int prt_set_instances(prt_ctx* c, const float* xf, const uint32_t* mi, int32_t n
 
 int prt_set_instance_materials(prt_ctx* c, const int32_t* kinds, int32_t n) {
   if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   if (n == 0 || !kinds) {
     c->inst_kind.clear();
   } else {
@@ -1582,6 +1739,7 @@ int prt_set_instance_materials(prt_ctx* c, const int32_t* kinds, int32_t n) {
 
 int prt_set_area_lights(prt_ctx* c, const prt_area_light* a, int32_t n) {
   if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   if (n < 0 || n > 1 || (n == 1 && !a)) return fail(PRT_ERR_UNSUPPORTED, "at most one area light");
   if (n == 0) {
     c->area = 0;
@@ -1613,6 +1771,7 @@ int prt_set_lights(prt_ctx* c, const prt_lights* l) {
 
 int prt_set_sky(prt_ctx* c, const float* rgb, int32_t w, int32_t h) {
   if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   int rc = drain(c);
   if (rc) return rc;
   if (!rgb || w <= 0 || h <= 0) {
@@ -1678,6 +1837,7 @@ int prt_set_postfx(prt_ctx* c, const prt_postfx* pfx) {
 
 int prt_reset_accumulation(prt_ctx* c, int32_t full) {
   if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   PRT_FOR_MEMBERS(prt_reset_accumulation(m, full));
   if (!c->acc.p) return PRT_OK;
   HIP_TRY(hipSetDevice(c->device));
@@ -1708,6 +1868,7 @@ uint64_t acc_blob_bytes(uint64_t n) { return sizeof(AccHeader) + n * (16 + 4 + 4
 
 int prt_ray_totals(prt_ctx* c, uint64_t* segments, uint64_t* shadow_rays, int32_t reset) {
   if (!c || !segments || !shadow_rays) return fail(PRT_ERR_INVALID_ARGUMENT, "bad ray totals arguments");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   std::vector<prt_ctx*> all{c};
   all.insert(all.end(), c->members.begin(), c->members.end());
   uint64_t seg = 0, sh = 0;
@@ -1738,6 +1899,7 @@ int prt_accumulation_bytes(prt_ctx* c, uint64_t* bytes) {
 
 int prt_save_accumulation(prt_ctx* c, void* blob, uint64_t bytes) {
   if (!c || !blob) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/blob is NULL");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   if (!c->members.empty()) return fail(PRT_ERR_UNSUPPORTED, "accumulation checkpoints of a local group");
   if (!c->acc.p) return fail(PRT_ERR_NOT_READY, "nothing accumulated yet");
   const uint64_t n = (uint64_t)c->accW * c->accH;
@@ -1765,6 +1927,7 @@ int prt_save_accumulation(prt_ctx* c, void* blob, uint64_t bytes) {
 
 int prt_load_accumulation(prt_ctx* c, const void* blob, uint64_t bytes) {
   if (!c || !blob) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/blob is NULL");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   if (!c->members.empty()) return fail(PRT_ERR_UNSUPPORTED, "accumulation checkpoints of a local group");
   AccHeader hd{};
   if (bytes < sizeof(hd)) return fail(PRT_ERR_INVALID_ARGUMENT, "truncated accumulation blob");
@@ -1806,11 +1969,13 @@ int prt_render(prt_ctx* c, const prt_render_params* p, float* avg_rgba, uint32_t
     if (dev_out) rgb_dev = rgb8;
     else { HIP_TRY(c->rgb8.ensure(np * 4)); rgb_dev = c->rgb8.as<uint32_t>(); }
   }
+  // frames in flight only for device outputs without stats (prt_set_frames_in_flight)
+  const bool sync = !dev_out || stats;
   if (c->sh_kind != 0) {
-    rc = render_sharded(c, p, avg_dev, rgb_dev, stats);
+    rc = render_sharded(c, p, avg_dev, rgb_dev, stats, sync);
   } else {
     const TileMap M = make_tilemap(p->width, p->height, 8, 0, 1);
-    rc = run_render(c, p, M, avg_dev, rgb_dev, nullptr, stats != nullptr);
+    rc = run_render(c, p, M, avg_dev, rgb_dev, nullptr, stats != nullptr, 0, sync);
     if (!rc && stats) rc = read_stats(c, stats);
   }
   if (rc) return rc;
@@ -1846,7 +2011,7 @@ int prt_tile_pixel_map(int32_t W, int32_t H, int32_t ts, int32_t rank, int32_t w
 int prt_render_tiles(prt_ctx* c, const prt_render_params* p, int32_t ts, int32_t rank, int32_t world,
                      float* tiles_dev, prt_stats* stats) {
   if (!c || !tiles_dev) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/tiles is NULL");
-  int rc = check_params(p);
+    int rc = check_params(p);
   if (rc) return rc;
   if (ts <= 0 || (ts % 8) != 0 || world <= 0 || rank < 0 || rank >= world)
     return fail(PRT_ERR_INVALID_ARGUMENT, "bad tile geometry");
@@ -1856,7 +2021,9 @@ int prt_render_tiles(prt_ctx* c, const prt_render_params* p, int32_t ts, int32_t
   if (M0.items > M.items)  // pad the tail of the (equal-size) per-rank buffer
     HIP_TRY(hipMemsetAsync(reinterpret_cast<float4*>(tiles_dev) + M.items, 0, sizeof(float4) * (M0.items - M.items),
                            c->stream));
-  rc = run_render(c, p, M, nullptr, nullptr, reinterpret_cast<float4*>(tiles_dev), stats != nullptr, rank);
+  // (device tile buffer: a frame in flight unless stats are asked for)
+  rc = run_render(c, p, M, nullptr, nullptr, reinterpret_cast<float4*>(tiles_dev), stats != nullptr, rank,
+                  stats != nullptr);
   if (!rc && stats) rc = read_stats(c, stats);
   return rc;
 }
@@ -1864,6 +2031,7 @@ int prt_render_tiles(prt_ctx* c, const prt_render_params* p, int32_t ts, int32_t
 int prt_untile(prt_ctx* c, const float* gathered, int32_t W, int32_t H, int32_t ts, int32_t world, float* avg_dev,
                uint32_t* rgb8_dev) {
   if (!c || !gathered) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx/gathered is NULL");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   int64_t per = 0;
   int rc = prt_tile_buffer_pixels(W, H, ts, world, &per);
   if (rc) return rc;
@@ -1879,6 +2047,7 @@ int prt_untile(prt_ctx* c, const float* gathered, int32_t W, int32_t H, int32_t 
 
 int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t out_flags, prt_stats* stats) {
   if (!c || !hits || W <= 0 || H <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad arguments");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   HIP_TRY(hipSetDevice(c->device));
   SceneDev S;
   int rc = scene_ready(c, S);
@@ -1920,6 +2089,7 @@ int prt_trace_primary(prt_ctx* c, int32_t W, int32_t H, prt_hit* hits, uint32_t 
 static int ray_query(prt_ctx* c, int32_t n, const float* O, const float* D, const float* tmax, void* out, bool any) {
   if (!c || n < 0 || (n > 0 && (!O || !D || !out)) || (any && n > 0 && !tmax))
     return fail(PRT_ERR_INVALID_ARGUMENT, "bad ray query arguments");
+  PRT_JOIN(c);
   if (n == 0) return PRT_OK;
   HIP_TRY(hipSetDevice(c->device));
   SceneDev S;
@@ -1969,6 +2139,7 @@ int prt_shard_unique_id(uint8_t id[PRT_SHARD_ID_BYTES]) {
 
 int prt_shard_init_rccl(prt_ctx* c, const uint8_t id[PRT_SHARD_ID_BYTES], int32_t rank, int32_t world, int32_t tile) {
   if (!c || !id || world <= 0 || rank < 0 || rank >= world) return fail(PRT_ERR_INVALID_ARGUMENT, "bad shard rank / world");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   if (c->sh_kind != 0) return fail(PRT_ERR_INVALID_ARGUMENT, "context is already sharded");
   int rc = shard_setup(c, tile);
   if (rc) return rc;
@@ -1991,6 +2162,7 @@ int prt_shard_init_rccl(prt_ctx* c, const uint8_t id[PRT_SHARD_ID_BYTES], int32_
 
 int prt_shard_attach_rccl(prt_ctx* c, void* comm, int32_t tile) {
   if (!c || !comm) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx / comm is NULL");
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
   if (c->sh_kind != 0) return fail(PRT_ERR_INVALID_ARGUMENT, "context is already sharded");
   int rc = shard_setup(c, tile);
   if (rc) return rc;

@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIBPATH = os.path.join(HERE, "libprt.so")
 
 PRT_OK = 0
-ABI_VERSION = 8  # PRT_ABI_VERSION of the include/prt.h these structs mirror
+ABI_VERSION = 9  # PRT_ABI_VERSION of the include/prt.h these structs mirror
 FLAG_AA, FLAG_ACCUMULATE, FLAG_GAMMA, FLAG_NORMALMAP, FLAG_SKYBOX, FLAG_LIGHTED, FLAG_STOCHASTIC = (1 << i for i in range(7))
 FLAGS_DEFAULT = 0x7F
 OUT_DEVICE = 1
@@ -27,7 +27,7 @@ EXPORTS = [
     "prt_untile", "prt_trace_primary", "prt_intersect", "prt_occluded", "prt_get_scene_info", "prt_set_bvh_builder",
     "prt_set_instance_materials", "prt_set_area_lights", "prt_shard_unique_id", "prt_shard_init_rccl",
     "prt_shard_attach_rccl", "prt_create_group", "prt_get_shard_info", "prt_accumulation_bytes",
-    "prt_save_accumulation", "prt_load_accumulation", "prt_ray_totals",
+    "prt_save_accumulation", "prt_load_accumulation", "prt_ray_totals", "prt_set_frames_in_flight", "prt_finish",
 ]
 SHARD_ID_BYTES = 128
 SHARD_NONE, SHARD_RCCL, SHARD_GROUP = 0, 1, 2  # prt_shard_info.transport
@@ -129,6 +129,8 @@ def load():
         "prt_create": ([C.POINTER(DeviceDesc), C.POINTER(vp)], C.c_int),
         "prt_destroy": ([vp], C.c_int),
         "prt_set_stream": ([vp, vp], C.c_int),
+        "prt_set_frames_in_flight": ([vp, i32], C.c_int),
+        "prt_finish": ([vp], C.c_int),
         "prt_set_textures": ([vp, C.POINTER(Texture), i32], C.c_int),
         "prt_set_meshes": ([vp, C.POINTER(Mesh), i32], C.c_int),
         "prt_set_instances": ([vp, vp, vp, i32], C.c_int),

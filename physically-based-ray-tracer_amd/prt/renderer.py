@@ -340,6 +340,15 @@ class Context:
     def set_stream(self, stream_ptr):
         check(self.L.prt_set_stream(self.h, stream_ptr))
 
+    def set_frames_in_flight(self, n):
+        """prt_set_frames_in_flight: with n = 2 a render with device outputs overlaps the previous one; its outputs
+        are complete in the context stream's order once the next render is enqueued or finish() was called."""
+        check(self.L.prt_set_frames_in_flight(self.h, int(n)))
+
+    def finish(self):
+        """prt_finish: the context stream waits for every frame in flight."""
+        check(self.L.prt_finish(self.h))
+
 
 def _checked(st):
     """Stats of a call whose context has dropped a traversal stack group (prt_stats.stack_overflows) raise:

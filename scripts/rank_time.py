@@ -15,6 +15,7 @@ import prt  # noqa: E402
 from prt import scenes  # noqa: E402
 
 args = sys.argv[1:]
+INFLIGHT = int(os.environ.get("PRT_RANK_INFLIGHT", "1"))  # frames in flight (prt_set_frames_in_flight)
 C5 = bool(args) and args[0] == "c5"
 if C5:
     args = args[1:]
@@ -25,6 +26,7 @@ ctx = prt.Context(0)
 ctx.set_stream(torch.cuda.current_stream().cuda_stream)
 ctx.set_scene(prt.Scene.from_data(sd))
 ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
+ctx.set_frames_in_flight(INFLIGHT)
 base = None
 WORLDS = [int(a) for a in args] or [1, 2, 4, 8]
 for world in WORLDS:
@@ -34,7 +36,7 @@ for world in WORLDS:
         ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i)
     ctx.ray_totals(reset=True)
     torch.cuda.synchronize()
-    n = 2 if C5 else 5
+    n = 2 if C5 else 8
     t0 = time.perf_counter()
     for i in range(n):
         ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i)
@@ -42,5 +44,5 @@ for world in WORLDS:
     ms = (time.perf_counter() - t0) * 1e3 / n
     seg, sh = ctx.ray_totals(reset=True)
     base = base or ms * world
-    print(f"world {world}: rank-0 frame {ms:.3f} ms  rays {(seg + sh) // n}  "
+    print(f"world {world}: rank-0 frame {ms:.3f} ms  rays {(seg + sh) // n}  inflight {INFLIGHT}  "
           f"ideal {base / world:.3f} ms  efficiency {base / world / ms:.2f}", flush=True)

@@ -1,0 +1,154 @@
+"""Frames in flight (include/prt.h prt_set_frames_in_flight, ABI 9): with 2 frames in flight a prt_render with
+device outputs enqueues its wavefront chain on one of two internal streams, so consecutive calls overlap, while the
+accumulation (the reference's progressive mean, Core/Renderer.cpp:81-104) and a sharded frame's gather stay in call
+order.  Every frame must equal the one-at-a-time render bit for bit: outputs, ray totals, through instance updates
+(the instance BVH refitted between frames), a camera change with an accumulation reset, a stats call in between,
+the merged and unmerged pipelines and the RCCL gather."""
+import numpy as np
+import pytest
+
+from helpers import gpu_scene
+from prt import scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(c, sd, W, H, n, moves, stream):
+    """n accumulating frames with device outputs (one output pair per frame), instance moves before frame
+    `moves`, a camera change + accumulation reset before frame n - 2 and a stats render at the end."""
+    import torch
+    import prt
+    outs = []
+    inst = [(m, np.array(T, np.float32)) for m, T in sd.instances]
+    for f in range(n):
+        if f == moves:
+            inst = [(m, _shift(T, m)) for m, T in inst]
+            c.set_instances(inst)
+        if f == n - 2:
+            cam = prt.Camera(np.asarray(sd.cam_pos, np.float32) + np.float32(0.25), sd.cam_target,
+                             np.float32(W) / np.float32(H))
+            c.set_camera(cam)
+            c.reset_accumulation(full=False)
+        with torch.cuda.stream(stream):
+            avg = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+            rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        c.render(W, H, 4, 3, frame_index=2 * f, avg=avg.data_ptr(), rgb8=rgb.data_ptr(), device_out=True,
+                 stats=False)
+        outs.append((avg, rgb))
+    a, r, st = c.render(W, H, 4, 3, frame_index=2 * n)  # host outputs + stats: joins the frames in flight
+    torch.cuda.synchronize()
+    seg, sh = c.ray_totals(reset=True)
+    return [(o.cpu().numpy(), g.cpu().numpy()) for o, g in outs], (a, r, st.segments, st.shadow_rays), (seg, sh)
+
+
+def _shift(T, m):
+    T = T.copy()
+    if m == 1:  # the tori move, the heightfield stays
+        T[0, 3] += np.float32(0.07)
+        T[2, 3] -= np.float32(0.05)
+    return T
+
+
+@pytest.mark.parametrize("merge", ["default", "0"])
+def test_frames_in_flight_match_one_at_a_time(monkeypatch, merge):
+    import torch
+    import prt
+    if merge == "0":
+        monkeypatch.setenv("PRT_MERGE", "0")
+    else:
+        monkeypatch.delenv("PRT_MERGE", raising=False)
+    sd = scenes.instance_field(120, seed=9)  # above 64 instances: the instance BVH is refitted between frames
+    W, H, n = 96, 64, 7
+    stream = torch.cuda.Stream()
+    res = []
+    for fl in (1, 2):
+        c = prt.Context(0)
+        try:
+            c.set_stream(stream.cuda_stream)
+            gpu_scene(c, sd, W, H)
+            c.set_frames_in_flight(fl)
+            res.append(_frames(c, sd, W, H, n, 3, stream))
+        finally:
+            c.close()
+    (f1, last1, tot1), (f2, last2, tot2) = res
+    for k, ((a1, r1), (a2, r2)) in enumerate(zip(f1, f2)):
+        assert np.array_equal(a1, a2) and np.array_equal(r1, r2), k
+    assert np.array_equal(last1[0], last2[0]) and np.array_equal(last1[1], last2[1])
+    assert last1[2:] == last2[2:] and tot1 == tot2
+
+
+def test_frames_in_flight_outputs_in_stream_order_after_next_call():
+    """A call's device outputs are complete in the context stream's order once the next call is enqueued (or
+    prt_finish): a copy enqueued on the caller's stream right then sees the finished frame."""
+    import torch
+    import prt
+    sd = scenes.multi_instance(scenes.config_small(60, 40))
+    W, H = 100, 70
+    stream = torch.cuda.Stream()
+    ref = prt.Context(0)
+    c = prt.Context(0)
+    try:
+        gpu_scene(ref, sd, W, H)
+        want = [ref.render(W, H, 4, 3, frame_index=2 * f)[0] for f in range(3)]
+        c.set_stream(stream.cuda_stream)
+        gpu_scene(c, sd, W, H)
+        c.set_frames_in_flight(2)
+        got = []
+        with torch.cuda.stream(stream):
+            outs = [torch.zeros((W * H, 4), dtype=torch.float32, device="cuda") for _ in range(3)]
+        for f in range(3):
+            c.render(W, H, 4, 3, frame_index=2 * f, avg=outs[f].data_ptr(), device_out=True, stats=False)
+            if f > 0:
+                with torch.cuda.stream(stream):
+                    got.append(outs[f - 1].clone())
+        c.finish()
+        with torch.cuda.stream(stream):
+            got.append(outs[2].clone())
+        stream.synchronize()
+        for f in range(3):
+            assert np.array_equal(got[f].cpu().numpy(), want[f]), f
+    finally:
+        c.close()
+        ref.close()
+
+
+def test_frames_in_flight_rccl_world1():
+    """An RCCL shard (world 1: the ncclGather path) with 2 frames in flight: each call's gather and untile run on
+    its slot's stream after the previous call's, and every frame equals the unsharded one."""
+    import torch
+    import prt
+    sd = scenes.multi_instance(scenes.config_small(50, 40))
+    W, H = 90, 60
+    ref = prt.Context(0)
+    c = prt.Context(0)
+    try:
+        gpu_scene(ref, sd, W, H)
+        want = [ref.render(W, H, 4, 3, frame_index=2 * f)[:2] for f in range(4)]
+        c.shard_rccl(prt.Context.shard_unique_id(), 0, 1, 32)
+        gpu_scene(c, sd, W, H)
+        c.set_frames_in_flight(2)
+        outs = [(torch.zeros((W * H, 4), dtype=torch.float32, device="cuda"),
+                 torch.zeros(W * H, dtype=torch.int32, device="cuda")) for _ in range(4)]
+        for f, (o, g) in enumerate(outs):
+            c.render(W, H, 4, 3, frame_index=2 * f, avg=o.data_ptr(), rgb8=g.data_ptr(), device_out=True, stats=False)
+        c.finish()
+        torch.cuda.synchronize()
+        for f, ((o, g), (a, r)) in enumerate(zip(outs, want)):
+            assert np.array_equal(o.cpu().numpy(), a), f
+            assert np.array_equal(g.cpu().numpy().view(np.uint32), r), f
+    finally:
+        c.close()
+        ref.close()
+
+
+def test_frames_in_flight_refused_on_local_group():
+    import prt
+    g = prt.Context(group=[0, 0], tile=16)
+    try:
+        with pytest.raises(prt.PrtError):
+            g.set_frames_in_flight(2)
+        g.set_frames_in_flight(1)
+        with pytest.raises(prt.PrtError):
+            g.set_frames_in_flight(3)
+    finally:
+        g.close()
