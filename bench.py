@@ -204,7 +204,7 @@ def main():
                     help="c4 = the metric's workload (default); c5 = C4 + a quad area light with MIS at 4K, 16 spp, depth 8")
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
+    ap.add_argument("--inflight", type=int, default=1, choices=[1, 2, 3, 4],
                     help="frames in flight (prt_set_frames_in_flight): 2 overlaps consecutive frames' wavefront "
                          "chains, accumulation and gathers stay in call order")
     ap.add_argument("--host-out", action="store_true",

@@ -90,8 +90,9 @@ struct ItemGroup {
   WaveState ws;
 };
 // a frame in flight (prt_set_frames_in_flight): the wavefront chain of one call on its own stream.  Slot 0 uses the
-// context's own wavefront state and frame buffer, slot 1 its own; done = the call's last work (the accumulation,
-// and for a sharded frame its gather and untile), which the next call's accumulation waits for
+// context's own wavefront state and frame buffer, the others their own; done = the call's last work (the
+// accumulation, and for a sharded frame its gather and untile), which the next call's accumulation waits for
+constexpr int kMaxFlights = 4;
 struct Flight {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
@@ -206,7 +207,7 @@ struct prt_ctx {
   bool layout_checked = false;    // check_layout_once done
   // frames in flight (prt_set_frames_in_flight): 1 = every call complete in the context stream's order
   int32_t inflight = 1;
-  Flight fl[2];
+  Flight fl[kMaxFlights];
   int32_t next_fl = 0, last_fl = -1;  // the slot of the next call / of the last call still ordering accumulation
   hipEvent_t fl_fork = nullptr;
 };
@@ -307,15 +308,27 @@ int ensure_instances(prt_ctx* c) {
   // BLASInstances every frame as the reference does (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770)
   c->use_tlas = use_tlas;
   // The instance BVH.  The reference rebuilds it every frame (Core/Renderer.cpp:33-41).  Here the host SAH builder
-  // builds it when the set of instances changes (its count; or every call with PRT_TLAS_HOST=1, the A/B form);
-  // otherwise it is refitted on the device behind k_refit (prt_tlas.hip), and rebuilt on the device (PLOC +
-  // SAH-optimal collapse over the current boxes, gpu_build_tlas8) once refitting has raised the tree's node-area
-  // cost above PRT_TLAS_REBUILD (default 1.05) times its cost right after the last build (0: refit only).  The cost is
-  // measured on the device after every refit and read back without a host wait (a pinned copy behind an event):
-  // a frame decides on the latest cost already available.  No host BVH work and no host wait per frame.
+  // builds it when the set of instances changes (its count; or every call with PRT_TLAS_HOST=1, the A/B form).
+  // Every other update:
+  //  - up to kGpuSmallBuild instances (default): rebuilt on the device for every update, the reference's per-frame
+  //    BVH::Build, by one workgroup in one launch on a side stream from the side stream's own refit of the
+  //    instance records (gpu_rebuild_tlas_small), committed over the front tree by a copy kernel on the render
+  //    stream -- no host BVH work and no host wait (PRT_TLAS_SMALL=0 turns it off);
+  //  - otherwise refitted on the device behind k_refit (prt_tlas.hip), and rebuilt on the device by the multi-launch
+  //    builder (PLOC + SAH-optimal collapse over host-computed boxes, gpu_build_tlas8: one host round trip per PLOC
+  //    iteration and collapse level) once refitting has raised the tree's node-area cost above PRT_TLAS_REBUILD
+  //    (default 1.05) times its cost right after the last build, or after PRT_TLAS_MAX_REFITS refits (0: refit
+  //    only).  The cost is measured on the device after every refit and read back without a host wait (a pinned
+  //    copy behind an event): a frame decides on the latest cost already available.
+  // PRT_TLAS_REBUILD=always / <ratio> / 0 overrides the policy of either builder.
   const char* th = std::getenv("PRT_TLAS_HOST");
+  const bool host_tlas = th && std::atoi(th) == 1;
   const char* tr = std::getenv("PRT_TLAS_REBUILD");
-  const bool rebuild_always = tr && std::strcmp(tr, "always") == 0;  // A/B: a device rebuild for every update
+  const char* ts = std::getenv("PRT_TLAS_SMALL");
+  const bool small_ok = !(ts && std::atoi(ts) == 0) && n <= kGpuSmallBuild && !host_tlas;
+  // the builder of the current tree decides the default policy (its instance count is unchanged on a refit)
+  const bool small_now = (use_tlas && c->tlas_n == n && !host_tlas) ? c->tlas_small : small_ok;
+  const bool rebuild_always = tr ? std::strcmp(tr, "always") == 0 : small_now;
   const double rebuild_ratio = rebuild_always ? 0.0 : (tr ? std::atof(tr) : 1.05);
   // and at the latest after PRT_TLAS_MAX_REFITS refits (default 8): the node-area cost understates what a node
   // stretched across the scene costs the rays that must now open it
@@ -361,7 +374,7 @@ int ensure_instances(prt_ctx* c) {
                                 c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(), c->tlas_aabb.as<float>()));
     return PRT_OK;
   };
-  if (c->use_tlas && c->tlas_n == n && !(th && std::atoi(th) == 1)) {
+  if (c->use_tlas && c->tlas_n == n && !host_tlas) {
     bool rebuild = rebuild_always ||
                    (rebuild_ratio > 0 && max_refits > 0 && c->tlas_since_build >= max_refits);
     if (rebuild_ratio > 0) {
@@ -517,10 +530,7 @@ int ensure_instances(prt_ctx* c) {
     c->tlas_nodes = (uint32_t)c->tlas_host.nodes.size();
     // the sync-free device rebuild (up to kGpuSmallBuild instances): the front buffers hold any tree of n instances,
     // and the stacks are sized one level deeper than the host tree so a device tree of that depth is usable
-    // (PRT_TLAS_SMALL=1 opts in: the single-workgroup builder has not yet run on the GPU in this tree)
-    const char* ts = std::getenv("PRT_TLAS_SMALL");
-    c->tlas_small = ts && std::atoi(ts) == 1 && n <= kGpuSmallBuild && !(th && std::atoi(th) == 1) &&
-                    (rebuild_always || rebuild_ratio > 0);
+    c->tlas_small = small_ok && (rebuild_always || rebuild_ratio > 0);
     if (c->tlas_small) {
       c->tlas_depth_cap = c->tlas_depth + 1;
       c->tlas_depth = c->tlas_depth_cap;
@@ -548,7 +558,7 @@ int ensure_instances(prt_ctx* c) {
     if (c->tlas_n != n) c->tlas_rebuilds = c->tlas_refits = 0;
     c->tlas_since_build = 0;
     c->tlas_n = n;
-    if (rebuild_ratio > 0 && !(th && std::atoi(th) == 1)) {  // the cost right after the build (its refit's boxes)
+    if (rebuild_ratio > 0 && !host_tlas) {  // the cost right after the build (its refit's boxes)
       rc = refit_tree();
       if (rc) return rc;
       c->tlas_base_cost = 0;
@@ -775,6 +785,11 @@ int injected_failure(int32_t rank) {
   return PRT_OK;
 }
 
+// the wavefront state and frame buffer of a call: slot 0 of the frames in flight and a call in the context stream's
+// order share the context's own (they never overlap: the latter joins the flights first)
+WaveState& flight_ws(prt_ctx* c, Flight* fl) { return (fl && fl != &c->fl[0]) ? fl->ws : c->ws; }
+DevBuf& flight_frames(prt_ctx* c, Flight* fl) { return (fl && fl != &c->fl[0]) ? fl->frames : c->frames; }
+
 // A call's work items (pixels x reference frames) index the shadow-queue entries as 4 x item + k in 29 bits
 // (prt_wave2.hip kShIndexMask; the light class takes the top 3), so one pass holds at most 2^27 items
 constexpr uint64_t kMaxPassItems = 1ull << 27;
@@ -852,7 +867,7 @@ int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int
   const int32_t fmax = (int32_t)std::max<uint64_t>(1, max_items / std::max<uint64_t>(per, 1));
   const int32_t npass = F > fmax ? (F + fmax - 1) / fmax : 1;
   const int32_t F0 = std::min(F, fmax);
-  DevBuf& frames = fl ? fl->frames : c->frames;
+  DevBuf& frames = flight_frames(c, fl);
   HIP_TRY(frames.ensure(sizeof(float4) * (size_t)std::max<uint64_t>(per * (uint64_t)F0, 1)));
   TraceArgs& A = R.A;
   A.W = p->width; A.H = p->height; A.bounces = p->bounces; A.flags = p->flags; A.mode = p->render_mode;
@@ -875,7 +890,7 @@ int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int
       c->grp.push_back(std::move(ig));
     }
     if (g > 0 && !c->fork) HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
-    WaveState& w = g == 0 ? (fl ? fl->ws : c->ws) : c->grp[g - 1].ws;
+    WaveState& w = g == 0 ? flight_ws(c, fl) : c->grp[g - 1].ws;
     rc = ensure_wave(w, (uint32_t)(n0 * (g + 1) / G - n0 * g / G), p->bounces, ext, merge);
     if (rc) return rc;
   }
@@ -900,7 +915,7 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
   int rc = PRT_OK;
   const uint32_t G = R.groups;
   const hipStream_t st = fl ? fl->stream : c->stream;
-  WaveState& ws0 = fl ? fl->ws : c->ws;
+  WaveState& ws0 = flight_ws(c, fl);
   LaunchCfg L{st, occ_for(c), 1};
   auto gws = [&](uint32_t g) -> WaveState& { return g == 0 ? ws0 : c->grp[g - 1].ws; };
   auto gcfg = [&](uint32_t g) { return LaunchCfg{g == 0 ? st : c->grp[g - 1].stream, L.occ, G}; };
@@ -928,7 +943,7 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
     A.frame_index = p->frame_index + f0;
     A.frames = Fb;
     const uint64_t nb = per * (uint64_t)Fb;  // this pass's items, cut into G contiguous ranges
-    float4* frames = (fl ? fl->frames : c->frames).as<float4>();
+    float4* frames = flight_frames(c, fl).as<float4>();
     if (G > 1) {  // the groups' streams start after everything already on the context stream
       HIP_TRY(hipEventRecord(c->fork, st));
       for (uint32_t g = 1; g < G; g++) HIP_TRY(hipStreamWaitEvent(gcfg(g).stream, c->fork, 0));
@@ -1004,7 +1019,8 @@ Flight* flight_for(prt_ctx* c, bool sync) {
   return (c->inflight > 1 && !sync && c->sh_kind != 2) ? &c->fl[c->next_fl] : nullptr;
 }
 // the call of slot f is enqueued: its stream forked from the context stream (fork_flight) before its first work;
-// here the previous call joins the context stream (its outputs are complete in the caller's order from now on)
+// land_flight then joins the call inflight - 1 back into the context stream (its outputs are complete in the
+// caller's order from now on), so up to `inflight` calls overlap
 int fork_flight(prt_ctx* c, Flight& f) {
   HIP_TRY(hipEventRecord(c->fl_fork, c->stream));
   HIP_TRY(hipStreamWaitEvent(f.stream, c->fl_fork, 0));
@@ -1012,15 +1028,15 @@ int fork_flight(prt_ctx* c, Flight& f) {
 }
 int land_flight(prt_ctx* c, Flight& f) {
   HIP_TRY(hipEventRecord(f.done, f.stream));
-  const int32_t s = (int32_t)(&f - c->fl);
-  Flight& o = c->fl[s ^ 1];
+  const int32_t s = (int32_t)(&f - c->fl), nxt = (s + 1) % c->inflight;
+  Flight& o = c->fl[nxt];  // the call inflight - 1 back, whose slot the next call takes
   if (o.pending) {
     HIP_TRY(hipStreamWaitEvent(c->stream, o.done, 0));
     o.pending = false;
   }
   f.pending = true;
   c->last_fl = s;
-  c->next_fl = s ^ 1;
+  c->next_fl = nxt;
   return PRT_OK;
 }
 // the event the next call's accumulation waits for: the last call still in flight (none: the context stream orders)
@@ -1489,16 +1505,16 @@ int prt_set_stream(prt_ctx* c, void* s) {
 
 int prt_set_frames_in_flight(prt_ctx* c, int32_t n) {
   if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
-  if (n < 1 || n > 2) return fail(PRT_ERR_INVALID_ARGUMENT, "frames in flight must be 1 or 2");
+  if (n < 1 || n > kMaxFlights) return fail(PRT_ERR_INVALID_ARGUMENT, "frames in flight must be 1 to 4");
   if (n > 1 && c->sh_kind == 2) return fail(PRT_ERR_UNSUPPORTED, "frames in flight on a local shard group");
   PRT_JOIN(c);
   HIP_TRY(hipSetDevice(c->device));
-  if (n > 1 && !c->fl_fork) {
+  if (n > 1) {
     for (Flight& f : c->fl) {
       if (!f.stream) HIP_TRY(hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking));
       if (!f.done) HIP_TRY(hipEventCreateWithFlags(&f.done, hipEventDisableTiming));
     }
-    HIP_TRY(hipEventCreateWithFlags(&c->fl_fork, hipEventDisableTiming));
+    if (!c->fl_fork) HIP_TRY(hipEventCreateWithFlags(&c->fl_fork, hipEventDisableTiming));
   }
   c->inflight = n;
   c->next_fl = 0;

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Instance-BVH drift: N tori drift across the field for F frames (every instance moved before every
-frame, wrapping at the field's edge; frames queued back to back, 1280x720, 2 spp, depth 3).  For the refit-only
-tree (PRT_TLAS_REBUILD=0) and the default (device rebuild once the refitted tree's SAH cost exceeds 1.2x its cost
-after the last build): ms per frame over the drift, then ms per frame of static frames at the final positions,
-against a fresh host SAH tree over the same positions (PRT_TLAS_HOST=1)."""
+"""Instance-BVH drift: N tori drift across the field for F frames (every instance moved before
+every frame, wrapping at the field's edge; frames queued back to back, 1280x720, 2 spp, depth 3).  Per rebuild
+policy: ms per frame over the drift, the host time spent inside set_instances per frame, then ms per frame of
+static frames at the final positions against a fresh host SAH tree over the same positions (PRT_TLAS_HOST=1).
+Modes (TLAS_MODES): default = refit only / the default (up to 4,096 instances: the single-workgroup builder for
+every frame) / the multi-launch builder on the node-area trigger and every frame."""
 import os
 import sys
 import time
@@ -35,36 +36,42 @@ def drift(inst):
     return out
 
 
+HOST_MS = []  # host time inside set_instances, per call
+
+
 def timed(ctx, avg, rgb, n, inst=None):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(n):
         if inst is not None:
             inst = drift(inst)
+            h0 = time.perf_counter()
             ctx.set_instances(inst)
+            HOST_MS.append((time.perf_counter() - h0) * 1e3)
         ctx.render(W, H, 2, 3, frame_index=i, avg=avg.data_ptr(), rgb8=rgb.data_ptr(), device_out=True, stats=False)
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) * 1e3 / n, inst
 
 
-MODES = [("refit only", "0", None), ("device rebuild", None, None), ("device rebuild every frame", "always", None)]
+MODES = [("refit only", "0", None), ("default (single-workgroup builder, every frame)", None, None),
+         ("multi-launch builder, trigger", "1.05", "M"), ("multi-launch builder, every frame", "always", "M")]
 if os.environ.get("TLAS_MODES") == "trbvh":  # A/B of the device tree's treelet-restructuring passes
     MODES = [(f"device rebuild every frame, {k} TRBVH passes", "always", k) for k in ("0", "1", "2", "3")]
 if os.environ.get("TLAS_MODES") == "radius":  # A/B of the device tree's PLOC radius (0 / 1 TRBVH passes)
     MODES = [(f"device rebuild every frame, PLOC radius {r}, {k} TRBVH passes", "always", k + ":" + r)
              for r, k in (("64", "0"), ("512", "0"), ("512", "1"))]
-if os.environ.get("TLAS_MODES") == "small":  # the single-workgroup sync-free builder (PRT_TLAS_SMALL=1)
-    MODES = [("refit only", "0", None), ("small builder, trigger", None, "S"),
-             ("small builder, every frame", "always", "S"), ("multi-launch builder, every frame", "always", None)]
+if os.environ.get("TLAS_MODES") == "small":  # the single-workgroup builder's policies
+    MODES = [("small builder, trigger", "1.05", None), ("small builder, every frame", "always", None)]
 for mode, env, trbvh in MODES + MODES:
     os.environ.pop("PRT_TLAS_SMALL", None)
-    if trbvh == "S":
-        os.environ["PRT_TLAS_SMALL"] = "1"
+    if trbvh == "M":  # the multi-launch builder
+        os.environ["PRT_TLAS_SMALL"] = "0"
         trbvh = None
     if trbvh is None:
         os.environ.pop("PRT_TLAS_TRBVH", None)
         os.environ.pop("PRT_TLAS_PLOC_R", None)
-    else:
+    else:  # (the treelet / radius knobs are the multi-launch builder's)
+        os.environ["PRT_TLAS_SMALL"] = "0"
         os.environ["PRT_TLAS_TRBVH"] = trbvh.split(":")[0]
         if ":" in trbvh:
             os.environ["PRT_TLAS_PLOC_R"] = trbvh.split(":")[1]
@@ -83,6 +90,7 @@ for mode, env, trbvh in MODES + MODES:
     timed(ctx, avg, rgb, 2)
     t_first, _ = timed(ctx, avg, rgb, 10)
     blocks = []
+    HOST_MS.clear()
     for b in range(F // 20):
         ms, inst = timed(ctx, avg, rgb, 20, inst)
         blocks.append(round(ms, 3))
@@ -95,8 +103,10 @@ for mode, env, trbvh in MODES + MODES:
     os.environ.pop("PRT_TLAS_SMALL", None)
     t_fresh, _ = timed(ctx, avg, rgb, 20)
     hd = ctx.scene_info().tlas_depth
+    hms = np.array(HOST_MS)
     print(f"{N} instances, {F} frames, {mode}: static frame at start {t_first:.3f} ms; drift ms/frame per 20 frames "
-          f"{blocks}; {si.tlas_rebuilds} device rebuilds / {si.tlas_refits} refits; static frame at the end "
+          f"{blocks}; set_instances host time median {np.median(hms):.3f} / max {hms.max():.3f} ms; "
+          f"{si.tlas_rebuilds} device rebuilds / {si.tlas_refits} refits; static frame at the end "
           f"{t_end:.3f} ms vs fresh host SAH tree {t_fresh:.3f} ms (depth {hd}) ({100 * (t_end / t_fresh - 1):+.1f} %)",
           flush=True)
     ctx.close()

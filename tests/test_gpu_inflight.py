@@ -49,8 +49,8 @@ def _shift(T, m):
     return T
 
 
-@pytest.mark.parametrize("merge", ["default", "0"])
-def test_frames_in_flight_match_one_at_a_time(monkeypatch, merge):
+@pytest.mark.parametrize("merge,flights", [("default", 2), ("default", 4), ("0", 3)])
+def test_frames_in_flight_match_one_at_a_time(monkeypatch, merge, flights):
     import torch
     import prt
     if merge == "0":
@@ -61,7 +61,7 @@ def test_frames_in_flight_match_one_at_a_time(monkeypatch, merge):
     W, H, n = 96, 64, 7
     stream = torch.cuda.Stream()
     res = []
-    for fl in (1, 2):
+    for fl in (1, flights):
         c = prt.Context(0)
         try:
             c.set_stream(stream.cuda_stream)
@@ -77,9 +77,10 @@ def test_frames_in_flight_match_one_at_a_time(monkeypatch, merge):
     assert last1[2:] == last2[2:] and tot1 == tot2
 
 
-def test_frames_in_flight_outputs_in_stream_order_after_next_call():
-    """A call's device outputs are complete in the context stream's order once the next call is enqueued (or
-    prt_finish): a copy enqueued on the caller's stream right then sees the finished frame."""
+@pytest.mark.parametrize("flights", [2, 3])
+def test_frames_in_flight_outputs_in_stream_order(flights):
+    """A call's device outputs are complete in the context stream's order once flights - 1 more calls are enqueued
+    (or after prt_finish): a copy enqueued on the caller's stream right then sees the finished frame."""
     import torch
     import prt
     sd = scenes.multi_instance(scenes.config_small(60, 40))
@@ -89,23 +90,27 @@ def test_frames_in_flight_outputs_in_stream_order_after_next_call():
     c = prt.Context(0)
     try:
         gpu_scene(ref, sd, W, H)
-        want = [ref.render(W, H, 4, 3, frame_index=2 * f)[0] for f in range(3)]
+        n = 5
+        want = [ref.render(W, H, 4, 3, frame_index=2 * f)[0] for f in range(n)]
         c.set_stream(stream.cuda_stream)
         gpu_scene(c, sd, W, H)
-        c.set_frames_in_flight(2)
-        got = []
+        c.set_frames_in_flight(flights)
+        got = {}
         with torch.cuda.stream(stream):
-            outs = [torch.zeros((W * H, 4), dtype=torch.float32, device="cuda") for _ in range(3)]
-        for f in range(3):
+            outs = [torch.zeros((W * H, 4), dtype=torch.float32, device="cuda") for _ in range(n)]
+        for f in range(n):
             c.render(W, H, 4, 3, frame_index=2 * f, avg=outs[f].data_ptr(), device_out=True, stats=False)
-            if f > 0:
+            k = f - (flights - 1)
+            if k >= 0:
                 with torch.cuda.stream(stream):
-                    got.append(outs[f - 1].clone())
+                    got[k] = outs[k].clone()
         c.finish()
         with torch.cuda.stream(stream):
-            got.append(outs[2].clone())
+            for k in range(n):
+                if k not in got:
+                    got[k] = outs[k].clone()
         stream.synchronize()
-        for f in range(3):
+        for f in range(n):
             assert np.array_equal(got[f].cpu().numpy(), want[f]), f
     finally:
         c.close()
@@ -126,7 +131,7 @@ def test_frames_in_flight_rccl_world1():
         want = [ref.render(W, H, 4, 3, frame_index=2 * f)[:2] for f in range(4)]
         c.shard_rccl(prt.Context.shard_unique_id(), 0, 1, 32)
         gpu_scene(c, sd, W, H)
-        c.set_frames_in_flight(2)
+        c.set_frames_in_flight(3)
         outs = [(torch.zeros((W * H, 4), dtype=torch.float32, device="cuda"),
                  torch.zeros(W * H, dtype=torch.int32, device="cuda")) for _ in range(4)]
         for f, (o, g) in enumerate(outs):
@@ -149,6 +154,6 @@ def test_frames_in_flight_refused_on_local_group():
             g.set_frames_in_flight(2)
         g.set_frames_in_flight(1)
         with pytest.raises(prt.PrtError):
-            g.set_frames_in_flight(3)
+            g.set_frames_in_flight(0)
     finally:
         g.close()

@@ -516,29 +516,31 @@ def test_device_tlas_moving_instances(gpu_ctx, monkeypatch, n):
     assert np.array_equal(a_h, out[-1].cpu().numpy())
 
 
-@pytest.mark.parametrize("mode", ["default", "always", "large", "small", "small_always"])
+@pytest.mark.parametrize("mode", ["default", "small_trigger", "multi_trigger", "multi_always", "large"])
 def test_device_tlas_rebuild_long_motion(gpu_ctx, monkeypatch, mode):
-    """1,000 tori drift across the field for 120 frames (every instance moves before every frame, the
-    frames queued back to back with device outputs and no host wait).  The instance BVH is rebuilt on the device:
-    up to 4,096 instances by one workgroup in one launch on a side stream (k_build_small: PLOC + SAH-optimal
-    collapse), committed by a copy kernel on the render stream (PRT_TLAS_SMALL=1: "small", "small_always"), else
-    by the multi-launch builder ("default", "always"; "large": 5,000 instances, 40 frames) -- on the default trigger
-    (node-area cost 1.05x the last build's, or 8 refits) or for every frame (PRT_TLAS_REBUILD=always, as the
-    reference's per-frame BVH::Build).  Every 10th frame equals the oracle's render of that frame's transforms, and
-    the device rebuilds happened."""
+    """1,000 tori drift across the field for 120 frames (every instance moves before every
+    frame, the frames queued back to back with device outputs and no host wait).  The instance BVH is rebuilt on the
+    device: by default (up to 4,096 instances) for every frame, the reference's per-frame BVH::Build, by one
+    workgroup in one launch on a side stream (k_build_small: PLOC + SAH-optimal collapse), committed by a copy
+    kernel on the render stream; "small_trigger": the same builder on the node-area trigger (PRT_TLAS_REBUILD=1.05);
+    the multi-launch builder (PRT_TLAS_SMALL=0) on the trigger or every frame; "large": 5,000 instances, 40 frames
+    (above the single-workgroup limit: multi-launch builder, trigger).  Every 10th frame equals the oracle's render
+    of that frame's transforms, and the device rebuilds happened (every frame: one per set_instances after the host
+    build of the first)."""
     import dataclasses
     import torch
     import prt
     monkeypatch.delenv("PRT_TLAS_HOST", raising=False)
     monkeypatch.delenv("PRT_TLAS_REBUILD", raising=False)
-    n, nframes = (5000, 40) if mode == "large" else (1000, 120)
     monkeypatch.delenv("PRT_TLAS_SMALL", raising=False)
-    if mode.startswith("small"):
-        if os.environ.get("PRT_TEST_TLAS_SMALL") != "1":  # opt-in until the builder has run on the GPU (DESIGN §8)
-            pytest.skip("single-workgroup instance-BVH builder: PRT_TEST_TLAS_SMALL=1 runs it")
-        monkeypatch.setenv("PRT_TLAS_SMALL", "1")
+    n, nframes = (5000, 40) if mode == "large" else (1000, 120)
+    if mode.startswith("multi"):
+        monkeypatch.setenv("PRT_TLAS_SMALL", "0")
+    if mode.endswith("trigger"):
+        monkeypatch.setenv("PRT_TLAS_REBUILD", "1.05")
     if mode.endswith("always"):
         monkeypatch.setenv("PRT_TLAS_REBUILD", "always")
+    every_frame = mode in ("default", "multi_always")
     sd0 = scenes.instance_field(n, seed=17)
     W, H = 64, 48
     flags = oracle.DEFAULT_FLAGS & ~oracle.ACCUMULATE
@@ -572,8 +574,10 @@ def test_device_tlas_rebuild_long_motion(gpu_ctx, monkeypatch, mode):
         torch.cuda.synchronize()
         si = c.scene_info()
         assert si.tlas_rebuilds >= 1 and si.tlas_depth > 0, (si.tlas_rebuilds, si.tlas_refits)
-        if mode.endswith("always"):  # one device rebuild per set_instances after the host build of the first
+        if every_frame:  # one device rebuild per set_instances after the host build of the first
             assert si.tlas_rebuilds == nframes and si.tlas_refits == 0, (si.tlas_rebuilds, si.tlas_refits)
+        else:
+            assert si.tlas_refits > 0, (si.tlas_rebuilds, si.tlas_refits)
         for f, o in out.items():
             a_o, _, _, _ = oracle.OracleScene(frames[f], W, H).render(W, H, spp=2, bounces=3, flags=flags)
             assert np.array_equal(o.cpu().numpy(), a_o), f
