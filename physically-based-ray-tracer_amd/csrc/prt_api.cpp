@@ -917,8 +917,16 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
   const hipStream_t st = fl ? fl->stream : c->stream;
   WaveState& ws0 = flight_ws(c, fl);
   LaunchCfg L{st, occ_for(c), 1};
+  // frames in flight: PRT_FLIGHT_GRID = 2 / 4 runs each chain's wavefront grids at 1/2 / 1/4 of the resident blocks
+  // (A/B: the chains' persistent traversal launches co-reside instead of taking the whole GPU in turns)
+  uint32_t Gw = G;
+  if (fl) {
+    const char* e = std::getenv("PRT_FLIGHT_GRID");
+    const int v = e ? std::atoi(e) : 1;
+    Gw = v >= 4 ? 4u : (v >= 2 ? 2u : 1u);
+  }
   auto gws = [&](uint32_t g) -> WaveState& { return g == 0 ? ws0 : c->grp[g - 1].ws; };
-  auto gcfg = [&](uint32_t g) { return LaunchCfg{g == 0 ? st : c->grp[g - 1].stream, L.occ, G}; };
+  auto gcfg = [&](uint32_t g) { return LaunchCfg{g == 0 ? st : c->grp[g - 1].stream, L.occ, Gw}; };
   // the call's own events (prt_stats ms / ms_trace) only with stats: each record is a gap between kernels
   if (want_stats) HIP_TRY(hipEventRecord(c->ev[0], st));
   // PRT_TAIL=0 switches the cooperative traversal tail off (prt_persist.h; A/B runs only)

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Render-stream timeline of a rocprofv3 --kernel-trace session (its kernel_trace.csv): per kernel name, the
+dispatches, total and mean duration; the idle time of the GPU (no kernel of any queue running); and, for one
+kernel (--focus, default k_build_small), how much of each of its dispatches ran while no other kernel ran.
+usage: scripts/timeline.py <kernel_trace.csv> [--focus NAME]"""
+import collections
+import csv
+import sys
+
+
+def main():
+    path = sys.argv[1]
+    focus = sys.argv[sys.argv.index("--focus") + 1] if "--focus" in sys.argv else "k_build_small"
+    rows = []
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").split("::")[-1].split("<")[0]
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
+    rows.sort()
+    t0, t1 = rows[0][0], max(e for _, e, _ in rows)
+    per = collections.defaultdict(list)
+    for s, e, n in rows:
+        per[n].append(e - s)
+    # union of busy intervals
+    busy, cur_s, cur_e = 0, None, None
+    for s, e, _ in rows:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    print(f"span {(t1 - t0) / 1e6:.3f} ms, GPU busy {busy / 1e6:.3f} ms, idle {(t1 - t0 - busy) / 1e6:.3f} ms")
+    for n, d in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+        print(f"  {n:28s} {len(d):6d} dispatches  total {sum(d) / 1e6:9.3f} ms  mean {sum(d) / len(d) / 1e3:9.1f} us")
+    alone = []
+    for s, e, n in rows:
+        if n != focus:
+            continue
+        # time of [s, e) not covered by any other kernel
+        cov = sorted((max(s, s2), min(e, e2)) for s2, e2, n2 in rows if n2 != focus and s2 < e and e2 > s)
+        c, ce = 0, s
+        for a, b in cov:
+            if b <= ce:
+                continue
+            c += b - max(a, ce)
+            ce = b
+        alone.append((e - s - c) / 1e3)
+    if alone:
+        alone.sort()
+        print(f"{focus}: {len(alone)} dispatches, alone on the GPU median {alone[len(alone) // 2]:.1f} us, "
+              f"max {alone[-1]:.1f} us, total {sum(alone) / 1e3:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()

@@ -62,7 +62,9 @@ if os.environ.get("TLAS_MODES") == "radius":  # A/B of the device tree's PLOC ra
              for r, k in (("64", "0"), ("512", "0"), ("512", "1"))]
 if os.environ.get("TLAS_MODES") == "small":  # the single-workgroup builder's policies
     MODES = [("small builder, trigger", "1.05", None), ("small builder, every frame", "always", None)]
-for mode, env, trbvh in MODES + MODES:
+if os.environ.get("TLAS_MODES") == "default":  # the default policy only, once (timeline sessions)
+    MODES = MODES[1:2]
+for mode, env, trbvh in MODES + (MODES if os.environ.get("TLAS_MODES") != "default" else []):
     os.environ.pop("PRT_TLAS_SMALL", None)
     if trbvh == "M":  # the multi-launch builder
         os.environ["PRT_TLAS_SMALL"] = "0"
