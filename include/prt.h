@@ -326,6 +326,9 @@ typedef struct {
     int32_t tlas_depth;     /* levels of the instance BVH the rays walk (0: instances tested as a linear list) */
     int32_t tlas_rebuilds;  /* (ABI 8) device rebuilds of the instance BVH since the instance count last changed */
     int32_t tlas_refits;    /* (ABI 8) device refits of it since then (prt_set_instances with the same count) */
+    int32_t tlas_rejected;  /* (ABI 9) device rebuilds not committed since the context was created (deeper than
+                               the traversal stacks were sized for; the refitted tree stayed).  Reading it waits
+                               for the context's queued work. */
 } prt_scene_info;
 int prt_get_scene_info(prt_ctx* ctx, prt_scene_info* info);
 

@@ -162,6 +162,7 @@ struct prt_ctx {
   uint32_t tlas_nodes = 0;
   int32_t tlas_rebuilds = 0, tlas_refits = 0;  // since the instance count last changed (diagnostics)
   int32_t tlas_since_build = 0;                 // refits since the last build
+  bool tlas_build_pending = false;  // tlas_small: a build on the side stream awaits its commit at the next update
   DevBuf spill;  // traversal stack levels beyond the LDS ones (BVHs deeper than 17 levels)
   DevBuf diag;   // SceneDev::diag device counters ([0] traversal stack overflows, cumulative per context)
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
@@ -257,16 +258,16 @@ int max_leaf_tris() {
 // waves/SIMD of the persistent traversal kernels: the LDS stack (8 / 9 / 11 / 14 / 18 groups at 8 / 7 / 6 / 5 / 4
 // waves) must hold max_depth - 1 groups; deeper BVHs (depth_ok caps them at kMaxBvhDepth = 64 levels) run the
 // 4-wave form with HBM spill columns (ensure_spill)
-int occ_for(const prt_ctx* c) {
+int occ_at(int d) {  // the occupancy a stack of d levels allows (PRT_OCC caps it; 8 only on request)
   const char* e = std::getenv("PRT_OCC");
-  int want = e ? std::atoi(e) : 7;
-  const int d = stack_depth(c);
+  const int want = e ? std::atoi(e) : 7;
   if (want >= 8 && d <= 9) return 8;
   if (want >= 7 && d <= 10) return 7;
   if (want >= 6 && d <= 12) return 6;
   if (want >= 5 && d <= 15) return 5;
   return 4;
 }
+int occ_for(const prt_ctx* c) { return occ_at(stack_depth(c)); }
 
 // instance refit on the device (prt_refit.h): one async copy of the transforms + k_refit, both on the
 // render stream, so frames already queued keep reading the previous instances
@@ -391,10 +392,14 @@ int ensure_instances(prt_ctx* c) {
         else if (c->tlas_base_cost > 0 && c->tlas_cost_h[1] > rebuild_ratio * c->tlas_base_cost) rebuild = true;
       }
     }
-    if (rebuild && c->tlas_small) {
-      // sync-free: the side stream refits its own copy of the instance records, one workgroup builds the tree into
-      // the back buffers, and the render stream copies it over the front tree when it is valid (k_tlas_commit); the
-      // back buffers are written again only after that copy (tlas_back_free).  No host wait.
+    if (c->tlas_small) {
+      // Single-workgroup builder, pipelined by one frame.  1. The build launched at the previous update (from that
+      // frame's boxes) replaces the front tree: a copy kernel on the render stream, skipped when the build came out
+      // deeper than the stacks were sized for (k_tlas_commit).  2. The front tree is refitted over this frame's
+      // boxes (k_refit above): conservative for these positions whatever topology it has.  3. This frame's boxes
+      // start the next build on the side stream (its own refit of the instance records, one workgroup, the back
+      // buffers, which the commit above must have read first: tlas_back_free), committed by the next update.  The
+      // build thus has a whole frame to run beside the rendering; nothing waits on the host.
       if (!c->tlas_stream) {
         int lo = 0, hi = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -402,48 +407,64 @@ int ensure_instances(prt_ctx* c) {
         HIP_TRY(hipEventCreateWithFlags(&c->tlas_built, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&c->tlas_back_free, hipEventDisableTiming));
       }
-      if (c->tlas_back_busy) HIP_TRY(hipStreamWaitEvent(c->tlas_stream, c->tlas_back_free, 0));
-      const size_t scr = gpu_small_scratch_bytes(n);
-      if (c->tlas_fat.bytes < 48ull * n || c->tlas_tris.bytes < sizeof(TriMT) * (size_t)n ||
-          c->tlas8_b.bytes < sizeof(Node8) * (size_t)n || c->tlas_slot_b.bytes < 32ull * n ||
-          c->tlas_order_b.bytes < 4ull * n || c->tlas_meta_b.bytes < sizeof(TlasMeta) || c->tlas_small_scr.bytes < scr ||
-          c->tlas_small_out.bytes < 4ull * (4 + kTlasMaxLevels) || c->tlas_src.bytes < sizeof(InstSrc) * (size_t)n ||
-          c->tlas_inst.bytes < sizeof(InstDev) * (size_t)n) {
-        HIP_TRY(hipStreamSynchronize(c->tlas_stream));  // the back buffers are free (tlas_back_free) before realloc
-        HIP_TRY(c->tlas_fat.ensure(48ull * n));
-        HIP_TRY(c->tlas_tris.ensure(sizeof(TriMT) * (size_t)n));
-        HIP_TRY(c->tlas8_b.ensure(sizeof(Node8) * (size_t)n));
-        HIP_TRY(c->tlas_slot_b.ensure(32ull * n));
-        HIP_TRY(c->tlas_order_b.ensure(4ull * n));
-        HIP_TRY(c->tlas_meta_b.ensure(sizeof(TlasMeta)));
-        HIP_TRY(c->tlas_small_scr.ensure(scr));
-        HIP_TRY(c->tlas_small_out.ensure(4ull * (4 + kTlasMaxLevels)));
-        HIP_TRY(c->tlas_src.ensure(sizeof(InstSrc) * (size_t)n));
-        HIP_TRY(c->tlas_inst.ensure(sizeof(InstDev) * (size_t)n));
+      const bool committed = c->tlas_build_pending;
+      if (committed) {
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->tlas_built, 0));
+        HIP_TRY(launch_tlas_commit(c->stream, c->tlas_meta_b.as<TlasMeta>(), c->tlas8_b.as<Node8>(),
+                                   c->tlas_slot_b.as<uint32_t>(), c->tlas_order_b.as<uint32_t>(),
+                                   c->tlas_meta.as<TlasMeta>(), c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(),
+                                   c->tlas_order.as<uint32_t>(), c->diag.as<uint32_t>() + 2));
+        HIP_TRY(hipEventRecord(c->tlas_back_free, c->stream));
+        c->tlas_back_busy = true;
+        c->tlas_build_pending = false;
       }
-      HIP_TRY(hipMemcpyAsync(c->tlas_src.p, src.data(), sizeof(InstSrc) * (size_t)n, hipMemcpyHostToDevice,
-                             c->tlas_stream));
-      HIP_TRY(launch_refit(c->tlas_stream, c->tlas_src.as<InstSrc>(), n, c->tlas_inst.as<InstDev>()));
-      HIP_TRY(gpu_rebuild_tlas_small(c->tlas_stream, c->tlas_inst.as<InstDev>(), n, c->tlas_fat.as<float>(),
-                                     c->tlas_tris.as<TriMT>(), c->tlas_small_scr.p, c->tlas_small_out.as<uint32_t>(),
-                                     c->tlas8_b.as<Node8>(), c->tlas_slot_b.as<uint32_t>(),
-                                     c->tlas_order_b.as<uint32_t>(), c->tlas_meta_b.as<TlasMeta>(), c->tlas_depth_cap));
-      HIP_TRY(hipEventRecord(c->tlas_built, c->tlas_stream));
-      HIP_TRY(hipStreamWaitEvent(c->stream, c->tlas_built, 0));
-      HIP_TRY(launch_tlas_commit(c->stream, c->tlas_meta_b.as<TlasMeta>(), c->tlas8_b.as<Node8>(),
-                                 c->tlas_slot_b.as<uint32_t>(), c->tlas_order_b.as<uint32_t>(),
-                                 c->tlas_meta.as<TlasMeta>(), c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(),
-                                 c->tlas_order.as<uint32_t>()));
-      HIP_TRY(hipEventRecord(c->tlas_back_free, c->stream));
-      c->tlas_back_busy = true;
-      int rc = refit_tree();  // over this frame's boxes (k_refit above); its aabb for the cost
+      int rc = refit_tree();
       if (rc) return rc;
-      c->tlas_base_cost = 0;
-      c->tlas_cost_pending[1] = false;
-      rc = measure_cost(0);
+      if (committed) {  // the trigger's reference cost: the committed tree over this frame's boxes
+        c->tlas_base_cost = 0;
+        c->tlas_cost_pending[1] = false;
+        rc = measure_cost(0);
+      } else if (!rebuild && !c->tlas_cost_pending[1]) {
+        rc = measure_cost(1);  // at most one refit cost in flight
+      }
       if (rc) return rc;
-      c->tlas_rebuilds++;
-      c->tlas_since_build = 0;
+      c->tlas_since_build++;
+      if (!rebuild) c->tlas_refits++;  // (an update that starts a build counts as a rebuild)
+      if (rebuild) {
+        if (c->tlas_back_busy) HIP_TRY(hipStreamWaitEvent(c->tlas_stream, c->tlas_back_free, 0));
+        const size_t scr = gpu_small_scratch_bytes(n);
+        if (c->tlas_fat.bytes < 48ull * n || c->tlas_tris.bytes < sizeof(TriMT) * (size_t)n ||
+            c->tlas8_b.bytes < sizeof(Node8) * (size_t)n || c->tlas_slot_b.bytes < 32ull * n ||
+            c->tlas_order_b.bytes < 4ull * n || c->tlas_meta_b.bytes < sizeof(TlasMeta) ||
+            c->tlas_small_scr.bytes < scr || c->tlas_small_out.bytes < 4ull * (4 + kTlasMaxLevels) ||
+            c->tlas_src.bytes < sizeof(InstSrc) * (size_t)n || c->tlas_inst.bytes < sizeof(InstDev) * (size_t)n) {
+          const int drc = drain(c);  // the back buffers are free (commit read them) before they are reallocated
+          if (drc) return drc;
+          HIP_TRY(hipStreamSynchronize(c->tlas_stream));
+          HIP_TRY(c->tlas_fat.ensure(48ull * n));
+          HIP_TRY(c->tlas_tris.ensure(sizeof(TriMT) * (size_t)n));
+          HIP_TRY(c->tlas8_b.ensure(sizeof(Node8) * (size_t)n));
+          HIP_TRY(c->tlas_slot_b.ensure(32ull * n));
+          HIP_TRY(c->tlas_order_b.ensure(4ull * n));
+          HIP_TRY(c->tlas_meta_b.ensure(sizeof(TlasMeta)));
+          HIP_TRY(c->tlas_small_scr.ensure(scr));
+          HIP_TRY(c->tlas_small_out.ensure(4ull * (4 + kTlasMaxLevels)));
+          HIP_TRY(c->tlas_src.ensure(sizeof(InstSrc) * (size_t)n));
+          HIP_TRY(c->tlas_inst.ensure(sizeof(InstDev) * (size_t)n));
+        }
+        HIP_TRY(hipMemcpyAsync(c->tlas_src.p, src.data(), sizeof(InstSrc) * (size_t)n, hipMemcpyHostToDevice,
+                               c->tlas_stream));
+        HIP_TRY(launch_refit(c->tlas_stream, c->tlas_src.as<InstSrc>(), n, c->tlas_inst.as<InstDev>()));
+        HIP_TRY(gpu_rebuild_tlas_small(c->tlas_stream, c->tlas_inst.as<InstDev>(), n, c->tlas_fat.as<float>(),
+                                       c->tlas_tris.as<TriMT>(), c->tlas_small_scr.p, c->tlas_small_out.as<uint32_t>(),
+                                       c->tlas8_b.as<Node8>(), c->tlas_slot_b.as<uint32_t>(),
+                                       c->tlas_order_b.as<uint32_t>(), c->tlas_meta_b.as<TlasMeta>(),
+                                       c->tlas_depth_cap));
+        HIP_TRY(hipEventRecord(c->tlas_built, c->tlas_stream));
+        c->tlas_build_pending = true;
+        c->tlas_rebuilds++;
+        c->tlas_since_build = 0;
+      }
     } else if (rebuild) {
       // boxes of the instances' current transforms (the same refit_instance as k_refit), built on the side stream
       // into the back buffers: the frames already queued keep walking the current tree, the host waits only for
@@ -531,8 +552,12 @@ int ensure_instances(prt_ctx* c) {
     // the sync-free device rebuild (up to kGpuSmallBuild instances): the front buffers hold any tree of n instances,
     // and the stacks are sized one level deeper than the host tree so a device tree of that depth is usable
     c->tlas_small = small_ok && (rebuild_always || rebuild_ratio > 0);
+    c->tlas_build_pending = false;  // a build still on the side stream was for the previous instance set
     if (c->tlas_small) {
-      c->tlas_depth_cap = c->tlas_depth + 1;
+      // one level of slack for the device trees, unless it would cost the traversal kernels a wave per SIMD (a
+      // deeper build is then not committed, the refitted tree stays: prt_scene_info.tlas_rejected counts them)
+      const int d0 = c->max_depth + c->tlas_depth;
+      c->tlas_depth_cap = c->tlas_depth + (occ_at(d0 + 1) == occ_at(d0) ? 1 : 0);
       c->tlas_depth = c->tlas_depth_cap;
     }
     const size_t cap_nodes = c->tlas_small ? std::max<size_t>(c->tlas_host.nodes.size(), (size_t)n)
@@ -2263,6 +2288,14 @@ int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
   info->tlas_depth = c->use_tlas ? c->tlas_depth : 0;
   info->tlas_rebuilds = c->tlas_rebuilds;
   info->tlas_refits = c->tlas_refits;
+  if (c->diag.p) {  // the commit kernel's count (diag word 2), after the queued work
+    PRT_JOIN(c);
+    uint32_t rej = 0;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(&rej, c->diag.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    info->tlas_rejected = (int32_t)rej;
+  }
   info->build_ms = c->build_ms;
   info->builder = c->built_with;
   info->device_bytes = (int64_t)(c->nodes8.bytes + c->tris.bytes + c->stri.bytes + c->texels.bytes + c->sky.bytes +

@@ -33,7 +33,8 @@ hipError_t gpu_rebuild_tlas_small(hipStream_t s, const InstDev* inst, int32_t n,
                                   TlasMeta* meta, int depth_cap);
 // the back tree copied over the front one when valid (one workgroup, in the render stream's order)
 hipError_t launch_tlas_commit(hipStream_t s, const TlasMeta* mb, const Node8* nb, const uint32_t* sb,
-                              const uint32_t* ob, TlasMeta* mf, Node8* nf, uint32_t* sf, uint32_t* of);
+                              const uint32_t* ob, TlasMeta* mf, Node8* nf, uint32_t* sf, uint32_t* of,
+                              uint32_t* rejected);
 // the refit over the device meta's levels, one workgroup, one launch
 hipError_t launch_tlas_refit_meta(hipStream_t s, const InstDev* inst, const TlasMeta* meta, const uint32_t* order,
                                   Node8* nodes, const uint32_t* slot, float* aabb);

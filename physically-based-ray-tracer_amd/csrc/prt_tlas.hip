@@ -172,8 +172,12 @@ __global__ void __launch_bounds__(1024) k_tlas_small_finish(Node8* __restrict__ 
 __global__ void __launch_bounds__(1024) k_tlas_commit(const TlasMeta* __restrict__ mb, const Node8* __restrict__ nb,
                                                       const uint32_t* __restrict__ sb, const uint32_t* __restrict__ ob,
                                                       TlasMeta* __restrict__ mf, Node8* __restrict__ nf,
-                                                      uint32_t* __restrict__ sf, uint32_t* __restrict__ of) {
-  if (!mb->valid) return;
+                                                      uint32_t* __restrict__ sf, uint32_t* __restrict__ of,
+                                                      uint32_t* __restrict__ rejected) {
+  if (!mb->valid) {  // deeper than the stacks were sized for (or a failed build): the current tree stays
+    if (threadIdx.x == 0) atomicAdd(rejected, 1u);
+    return;
+  }
   const uint32_t nn = mb->n_nodes;
   const uint4* ns = reinterpret_cast<const uint4*>(nb);
   uint4* nd = reinterpret_cast<uint4*>(nf);
@@ -281,8 +285,9 @@ hipError_t gpu_rebuild_tlas_small(hipStream_t s, const InstDev* inst, int32_t n,
 }
 
 hipError_t launch_tlas_commit(hipStream_t s, const TlasMeta* mb, const Node8* nb, const uint32_t* sb,
-                              const uint32_t* ob, TlasMeta* mf, Node8* nf, uint32_t* sf, uint32_t* of) {
-  hipLaunchKernelGGL(k_tlas_commit, dim3(1), dim3(1024), 0, s, mb, nb, sb, ob, mf, nf, sf, of);
+                              const uint32_t* ob, TlasMeta* mf, Node8* nf, uint32_t* sf, uint32_t* of,
+                              uint32_t* rejected) {
+  hipLaunchKernelGGL(k_tlas_commit, dim3(1), dim3(1024), 0, s, mb, nb, sb, ob, mf, nf, sf, of, rejected);
   return hipGetLastError();
 }
 

@@ -108,7 +108,7 @@ for mode, env, trbvh in MODES + (MODES if os.environ.get("TLAS_MODES") != "defau
     hms = np.array(HOST_MS)
     print(f"{N} instances, {F} frames, {mode}: static frame at start {t_first:.3f} ms; drift ms/frame per 20 frames "
           f"{blocks}; set_instances host time median {np.median(hms):.3f} / max {hms.max():.3f} ms; "
-          f"{si.tlas_rebuilds} device rebuilds / {si.tlas_refits} refits; static frame at the end "
+          f"{si.tlas_rebuilds} device rebuilds ({si.tlas_rejected} not committed) / {si.tlas_refits} refits; static frame at the end "
           f"{t_end:.3f} ms vs fresh host SAH tree {t_fresh:.3f} ms (depth {hd}) ({100 * (t_end / t_fresh - 1):+.1f} %)",
           flush=True)
     ctx.close()
