@@ -13,9 +13,16 @@ def main():
     focus = sys.argv[sys.argv.index("--focus") + 1] if "--focus" in sys.argv else "k_build_small"
     rows = []
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "").split("::")[-1].split("<")[0]
+        name = r["Kernel_Name"]
+        if "(anonymous namespace)::" in name:
+            name = name.split("(anonymous namespace)::")[1]
+        name = name.split("(")[0].replace("void ", "").split("::")[-1].split("<")[0]
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     rows.sort()
+    if "--window" in sys.argv:  # only the dispatches inside [start, end] ms after the first
+        a, b = (float(x) for x in sys.argv[sys.argv.index("--window") + 1].split(":"))
+        base = rows[0][0]
+        rows = [r for r in rows if a * 1e6 <= r[0] - base <= b * 1e6]
     t0, t1 = rows[0][0], max(e for _, e, _ in rows)
     per = collections.defaultdict(list)
     for s, e, n in rows:
@@ -31,6 +38,15 @@ def main():
             cur_e = max(cur_e, e)
     busy += cur_e - cur_s
     print(f"span {(t1 - t0) / 1e6:.3f} ms, GPU busy {busy / 1e6:.3f} ms, idle {(t1 - t0 - busy) / 1e6:.3f} ms")
+    # concurrency: time with k kernels running at once
+    edges = sorted([(s, 1) for s, _, _ in rows] + [(e, -1) for _, e, _ in rows])
+    conc = collections.Counter()
+    k, last = 0, edges[0][0]
+    for t, d in edges:
+        conc[k] += t - last
+        k += d
+        last = t
+    print("  time with k kernels running: " + ", ".join(f"{k}: {v / 1e6:.3f} ms" for k, v in sorted(conc.items())))
     for n, d in sorted(per.items(), key=lambda kv: -sum(kv[1])):
         print(f"  {n:28s} {len(d):6d} dispatches  total {sum(d) / 1e6:9.3f} ms  mean {sum(d) / len(d) / 1e3:9.1f} us")
     alone = []
