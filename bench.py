@@ -5,7 +5,10 @@ Workload (config C4, the 1M-triangle scene the north-star target is quoted on; i
 1000x500-quad heightfield = 1,000,000 triangles, procedural textures, 4 point + directional + spot
 light, equirect sky, camera (0.3,3,-7) -> origin, all reference features on (AA, accumulate, gamma,
 normal map, skybox, lighted, stochastic NEE).  A step = one prt_render of the full 4-spp frame
-(2 reference frames x 2 AA paths per pixel), inputs resident in HBM.
+(2 reference frames x 2 AA paths per pixel), inputs resident in HBM.  Two frames are in flight by default
+(prt_set_frames_in_flight): step k+1's wavefront chain overlaps step k's on the GPU, the accumulation (and the
+sharded gather) stay in step order, and every step's image is bit-identical to rendering them one at a time; the
+K timed steps are all complete when the closing synchronize returns.
 
 Mrays/s = (closest-hit segments + any-hit shadow rays) / time, counted on the device.
 --gpus N > 1: one process per GPU.  Run without WORLD_SIZE in the environment, bench.py starts the N ranks
@@ -204,9 +207,10 @@ def main():
                     help="c4 = the metric's workload (default); c5 = C4 + a quad area light with MIS at 4K, 16 spp, depth 8")
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=1, choices=[1, 2, 3, 4],
-                    help="frames in flight (prt_set_frames_in_flight): 2 overlaps consecutive frames' wavefront "
-                         "chains, accumulation and gathers stay in call order")
+    ap.add_argument("--inflight", type=int, default=2, choices=[1, 2, 3, 4],
+                    help="frames in flight (prt_set_frames_in_flight, default 2): consecutive frames' wavefront "
+                         "chains overlap on internal streams; accumulation and gathers stay in call order, the "
+                         "images are bit-identical to 1")
     ap.add_argument("--host-out", action="store_true",
                     help="outputs (avg + rgb8) to host memory every step: the PCIe-inclusive rate (not the contract value)")
     args = ap.parse_args()
@@ -392,6 +396,7 @@ def main():
                        "parallelism": f"pixel-tile{args.tile} x{world} (RCCL gather in prt_render)" if world > 1
                        else "single-gpu",
                        "outputs": "host memory (PCIe-inclusive)" if args.host_out else "device (HBM-resident)",
+                       "frames_in_flight": args.inflight,
                        "rays_per_step": int(rays / args.steps), "segments_per_step": int(seg / args.steps),
                        "shadow_per_step": int(shadow / args.steps),
                        "mpix_per_s": round(W * H / (ms_step / 1e3) / 1e6, 2),

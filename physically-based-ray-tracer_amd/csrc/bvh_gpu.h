@@ -30,8 +30,11 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
 // deeper than max_levels); level_end (device, max_levels words): level d's nodes are [level_end[d-1], level_end[d])
 constexpr int32_t kGpuSmallBuild = 4096;
 size_t gpu_small_scratch_bytes(int32_t n);
+// the build's counter words inside that scratch (diagnostics: phase clock at [8..19], PLOC iterations at [7])
+uint32_t* gpu_small_ctr(void* scratch, int32_t n);
 hipError_t gpu_build_blas8_small(hipStream_t s, const float* tri_dev, int32_t n, int max_leaf, Node8* nodes_out,
-                                 TriMT* tris_out, void* scratch, uint32_t* out, uint32_t* level_end, int max_levels);
+                                 TriMT* tris_out, void* scratch, uint32_t* out, uint32_t* level_end, int max_levels,
+                                 int radius = 0);
 // rebase a mesh's nodes into the concatenated arrays (in place) and record ShadeTri.pad[0] for its primitives
 hipError_t gpu_blas_finish(hipStream_t s, Node8* nodes, uint32_t n_nodes, uint32_t node_base, const TriMT* tris,
                            uint32_t n_tris, uint32_t tri_base, ShadeTri* stri, uint32_t prim_base);

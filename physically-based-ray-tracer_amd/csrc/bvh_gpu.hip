@@ -737,7 +737,7 @@ __global__ void __launch_bounds__(kB) k_collapse(const float4* __restrict__ tri,
 // scratch arrays are the multi-launch builder's (global, touched by this one workgroup only: plain loads see the
 // workgroup's own stores after a barrier).
 constexpr int kSmallThreads = 1024;
-constexpr int kSmallR = 512;  // PLOC search radius (as the instance BVH's multi-launch build)
+constexpr int kSmallR = 512;  // default PLOC search radius (as the instance BVH's multi-launch build)
 struct SmallScratch {
   unsigned long long* keys;  // n sorted keys
   int *left, *right;         // 2n - 1
@@ -768,9 +768,20 @@ __device__ __forceinline__ uint32_t small_scan(uint32_t v, uint32_t* wsum, uint3
   return before + x - v;
 }
 
+// diagnostic phase clock (s_memrealtime, 100 MHz) of the single-workgroup build: ctr[8 + 2k] (64-bit), read back by
+// the host with PRT_TLAS_SMALL_TIMES=1 (gpu_small_times)
+__device__ __forceinline__ void small_stamp(uint32_t* ctr, int k) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    ctr[8 + 2 * k] = (uint32_t)t;
+    ctr[9 + 2 * k] = (uint32_t)(t >> 32);
+  }
+}
+
 __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __restrict__ tri, int n, int max_leaf,
                                                                SmallScratch sc, Node8* nodes, TriMT* tris,
-                                                               uint32_t* out, uint32_t* level_end, int max_levels) {
+                                                               uint32_t* out, uint32_t* level_end, int max_levels,
+                                                               int radius) {
   __shared__ union {
     unsigned long long keys[kGpuSmallBuild];
     float sbox[6 * kGpuSmallBuild];
@@ -782,6 +793,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   __shared__ int s_next;
   __shared__ uint32_t s_err;
   const int tid = (int)threadIdx.x;
+  small_stamp(sc.ctr, 0);
   if (tid < 3) { cb[tid] = 0xFFFFFFFFu; cb[3 + tid] = 0u; }
   if (tid == 0) { s_err = 0u; s_next = n - 2; }
   __syncthreads();
@@ -817,6 +829,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
     U.keys[i] = key;
   }
   __syncthreads();
+  small_stamp(sc.ctr, 1);
   // 2. bitonic sort (ascending; keys are unique)
   for (int k = 2; k <= P; k <<= 1)
     for (int j = k >> 1; j > 0; j >>= 1) {
@@ -829,6 +842,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
       }
       __syncthreads();
     }
+  small_stamp(sc.ctr, 2);
   // 3. leaves (k_ploc_leaves): binary leaf n - 1 + i = the i-th prim in key order
   for (int i = tid; i < n; i += kSmallThreads) {
     const unsigned long long key = U.keys[i];
@@ -845,14 +859,16 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   for (int i = tid; i < n; i += kSmallThreads)
     for (int k = 0; k < 6; k++) U.sbox[6 * i + k] = sc.box[6 * (size_t)(n - 1 + i) + k];
   __syncthreads();
+  small_stamp(sc.ctr, 3);
   // 4. PLOC iterations (k_ploc_nn / k_ploc_merge / compaction), the cluster list and boxes in LDS
   int m = n;
+  uint32_t ploc_iters = 0;
   while (m > 1) {
     for (int i = tid; i < m; i += kSmallThreads) {
       const float* bi = U.sbox + 6 * i;
       float best = 3.4e38f;
       int bj = -1;
-      for (int j = max(0, i - kSmallR); j <= min(m - 1, i + kSmallR); j++) {
+      for (int j = max(0, i - radius); j <= min(m - 1, i + radius); j++) {
         if (j == i) continue;
         const float* b6 = U.sbox + 6 * j;
         const float dx = fmaxf(bi[3], b6[3]) - fminf(bi[0], b6[0]);
@@ -905,8 +921,11 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
     }
     if (total >= (uint32_t)m) { if (tid == 0) s_err |= 2u; total = 1; }  // no merge: cannot happen
     m = (int)total;
+    ploc_iters++;
     __syncthreads();
   }
+  small_stamp(sc.ctr, 4);
+  if (tid == 0) sc.ctr[7] = ploc_iters;
   if (tid == 0 && s_next != -1 && n > 1) s_err |= 4u;  // not exactly n - 1 internal nodes
   // 5. the collapse, one level per pass, behind barriers (k_collapse)
   if (tid == 0) {
@@ -938,6 +957,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
     __syncthreads();
     Task* tt = ta; ta = tb; tb = tt;
   }
+  small_stamp(sc.ctr, 5);
   if (tid == 0) {
     const uint32_t c0 = ld_sc1_u(sc.ctr + 0), c1 = ld_sc1_u(sc.ctr + 1), c3 = ld_sc1_u(sc.ctr + 3);
     out[0] = c0;
@@ -1143,8 +1163,16 @@ size_t gpu_small_scratch_bytes(int32_t n) {
          al(16);
 }
 
+uint32_t* gpu_small_ctr(void* scratch, int32_t n) {
+  const size_t nn = 2 * (size_t)std::max(n, 1) - 1, ni = (size_t)std::max(n - 1, 1);
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  return reinterpret_cast<uint32_t*>(static_cast<char*>(scratch) + al(8 * (size_t)n) + 3 * al(4 * nn) + al(24 * nn) +
+                                     al(64 * ni) + al(4 * ni) + 2 * al(sizeof(Task) * (size_t)n));
+}
+
 hipError_t gpu_build_blas8_small(hipStream_t s, const float* tri_dev, int32_t n, int max_leaf, Node8* nodes_out,
-                                 TriMT* tris_out, void* scratch, uint32_t* out, uint32_t* level_end, int max_levels) {
+                                 TriMT* tris_out, void* scratch, uint32_t* out, uint32_t* level_end, int max_levels,
+                                 int radius) {
   if (n <= 0 || n > kGpuSmallBuild) return hipErrorInvalidValue;
   const size_t nn = 2 * (size_t)n - 1, ni = (size_t)std::max(n - 1, 1);
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -1162,7 +1190,7 @@ hipError_t gpu_build_blas8_small(hipStream_t s, const float* tri_dev, int32_t n,
   sc.ctr = reinterpret_cast<uint32_t*>(p);
   if (n == 1) sc.dp = DpTab{nullptr, nullptr};  // the root is the single leaf
   hipLaunchKernelGGL(k_build_small, dim3(1), dim3(kSmallThreads), 0, s, reinterpret_cast<const float4*>(tri_dev), n,
-                     max_leaf, sc, nodes_out, tris_out, out, level_end, max_levels);
+                     max_leaf, sc, nodes_out, tris_out, out, level_end, max_levels, radius > 0 ? radius : kSmallR);
   return hipGetLastError();
 }
 

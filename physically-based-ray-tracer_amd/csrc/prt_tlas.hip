@@ -1,3 +1,5 @@
+#include <cstdio>
+#include <cstdlib>
 // prt_tlas.hip -- the instance BVH (TLAS) refitted on the device, in stream order right after k_refit.
 //
 // The reference rebuilds its TLAS every frame after physics moved the game objects (Core/Renderer.cpp:33-41:
@@ -277,10 +279,23 @@ hipError_t gpu_rebuild_tlas_small(hipStream_t s, const InstDev* inst, int32_t n,
                                   TlasMeta* meta, int depth_cap) {
   if (n <= 0 || n > kGpuSmallBuild) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_inst_fat_dev, dim3((n + 255) / 256), dim3(256), 0, s, inst, n, reinterpret_cast<float4*>(fat));
-  const hipError_t e = gpu_build_blas8_small(s, fat, n, 1, nodes, tris, scratch, out, out + 4, kTlasMaxLevels);
+  // PLOC search radius of the single-workgroup build (PRT_TLAS_SMALL_R, default 512: every cluster of a
+  // 1,000-instance tree sees all others)
+  const char* re = std::getenv("PRT_TLAS_SMALL_R");
+  const hipError_t e = gpu_build_blas8_small(s, fat, n, 1, nodes, tris, scratch, out, out + 4, kTlasMaxLevels,
+                                             re ? std::atoi(re) : 0);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_tlas_small_finish, dim3(1), dim3(1024), 0, s, nodes, tris, slot, order, out, out + 4,
                      (uint32_t)depth_cap, meta);
+  if (std::getenv("PRT_TLAS_SMALL_TIMES")) {  // diagnostic: the build's phase clock (waits for the side stream)
+    uint32_t w[20];
+    if (hipMemcpyAsync(w, gpu_small_ctr(scratch, n), sizeof(w), hipMemcpyDeviceToHost, s) == hipSuccess &&
+        hipStreamSynchronize(s) == hipSuccess) {
+      auto t = [&](int k) { return (double)(((unsigned long long)w[9 + 2 * k] << 32) | w[8 + 2 * k]) / 100.0; };
+      std::fprintf(stderr, "prt: small build n=%d: bounds+morton %.1f, sort %.1f, leaves %.1f, ploc %.1f (%u iterations), "
+                   "collapse %.1f us\n", n, t(1) - t(0), t(2) - t(1), t(3) - t(2), t(4) - t(3), w[7], t(5) - t(4));
+    }
+  }
   return hipGetLastError();
 }
 
