@@ -207,16 +207,25 @@ def main():
                     help="c4 = the metric's workload (default); c5 = C4 + a quad area light with MIS at 4K, 16 spp, depth 8")
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2, choices=[1, 2, 3, 4],
-                    help="frames in flight (prt_set_frames_in_flight, default 2): consecutive frames' wavefront "
-                         "chains overlap on internal streams; accumulation and gathers stay in call order, the "
-                         "images are bit-identical to 1")
+    ap.add_argument("--inflight", type=int, default=None, choices=[1, 2, 3, 4],
+                    help="frames in flight (prt_set_frames_in_flight; default 2 at N <= 2 GPUs, 4 above): "
+                         "consecutive frames' wavefront chains overlap on internal streams; accumulation and "
+                         "gathers stay in call order, the images are bit-identical to 1")
     ap.add_argument("--host-out", action="store_true",
                     help="outputs (avg + rgb8) to host memory every step: the PCIe-inclusive rate (not the contract value)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
+    # Frames in flight: the best measured setting per share size (profiles/r05_inflight.txt): 2 for the whole or
+    # half frame (the chains' launch tails overlap), 4 for the small, latency-bound shares of 4-8 GPUs.  Each chain
+    # runs on its own HIP stream, and HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
+    # default) round-robin: with more chains than free queues two chains share one and serialise, so the runtime
+    # gets 8 (set before anything initialises HIP; an explicit setting in the environment wins)
+    if args.inflight is None:
+        args.inflight = 2 if args.gpus <= 2 else 4
+    if args.inflight > 2:
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
     import torch
     import prt
@@ -397,6 +406,7 @@ def main():
                        else "single-gpu",
                        "outputs": "host memory (PCIe-inclusive)" if args.host_out else "device (HBM-resident)",
                        "frames_in_flight": args.inflight,
+                       "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default (4)"),
                        "rays_per_step": int(rays / args.steps), "segments_per_step": int(seg / args.steps),
                        "shadow_per_step": int(shadow / args.steps),
                        "mpix_per_s": round(W * H / (ms_step / 1e3) / 1e6, 2),

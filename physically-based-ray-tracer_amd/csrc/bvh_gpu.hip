@@ -784,8 +784,9 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
                                                                int radius) {
   __shared__ union {
     unsigned long long keys[kGpuSmallBuild];
-    float sbox[6 * kGpuSmallBuild];
+    float sbox[6 * kGpuSmallBuild];  // cluster boxes, component-major: sbox[k * kGpuSmallBuild + i] (conflict-free)
   } U;
+  auto SB = [&](int i, int k) -> float& { return U.sbox[k * kGpuSmallBuild + i]; };
   __shared__ int sclus[kGpuSmallBuild];
   __shared__ int snn[kGpuSmallBuild];
   __shared__ uint32_t wsum[kSmallThreads / 64];
@@ -857,7 +858,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   }
   __syncthreads();  // the keys are read: U becomes the cluster boxes
   for (int i = tid; i < n; i += kSmallThreads)
-    for (int k = 0; k < 6; k++) U.sbox[6 * i + k] = sc.box[6 * (size_t)(n - 1 + i) + k];
+    for (int k = 0; k < 6; k++) SB(i, k) = sc.box[6 * (size_t)(n - 1 + i) + k];
   __syncthreads();
   small_stamp(sc.ctr, 3);
   // 4. PLOC iterations (k_ploc_nn / k_ploc_merge / compaction), the cluster list and boxes in LDS
@@ -865,20 +866,20 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   uint32_t ploc_iters = 0;
   while (m > 1) {
     for (int i = tid; i < m; i += kSmallThreads) {
-      const float* bi = U.sbox + 6 * i;
+      const float b0 = SB(i, 0), b1 = SB(i, 1), b2 = SB(i, 2), b3 = SB(i, 3), b4 = SB(i, 4), b5 = SB(i, 5);
       float best = 3.4e38f;
       int bj = -1;
-      for (int j = max(0, i - radius); j <= min(m - 1, i + radius); j++) {
-        if (j == i) continue;
-        const float* b6 = U.sbox + 6 * j;
-        const float dx = fmaxf(bi[3], b6[3]) - fminf(bi[0], b6[0]);
-        const float dy = fmaxf(bi[4], b6[4]) - fminf(bi[1], b6[1]);
-        const float dz = fmaxf(bi[5], b6[5]) - fminf(bi[2], b6[2]);
+      // The pair order of the multi-launch builder's tie rule -- equal areas go to the smaller (min, max) pair --
+      // is the order of j here (below i: min = j; above i: min = i, max = j), so the first minimum in j wins
+      auto cand = [&](int j) {
+        const float dx = fmaxf(b3, SB(j, 3)) - fminf(b0, SB(j, 0));
+        const float dy = fmaxf(b4, SB(j, 4)) - fminf(b1, SB(j, 1));
+        const float dz = fmaxf(b5, SB(j, 5)) - fminf(b2, SB(j, 2));
         const float a = dx * dy + dy * dz + dz * dx;
-        const bool better = a < best || (a == best && bj >= 0 && (min(i, j) < min(i, bj) ||
-                                                                  (min(i, j) == min(i, bj) && max(i, j) < max(i, bj))));
-        if (bj < 0 || better) { best = a; bj = j; }
-      }
+        if (bj < 0 || a < best) { best = a; bj = j; }
+      };
+      for (int j = max(0, i - radius); j < i; j++) cand(j);
+      for (int j = i + 1; j <= min(m - 1, i + radius); j++) cand(j);
       snn[i] = bj;
     }
     __syncthreads();
@@ -895,14 +896,14 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
       keep |= 1u << e;
       if (!mutual) {
         nc[e] = sclus[i];
-        for (int k = 0; k < 6; k++) nb[e][k] = U.sbox[6 * i + k];
+        for (int k = 0; k < 6; k++) nb[e][k] = SB(i, k);
         continue;
       }
       const int lc = sclus[i], rc = sclus[j];
       const int p = atomicSub(&s_next, 1);
-      if (p < 0) { atomicOr(&s_err, 1u); nc[e] = lc; for (int k = 0; k < 6; k++) nb[e][k] = U.sbox[6 * i + k]; continue; }
+      if (p < 0) { atomicOr(&s_err, 1u); nc[e] = lc; for (int k = 0; k < 6; k++) nb[e][k] = SB(i, k); continue; }
       float lb[6], rb[6];
-      for (int k = 0; k < 6; k++) { lb[k] = U.sbox[6 * i + k]; rb[k] = U.sbox[6 * j + k]; }
+      for (int k = 0; k < 6; k++) { lb[k] = SB(i, k); rb[k] = SB(j, k); }
       for (int k = 0; k < 3; k++) { nb[e][k] = fminf(lb[k], rb[k]); nb[e][3 + k] = fmaxf(lb[3 + k], rb[3 + k]); }
       for (int k = 0; k < 6; k++) sc.box[6 * (size_t)p + k] = nb[e][k];
       sc.left[p] = lc;
@@ -916,11 +917,12 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
     for (int e = 0; e < 4; e++) {
       if (!((keep >> e) & 1u)) continue;
       sclus[pos] = nc[e];
-      for (int k = 0; k < 6; k++) U.sbox[6 * pos + k] = nb[e][k];
+      for (int k = 0; k < 6; k++) SB(pos, k) = nb[e][k];
       pos++;
     }
     if (total >= (uint32_t)m) { if (tid == 0) s_err |= 2u; total = 1; }  // no merge: cannot happen
     m = (int)total;
+    if (tid == 0 && ploc_iters < 40) sc.ctr[20 + ploc_iters] = (uint32_t)m;  // diagnostic: clusters left
     ploc_iters++;
     __syncthreads();
   }

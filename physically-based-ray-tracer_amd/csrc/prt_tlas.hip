@@ -288,12 +288,15 @@ hipError_t gpu_rebuild_tlas_small(hipStream_t s, const InstDev* inst, int32_t n,
   hipLaunchKernelGGL(k_tlas_small_finish, dim3(1), dim3(1024), 0, s, nodes, tris, slot, order, out, out + 4,
                      (uint32_t)depth_cap, meta);
   if (std::getenv("PRT_TLAS_SMALL_TIMES")) {  // diagnostic: the build's phase clock (waits for the side stream)
-    uint32_t w[20];
+    uint32_t w[60];
     if (hipMemcpyAsync(w, gpu_small_ctr(scratch, n), sizeof(w), hipMemcpyDeviceToHost, s) == hipSuccess &&
         hipStreamSynchronize(s) == hipSuccess) {
       auto t = [&](int k) { return (double)(((unsigned long long)w[9 + 2 * k] << 32) | w[8 + 2 * k]) / 100.0; };
       std::fprintf(stderr, "prt: small build n=%d: bounds+morton %.1f, sort %.1f, leaves %.1f, ploc %.1f (%u iterations), "
-                   "collapse %.1f us\n", n, t(1) - t(0), t(2) - t(1), t(3) - t(2), t(4) - t(3), w[7], t(5) - t(4));
+                   "collapse %.1f us; clusters after each iteration:", n, t(1) - t(0), t(2) - t(1), t(3) - t(2),
+                   t(4) - t(3), w[7], t(5) - t(4));
+      for (uint32_t k = 0; k < w[7] && k < 40; k++) std::fprintf(stderr, " %u", w[20 + k]);
+      std::fprintf(stderr, "\n");
     }
   }
   return hipGetLastError();
