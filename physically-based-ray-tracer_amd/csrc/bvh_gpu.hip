@@ -789,6 +789,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   auto SB = [&](int i, int k) -> float& { return U.sbox[k * kGpuSmallBuild + i]; };
   __shared__ int sclus[kGpuSmallBuild];
   __shared__ int snn[kGpuSmallBuild];
+  __shared__ int snew[kGpuSmallBuild];  // cluster position after the compaction (PLOC incremental neighbours)
   __shared__ uint32_t wsum[kSmallThreads / 64];
   __shared__ uint32_t cb[6];
   __shared__ int s_next;
@@ -861,11 +862,20 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
     for (int k = 0; k < 6; k++) SB(i, k) = sc.box[6 * (size_t)(n - 1 + i) + k];
   __syncthreads();
   small_stamp(sc.ctr, 3);
-  // 4. PLOC iterations (k_ploc_nn / k_ploc_merge / compaction), the cluster list and boxes in LDS
+  // 4. PLOC iterations (k_ploc_nn / k_ploc_merge / compaction), the cluster list and boxes in LDS.
+  // Incremental neighbours: once a search window covers every cluster (m - 1 <= radius), a cluster whose nearest
+  // neighbour was not merged keeps it -- a merged cluster's box contains each of its parts, so no new cluster is
+  // nearer than the old neighbour -- and only new clusters and those whose neighbour was merged search again
+  // (snn = -1).  An iteration that merges nothing (possible only through exact area ties) searches everything
+  // again; a second one in a row is an error.
+  for (int i = tid; i < n; i += kSmallThreads) snn[i] = -1;
+  __syncthreads();
   int m = n;
   uint32_t ploc_iters = 0;
+  bool incr = false, stalled = false;  // (uniform across the workgroup)
   while (m > 1) {
     for (int i = tid; i < m; i += kSmallThreads) {
+      if (incr && snn[i] >= 0) continue;
       const float b0 = SB(i, 0), b1 = SB(i, 1), b2 = SB(i, 2), b3 = SB(i, 3), b4 = SB(i, 4), b5 = SB(i, 5);
       float best = 3.4e38f;
       int bj = -1;
@@ -884,7 +894,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
     }
     __syncthreads();
     // merge: thread t owns clusters 4t .. 4t + 3 (m <= 4 x 1024)
-    int nc[4];
+    int nc[4], onn[4];  // onn: the kept neighbour's old position, or -1 (search again)
     float nb[4][6];
     uint32_t keep = 0;
     for (int e = 0; e < 4; e++) {
@@ -894,7 +904,10 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
       const bool mutual = j >= 0 && snn[j] == i;
       if (mutual && i > j) continue;  // merged into the cluster at j
       keep |= 1u << e;
+      onn[e] = -1;
       if (!mutual) {
+        const int jj = j >= 0 ? snn[j] : -1;
+        if (j >= 0 && !(jj >= 0 && snn[jj] == j)) onn[e] = j;  // the neighbour survives this iteration
         nc[e] = sclus[i];
         for (int k = 0; k < 6; k++) nb[e][k] = SB(i, k);
         continue;
@@ -913,14 +926,28 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
       nc[e] = p;
     }
     uint32_t total = 0;
-    uint32_t pos = small_scan((uint32_t)__popc(keep), wsum, &total);  // (its barriers order the reads above)
+    const uint32_t pos0 = small_scan((uint32_t)__popc(keep), wsum, &total);  // (its barriers order the reads above)
+    uint32_t pos = pos0;
+    for (int e = 0; e < 4; e++)
+      if ((keep >> e) & 1u) snew[4 * tid + e] = (int)pos++;
+    __syncthreads();
+    pos = pos0;
+    const bool global = m - 1 <= radius;  // this iteration's search windows covered every cluster
     for (int e = 0; e < 4; e++) {
       if (!((keep >> e) & 1u)) continue;
       sclus[pos] = nc[e];
       for (int k = 0; k < 6; k++) SB(pos, k) = nb[e][k];
+      snn[pos] = onn[e] >= 0 ? snew[onn[e]] : -1;
       pos++;
     }
-    if (total >= (uint32_t)m) { if (tid == 0) s_err |= 2u; total = 1; }  // no merge: cannot happen
+    if (total >= (uint32_t)m) {  // no merge (exact ties under kept neighbours): search everything again
+      if (stalled || !incr) { if (tid == 0) s_err |= 2u; total = 1; }
+      stalled = true;
+      incr = false;
+    } else {
+      stalled = false;
+      incr = global;
+    }
     m = (int)total;
     if (tid == 0 && ploc_iters < 40) sc.ctr[20 + ploc_iters] = (uint32_t)m;  // diagnostic: clusters left
     ploc_iters++;

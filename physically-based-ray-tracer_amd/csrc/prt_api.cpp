@@ -393,13 +393,14 @@ int ensure_instances(prt_ctx* c) {
       }
     }
     if (c->tlas_small) {
-      // Single-workgroup builder, pipelined by one frame.  1. The build launched at the previous update (from that
-      // frame's boxes) replaces the front tree: a copy kernel on the render stream, skipped when the build came out
-      // deeper than the stacks were sized for (k_tlas_commit).  2. The front tree is refitted over this frame's
-      // boxes (k_refit above): conservative for these positions whatever topology it has.  3. This frame's boxes
-      // start the next build on the side stream (its own refit of the instance records, one workgroup, the back
-      // buffers, which the commit above must have read first: tlas_back_free), committed by the next update.  The
-      // build thus has a whole frame to run beside the rendering; nothing waits on the host.
+      // Single-workgroup builder.  A build: the side stream refits its own copy of the instance records and one
+      // workgroup builds the tree into the back buffers (gpu_rebuild_tlas_small); a commit: a copy kernel on the
+      // render stream replaces the front tree with a finished build, unless it came out deeper than the stacks
+      // were sized for (k_tlas_commit); the back buffers are written again only after that copy (tlas_back_free).
+      // Then the front tree is refitted over this frame's boxes (k_refit above).  By default the build of this
+      // update's boxes is committed at once (the render stream waits for it, as the reference's BVH::Build
+      // precedes the frame); PRT_TLAS_PIPELINE=1 commits it at the next update instead (the build then runs
+      // beside this frame's rendering; measured slower, profiles/r05_tlas_rebuild.txt).  No host wait either way.
       if (!c->tlas_stream) {
         int lo = 0, hi = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -407,30 +408,9 @@ int ensure_instances(prt_ctx* c) {
         HIP_TRY(hipEventCreateWithFlags(&c->tlas_built, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&c->tlas_back_free, hipEventDisableTiming));
       }
-      const bool committed = c->tlas_build_pending;
-      if (committed) {
-        HIP_TRY(hipStreamWaitEvent(c->stream, c->tlas_built, 0));
-        HIP_TRY(launch_tlas_commit(c->stream, c->tlas_meta_b.as<TlasMeta>(), c->tlas8_b.as<Node8>(),
-                                   c->tlas_slot_b.as<uint32_t>(), c->tlas_order_b.as<uint32_t>(),
-                                   c->tlas_meta.as<TlasMeta>(), c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(),
-                                   c->tlas_order.as<uint32_t>(), c->diag.as<uint32_t>() + 2));
-        HIP_TRY(hipEventRecord(c->tlas_back_free, c->stream));
-        c->tlas_back_busy = true;
-        c->tlas_build_pending = false;
-      }
-      int rc = refit_tree();
-      if (rc) return rc;
-      if (committed) {  // the trigger's reference cost: the committed tree over this frame's boxes
-        c->tlas_base_cost = 0;
-        c->tlas_cost_pending[1] = false;
-        rc = measure_cost(0);
-      } else if (!rebuild && !c->tlas_cost_pending[1]) {
-        rc = measure_cost(1);  // at most one refit cost in flight
-      }
-      if (rc) return rc;
-      c->tlas_since_build++;
-      if (!rebuild) c->tlas_refits++;  // (an update that starts a build counts as a rebuild)
-      if (rebuild) {
+      const char* tp = std::getenv("PRT_TLAS_PIPELINE");
+      const bool pipelined = tp && std::atoi(tp) == 1;
+      auto launch_build = [&]() -> int {
         if (c->tlas_back_busy) HIP_TRY(hipStreamWaitEvent(c->tlas_stream, c->tlas_back_free, 0));
         const size_t scr = gpu_small_scratch_bytes(n);
         if (c->tlas_fat.bytes < 48ull * n || c->tlas_tris.bytes < sizeof(TriMT) * (size_t)n ||
@@ -464,7 +444,38 @@ int ensure_instances(prt_ctx* c) {
         c->tlas_build_pending = true;
         c->tlas_rebuilds++;
         c->tlas_since_build = 0;
+        return PRT_OK;
+      };
+      int rc = PRT_OK;
+      if (rebuild && !pipelined) rc = launch_build();
+      if (rc) return rc;
+      const bool committed = c->tlas_build_pending;
+      if (committed) {
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->tlas_built, 0));
+        HIP_TRY(launch_tlas_commit(c->stream, c->tlas_meta_b.as<TlasMeta>(), c->tlas8_b.as<Node8>(),
+                                   c->tlas_slot_b.as<uint32_t>(), c->tlas_order_b.as<uint32_t>(),
+                                   c->tlas_meta.as<TlasMeta>(), c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(),
+                                   c->tlas_order.as<uint32_t>(), c->diag.as<uint32_t>() + 2));
+        HIP_TRY(hipEventRecord(c->tlas_back_free, c->stream));
+        c->tlas_back_busy = true;
+        c->tlas_build_pending = false;
       }
+      rc = refit_tree();
+      if (rc) return rc;
+      if (committed) {  // the trigger's reference cost: the committed tree over this frame's boxes
+        c->tlas_base_cost = 0;
+        c->tlas_cost_pending[1] = false;
+        rc = measure_cost(0);
+      } else if (!rebuild && !c->tlas_cost_pending[1]) {
+        rc = measure_cost(1);  // at most one refit cost in flight
+      }
+      if (rc) return rc;
+      if (!rebuild) {  // (an update that starts a build counts as a rebuild)
+        c->tlas_refits++;
+        c->tlas_since_build++;
+      }
+      if (rebuild && pipelined) rc = launch_build();
+      if (rc) return rc;
     } else if (rebuild) {
       // boxes of the instances' current transforms (the same refit_instance as k_refit), built on the side stream
       // into the back buffers: the frames already queued keep walking the current tree, the host waits only for
