@@ -208,7 +208,7 @@ def main():
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=None, choices=[1, 2, 3, 4],
-                    help="frames in flight (prt_set_frames_in_flight; default 2 at N <= 2 GPUs, 4 above): "
+                    help="frames in flight (prt_set_frames_in_flight; default 2, 4 at N >= 8 GPUs): "
                          "consecutive frames' wavefront chains overlap on internal streams; accumulation and "
                          "gathers stay in call order, the images are bit-identical to 1")
     ap.add_argument("--host-out", action="store_true",
@@ -217,13 +217,13 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
-    # Frames in flight: the best measured setting per share size (profiles/r05_inflight.txt): 2 for the whole or
-    # half frame (the chains' launch tails overlap), 4 for the small, latency-bound shares of 4-8 GPUs.  Each chain
+    # Frames in flight: the best measured setting per share size (profiles/r05_inflight.txt): 2 for the shares of
+    # 1-4 GPUs (the chains' launch tails overlap), 4 for the small, latency-bound share of 8 GPUs.  Each chain
     # runs on its own HIP stream, and HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
     # default) round-robin: with more chains than free queues two chains share one and serialise, so the runtime
     # gets 8 (set before anything initialises HIP; an explicit setting in the environment wins)
     if args.inflight is None:
-        args.inflight = 2 if args.gpus <= 2 else 4
+        args.inflight = 4 if args.gpus >= 8 else 2
     if args.inflight > 2:
         os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 

@@ -565,10 +565,14 @@ int ensure_instances(prt_ctx* c) {
     c->tlas_small = small_ok && (rebuild_always || rebuild_ratio > 0);
     c->tlas_build_pending = false;  // a build still on the side stream was for the previous instance set
     if (c->tlas_small) {
-      // one level of slack for the device trees, unless it would cost the traversal kernels a wave per SIMD (a
-      // deeper build is then not committed, the refitted tree stays: prt_scene_info.tlas_rejected counts them)
+      // one level of slack for the device trees (a deeper build is not committed and the refitted tree stays:
+      // prt_scene_info.tlas_rejected counts them).  PRT_TLAS_SLACK=auto drops the slack where it costs the traversal
+      // kernels a wave per SIMD: on the 1,000-instance drift that rejected 20 % of the builds and was slower than
+      // running one wave fewer (profiles/r05_tlas_rebuild.txt)
       const int d0 = c->max_depth + c->tlas_depth;
-      c->tlas_depth_cap = c->tlas_depth + (occ_at(d0 + 1) == occ_at(d0) ? 1 : 0);
+      const char* sl = std::getenv("PRT_TLAS_SLACK");
+      const bool slack = !(sl && std::strcmp(sl, "auto") == 0) || occ_at(d0 + 1) == occ_at(d0);
+      c->tlas_depth_cap = c->tlas_depth + (slack ? 1 : 0);
       c->tlas_depth = c->tlas_depth_cap;
     }
     const size_t cap_nodes = c->tlas_small ? std::max<size_t>(c->tlas_host.nodes.size(), (size_t)n)
