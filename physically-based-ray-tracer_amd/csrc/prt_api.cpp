@@ -965,8 +965,13 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
     const int v = e ? std::atoi(e) : 1;
     Gw = v >= 4 ? 4u : (v >= 2 ? 2u : 1u);
   }
+  // The single-workgroup instance-BVH build (tlas_small, one 1,024-thread workgroup with ~144 KB of LDS) can only
+  // start on a CU the traversal waves have left; the traversal launches that follow must then not need that CU, or
+  // they end only after the build: their grid leaves one CU's worth of blocks out (PRT_SPARE_CU=0 / 1 forces it)
+  const char* esc = std::getenv("PRT_SPARE_CU");
+  const uint32_t spare = esc ? (std::atoi(esc) ? 1u : 0u) : ((c->use_tlas && c->tlas_small) ? 1u : 0u);
   auto gws = [&](uint32_t g) -> WaveState& { return g == 0 ? ws0 : c->grp[g - 1].ws; };
-  auto gcfg = [&](uint32_t g) { return LaunchCfg{g == 0 ? st : c->grp[g - 1].stream, L.occ, Gw}; };
+  auto gcfg = [&](uint32_t g) { return LaunchCfg{g == 0 ? st : c->grp[g - 1].stream, L.occ, Gw, spare}; };
   // the call's own events (prt_stats ms / ms_trace) only with stats: each record is a gap between kernels
   if (want_stats) HIP_TRY(hipEventRecord(c->ev[0], st));
   // PRT_TAIL=0 switches the cooperative traversal tail off (prt_persist.h; A/B runs only)

@@ -20,6 +20,8 @@ struct LaunchCfg {
   int occ;     // persistent traversal waves/SIMD: 8 / 7 / 6 / 5 / 4 (8 / 9 / 11 / 14 / 18 LDS stack groups)
   uint32_t groups = 1;  // concurrent item groups of the call: every wavefront grid is 1/groups of the resident
                         // blocks, so the groups' launch chains co-reside on the SIMDs (prt_api.cpp)
+  uint32_t spare_cus = 0;  // CUs' worth of persistent traversal blocks left out of the grid (prt_api.cpp: room for
+                           // the instance-BVH build beside the traversal)
 };
 
 // wavefront pipeline buffers (SoA over n work items; R/T hold (bounces-1) x n entries)

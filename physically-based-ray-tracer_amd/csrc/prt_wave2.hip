@@ -820,10 +820,10 @@ template <int STACK, int WAVES, int TAILN>
 void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
   static_assert(2 * STACK * 256 + 264 + 4 * 3 * TAILN <= 163840 / (4 * WAVES), "LDS over the occupancy budget");
   if (S.tlas)
-    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, true>), dim3(256u * 4u * WAVES / c.groups), dim3(64), 0,
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, true>), dim3((256u - c.spare_cus) * 4u * WAVES / c.groups), dim3(64), 0,
                        c.stream, S, B, it, iters);
   else
-    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, false>), dim3(256u * 4u * WAVES / c.groups), dim3(64), 0,
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, false>), dim3((256u - c.spare_cus) * 4u * WAVES / c.groups), dim3(64), 0,
                        c.stream, S, B, it, iters);
 }
 // persistent traversal occupancy (waves/SIMD) -> LDS stack groups per lane; a BVH deeper than the 18 LDS
