@@ -959,10 +959,12 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
   LaunchCfg L{st, occ_for(c), 1};
   // frames in flight: PRT_FLIGHT_GRID = 2 / 4 runs each chain's wavefront grids at 1/2 / 1/4 of the resident blocks
   // (A/B: the chains' persistent traversal launches co-reside instead of taking the whole GPU in turns)
+  // (default: half grids from 4 frames in flight on: world-8 share of C4 1.23-1.28 -> 1.15 ms, world 1 unchanged,
+  // profiles/r05_inflight.txt)
   uint32_t Gw = G;
   if (fl) {
     const char* e = std::getenv("PRT_FLIGHT_GRID");
-    const int v = e ? std::atoi(e) : 1;
+    const int v = e ? std::atoi(e) : (c->inflight >= 4 ? 2 : 1);
     Gw = v >= 4 ? 4u : (v >= 2 ? 2u : 1u);
   }
   // The single-workgroup instance-BVH build (tlas_small, one 1,024-thread workgroup with ~144 KB of LDS) can only
@@ -975,6 +977,7 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
   // the call's own events (prt_stats ms / ms_trace) only with stats: each record is a gap between kernels
   if (want_stats) HIP_TRY(hipEventRecord(c->ev[0], st));
   // PRT_TAIL=0 switches the cooperative traversal tail off (prt_persist.h; A/B runs only)
+  if (const char* so = std::getenv("PRT_SORT_OCT"); so && std::atoi(so) == 1) A.flags |= kSortOct;  // A/B
   const char* et = std::getenv("PRT_TAIL");
   const int32_t coop = (et && std::atoi(et) == 0) ? 0 : 1;
   // per-launch traversal timers (HIP events around every k_trace launch) with stats, unless
