@@ -977,7 +977,6 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
   // the call's own events (prt_stats ms / ms_trace) only with stats: each record is a gap between kernels
   if (want_stats) HIP_TRY(hipEventRecord(c->ev[0], st));
   // PRT_TAIL=0 switches the cooperative traversal tail off (prt_persist.h; A/B runs only)
-  if (const char* so = std::getenv("PRT_SORT_OCT"); so && std::atoi(so) == 1) A.flags |= kSortOct;  // A/B
   const char* et = std::getenv("PRT_TAIL");
   const int32_t coop = (et && std::atoi(et) == 0) ? 0 : 1;
   // per-launch traversal timers (HIP events around every k_trace launch) with stats, unless

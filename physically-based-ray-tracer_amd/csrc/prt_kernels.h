@@ -50,9 +50,6 @@ inline uint64_t tile_image_pixels(const TileMap& m) {
   return n;
 }
 
-// TraceArgs::flags bit set by the library itself (PRT_SORT_OCT, A/B): a shading block queues its next rays in
-// direction-octant order
-constexpr uint32_t kSortOct = 1u << 30;
 struct TraceArgs {
   int32_t W, H;
   int32_t bounces;

@@ -91,36 +91,6 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, uint32_t n, 
   return off + before;
 }
 
-// block-aggregated append of at most one entry per lane, the block's entries ordered by key (0 .. NB-1; NB = no
-// entry): key 0 first, then 1, ...  sm: >= NB * 4 + 1 words of LDS (blocks of up to 256 threads).  All threads of
-// the block must call it.
-template <uint32_t NB>
-__device__ __forceinline__ uint32_t block_append_keyed(uint32_t* counter, uint32_t key, uint32_t* sm) {
-  const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const uint64_t lt = (1ull << lane_id()) - 1ull;
-  uint32_t before = 0;
-#pragma unroll
-  for (uint32_t b = 0; b < NB; b++) {
-    const uint64_t m = __ballot(key == b);
-    if (lane_id() == 0) sm[b * nw + w] = (uint32_t)__popcll(m);
-    if (key == b) before = (uint32_t)__popcll(m & lt);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t tot = 0;
-    for (uint32_t k = 0; k < NB * nw; k++) {  // exclusive prefix, key-major
-      const uint32_t c = sm[k];
-      sm[k] = tot;
-      tot += c;
-    }
-    sm[NB * nw] = tot ? atomicAdd(counter, tot) : 0u;
-  }
-  __syncthreads();
-  const uint32_t off = key < NB ? sm[NB * nw] + sm[key * nw + w] + before : 0u;
-  __syncthreads();
-  return off;
-}
-
 // hit record word: prim in the low S.pbits bits (enough for the largest mesh), instance above (prt_api.cpp
 // checks that both fit in 32 bits)
 __device__ __forceinline__ uint32_t pack_hit(const SceneDev& S, uint32_t prim, uint32_t inst) {

@@ -336,7 +336,6 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
   }
   __shared__ uint32_t pref[kNSub + 1];
   __shared__ uint32_t sm[8];
-  __shared__ uint32_t smk[9 * (kBlock / 64) + 1];  // kSortOct: the block's next rays by direction octant
   const uint32_t* q = (iter & 1) ? B.q1 : B.q0;
   uint32_t* qn = (iter & 1) ? B.q0 : B.q1;
   const uint32_t sub = blockIdx.x % kNSub;
@@ -399,7 +398,6 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
     uint32_t status = kStMiss, emissive = 0;
     bool next = false;
     bool area_ray = false;
-    uint32_t noct = 8;  // the next ray's direction octant (8: a primary ray or a dielectric continuation)
     if (nr) {
       const float4 o = EXT ? Bc.ro[item] : ro_c, d = EXT ? Bc.rd[item] : rd_c;
       const V3 D = v3(d.x, d.y, d.z);
@@ -467,7 +465,6 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
             Bc.rd[item] = make_float4(nr2.D.x, nr2.D.y, nr2.D.z, 0.0f);
             Bc.info[item] = (depth + 1u) | (path << 8);
             next = true;
-            noct = (dir.x < 0.0f ? 1u : 0u) | (dir.y < 0.0f ? 2u : 0u) | (dir.z < 0.0f ? 4u : 0u);
           }
         }
       }
@@ -485,8 +482,7 @@ __global__ void __launch_bounds__(kBlock, EXT ? 3 : 1) k_shade2(SceneDev S, Trac
       Bc.rinfo[item] = depth | (path << 8) | (status << 16) | ((uint32_t)kind << 20) | (next ? kRiQueued : 0u) | emissive |
                        (EXT ? 0u : kResFresh);
     }
-    const uint32_t slot = (fl & kSortOct) ? block_append_keyed<9>(ncnt, next ? noct : 9u, smk)
-                                          : block_append(ncnt, next ? 1u : 0u, sm);
+    const uint32_t slot = block_append(ncnt, next ? 1u : 0u, sm);
     if (next) qn[sub * Bc.qcap + slot] = item;
   }
 }
