@@ -208,7 +208,7 @@ def main():
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=None, choices=[1, 2, 3, 4],
-                    help="frames in flight (prt_set_frames_in_flight; default 2, 4 at N >= 8 GPUs): "
+                    help="frames in flight (prt_set_frames_in_flight; default 2 on one GPU, 4 on several): "
                          "consecutive frames' wavefront chains overlap on internal streams; accumulation and "
                          "gathers stay in call order, the images are bit-identical to 1")
     ap.add_argument("--host-out", action="store_true",
@@ -217,15 +217,15 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
-    # Frames in flight: the best measured setting per share size (profiles/r05_inflight.txt): 2 for the shares of
-    # 1-4 GPUs (the chains' launch tails overlap), 4 for the small, latency-bound share of 8 GPUs.  Each chain
-    # runs on its own HIP stream, and HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
-    # default) round-robin: with more chains than free queues two chains share one and serialise, so the runtime
-    # gets 8 (set before anything initialises HIP; an explicit setting in the environment wins)
+    # Frames in flight: the best measured setting per share size (profiles/r05_inflight.txt): 2 for the whole
+    # frame, 4 (with half grids per chain) for the shares of 2-8 GPUs.  Each chain runs on its own HIP stream, and
+    # HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default) round-robin: with more
+    # chains than free queues two chains share one and serialise behind each other's waits, so above 2 chains the
+    # runtime is given 8 queues (set before anything initialises HIP)
     if args.inflight is None:
-        args.inflight = 4 if args.gpus >= 8 else 2
-    if args.inflight > 2:
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+        args.inflight = 4 if args.gpus >= 2 else 2
+    if args.inflight > 2 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
     import torch
     import prt

@@ -873,7 +873,9 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   int m = n;
   uint32_t ploc_iters = 0;
   bool incr = false, stalled = false;  // (uniform across the workgroup)
+  unsigned long long tp_nn = 0, tp_merge = 0, tp_compact = 0, tp0 = 0;  // diagnostic phase clock (thread 0)
   while (m > 1) {
+    if (tid == 0) tp0 = __builtin_amdgcn_s_memrealtime();
     for (int i = tid; i < m; i += kSmallThreads) {
       if (incr && snn[i] >= 0) continue;
       const float b0 = SB(i, 0), b1 = SB(i, 1), b2 = SB(i, 2), b3 = SB(i, 3), b4 = SB(i, 4), b5 = SB(i, 5);
@@ -893,6 +895,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
       snn[i] = bj;
     }
     __syncthreads();
+    if (tid == 0) { const unsigned long long t = __builtin_amdgcn_s_memrealtime(); tp_nn += t - tp0; tp0 = t; }
     // merge: thread t owns clusters 4t .. 4t + 3 (m <= 4 x 1024)
     int nc[4], onn[4];  // onn: the kept neighbour's old position, or -1 (search again)
     float nb[4][6];
@@ -927,6 +930,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
     }
     uint32_t total = 0;
     const uint32_t pos0 = small_scan((uint32_t)__popc(keep), wsum, &total);  // (its barriers order the reads above)
+    if (tid == 0) { const unsigned long long t = __builtin_amdgcn_s_memrealtime(); tp_merge += t - tp0; tp0 = t; }
     uint32_t pos = pos0;
     for (int e = 0; e < 4; e++)
       if ((keep >> e) & 1u) snew[4 * tid + e] = (int)pos++;
@@ -952,6 +956,12 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
     if (tid == 0 && ploc_iters < 40) sc.ctr[20 + ploc_iters] = (uint32_t)m;  // diagnostic: clusters left
     ploc_iters++;
     __syncthreads();
+    if (tid == 0) tp_compact += __builtin_amdgcn_s_memrealtime() - tp0;
+  }
+  if (tid == 0) {
+    sc.ctr[60] = (uint32_t)tp_nn;
+    sc.ctr[61] = (uint32_t)tp_merge;
+    sc.ctr[62] = (uint32_t)tp_compact;
   }
   small_stamp(sc.ctr, 4);
   if (tid == 0) sc.ctr[7] = ploc_iters;

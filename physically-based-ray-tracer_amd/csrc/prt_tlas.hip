@@ -288,7 +288,7 @@ hipError_t gpu_rebuild_tlas_small(hipStream_t s, const InstDev* inst, int32_t n,
   hipLaunchKernelGGL(k_tlas_small_finish, dim3(1), dim3(1024), 0, s, nodes, tris, slot, order, out, out + 4,
                      (uint32_t)depth_cap, meta);
   if (std::getenv("PRT_TLAS_SMALL_TIMES")) {  // diagnostic: the build's phase clock (waits for the side stream)
-    uint32_t w[60];
+    uint32_t w[64];
     if (hipMemcpyAsync(w, gpu_small_ctr(scratch, n), sizeof(w), hipMemcpyDeviceToHost, s) == hipSuccess &&
         hipStreamSynchronize(s) == hipSuccess) {
       auto t = [&](int k) { return (double)(((unsigned long long)w[9 + 2 * k] << 32) | w[8 + 2 * k]) / 100.0; };
@@ -296,7 +296,8 @@ hipError_t gpu_rebuild_tlas_small(hipStream_t s, const InstDev* inst, int32_t n,
                    "collapse %.1f us; clusters after each iteration:", n, t(1) - t(0), t(2) - t(1), t(3) - t(2),
                    t(4) - t(3), w[7], t(5) - t(4));
       for (uint32_t k = 0; k < w[7] && k < 40; k++) std::fprintf(stderr, " %u", w[20 + k]);
-      std::fprintf(stderr, "\n");
+      std::fprintf(stderr, "; ploc split: neighbours %.1f, merge %.1f, compaction %.1f us\n", w[60] / 100.0,
+                   w[61] / 100.0, w[62] / 100.0);
     }
   }
   return hipGetLastError();
