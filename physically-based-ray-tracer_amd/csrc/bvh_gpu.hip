@@ -876,42 +876,23 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   unsigned long long tp_nn = 0, tp_merge = 0, tp_compact = 0, tp0 = 0;  // diagnostic phase clock (thread 0)
   while (m > 1) {
     if (tid == 0) tp0 = __builtin_amdgcn_s_memrealtime();
-    // Wave-wide scan: a wave's 64 clusters [ib, ib + 64) walk the union of their windows in ascending j, 64
-    // candidate boxes at a time loaded one per lane and broadcast lane by lane (v_readlane), so the inner loop has
-    // no LDS round trip; each lane keeps the candidates inside its own window.  The first minimum in j wins, the
-    // pair order of the multi-launch builder's tie rule (below i: min = j; above i: min = i, max = j).
-    const int lane = tid & 63;
-    const bool wide = radius >= m - 1;  // every window covers every cluster
-    for (int ib = tid & ~63; ib < m; ib += kSmallThreads) {
-      const int i = ib + lane;
-      const bool own = i < m && !(incr && snn[i] >= 0);
-      if (__ballot(own) == 0ull) continue;
-      const int ii = min(i, m - 1);
-      const float b0 = SB(ii, 0), b1 = SB(ii, 1), b2 = SB(ii, 2), b3 = SB(ii, 3), b4 = SB(ii, 4), b5 = SB(ii, 5);
+    for (int i = tid; i < m; i += kSmallThreads) {
+      if (incr && snn[i] >= 0) continue;
+      const float b0 = SB(i, 0), b1 = SB(i, 1), b2 = SB(i, 2), b3 = SB(i, 3), b4 = SB(i, 4), b5 = SB(i, 5);
       float best = 3.4e38f;
       int bj = -1;
-      const int lo = max(0, ib - radius), hi = min(m - 1, ib + 63 + radius);
-      for (int j0 = lo; j0 <= hi; j0 += 64) {
-        const int jl = min(j0 + lane, hi);
-        const float c0 = SB(jl, 0), c1 = SB(jl, 1), c2 = SB(jl, 2), c3 = SB(jl, 3), c4 = SB(jl, 4), c5 = SB(jl, 5);
-        const int cnt = min(64, hi - j0 + 1);
-        for (int t = 0; t < cnt; t++) {
-          const int j = j0 + t;
-          const float x0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c0), t));
-          const float x1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c1), t));
-          const float x2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c2), t));
-          const float x3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c3), t));
-          const float x4 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c4), t));
-          const float x5 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c5), t));
-          const float dx = fmaxf(b3, x3) - fminf(b0, x0);
-          const float dy = fmaxf(b4, x4) - fminf(b1, x1);
-          const float dz = fmaxf(b5, x5) - fminf(b2, x2);
-          const float a = dx * dy + dy * dz + dz * dx;
-          const bool inwin = j != i && (wide || (j >= i - radius && j <= i + radius));
-          if (inwin && (bj < 0 || a < best)) { best = a; bj = j; }
-        }
-      }
-      if (own) snn[i] = bj;
+      // The pair order of the multi-launch builder's tie rule -- equal areas go to the smaller (min, max) pair --
+      // is the order of j here (below i: min = j; above i: min = i, max = j), so the first minimum in j wins
+      auto cand = [&](int j) {
+        const float dx = fmaxf(b3, SB(j, 3)) - fminf(b0, SB(j, 0));
+        const float dy = fmaxf(b4, SB(j, 4)) - fminf(b1, SB(j, 1));
+        const float dz = fmaxf(b5, SB(j, 5)) - fminf(b2, SB(j, 2));
+        const float a = dx * dy + dy * dz + dz * dx;
+        if (bj < 0 || a < best) { best = a; bj = j; }
+      };
+      for (int j = max(0, i - radius); j < i; j++) cand(j);
+      for (int j = i + 1; j <= min(m - 1, i + radius); j++) cand(j);
+      snn[i] = bj;
     }
     __syncthreads();
     if (tid == 0) { const unsigned long long t = __builtin_amdgcn_s_memrealtime(); tp_nn += t - tp0; tp0 = t; }
