@@ -96,6 +96,9 @@ class ShardedFrame:
     def _render(self, spp, bounces, avg_ptr, rgb8_ptr, frame_index, flags, stats):
         st = self.ctx.render_tiles(self.W, self.H, spp, bounces, self.tile, self.rank, self.world,
                                    self.tiles.data_ptr(), flags=flags, frame_index=frame_index, stats=stats)
+        # with frames in flight the tile render may still be on an internal stream: the gather torch queues on
+        # the context stream must come after it (prt_finish joins it there, no host wait)
+        self.ctx.finish()
         self.dist.gather(self.tiles, list(self.gathered.unbind(0)) if self.rank == 0 else None, dst=0)
         if self.rank == 0:
             self.ctx.untile(self.gathered.data_ptr(), self.W, self.H, self.tile, self.world, avg_ptr, rgb8_ptr)

@@ -55,6 +55,16 @@ def test_no_device_fails_loudly():
     assert rc == -2 and b"no HIP device" in L.prt_last_error()
 
 
+def test_null_context_refused():
+    """Entry points that take a context refuse NULL with PRT_ERR_INVALID_ARGUMENT (no device needed), ABI 9's
+    frames-in-flight pair included."""
+    L = prt.load()
+    assert L.prt_set_frames_in_flight(None, 2) == -1 and b"NULL" in L.prt_last_error()
+    assert L.prt_finish(None) == -1
+    assert L.prt_set_instance_materials(None, None, 0) == -1
+    assert L.prt_set_stream(None, None) == -1
+
+
 def test_tile_geometry():
     L = prt.load()
     n = C.c_int64()

@@ -146,6 +146,46 @@ def test_frames_in_flight_rccl_world1():
         ref.close()
 
 
+def test_frames_in_flight_sharded_frame_world1():
+    """prt.tiles.ShardedFrame (the caller's torch.distributed gather) with 3 frames in flight: the tile render of a
+    call may still be on an internal stream when torch queues the gather, so ShardedFrame joins it first
+    (prt_finish); every accumulated frame equals the unsharded one."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    import prt
+    sd = scenes.multi_instance(scenes.config_small(50, 40))
+    W, H, n = 96, 64, 4
+    ref = prt.Context(0)
+    c = prt.Context(0)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        gpu_scene(ref, sd, W, H)
+        want = [ref.render(W, H, 4, 3, frame_index=2 * f)[:2] for f in range(n)]
+        gpu_scene(c, sd, W, H)
+        shard = prt.tiles.ShardedFrame(c, dist, W, H, 32, device="cuda")
+        c.set_frames_in_flight(3)
+        got = []
+        for f in range(n):
+            avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+            rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+            shard.render(4, 3, avg.data_ptr(), rgb.data_ptr(), frame_index=2 * f, stats=False)
+            got.append((avg, rgb))
+        torch.cuda.synchronize()
+        for f, ((o, g), (a, r)) in enumerate(zip(got, want)):
+            assert np.array_equal(o.cpu().numpy(), a), f
+            assert np.array_equal(g.cpu().numpy().view(np.uint32), r), f
+    finally:
+        c.close()
+        ref.close()
+        dist.destroy_process_group()
+
+
 def test_frames_in_flight_refused_on_local_group():
     import prt
     g = prt.Context(group=[0, 0], tile=16)

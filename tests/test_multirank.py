@@ -37,6 +37,9 @@ class _OracleRankCtx:
         self.shard.tiles.copy_(torch.from_numpy(buf))
         return None
 
+    def finish(self):  # prt_finish: nothing in flight on a CPU rank
+        pass
+
     def untile(self, gathered_ptr, width, height, tile, world, avg_ptr, rgb8_ptr):
         from prt import tiles
         assert gathered_ptr == self.shard.gathered.data_ptr()
