@@ -649,7 +649,9 @@ __device__ __forceinline__ void collapse_task(const Task tk, const float4* __res
   uint8_t e[3];
   for (int k = 0; k < 3; k++) e[k] = grid_exp(nhi[k] - p[k], 255.0);
   nd.ex = e[0]; nd.ey = e[1]; nd.ez = e[2];
-  const double sc[3] = {ldexp(1.0, (int)e[0] - 127), ldexp(1.0, (int)e[1] - 127), ldexp(1.0, (int)e[2] - 127)};
+  // the grid step 2^(e - 127) and its exact inverse: (x - p) * 2^(127 - e) is the quotient (x - p) / 2^(e - 127) bit
+  // for bit, without a double division
+  const double isc[3] = {ldexp(1.0, 127 - (int)e[0]), ldexp(1.0, 127 - (int)e[1]), ldexp(1.0, 127 - (int)e[2])};
   uint32_t ninterior = 0, ntri = 0;
   for (int i = 0; i < nc; i++) {
     if (is_leaf(ch[i])) ntri += count[ch[i]];
@@ -674,8 +676,8 @@ __device__ __forceinline__ void collapse_task(const Task tk, const float4* __res
     uint8_t* ql[3] = {&nd.qlox[s], &nd.qloy[s], &nd.qloz[s]};
     uint8_t* qh[3] = {&nd.qhix[s], &nd.qhiy[s], &nd.qhiz[s]};
     for (int k = 0; k < 3; k++) {
-      *ql[k] = (uint8_t)fmin(255.0, fmax(0.0, floor(((double)clo[i][k] - p[k]) / sc[k])));
-      *qh[k] = (uint8_t)fmin(255.0, fmax(0.0, ceil(((double)chi[i][k] - p[k]) / sc[k])));
+      *ql[k] = (uint8_t)fmin(255.0, fmax(0.0, floor(((double)clo[i][k] - p[k]) * isc[k])));
+      *qh[k] = (uint8_t)fmin(255.0, fmax(0.0, ceil(((double)chi[i][k] - p[k]) * isc[k])));
     }
     const int c = ch[i];
     if (is_leaf(c)) {
@@ -737,7 +739,9 @@ __global__ void __launch_bounds__(kB) k_collapse(const float4* __restrict__ tri,
 // scratch arrays are the multi-launch builder's (global, touched by this one workgroup only: plain loads see the
 // workgroup's own stores after a barrier).
 constexpr int kSmallThreads = 1024;
-constexpr int kSmallR = 512;  // default PLOC search radius (as the instance BVH's multi-launch build)
+// default PLOC search radius: 64 places (1,000 drifting instances: PLOC 0.57-0.60 against 1.13-1.21 ms at 512, frames
+// after the rebuild as fast, profiles/r05_tlas_rebuild.txt sessions q-t)
+constexpr int kSmallR = 64;
 struct SmallScratch {
   unsigned long long* keys;  // n sorted keys
   int *left, *right;         // 2n - 1
@@ -779,9 +783,7 @@ __device__ __forceinline__ void small_stamp(uint32_t* ctr, int k) {
 }
 
 __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __restrict__ tri, int n, int max_leaf,
-                                                               SmallScratch sc, Node8* nodes, TriMT* tris,
-                                                               uint32_t* out, uint32_t* level_end, int max_levels,
-                                                               int radius) {
+                                                               SmallScratch sc, int radius) {
   __shared__ union {
     unsigned long long keys[kGpuSmallBuild];
     float sbox[6 * kGpuSmallBuild];  // cluster boxes, component-major: sbox[k * kGpuSmallBuild + i] (conflict-free)
@@ -793,11 +795,12 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   __shared__ uint32_t wsum[kSmallThreads / 64];
   __shared__ uint32_t cb[6];
   __shared__ int s_next;
+  __shared__ int s_ns;  // clusters searching in an incremental PLOC iteration
   __shared__ uint32_t s_err;
   const int tid = (int)threadIdx.x;
   small_stamp(sc.ctr, 0);
   if (tid < 3) { cb[tid] = 0xFFFFFFFFu; cb[3 + tid] = 0u; }
-  if (tid == 0) { s_err = 0u; s_next = n - 2; }
+  if (tid == 0) { s_err = 0u; s_next = n - 2; s_ns = 0; }
   __syncthreads();
   // 1. centroid bounds (k_centroid_bounds) and Morton keys (k_morton), padded to a power of two with ~0
   for (int i = tid; i < n; i += kSmallThreads) {
@@ -876,23 +879,52 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   unsigned long long tp_nn = 0, tp_merge = 0, tp_compact = 0, tp0 = 0;  // diagnostic phase clock (thread 0)
   while (m > 1) {
     if (tid == 0) tp0 = __builtin_amdgcn_s_memrealtime();
-    for (int i = tid; i < m; i += kSmallThreads) {
-      if (incr && snn[i] >= 0) continue;
-      const float b0 = SB(i, 0), b1 = SB(i, 1), b2 = SB(i, 2), b3 = SB(i, 3), b4 = SB(i, 4), b5 = SB(i, 5);
-      float best = 3.4e38f;
-      int bj = -1;
-      // The pair order of the multi-launch builder's tie rule -- equal areas go to the smaller (min, max) pair --
-      // is the order of j here (below i: min = j; above i: min = i, max = j), so the first minimum in j wins
-      auto cand = [&](int j) {
-        const float dx = fmaxf(b3, SB(j, 3)) - fminf(b0, SB(j, 0));
-        const float dy = fmaxf(b4, SB(j, 4)) - fminf(b1, SB(j, 1));
-        const float dz = fmaxf(b5, SB(j, 5)) - fminf(b2, SB(j, 2));
-        const float a = dx * dy + dy * dz + dz * dx;
-        if (bj < 0 || a < best) { best = a; bj = j; }
-      };
-      for (int j = max(0, i - radius); j < i; j++) cand(j);
-      for (int j = i + 1; j <= min(m - 1, i + radius); j++) cand(j);
-      snn[i] = bj;
+    if (!incr) {
+      // every cluster searches its window, one cluster per lane (neighbouring lanes read neighbouring boxes)
+      for (int i = tid; i < m; i += kSmallThreads) {
+        const float b0 = SB(i, 0), b1 = SB(i, 1), b2 = SB(i, 2), b3 = SB(i, 3), b4 = SB(i, 4), b5 = SB(i, 5);
+        float best = 3.4e38f;
+        int bj = -1;
+        // The pair order of the multi-launch builder's tie rule -- equal areas go to the smaller (min, max) pair --
+        // is the order of j here (below i: min = j; above i: min = i, max = j), so the first minimum in j wins
+        auto cand = [&](int j) {
+          const float dx = fmaxf(b3, SB(j, 3)) - fminf(b0, SB(j, 0));
+          const float dy = fmaxf(b4, SB(j, 4)) - fminf(b1, SB(j, 1));
+          const float dz = fmaxf(b5, SB(j, 5)) - fminf(b2, SB(j, 2));
+          const float a = dx * dy + dy * dz + dz * dx;
+          if (bj < 0 || a < best) { best = a; bj = j; }
+        };
+        for (int j = max(0, i - radius); j < i; j++) cand(j);
+        for (int j = i + 1; j <= min(m - 1, i + radius); j++) cand(j);
+        snn[i] = bj;
+      }
+    } else {
+      // incremental: only the clusters listed here search, over every cluster (the last window covered them all),
+      // one wave per cluster -- a lane per candidate, then the wave's minimum of (area, j), the same first minimum in
+      // j as above.  One lane per searching cluster left most lanes idle while a few scanned m candidates in a row.
+      for (int i = tid; i < m; i += kSmallThreads)
+        if (snn[i] < 0) snew[atomicAdd(&s_ns, 1)] = i;  // (snew is free until the merge step)
+      __syncthreads();
+      const int ns = s_ns, lane = tid & 63;
+      for (int s = tid >> 6; s < ns; s += kSmallThreads / 64) {
+        const int i = snew[s];
+        const float b0 = SB(i, 0), b1 = SB(i, 1), b2 = SB(i, 2), b3 = SB(i, 3), b4 = SB(i, 4), b5 = SB(i, 5);
+        unsigned long long best = ~0ull;
+        for (int j = lane; j < m; j += 64) {
+          if (j == i) continue;
+          const float dx = fmaxf(b3, SB(j, 3)) - fminf(b0, SB(j, 0));
+          const float dy = fmaxf(b4, SB(j, 4)) - fminf(b1, SB(j, 1));
+          const float dz = fmaxf(b5, SB(j, 5)) - fminf(b2, SB(j, 2));
+          const float a = dx * dy + dy * dz + dz * dx;  // >= 0: its bits order as the value
+          const unsigned long long key = ((unsigned long long)__float_as_uint(a) << 32) | (uint32_t)j;
+          best = key < best ? key : best;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          const unsigned long long other = __shfl_xor(best, o);
+          best = other < best ? other : best;
+        }
+        if (lane == 0) snn[i] = (int)(uint32_t)best;
+      }
     }
     __syncthreads();
     if (tid == 0) { const unsigned long long t = __builtin_amdgcn_s_memrealtime(); tp_nn += t - tp0; tp0 = t; }
@@ -954,6 +986,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
     }
     m = (int)total;
     if (tid == 0 && ploc_iters < 40) sc.ctr[20 + ploc_iters] = (uint32_t)m;  // diagnostic: clusters left
+    if (tid == 0) s_ns = 0;
     ploc_iters++;
     __syncthreads();
     if (tid == 0) tp_compact += __builtin_amdgcn_s_memrealtime() - tp0;
@@ -966,8 +999,38 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   small_stamp(sc.ctr, 4);
   if (tid == 0) sc.ctr[7] = ploc_iters;
   if (tid == 0 && s_next != -1 && n > 1) s_err |= 4u;  // not exactly n - 1 internal nodes
-  // 5. the collapse, one level per pass, behind barriers (k_collapse)
+  if (tid == 0) st_sc1_u(sc.ctr + 4, s_err);  // for k_collapse_small
+}
+
+// 5. the collapse of the single-workgroup build, one level per pass behind barriers (k_collapse), in a launch of its
+// own: a collapse task is one lane's long serial walk (the slot expansion, the octant assignment, the leaves), which
+// at the PLOC kernel's 128 VGPRs ran from scratch (~80 us a level); at 256 threads it has the registers it needs.
+// The binary tree it walks (children, counts, decisions, keys) is copied to LDS first: every walk is a chain of
+// dependent loads, ~100 cycles each from LDS instead of an L2 round trip.
+constexpr int kCollapseThreads = 256;
+__global__ void __launch_bounds__(kCollapseThreads) k_collapse_small(const float4* __restrict__ tri, int n,
+                                                                     int max_leaf, SmallScratch sc, Node8* nodes,
+                                                                     TriMT* tris, uint32_t* out, uint32_t* level_end,
+                                                                     int max_levels, SmallTlasOut tlas) {
+  __shared__ int lleft[kGpuSmallBuild], lright[kGpuSmallBuild];
+  __shared__ uint32_t ldec[kGpuSmallBuild];
+  __shared__ uint32_t lcount[2 * kGpuSmallBuild];
+  __shared__ unsigned long long lkeys[kGpuSmallBuild];
+  __shared__ uint32_t s_err;
+  const int tid = (int)threadIdx.x;
+  for (int i = tid; i < 2 * n - 1; i += kCollapseThreads) {
+    if (i < n - 1) {
+      lleft[i] = sc.left[i];
+      lright[i] = sc.right[i];
+      if (sc.dp.dec) ldec[i] = sc.dp.dec[i];
+    }
+    lcount[i] = sc.count[i];
+    if (i < n) lkeys[i] = sc.keys[i];
+  }
+  DpTab ldp = sc.dp;
+  if (ldp.dec) ldp.dec = ldec;
   if (tid == 0) {
+    s_err = ld_sc1_u(sc.ctr + 4);
     sc.ta[0] = Task{0, 0u};
     st_sc1_u(sc.ctr + 0, 1u); st_sc1_u(sc.ctr + 1, 0u); st_sc1_u(sc.ctr + 2, 0u); st_sc1_u(sc.ctr + 3, 0u);
     level_end[0] = 1u;
@@ -978,9 +1041,9 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
   int levels = 0;
   while (ntasks) {
     levels++;
-    for (uint32_t t = (uint32_t)tid; t < ntasks; t += kSmallThreads)
-      collapse_task(ta[t], tri, sc.keys, n, sc.left, sc.right, sc.box, nullptr, sc.count, max_leaf, tb, sc.ctr, nodes,
-                    tris, sc.dp);
+    for (uint32_t t = (uint32_t)tid; t < ntasks; t += kCollapseThreads)
+      collapse_task(ta[t], tri, lkeys, n, lleft, lright, sc.box, nullptr, lcount, max_leaf, tb, sc.ctr, nodes, tris,
+                    ldp);
     __syncthreads();
     ntasks = ld_sc1_u(sc.ctr + 2);
     const uint32_t used = ld_sc1_u(sc.ctr + 0);
@@ -996,14 +1059,43 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
     __syncthreads();
     Task* tt = ta; ta = tb; tb = tt;
   }
-  small_stamp(sc.ctr, 5);
+  __shared__ uint32_t s_out[4];
   if (tid == 0) {
     const uint32_t c0 = ld_sc1_u(sc.ctr + 0), c1 = ld_sc1_u(sc.ctr + 1), c3 = ld_sc1_u(sc.ctr + 3);
-    out[0] = c0;
-    out[1] = c1;
-    out[2] = (uint32_t)levels;
-    out[3] = s_err | ((c3 & 0x80000000u) ? 16u : 0u) | (c1 != (uint32_t)n ? 32u : 0u);
+    s_out[0] = c0;
+    s_out[1] = c1;
+    s_out[2] = (uint32_t)levels;
+    s_out[3] = s_err | ((c3 & 0x80000000u) ? 16u : 0u) | (c1 != (uint32_t)n ? 32u : 0u);
+    for (int k = 0; k < 4; k++) out[k] = s_out[k];
   }
+  __syncthreads();
+  if (tlas.slot) {  // the instance BVH's epilogue (k_tlas_slots' conversion, its refit order and its TlasMeta)
+    const uint32_t nn = s_out[0], nl = s_out[2];
+    const bool valid = s_out[3] == 0u && nn > 0u && nl >= 1u && nl <= tlas.depth_cap;
+    if (valid)
+      for (uint32_t j = (uint32_t)tid; j < nn; j += kCollapseThreads) {
+        Node8& nd = nodes[j];
+        for (uint32_t q = 0; q < 8; q++)
+          tlas.slot[8 * (size_t)j + q] =
+              (!((nd.imask >> q) & 1u) && nd.meta[q]) ? tris[nd.tri_base + (nd.meta[q] >> 3)].prim : 0xFFFFFFFFu;
+        nd.tri_base = 8u * j;
+        tlas.order[j] = j;
+      }
+    if (tid == 0) {  // TlasMeta: n_nodes, nlevels, valid, depth, level_off[max_levels], level_cnt[max_levels]
+      uint32_t* m = tlas.meta;
+      m[0] = valid ? nn : 0u;
+      m[1] = valid ? nl : 0u;
+      m[2] = valid ? 1u : 0u;
+      m[3] = valid ? nl : 0u;
+      if (valid)
+        for (uint32_t l = nl, k = 0; l-- > 0; k++) {
+          const uint32_t b = l == 0 ? 0u : level_end[l - 1];
+          m[4 + k] = b;
+          m[4 + max_levels + k] = level_end[l] - b;
+        }
+    }
+  }
+  small_stamp(sc.ctr, 5);
 }
 
 // ShadeTri.pad[0] = the primitive's TriMT record (the cooperative traversal tail, prt_persist.h)
@@ -1211,7 +1303,7 @@ uint32_t* gpu_small_ctr(void* scratch, int32_t n) {
 
 hipError_t gpu_build_blas8_small(hipStream_t s, const float* tri_dev, int32_t n, int max_leaf, Node8* nodes_out,
                                  TriMT* tris_out, void* scratch, uint32_t* out, uint32_t* level_end, int max_levels,
-                                 int radius) {
+                                 int radius, SmallTlasOut tlas) {
   if (n <= 0 || n > kGpuSmallBuild) return hipErrorInvalidValue;
   const size_t nn = 2 * (size_t)n - 1, ni = (size_t)std::max(n - 1, 1);
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -1229,7 +1321,9 @@ hipError_t gpu_build_blas8_small(hipStream_t s, const float* tri_dev, int32_t n,
   sc.ctr = reinterpret_cast<uint32_t*>(p);
   if (n == 1) sc.dp = DpTab{nullptr, nullptr};  // the root is the single leaf
   hipLaunchKernelGGL(k_build_small, dim3(1), dim3(kSmallThreads), 0, s, reinterpret_cast<const float4*>(tri_dev), n,
-                     max_leaf, sc, nodes_out, tris_out, out, level_end, max_levels, radius > 0 ? radius : kSmallR);
+                     max_leaf, sc, radius > 0 ? radius : kSmallR);
+  hipLaunchKernelGGL(k_collapse_small, dim3(1), dim3(kCollapseThreads), 0, s, reinterpret_cast<const float4*>(tri_dev),
+                     n, max_leaf, sc, nodes_out, tris_out, out, level_end, max_levels, tlas);
   return hipGetLastError();
 }
 

@@ -70,14 +70,15 @@ __device__ __forceinline__ void refit_node(const InstDev* __restrict__ inst, uin
   uint32_t e[3];
   for (int a = 0; a < 3; a++) e[a] = grid_exp((double)nhi[a] - p[a]);
   nd.ex = (uint8_t)e[0]; nd.ey = (uint8_t)e[1]; nd.ez = (uint8_t)e[2];
-  const double sc[3] = {ldexp(1.0, (int)e[0] - 127), ldexp(1.0, (int)e[1] - 127), ldexp(1.0, (int)e[2] - 127)};
+  // the grid step 2^(e - 127)'s exact inverse: the products are the quotients bit for bit (no double division)
+  const double isc[3] = {ldexp(1.0, 127 - (int)e[0]), ldexp(1.0, 127 - (int)e[1]), ldexp(1.0, 127 - (int)e[2])};
   uint8_t* ql[3] = {nd.qlox, nd.qloy, nd.qloz};
   uint8_t* qh[3] = {nd.qhix, nd.qhiy, nd.qhiz};
   for (uint32_t s = 0; s < 8; s++) {
     for (int a = 0; a < 3; a++) {
       if (used[s]) {
-        ql[a][s] = (uint8_t)fmin(255.0, fmax(0.0, floor(((double)clo[s][a] - p[a]) / sc[a])));
-        qh[a][s] = (uint8_t)fmin(255.0, fmax(0.0, ceil(((double)chi[s][a] - p[a]) / sc[a])));
+        ql[a][s] = (uint8_t)fmin(255.0, fmax(0.0, floor(((double)clo[s][a] - p[a]) * isc[a])));
+        qh[a][s] = (uint8_t)fmin(255.0, fmax(0.0, ceil(((double)chi[s][a] - p[a]) * isc[a])));
       } else {  // empty slot: an inverted box never hits
         ql[a][s] = 255;
         qh[a][s] = 0;
@@ -135,38 +136,6 @@ __global__ void k_inst_fat_dev(const InstDev* __restrict__ inst, int32_t n, floa
   fat[3 * (size_t)i] = lo;
   fat[3 * (size_t)i + 1] = hi;
   fat[3 * (size_t)i + 2] = lo;
-}
-
-// after k_build_small: instance slots (as k_tlas_slots), identity refit order, and the TlasMeta (levels deepest
-// first); valid = 0 when the build failed or is deeper than the stacks the context sized for its instance BVH
-__global__ void __launch_bounds__(1024) k_tlas_small_finish(Node8* __restrict__ nodes, const TriMT* __restrict__ tris,
-                                                            uint32_t* __restrict__ slot, uint32_t* __restrict__ order,
-                                                            const uint32_t* __restrict__ out,
-                                                            const uint32_t* __restrict__ level_end,
-                                                            uint32_t depth_cap, TlasMeta* __restrict__ meta) {
-  const uint32_t nn = out[0], levels = out[2];
-  const bool valid = out[3] == 0u && nn > 0u && levels >= 1u && levels <= depth_cap;
-  if (valid)
-    for (uint32_t j = threadIdx.x; j < nn; j += blockDim.x) {
-      Node8& nd = nodes[j];
-      for (uint32_t s = 0; s < 8; s++)
-        slot[8 * (size_t)j + s] = (!((nd.imask >> s) & 1u) && nd.meta[s]) ? tris[nd.tri_base + (nd.meta[s] >> 3)].prim
-                                                                            : 0xFFFFFFFFu;
-      nd.tri_base = 8u * j;
-      order[j] = j;
-    }
-  if (threadIdx.x == 0) {
-    meta->n_nodes = valid ? nn : 0u;
-    meta->nlevels = valid ? levels : 0u;
-    meta->depth = valid ? levels : 0u;
-    meta->valid = valid ? 1u : 0u;
-    if (valid)
-      for (uint32_t l = levels, k = 0; l-- > 0; k++) {
-        const uint32_t b = l == 0 ? 0u : level_end[l - 1];
-        meta->level_off[k] = b;
-        meta->level_cnt[k] = level_end[l] - b;
-      }
-  }
 }
 
 // the render stream's side of a device rebuild: the back tree replaces the front one when it is valid (the front
@@ -268,6 +237,11 @@ hipError_t gpu_build_tlas8(hipStream_t s, const float* boxes, int32_t n, float* 
   return hipGetLastError();
 }
 
+// the one-workgroup kernels around a device rebuild run beside the persistent traversal, which leaves no VGPRs free
+// on a SIMD it holds: a 4-wave workgroup finds room as soon as a few traversal waves have exited, a 16-wave one
+// waits for a whole CU to drain
+constexpr int kTlasSmallThreads = 256;
+
 hipError_t launch_tlas_cost(hipStream_t s, const Node8* nodes, uint32_t n_nodes, const float* aabb,
                             const InstDev* inst, const uint32_t* slot, double* out, const TlasMeta* meta) {
   hipLaunchKernelGGL(k_tlas_cost, dim3(1), dim3(1024), 0, s, nodes, n_nodes, aabb, inst, slot, out, meta);
@@ -279,14 +253,17 @@ hipError_t gpu_rebuild_tlas_small(hipStream_t s, const InstDev* inst, int32_t n,
                                   TlasMeta* meta, int depth_cap) {
   if (n <= 0 || n > kGpuSmallBuild) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_inst_fat_dev, dim3((n + 255) / 256), dim3(256), 0, s, inst, n, reinterpret_cast<float4*>(fat));
-  // PLOC search radius of the single-workgroup build (PRT_TLAS_SMALL_R, default 512: every cluster of a
-  // 1,000-instance tree sees all others)
+  // PLOC search radius of the single-workgroup build (PRT_TLAS_SMALL_R, default 64: bvh_gpu.hip kSmallR)
   const char* re = std::getenv("PRT_TLAS_SMALL_R");
+  static_assert(sizeof(TlasMeta) == 4 * (4 + 2 * kTlasMaxLevels), "TlasMeta words (the collapse launch writes them)");
+  SmallTlasOut to;
+  to.slot = slot;
+  to.order = order;
+  to.meta = reinterpret_cast<uint32_t*>(meta);
+  to.depth_cap = (uint32_t)depth_cap;
   const hipError_t e = gpu_build_blas8_small(s, fat, n, 1, nodes, tris, scratch, out, out + 4, kTlasMaxLevels,
-                                             re ? std::atoi(re) : 0);
+                                             re ? std::atoi(re) : 0, to);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_tlas_small_finish, dim3(1), dim3(1024), 0, s, nodes, tris, slot, order, out, out + 4,
-                     (uint32_t)depth_cap, meta);
   if (std::getenv("PRT_TLAS_SMALL_TIMES")) {  // diagnostic: the build's phase clock (waits for the side stream)
     uint32_t w[64];
     if (hipMemcpyAsync(w, gpu_small_ctr(scratch, n), sizeof(w), hipMemcpyDeviceToHost, s) == hipSuccess &&
@@ -306,13 +283,13 @@ hipError_t gpu_rebuild_tlas_small(hipStream_t s, const InstDev* inst, int32_t n,
 hipError_t launch_tlas_commit(hipStream_t s, const TlasMeta* mb, const Node8* nb, const uint32_t* sb,
                               const uint32_t* ob, TlasMeta* mf, Node8* nf, uint32_t* sf, uint32_t* of,
                               uint32_t* rejected) {
-  hipLaunchKernelGGL(k_tlas_commit, dim3(1), dim3(1024), 0, s, mb, nb, sb, ob, mf, nf, sf, of, rejected);
+  hipLaunchKernelGGL(k_tlas_commit, dim3(1), dim3(kTlasSmallThreads), 0, s, mb, nb, sb, ob, mf, nf, sf, of, rejected);
   return hipGetLastError();
 }
 
 hipError_t launch_tlas_refit_meta(hipStream_t s, const InstDev* inst, const TlasMeta* meta, const uint32_t* order,
                                   Node8* nodes, const uint32_t* slot, float* aabb) {
-  hipLaunchKernelGGL(k_tlas_refit_meta, dim3(1), dim3(1024), 0, s, inst, meta, order, nodes, slot, aabb);
+  hipLaunchKernelGGL(k_tlas_refit_meta, dim3(1), dim3(kTlasSmallThreads), 0, s, inst, meta, order, nodes, slot, aabb);
   return hipGetLastError();
 }
 
