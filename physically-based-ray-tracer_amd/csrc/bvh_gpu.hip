@@ -161,13 +161,16 @@ __global__ void __launch_bounds__(kB) k_radix_tree(const unsigned long long* __r
 // collapse table of internal node p from its children's (a binary leaf, id >= n - 1: one triangle, every C its
 // leaf cost); children's tables were written earlier in this launch (sc1, after the arrival atomic) or by an
 // earlier launch
+// WG: the children's tables were written by this workgroup (the single-workgroup build): plain loads after its
+// barriers, served by the L2 instead of the agent-coherent path
+template <bool WG = false>
 __device__ __forceinline__ void dp_node(const DpTab& dp, int p, int lc, int rc, const float* pb, const float* lb,
                                         const float* rb, int cnt, int n, int max_leaf) {
   double cl[9], cr[9];
   const double al = area6d(lb) * kDpTri, ar = area6d(rb) * kDpTri;
   for (int i = 1; i <= 8; i++) {
-    cl[i] = lc >= n - 1 ? al : ld_sc1_d(dp.C + 8 * (size_t)lc + i - 1);
-    cr[i] = rc >= n - 1 ? ar : ld_sc1_d(dp.C + 8 * (size_t)rc + i - 1);
+    cl[i] = lc >= n - 1 ? al : (WG ? dp.C[8 * (size_t)lc + i - 1] : ld_sc1_d(dp.C + 8 * (size_t)lc + i - 1));
+    cr[i] = rc >= n - 1 ? ar : (WG ? dp.C[8 * (size_t)rc + i - 1] : ld_sc1_d(dp.C + 8 * (size_t)rc + i - 1));
   }
   const double A = fmax(area6d(pb), 1e-30);
   const double leafc = cnt <= max_leaf ? A * kDpTri * (double)cnt : 1e300;
@@ -185,11 +188,15 @@ __device__ __forceinline__ void dp_node(const DpTab& dp, int p, int lc, int rc, 
   const double intc = A * kDpNode + D[8];
   if (cnt <= max_leaf && leafc <= intc) dec |= 1u << 31;
   double C = fmin(leafc, intc);
-  st_sc1_d(dp.C + 8 * (size_t)p, C);
+  auto put = [&](size_t at, double v) {
+    if (WG) dp.C[at] = v;
+    else st_sc1_d(dp.C + at, v);
+  };
+  put(8 * (size_t)p, C);
   for (int i = 2; i <= 8; i++) {
     if (C <= D[i]) dec |= 1u << (24 + i - 2);
     else C = D[i];
-    st_sc1_d(dp.C + 8 * (size_t)p + i - 1, C);
+    put(8 * (size_t)p + i - 1, C);
   }
   dp.dec[p] = dec;
 }
@@ -620,19 +627,27 @@ __device__ __forceinline__ void collapse_task(const Task tk, const float4* __res
   {
     double pc[3];
     for (int k = 0; k < 3; k++) pc[k] = 0.5 * (nlo[k] + nhi[k]);
+    // each child's centroid offset once (the greedy rounds below re-read it; the same double operations, so the
+    // same costs bit for bit as computing it per pair)
+    // (loops unrolled over all 8 children: constant indices keep cc in registers)
+    double cc[8][3];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int k = 0; k < 3; k++) cc[i][k] = i < nc ? 0.5 * ((double)clo[i][k] + (double)chi[i][k]) - pc[k] : 0.0;
     uint32_t used_c = 0, used_s = 0;
     for (int m = 0; m < nc; m++) {
       double best = 1e300;
       int bi = -1, bs = -1;
-      for (int i = 0; i < nc; i++) {
-        if (used_c & (1u << i)) continue;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        if (i >= nc || (used_c & (1u << i))) continue;
+#pragma unroll
         for (int s = 0; s < 8; s++) {
           if (used_s & (1u << s)) continue;
           double d = 0;
-          for (int k = 0; k < 3; k++) {
-            const double cc = 0.5 * ((double)clo[i][k] + (double)chi[i][k]) - pc[k];
-            d += ((s >> k) & 1) ? -cc : cc;
-          }
+#pragma unroll
+          for (int k = 0; k < 3; k++) d += ((s >> k) & 1) ? -cc[i][k] : cc[i][k];
           if (d < best) { best = d; bi = i; bs = s; }
         }
       }
@@ -957,7 +972,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __r
       sc.left[p] = lc;
       sc.right[p] = rc;
       sc.count[p] = sc.count[lc] + sc.count[rc];
-      if (sc.dp.C) dp_node(sc.dp, p, lc, rc, nb[e], lb, rb, (int)sc.count[p], n, max_leaf);
+      if (sc.dp.C) dp_node<true>(sc.dp, p, lc, rc, nb[e], lb, rb, (int)sc.count[p], n, max_leaf);
       nc[e] = p;
     }
     uint32_t total = 0;
