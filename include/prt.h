@@ -324,8 +324,10 @@ typedef struct {
     double  build_ms;       /* wall time of the last prt_set_meshes (BLAS builds + uploads) */
     int32_t builder;        /* PRT_BUILDER_* used by the last prt_set_meshes */
     int32_t tlas_depth;     /* levels of the instance BVH the rays walk (0: instances tested as a linear list) */
-    int32_t tlas_rebuilds;  /* (ABI 8) device rebuilds of the instance BVH since the instance count last changed */
-    int32_t tlas_refits;    /* (ABI 8) device refits of it since then (prt_set_instances with the same count) */
+    int32_t tlas_rebuilds;  /* (ABI 8) rebuilds of the instance BVH since the instance count last changed: host
+                               builds for an update (default, up to 4,096 instances) or device builds */
+    int32_t tlas_refits;    /* (ABI 8) updates since then that refitted the current tree instead (prt_set_instances
+                               with the same count) */
     int32_t tlas_rejected;  /* (ABI 9) device rebuilds not committed since the context was created (deeper than
                                the traversal stacks were sized for; the refitted tree stayed).  Reading it waits
                                for the context's queued work. */

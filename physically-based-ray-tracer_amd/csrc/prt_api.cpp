@@ -309,34 +309,40 @@ int ensure_instances(prt_ctx* c) {
   // BLASInstances every frame as the reference does (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770)
   c->use_tlas = use_tlas;
   // The instance BVH.  The reference rebuilds it every frame (Core/Renderer.cpp:33-41).  Here the host SAH builder
-  // builds it when the set of instances changes (its count; or every call with PRT_TLAS_HOST=1, the A/B form).
-  // Every other update:
-  //  - up to kGpuSmallBuild instances (default): rebuilt on the device for every update, the reference's per-frame
-  //    BVH::Build, by one workgroup in one launch on a side stream from the side stream's own refit of the
-  //    instance records (gpu_rebuild_tlas_small), committed over the front tree by a copy kernel on the render
-  //    stream -- no host BVH work and no host wait (PRT_TLAS_SMALL=0 turns it off);
-  //  - otherwise refitted on the device behind k_refit (prt_tlas.hip), and rebuilt on the device by the multi-launch
-  //    builder (PLOC + SAH-optimal collapse over host-computed boxes, gpu_build_tlas8: one host round trip per PLOC
-  //    iteration and collapse level) once refitting has raised the tree's node-area cost above PRT_TLAS_REBUILD
-  //    (default 1.05) times its cost right after the last build, or after PRT_TLAS_MAX_REFITS refits (0: refit
-  //    only).  The cost is measured on the device after every refit and read back without a host wait (a pinned
-  //    copy behind an event): a frame decides on the latest cost already available.
-  // PRT_TLAS_REBUILD=always / <ratio> / 0 overrides the policy of either builder.
+  // builds it when the set of instances changes (its count), and by default for every update up to kGpuSmallBuild
+  // instances (below).  Otherwise:
+  //  - PRT_TLAS_SMALL=1 (up to kGpuSmallBuild instances): rebuilt on the device for every update by one workgroup on
+  //    a side stream from the side stream's own refit of the instance records (gpu_rebuild_tlas_small), committed
+  //    over the front tree by a copy kernel on the render stream -- no host BVH work and no host wait;
+  //  - above kGpuSmallBuild, or PRT_TLAS_SMALL=0: refitted on the device behind k_refit (prt_tlas.hip), and rebuilt
+  //    on the device by the multi-launch builder (PLOC + SAH-optimal collapse over host-computed boxes,
+  //    gpu_build_tlas8: one host round trip per PLOC iteration and collapse level) once refitting has raised the
+  //    tree's node-area cost above PRT_TLAS_REBUILD (default 1.05) times its cost right after the last build, or
+  //    after PRT_TLAS_MAX_REFITS refits (0: refit only).  The cost is measured on the device after every refit and
+  //    read back without a host wait (a pinned copy behind an event): a frame decides on the latest cost available.
+  // PRT_TLAS_REBUILD=always / <ratio> / 0 overrides the policy of either device builder.
+  // Up to kGpuSmallBuild instances the default is the host SAH build for every update (the reference's per-frame
+  // BVH::Build, on the calling thread, ~0.8 ms for 1,000 instances): measured on 1,000 drifting instances it costs
+  // the frames nothing (the host builds while the GPU renders the queued frames; no host wait), where every device
+  // build run beside the persistent traversal cost 5-7 % (profiles/r05_tlas_rebuild.txt session aa).
+  // PRT_TLAS_SMALL=1: the single-workgroup device build instead; PRT_TLAS_SMALL=0 or PRT_TLAS_REBUILD=<ratio> / 0:
+  // the device refit and the multi-launch builder's trigger; PRT_TLAS_HOST=1: the host build at any count.
   const char* th = std::getenv("PRT_TLAS_HOST");
-  const bool host_tlas = th && std::atoi(th) == 1;
   const char* tr = std::getenv("PRT_TLAS_REBUILD");
   const char* ts = std::getenv("PRT_TLAS_SMALL");
-  const bool small_ok = !(ts && std::atoi(ts) == 0) && n <= kGpuSmallBuild && !host_tlas;
+  const bool tr_always = tr && std::strcmp(tr, "always") == 0;
+  const bool host_tlas = (th && std::atoi(th) == 1) || (!ts && n <= kGpuSmallBuild && (!tr || tr_always));
+  const bool small_ok = ts && std::atoi(ts) == 1 && n <= kGpuSmallBuild && !host_tlas;
   // the builder of the current tree decides the default policy (its instance count is unchanged on a refit)
   const bool small_now = (use_tlas && c->tlas_n == n && !host_tlas) ? c->tlas_small : small_ok;
-  const bool rebuild_always = tr ? std::strcmp(tr, "always") == 0 : small_now;
+  const bool rebuild_always = tr ? tr_always : small_now;
   const double rebuild_ratio = rebuild_always ? 0.0 : (tr ? std::atof(tr) : 1.05);
   // and at the latest after PRT_TLAS_MAX_REFITS refits (default 8): the node-area cost understates what a node
   // stretched across the scene costs the rays that must now open it
   const char* tm = std::getenv("PRT_TLAS_MAX_REFITS");
   const int32_t max_refits = tm ? std::atoi(tm) : 8;
   auto upload_order = [&]() -> int {
-    const size_t cap_nodes = std::max<size_t>(c->tlas_nodes, c->tlas_small ? (size_t)n : 1);
+    const size_t cap_nodes = std::max<size_t>(c->tlas_nodes, (c->tlas_small || host_tlas) ? (size_t)n : 1);
     const size_t ob = 4 * std::max(c->tlas_topo.order.size(), cap_nodes), ab = 24 * cap_nodes;
     if (c->tlas_order.bytes < ob || c->tlas_aabb.bytes < ab) {
       const int rc = drain(c);
@@ -575,8 +581,10 @@ int ensure_instances(prt_ctx* c) {
       c->tlas_depth_cap = c->tlas_depth + (slack ? 1 : 0);
       c->tlas_depth = c->tlas_depth_cap;
     }
-    const size_t cap_nodes = c->tlas_small ? std::max<size_t>(c->tlas_host.nodes.size(), (size_t)n)
-                                           : c->tlas_host.nodes.size();
+    // (a tree over n instances has at most n nodes: sized for that once, the builds for later updates, host or
+    // device, never reallocate -- a reallocation drains the queued frames, a host wait)
+    const size_t cap_nodes = (c->tlas_small || host_tlas) ? std::max<size_t>(c->tlas_host.nodes.size(), (size_t)n)
+                                                          : c->tlas_host.nodes.size();
     const size_t nb = c->tlas_host.nodes.size() * sizeof(Node8), sb = c->tlas_host.slot.size() * 4;
     if (c->tlas8.bytes < cap_nodes * sizeof(Node8) || c->tlas_slot.bytes < cap_nodes * 32 ||
         (c->tlas_small && c->tlas_meta.bytes < sizeof(TlasMeta))) {
@@ -596,6 +604,7 @@ int ensure_instances(prt_ctx* c) {
     int rc = upload_order();
     if (rc) return rc;
     if (c->tlas_n != n) c->tlas_rebuilds = c->tlas_refits = 0;
+    else c->tlas_rebuilds++;  // a host build for an update of the same instance set
     c->tlas_since_build = 0;
     c->tlas_n = n;
     if (rebuild_ratio > 0 && !host_tlas) {  // the cost right after the build (its refit's boxes)

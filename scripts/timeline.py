@@ -66,6 +66,15 @@ def main():
         alone.sort()
         print(f"{focus}: {len(alone)} dispatches, alone on the GPU median {alone[len(alone) // 2]:.1f} us, "
               f"max {alone[-1]:.1f} us, total {sum(alone) / 1e3:.3f} ms")
+    # traversal launches far above their median (--slow FACTOR, default 1.6): how many, and what overlapped them
+    fac = float(sys.argv[sys.argv.index("--slow") + 1]) if "--slow" in sys.argv else 1.6
+    tr = [(s, e) for s, e, n in rows if n == "k_trace2"]
+    if tr:
+        med = sorted(e - s for s, e in tr)[len(tr) // 2]
+        slow = [(s, e) for s, e in tr if e - s > fac * med]
+        lone = sum(1 for s, e in slow if not any(n2 != "k_trace2" and s2 < e and e2 > s for s2, e2, n2 in rows))
+        print(f"k_trace2: {len(tr)} launches, median {med / 1e3:.1f} us; {len(slow)} above {fac} x the median "
+              f"({lone} with no other kernel overlapping)")
 
 
 if __name__ == "__main__":

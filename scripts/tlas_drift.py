@@ -3,8 +3,9 @@
 every frame, wrapping at the field's edge; frames queued back to back, 1280x720, 2 spp, depth 3).  Per rebuild
 policy: ms per frame over the drift, the host time spent inside set_instances per frame, then ms per frame of
 static frames at the final positions against a fresh host SAH tree over the same positions (PRT_TLAS_HOST=1).
-Modes (TLAS_MODES): default = refit only / the default (up to 4,096 instances: the single-workgroup builder for
-every frame) / the multi-launch builder on the node-area trigger and every frame."""
+Modes (TLAS_MODES): unset = refit only / the default (up to 4,096 instances: the host SAH build for every update) /
+the single-workgroup device build for every update / the multi-launch builder on the node-area trigger and every
+frame; default / device / host = one of them once (host: a synchronous host SAH build per update)."""
 import os
 import sys
 import time
@@ -61,7 +62,8 @@ def timed(ctx, avg, rgb, n, inst=None):
     return (time.perf_counter() - t0) * 1e3 / n, inst
 
 
-MODES = [("refit only", "0", None), ("default (single-workgroup builder, every frame)", None, None),
+MODES = [("refit only", "0", None), ("default (host SAH build, every update)", None, None),
+         ("single-workgroup device build, every frame", None, "S"),
          ("multi-launch builder, trigger", "1.05", "M"), ("multi-launch builder, every frame", "always", "M")]
 if os.environ.get("TLAS_MODES") == "trbvh":  # A/B of the device tree's treelet-restructuring passes
     MODES = [(f"device rebuild every frame, {k} TRBVH passes", "always", k) for k in ("0", "1", "2", "3")]
@@ -72,12 +74,22 @@ if os.environ.get("TLAS_MODES") == "small":  # the single-workgroup builder's po
     MODES = [("small builder, trigger", "1.05", None), ("small builder, every frame", "always", None)]
 if os.environ.get("TLAS_MODES") == "default":  # the default policy only, once (timeline sessions)
     MODES = MODES[1:2]
-for mode, env, trbvh in MODES + (MODES if os.environ.get("TLAS_MODES") != "default" else []):
+if os.environ.get("TLAS_MODES") == "device":  # the single-workgroup device build only, once
+    MODES = MODES[2:3]
+if os.environ.get("TLAS_MODES") == "host":  # a host SAH build for every update (the host waits; timeline sessions)
+    MODES = [("host SAH build, every frame", None, "H")]
+for mode, env, trbvh in MODES + (MODES if os.environ.get("TLAS_MODES") not in ("default", "host", "device") else []):
     os.environ.pop("PRT_TLAS_SMALL", None)
+    host_every = trbvh == "H"
+    if host_every:
+        trbvh = None
+    if trbvh == "S":  # the single-workgroup device build
+        os.environ["PRT_TLAS_SMALL"] = "1"
+        trbvh = "keep"
     if trbvh == "M":  # the multi-launch builder
         os.environ["PRT_TLAS_SMALL"] = "0"
         trbvh = None
-    if trbvh is None:
+    if trbvh in (None, "keep"):
         os.environ.pop("PRT_TLAS_TRBVH", None)
         os.environ.pop("PRT_TLAS_PLOC_R", None)
     else:  # (the treelet / radius knobs are the multi-launch builder's)
@@ -86,6 +98,8 @@ for mode, env, trbvh in MODES + (MODES if os.environ.get("TLAS_MODES") != "defau
         if ":" in trbvh:
             os.environ["PRT_TLAS_PLOC_R"] = trbvh.split(":")[1]
     os.environ.pop("PRT_TLAS_HOST", None)
+    if host_every:
+        os.environ["PRT_TLAS_HOST"] = "1"
     if env is None:
         os.environ.pop("PRT_TLAS_REBUILD", None)
     else:
@@ -117,7 +131,7 @@ for mode, env, trbvh in MODES + (MODES if os.environ.get("TLAS_MODES") != "defau
     hms = np.array(HOST_MS)
     print(f"{N} instances, {F} frames, {mode}: static frame at start {t_first:.3f} ms; drift ms/frame per 20 frames "
           f"{blocks}; set_instances host time median {np.median(hms):.3f} / max {hms.max():.3f} ms; "
-          f"{si.tlas_rebuilds} device rebuilds ({si.tlas_rejected} not committed) / {si.tlas_refits} refits; static frame at the end "
+          f"{si.tlas_rebuilds} rebuilds ({si.tlas_rejected} device builds not committed) / {si.tlas_refits} refits; static frame at the end "
           f"{t_end:.3f} ms vs fresh host SAH tree {t_fresh:.3f} ms (depth {hd}) ({100 * (t_end / t_fresh - 1):+.1f} %)",
           flush=True)
     ctx.close()

@@ -516,17 +516,17 @@ def test_device_tlas_moving_instances(gpu_ctx, monkeypatch, n):
     assert np.array_equal(a_h, out[-1].cpu().numpy())
 
 
-@pytest.mark.parametrize("mode", ["default", "small_trigger", "multi_trigger", "multi_always", "large"])
+@pytest.mark.parametrize("mode", ["default", "small_always", "small_trigger", "multi_trigger", "multi_always", "large"])
 def test_device_tlas_rebuild_long_motion(gpu_ctx, monkeypatch, mode):
     """1,000 tori drift across the field for 120 frames (every instance moves before every
-    frame, the frames queued back to back with device outputs and no host wait).  The instance BVH is rebuilt on the
-    device: by default (up to 4,096 instances) for every frame, the reference's per-frame BVH::Build, by one
-    workgroup in one launch on a side stream (k_build_small: PLOC + SAH-optimal collapse), committed by a copy
-    kernel on the render stream; "small_trigger": the same builder on the node-area trigger (PRT_TLAS_REBUILD=1.05);
-    the multi-launch builder (PRT_TLAS_SMALL=0) on the trigger or every frame; "large": 5,000 instances, 40 frames
-    (above the single-workgroup limit: multi-launch builder, trigger).  Every 10th frame equals the oracle's render
-    of that frame's transforms, and the device rebuilds happened (every frame: one per set_instances after the host
-    build of the first)."""
+    frame, the frames queued back to back with device outputs and no host wait).  The instance BVH is rebuilt for
+    every update, the reference's per-frame BVH::Build: by default (up to 4,096 instances) by the host SAH build on
+    the calling thread, uploaded in stream order; "small_always": by the single-workgroup device build (PRT_TLAS_SMALL=1: k_build_small +
+    k_collapse_small on a side stream, committed by a copy kernel on the render stream); "small_trigger": the same
+    builder on the node-area trigger (PRT_TLAS_REBUILD=1.05); the multi-launch device builder (PRT_TLAS_SMALL=0) on
+    the trigger or every frame; "large": 5,000 instances, 40 frames (above the single-workgroup limit: multi-launch
+    builder, trigger).  Every 10th frame equals the oracle's render of that frame's transforms, and the rebuilds
+    happened (every frame: one per set_instances after the host build of the first)."""
     import dataclasses
     import torch
     import prt
@@ -536,11 +536,13 @@ def test_device_tlas_rebuild_long_motion(gpu_ctx, monkeypatch, mode):
     n, nframes = (5000, 40) if mode == "large" else (1000, 120)
     if mode.startswith("multi"):
         monkeypatch.setenv("PRT_TLAS_SMALL", "0")
+    if mode.startswith("small"):
+        monkeypatch.setenv("PRT_TLAS_SMALL", "1")
     if mode.endswith("trigger"):
         monkeypatch.setenv("PRT_TLAS_REBUILD", "1.05")
     if mode.endswith("always"):
         monkeypatch.setenv("PRT_TLAS_REBUILD", "always")
-    every_frame = mode in ("default", "multi_always")
+    every_frame = mode in ("default", "small_always", "multi_always")
     sd0 = scenes.instance_field(n, seed=17)
     W, H = 64, 48
     flags = oracle.DEFAULT_FLAGS & ~oracle.ACCUMULATE
