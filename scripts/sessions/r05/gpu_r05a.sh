@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # round-5 session a: the GPU suite (+ small-builder modes), then the frames-in-flight probe
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 bash scripts/gpu_suite.sh r05a; rc=$?
 case $rc in 0|1) ;; *) exit $rc ;; esac

@@ -2,7 +2,7 @@
 # round-5 session aa: the instance BVH rebuilt for every update by a builder thread (host SAH build beside the
 # frames, taken by a later update) as the default; the whole GPU suite; drift default / device / host; timeline
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05aa}
 bash scripts/gpu_suite.sh $T || exit $?

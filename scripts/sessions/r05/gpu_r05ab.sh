@@ -2,7 +2,7 @@
 # round-5 session ab: the host SAH build for every update as the default up to 4,096 instances; the whole GPU
 # suite; drift default / device; kernel timeline of the default drift
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05ab}
 bash scripts/gpu_suite.sh $T || exit $?

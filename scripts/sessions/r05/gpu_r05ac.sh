@@ -2,7 +2,7 @@
 # round-5 session ac: instance-BVH buffers sized for n nodes under the per-update host build (no reallocation);
 # the whole GPU suite; drift default (all policies once)
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05ac}
 bash scripts/gpu_suite.sh $T || exit $?

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # round-5 session b: the GPU suite (+ small-builder modes), the frames-in-flight probe and A/Bs
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05b}
 bash scripts/gpu_suite.sh $T; rc=$?

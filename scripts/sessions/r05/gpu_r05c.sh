@@ -2,7 +2,7 @@
 # round-5 session c: GPU suite on the library with up to 4 frames in flight and the single-workgroup instance-BVH
 # rebuild as the default, then rank shares / bench per frames in flight and the instance-BVH drift
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05c}
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rs --timeout 150 --timeout-method thread \

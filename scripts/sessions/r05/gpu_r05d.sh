@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # round-5 session d: kernel timeline of the default instance-BVH rebuild during drift; frames-in-flight grid A/B
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 T=${1:-r05d}

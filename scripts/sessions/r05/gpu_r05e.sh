@@ -2,7 +2,7 @@
 # round-5 session e: GPU suite, instance-BVH drift (pipelined single-workgroup rebuild), kernel traces of the
 # drift and of the world-8 share with 2 / 3 frames in flight
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 T=${1:-r05e}

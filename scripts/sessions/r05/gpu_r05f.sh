@@ -2,7 +2,7 @@
 # round-5 session f: the single-workgroup build's phase times per PLOC radius, drift per radius; frames in flight
 # with more hardware queues
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05f}
 for r in 512 128 64 32; do

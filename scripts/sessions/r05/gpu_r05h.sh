@@ -2,7 +2,7 @@
 # round-5 session h: GPU suite (SoA single-workgroup build), build phases, frames in flight per world with 8 hardware
 # queues, the bench line
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05h}
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rs --timeout 150 --timeout-method thread \

@@ -2,7 +2,7 @@
 # round-5 session i: GPU suite (incremental PLOC neighbours, blocking commit by default), build phases, drift of the
 # default / pipelined policies
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05i}
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rs --timeout 150 --timeout-method thread \

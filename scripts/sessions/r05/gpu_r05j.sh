@@ -2,7 +2,7 @@
 # round-5 session j: small-build PLOC radius (window vs global + incremental neighbours) and the depth slack, on
 # the 1,000-instance drift; long-motion tests
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05j}
 for r in 512 4096; do

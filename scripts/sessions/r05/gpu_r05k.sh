@@ -2,7 +2,7 @@
 # round-5 session k: traversal grid with one CU spare for the instance-BVH build, on the drift; world-8 share
 # with 4 frames in flight and half grids
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05k}
 for sp in 1 0 1 0; do

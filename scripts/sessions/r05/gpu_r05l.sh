@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # round-5 session l: octant-ordered next-ray appends (PRT_SORT_OCT) A/B with parity; 4-in-flight default grids
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05l}
 PRT_SORT_OCT=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_golden.py tests/test_golden_ref.py -m gpu -q -rs --timeout 150 --timeout-method thread > gpurun_out/${T}_sort_tests.log 2>&1; rc=$?

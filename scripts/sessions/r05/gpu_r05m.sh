@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # round-5 session m: bench.py frames in flight 2 vs 4 at N = 1 (C4, interleaved) and C5 one at a time vs 2
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05m}
 bench() {  # bench <tag> <args...>

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # round-5 session n: bench.py at N = 1 with 2 / 4 frames in flight and 4 / 8 hardware queues; PLOC phase split
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05n}
 bench() {  # bench <tag> <args...>

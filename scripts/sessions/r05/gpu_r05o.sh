@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # round-5 session o: wave-wide broadcast neighbour scan in the single-workgroup build: phases, drift, TLAS tests
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05o}
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_inflight.py -m gpu -q -rs --timeout 150 --timeout-method thread -k "long_motion or moving_instances or materials or in_flight or many_inst or tlas" > gpurun_out/${T}_tests.log 2>&1; rc=$?

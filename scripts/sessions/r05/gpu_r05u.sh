@@ -2,7 +2,7 @@
 # round-5 session u: the whole GPU suite on the library with the radius-64 two-launch instance-BVH build; drift at
 # the default (blocking commit) and pipelined; the default bench line
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05u}
 bash scripts/gpu_suite.sh $T || exit $?

@@ -2,7 +2,7 @@
 # round-5 session v: the instance-BVH build launches holding their CU's whole LDS (PRT_TLAS_FULL_CU 1 / 0), drift;
 # kernel timeline of 40 drifting frames
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05v}
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -rs --timeout 150 --timeout-method thread -k "long_motion or moving_instances or materials" > gpurun_out/${T}_tlas_tests.log 2>&1 || { tail -30 gpurun_out/${T}_tlas_tests.log; exit 1; }

@@ -2,7 +2,7 @@
 # round-5 session w: the resolve kernels load the ending paths' stack records and s1 up front (A: this tree; B:
 # ab/B, built with -DPRT_RES_AHEAD=0); the whole GPU suite on A, then interleaved bench / world-8 share A/B
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05w}
 bash scripts/gpu_suite.sh $T || exit $?

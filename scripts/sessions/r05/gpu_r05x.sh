@@ -2,7 +2,7 @@
 # round-5 session x: collapse octant assignment from precomputed centroid offsets, workgroup-scope DP table in the
 # single-workgroup build; the whole GPU suite, phase clock, drift
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05x}
 bash scripts/gpu_suite.sh $T || exit $?

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # round-5 session y: single-workgroup build PLOC radius 32 / 48 / 64 (phase clock, drift twice each, interleaved)
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05y}
 for r in 32 48 64; do

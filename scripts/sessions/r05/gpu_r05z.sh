@@ -2,7 +2,7 @@
 # round-5 session z: are the slow traversal launches of the drift the rebuild's?  Kernel traces of 40 drifting
 # frames with the default device rebuild and with a host SAH build per update, and of 40 static frames
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 T=${1:-r05z}
 for m in default host; do
