@@ -233,6 +233,28 @@ class Renderer {
     frame_ += (uint32_t)frames;
   }
 
+  // Tick with the outputs in device memory (float4 average, 0x00RRGGBB) and no stats: no host wait.  With frames
+  // in flight (SetFramesInFlight(n > 1), ABI 9) consecutive calls overlap on internal streams and a call's outputs
+  // are complete in the context stream's order once n - 1 more calls are made, or after Finish(); the
+  // accumulation stays in call order, so the images equal Tick()'s
+  void TickDevice(float* avg_dev, uint32_t* rgb8_dev, int32_t frames = 1) {
+    prt_render_params p{};
+    p.width = width_;
+    p.height = height_;
+    p.spp = frames * (AA ? 2 : 1);
+    p.bounces = bounces;
+    p.flags = Flags();
+    p.render_mode = (int32_t)renderingMode;
+    p.frame_index = frame_;
+    p.seed = 0;
+    const prt_postfx pf = camera.PostFx(isPostProcessed);
+    check(prt_set_postfx(ctx_, &pf));
+    check(prt_render(ctx_, &p, avg_dev, rgb8_dev, 1u, nullptr));
+    frame_ += (uint32_t)frames;
+  }
+  void SetFramesInFlight(int32_t n) { check(prt_set_frames_in_flight(ctx_, n)); }
+  void Finish() { check(prt_finish(ctx_)); }  // the frames in flight joined into the context stream
+
   // Camera::HandleInput returned true: new screen plane, accumulator memset (Core/Renderer.cpp:147)
   void CameraMoved() {
     const prt_camera c = camera.Plane();
