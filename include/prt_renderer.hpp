@@ -249,7 +249,7 @@ class Renderer {
     p.seed = 0;
     const prt_postfx pf = camera.PostFx(isPostProcessed);
     check(prt_set_postfx(ctx_, &pf));
-    check(prt_render(ctx_, &p, avg_dev, rgb8_dev, 1u, nullptr));
+    check(prt_render(ctx_, &p, avg_dev, rgb8_dev, PRT_OUT_DEVICE, nullptr));
     frame_ += (uint32_t)frames;
   }
   void SetFramesInFlight(int32_t n) { check(prt_set_frames_in_flight(ctx_, n)); }
