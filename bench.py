@@ -8,7 +8,8 @@ normal map, skybox, lighted, stochastic NEE).  A step = one prt_render of the fu
 (2 reference frames x 2 AA paths per pixel), inputs resident in HBM.  Two frames are in flight by default
 (prt_set_frames_in_flight): step k+1's wavefront chain overlaps step k's on the GPU, the accumulation (and the
 sharded gather) stay in step order, and every step's image is bit-identical to rendering them one at a time; the
-K timed steps are all complete when the closing synchronize returns.
+K timed steps are all complete when the closing synchronize returns.  Before them: the W warmup steps and, untimed
+as well, as many more as fill --warmup-s (0.5 s) of frames, the same count on every rank (config.warmup_steps_run).
 
 Mrays/s = (closest-hit segments + any-hit shadow rays) / time, counted on the device.
 --gpus N > 1: one process per GPU.  Run without WORLD_SIZE in the environment, bench.py starts the N ranks
@@ -211,6 +212,9 @@ def main():
                     help="frames in flight (prt_set_frames_in_flight; default 2 on one GPU, 4 on several): "
                          "consecutive frames' wavefront chains overlap on internal streams; accumulation and "
                          "gathers stay in call order, the images are bit-identical to 1")
+    ap.add_argument("--warmup-s", type=float, default=0.5,
+                    help="untimed warmup of at least this many seconds of frames besides the W steps (the same step "
+                         "count on every rank): a few milliseconds of frames leave the GPU below its clocks")
     ap.add_argument("--host-out", action="store_true",
                     help="outputs (avg + rgb8) to host memory every step: the PCIe-inclusive rate (not the contract value)")
     args = ap.parse_args()
@@ -282,8 +286,25 @@ def main():
                                   rgb8=rgb.data_ptr(), device_out=True, stats=stats)
         return st
 
-    for i in range(args.warmup):
+    # Warmup: the W steps asked for, then (untimed too) as many more as fill --warmup-s seconds at the rate the W
+    # steps ran, the same count on every rank (the frames' gathers are collective).  Two frames are a few ms at
+    # world 8, too short for the GPU to reach its clocks: C4's world-8 share measured 1.34-1.40 ms per frame cold
+    # against 1.14-1.17 ms warm (profiles/r05_warmup.txt)
+    torch.cuda.synchronize()
+    n0 = max(1, args.warmup)  # (at least one step, to time the rate)
+    tw = time.perf_counter()
+    for i in range(n0):
         step(i, False)
+    torch.cuda.synchronize()
+    per = (time.perf_counter() - tw) / n0
+    extra = int(min(2000, max(0.0, args.warmup_s - per * n0) / max(per, 1e-4))) if args.warmup_s > 0 else 0
+    if dist:
+        e = torch.tensor([extra], dtype=torch.int64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        extra = int(e.item())
+    for i in range(n0, n0 + extra):
+        step(i, False)
+    warm_steps = n0 + extra
     ctx.ray_totals(reset=True)  # waits for the warmup frames
     if dist:
         dist.barrier()
@@ -293,7 +314,7 @@ def main():
     # event timers of the traversal kernel (stats=True; its host wait coincides with the closing synchronize).
     t0 = time.perf_counter()
     for i in range(args.steps):
-        st = step(args.warmup + i, i == args.steps - 1)
+        st = step(warm_steps + i, i == args.steps - 1)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -405,7 +426,8 @@ def main():
                        "parallelism": f"pixel-tile{args.tile} x{world} (RCCL gather in prt_render)" if world > 1
                        else "single-gpu",
                        "outputs": "host memory (PCIe-inclusive)" if args.host_out else "device (HBM-resident)",
-                       "frames_in_flight": args.inflight,
+                       "frames_in_flight": args.inflight, "warmup_steps_run": warm_steps,
+                       "warmup_min_s": args.warmup_s,
                        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default (4)"),
                        "rays_per_step": int(rays / args.steps), "segments_per_step": int(seg / args.steps),
                        "shadow_per_step": int(shadow / args.steps),

@@ -29,11 +29,18 @@ ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(
 ctx.set_frames_in_flight(INFLIGHT)
 base = None
 WORLDS = [int(a) for a in args] or [1, 2, 4, 8]
+WARM_S = float(os.environ.get("PRT_RANK_WARM_S", "0.5"))  # untimed frames first (clocks; bench.py --warmup-s)
 for world in WORLDS:
     per = ctx.tile_buffer_pixels(W, H, 32, world)
     tiles = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
     for i in range(1 if C5 else 2):
         ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i)
+    torch.cuda.synchronize()
+    tw = time.perf_counter()
+    while time.perf_counter() - tw < WARM_S:  # (a share of a few ms otherwise runs below the GPU's clocks)
+        for i in range(4):
+            ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i)
+        torch.cuda.synchronize()
     ctx.ray_totals(reset=True)
     torch.cuda.synchronize()
     n = 2 if C5 else 8
