@@ -182,7 +182,10 @@ int prt_finish(prt_ctx* ctx);
 /* ---- scene (Scene / Model / Camera state) ---- */
 int prt_set_textures(prt_ctx* ctx, const prt_texture* textures, int32_t count);
 int prt_set_meshes(prt_ctx* ctx, const prt_mesh* meshes, int32_t count);
-/* transforms: 16*count floats, row-major BLASInstance::transform; mesh_index: count */
+/* transforms: 16*count floats, row-major BLASInstance::transform; mesh_index: count.  Above 64 instances the rays
+ * walk an instance BVH, rebuilt for every call up to 4,096 instances (a host SAH build, as the reference's per-frame
+ * BVH::Build, uploaded in stream order: no wait on the GPU), refitted on the device and rebuilt on its node-area
+ * trigger above that (PRT_TLAS_SMALL=1 selects the single-workgroup device build) */
 int prt_set_instances(prt_ctx* ctx, const float* transforms, const uint32_t* mesh_index, int32_t count);
 int prt_set_lights(prt_ctx* ctx, const prt_lights* lights);
 /* kinds: one PRT_MAT_* per instance (count = the instance count), or count 0 = all textured.  Reset by
