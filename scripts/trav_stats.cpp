@@ -49,6 +49,7 @@ uint32_t order_mask(uint32_t m, uint32_t oct) {
 
 // one lane's traversal as a list of iterations: tri tests done in each node visit
 struct Trace { std::vector<uint8_t> tris_per_visit; int pushes = 0; float t = kFar; };
+std::vector<uint64_t> g_visits;  // visits per node index (--hot: which nodes an LDS node cache would serve)
 
 Trace traverse(const BuiltBlas8& B, V O, V D, float tmax, bool any) {
   Trace tr;
@@ -59,6 +60,7 @@ Trace traverse(const BuiltBlas8& B, V O, V D, float tmax, bool any) {
   float ht = tmax;
   while (true) {
     const Node8& n = B.nodes[node];
+    if (!g_visits.empty()) g_visits[node]++;
     const float sc[3] = {std::ldexp(1.0f, (int)n.ex - 127), std::ldexp(1.0f, (int)n.ey - 127),
                          std::ldexp(1.0f, (int)n.ez - 127)};
     const float ax = (n.px - O.x) * rD.x, ay = (n.py - O.y) * rD.y, az = (n.pz - O.z) * rD.z;
@@ -214,6 +216,7 @@ int main(int argc, char** argv) {
   while ((n = std::fread(buf, 4, 4096, f)) > 0) rays.insert(rays.end(), buf, buf + n);
   std::fclose(f);
   const size_t R = rays.size() / 8;
+  if (argc > 3 && std::strcmp(argv[3], "--hot") == 0) g_visits.assign(B.nodes.size(), 0);
   for (int kind = 0; kind < 2; kind++) {
     std::vector<Trace> tr;
     double visits = 0, tris = 0, pushes = 0;
@@ -230,6 +233,19 @@ int main(int argc, char** argv) {
                 tr.size(), visits / tr.size(), tris / tr.size(), pushes / tr.size());
     std::fprintf(stderr, "{\"kind\": \"%s\", \"rays\": %zu, \"node_visits\": %.4f, \"tri_tests\": %.4f}\n",
                  kind ? "anyhit" : "closest", tr.size(), visits / tr.size(), tris / tr.size());
+    if (argc > 3 && std::strcmp(argv[3], "--hot") == 0) {  // share of node visits to node indices < K (BFS
+      // order: the top tree levels) and to the K most visited nodes
+      std::vector<uint64_t> hot = g_visits;
+      std::sort(hot.begin(), hot.end(), [](uint64_t a, uint64_t b) { return a > b; });
+      double tot = 0;
+      for (uint64_t v : g_visits) tot += (double)v;
+      for (size_t K : {1, 9, 16, 32, 48, 64, 73, 96, 128, 256, 512}) {
+        double a = 0, b = 0;
+        for (size_t i = 0; i < K && i < g_visits.size(); i++) { a += (double)g_visits[i]; b += (double)hot[i]; }
+        std::printf("    K=%4zu: first-K share %.4f  hottest-K share %.4f\n", K, a / tot, b / tot);
+      }
+      std::fill(g_visits.begin(), g_visits.end(), 0);
+    }
     if (argc > 3 && std::strcmp(argv[3], "--dist") == 0) {  // per-ray sequential steps: the launch tail
       std::vector<int> st;
       for (const Trace& t : tr) {
