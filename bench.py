@@ -215,6 +215,9 @@ def main():
     ap.add_argument("--warmup-s", type=float, default=0.5,
                     help="untimed warmup of at least this many seconds of frames besides the W steps (the same step "
                          "count on every rank): a few milliseconds of frames leave the GPU below its clocks")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="opt-in: GPU_MAX_HW_QUEUES for this process (set before HIP starts); default: the runtime's "
+                         "own setting (4 on the GPU box), which is what the library's users get")
     ap.add_argument("--host-out", action="store_true",
                     help="outputs (avg + rgb8) to host memory every step: the PCIe-inclusive rate (not the contract value)")
     args = ap.parse_args()
@@ -228,8 +231,8 @@ def main():
     # runtime is given 8 queues (set before anything initialises HIP)
     if args.inflight is None:
         args.inflight = 4 if args.gpus >= 2 else 2
-    if args.inflight > 2 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    if args.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
 
     import torch
     import prt

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PRT_ABI_VERSION 9
+#define PRT_ABI_VERSION 10
 
 typedef enum {
     PRT_OK = 0,
@@ -305,6 +305,29 @@ int prt_intersect(prt_ctx* ctx, int32_t n, const float* origins, const float* di
                   prt_hit* hits);
 int prt_occluded(prt_ctx* ctx, int32_t n, const float* origins, const float* dirs, const float* tmax,
                  int32_t* occluded);
+
+/* ---- shading-function probe (ABI 10): the device's own BRDF functions (the ones the shading kernels inline) on
+ * n host records, for known-answer tests of the BRDF restatement (Core/BRDF.cpp).  Record k: in[24 k ..], out[8 k ..].
+ *   EVAL         BRDF::evalCombinedBRDF (:439-452)     in N[0..2] L[3..5] V[6..8] material[9..16]    out rgb[0..2]
+ *   PROBABILITY  BRDF::getBrdfProbability (:504-526)   in N, V, material                          out p[0]
+ *   INDIRECT     BRDF::evalIndirectCombinedBRDF (:454-502, weight in = 1)  in N, V, material, u[17..18],
+ *                type[19] (1 diffuse, 2 specular)      out ok[0] dir[1..3] weight[4..6]
+ *   GGX_D        ggxD (:218-222)                       in alphaSquared[0] NdotH[1]                out D[0]
+ *   SMITH_G2     Smith_G2 height-correlated, divided by the denominator (:189-208)
+ *                                                      in alphaSquared[0] NdotL[1] NdotV[2]       out G2[0]
+ *   FRESNEL      evalFresnel Schlick (:84-87)          in f0[0..2] f90[3] NdotS[4]                out F[0..2]
+ *   SHADOWED_F90 shadowedF90 (:100-104)                in F0[0..2]                                out f90[0]
+ *   VNDF         sampleGGXVNDF (:224-269)              in Ve[0..2] alphaX[3] alphaY[4] u[5..6]    out H[0..2]
+ * material = base rgb, metalness, emissive rgb, roughness (MaterialProperties, Core/BRDF.h:165-176). */
+#define PRT_PROBE_EVAL 0
+#define PRT_PROBE_PROBABILITY 1
+#define PRT_PROBE_INDIRECT 2
+#define PRT_PROBE_GGX_D 3
+#define PRT_PROBE_SMITH_G2 4
+#define PRT_PROBE_FRESNEL 5
+#define PRT_PROBE_SHADOWED_F90 6
+#define PRT_PROBE_VNDF 7
+int prt_brdf_probe(prt_ctx* ctx, int32_t op, int32_t n, const float* in, float* out);
 
 /* ---- BLAS builder (the reference builds on the CPU, Core/tiny_bvh.h:1968-2284,3706-3781)
  * HOST_SAH (default): binned SAH binary tree + SAH-optimal 8-wide collapse on the host.

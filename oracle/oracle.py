@@ -80,6 +80,7 @@ def lib():
         L.orc_init_seed.restype = C.c_uint32
         L.orc_rng_floats.argtypes = [C.c_uint32, C.c_int32, C.c_void_p]
         L.orc_eval_combined_brdf.argtypes = [C.c_void_p] * 5
+        L.orc_brdf_probe.argtypes = [C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         L.orc_brdf_probability.argtypes = [C.c_void_p] * 3
         L.orc_brdf_probability.restype = C.c_float
         L.orc_eval_indirect.argtypes = [C.c_void_p] * 4 + [C.c_int32, C.c_void_p, C.c_void_p]
@@ -365,6 +366,15 @@ def eval_combined_brdf(N, L, V, mat8):
     lib().orc_eval_combined_brdf(f32(N).ctypes.data, f32(L).ctypes.data, f32(V).ctypes.data, f32(mat8).ctypes.data,
                                  o.ctypes.data)
     return o
+
+
+def brdf_probe(op, records):
+    """orc_brdf_probe: the restated BRDF functions on float32 [n, 24] records -> [n, 8] (include/prt.h PRT_PROBE_*)."""
+    rec = np.ascontiguousarray(records, np.float32).reshape(-1, 24)
+    out = np.zeros((rec.shape[0], 8), np.float32)
+    if lib().orc_brdf_probe(int(op), rec.shape[0], rec.ctypes.data, out.ctypes.data) != 0:
+        raise ValueError(f"bad probe op {op}")
+    return out
 
 
 def brdf_probability(mat8, V, N):

@@ -1320,6 +1320,39 @@ int orc_eval_indirect(const float* u2, const float* N, const float* V, const flo
     dir[0] = d.x; dir[1] = d.y; dir[2] = d.z; w[0] = wt.x; w[1] = wt.y; w[2] = wt.z;
     return ok;
 }
+/* the device's prt_brdf_probe on the host (include/prt.h PRT_PROBE_*): record k = in[24 k ..] -> out[8 k ..] */
+int orc_brdf_probe(int32_t op, int32_t n, const float* in, float* out) {
+    for (int32_t i = 0; i < n; i++) {
+        const float* a = in + 24 * (size_t)i;
+        float* o = out + 8 * (size_t)i;
+        for (int k = 0; k < 8; k++) o[k] = 0.0f;
+        f3 N = v3(a[0], a[1], a[2]), L = v3(a[3], a[4], a[5]), V = v3(a[6], a[7], a[8]);
+        mat_t m = mat_from8(a + 9);
+        switch (op) {
+        case 0: { f3 r = eval_combined(N, L, V, &m); o[0] = r.x; o[1] = r.y; o[2] = r.z; break; }
+        case 1: o[0] = brdf_probability(&m, V, N); break;
+        case 2: {
+            f2 u = {a[17], a[18]};
+            f3 d = v3(0, 0, 0), w = v3(1.0f, 1.0f, 1.0f);
+            int ok = eval_indirect(u, N, V, &m, (int)a[19], &d, &w);
+            o[0] = ok ? 1.0f : 0.0f; o[1] = d.x; o[2] = d.y; o[3] = d.z; o[4] = w.x; o[5] = w.y; o[6] = w.z;
+            break;
+        }
+        case 3: o[0] = ggx_d(a[0], a[1]); break;
+        case 4: o[0] = g2_lagarde(a[0], a[1], a[2]); break;
+        case 5: { f3 F = fresnel(v3(a[0], a[1], a[2]), a[3], a[4]); o[0] = F.x; o[1] = F.y; o[2] = F.z; break; }
+        case 6: o[0] = shadowed_f90(v3(a[0], a[1], a[2])); break;
+        case 7: {
+            f2 u = {a[5], a[6]};
+            f3 H = sample_vndf(v3(a[0], a[1], a[2]), a[3], a[4], u);
+            o[0] = H.x; o[1] = H.y; o[2] = H.z;
+            break;
+        }
+        default: return -1;
+        }
+    }
+    return 0;
+}
 void orc_sample_sky(orc_scene* s, const float* D, float* o) {
     f3 r = sample_sky(s, v3(D[0], D[1], D[2]));
     o[0] = r.x; o[1] = r.y; o[2] = r.z;

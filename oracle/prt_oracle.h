@@ -133,6 +133,7 @@ uint32_t orc_init_seed(uint32_t base);
 void orc_rng_floats(uint32_t seed, int32_t n, float* out);
 void orc_eval_combined_brdf(const float* N, const float* L, const float* V, const float* mat8, float* out3);
 float orc_brdf_probability(const float* mat8, const float* V, const float* N);
+int orc_brdf_probe(int32_t op, int32_t n, const float* in, float* out);  /* include/prt.h prt_brdf_probe records */
 int orc_eval_indirect(const float* u2, const float* N, const float* V, const float* mat8, int32_t type,
                       float* dir3, float* weight3);
 void orc_sample_sky(orc_scene* s, const float* D, float* out3);

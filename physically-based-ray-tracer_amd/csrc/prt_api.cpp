@@ -1574,8 +1574,12 @@ int prt_set_frames_in_flight(prt_ctx* c, int32_t n) {
   PRT_JOIN(c);
   HIP_TRY(hipSetDevice(c->device));
   if (n > 1) {
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    const char* ep = std::getenv("PRT_FLIGHT_PRIO");  // A/B (round 6): normal / high / low
+    const int prio = !ep ? 0 : (std::strcmp(ep, "high") == 0 ? hi : (std::strcmp(ep, "low") == 0 ? lo : 0));
     for (Flight& f : c->fl) {
-      if (!f.stream) HIP_TRY(hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking));
+      if (!f.stream) HIP_TRY(hipStreamCreateWithPriority(&f.stream, hipStreamNonBlocking, prio));
       if (!f.done) HIP_TRY(hipEventCreateWithFlags(&f.done, hipEventDisableTiming));
     }
     if (!c->fl_fork) HIP_TRY(hipEventCreateWithFlags(&c->fl_fork, hipEventDisableTiming));
@@ -2202,6 +2206,22 @@ int prt_intersect(prt_ctx* c, int32_t n, const float* O, const float* D, const f
 }
 int prt_occluded(prt_ctx* c, int32_t n, const float* O, const float* D, const float* tmax, int32_t* occ) {
   return ray_query(c, n, O, D, tmax, occ, true);
+}
+
+int prt_brdf_probe(prt_ctx* c, int32_t op, int32_t n, const float* in, float* out) {
+  if (!c || n < 0 || (n > 0 && (!in || !out)) || op < PRT_PROBE_EVAL || op > PRT_PROBE_VNDF)
+    return fail(PRT_ERR_INVALID_ARGUMENT, "bad BRDF probe arguments");
+  if (n == 0) return PRT_OK;
+  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
+  HIP_TRY(hipSetDevice(c->device));
+  DevBuf din, dout;
+  HIP_TRY(upload(din, in, 24ull * 4 * (size_t)n));
+  HIP_TRY(dout.ensure(8ull * 4 * (size_t)n));
+  hipError_t e = launch_brdf_probe(c->stream, op, n, din.as<float>(), dout.as<float>());
+  if (e == hipSuccess) e = hipMemcpyAsync(out, dout.p, 8ull * 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return fail(PRT_ERR_HIP, std::string("BRDF probe: ") + hipGetErrorString(e));
+  return PRT_OK;
 }
 
 int prt_shard_unique_id(uint8_t id[PRT_SHARD_ID_BYTES]) {

@@ -120,5 +120,7 @@ hipError_t launch_intersect(const LaunchCfg& c, const SceneDev& S, int32_t n, co
                             const float* tmax, HitOut* out);
 hipError_t launch_occluded(const LaunchCfg& c, const SceneDev& S, int32_t n, const float* O, const float* D,
                            const float* tmax, int32_t* out);
+// prt_brdf_probe: n records of 24 floats in, 8 out (include/prt.h PRT_PROBE_*)
+hipError_t launch_brdf_probe(hipStream_t s, int32_t op, int32_t n, const float* in, float* out);
 
 }  // namespace prt

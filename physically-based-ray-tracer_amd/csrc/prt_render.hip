@@ -280,6 +280,70 @@ hipError_t launch_occluded(const LaunchCfg& c, const SceneDev& S, int32_t n, con
   return hipGetLastError();
 }
 
+// ---- BRDF probe (prt_brdf_probe): the shading kernels' own device functions (prt_shade.h) on one record per thread
+__global__ void __launch_bounds__(kBlock) k_brdf_probe(int32_t op, int32_t n, const float* __restrict__ in,
+                                                       float* __restrict__ out) {
+  const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  const float* a = in + 24 * (size_t)i;
+  float* o = out + 8 * (size_t)i;
+  for (int k = 0; k < 8; k++) o[k] = 0.0f;
+  const V3 N = v3(a[0], a[1], a[2]), L = v3(a[3], a[4], a[5]), V = v3(a[6], a[7], a[8]);
+  Material m;
+  m.base = v3(a[9], a[10], a[11]);
+  m.metal = a[12];
+  m.emis = v3(a[13], a[14], a[15]);
+  m.rough = a[16];
+  switch (op) {
+    case 0: {  // PRT_PROBE_EVAL
+      const V3 r = eval_combined_brdf(N, L, V, m);
+      o[0] = r.x; o[1] = r.y; o[2] = r.z;
+      break;
+    }
+    case 1:  // PRT_PROBE_PROBABILITY
+      o[0] = brdf_probability(m, V, N);
+      break;
+    case 2: {  // PRT_PROBE_INDIRECT
+      V3 dir = v3(0.0f, 0.0f, 0.0f), w = v3(1.0f, 1.0f, 1.0f);
+      V2 u;
+      u.x = a[17]; u.y = a[18];
+      const bool ok = eval_indirect_brdf(u, N, V, m, (int)a[19], dir, w);
+      o[0] = ok ? 1.0f : 0.0f;
+      o[1] = dir.x; o[2] = dir.y; o[3] = dir.z;
+      o[4] = w.x; o[5] = w.y; o[6] = w.z;
+      break;
+    }
+    case 3:  // PRT_PROBE_GGX_D
+      o[0] = ggx_d(a[0], a[1]);
+      break;
+    case 4:  // PRT_PROBE_SMITH_G2
+      o[0] = smith_g2_lagarde(a[0], a[1], a[2]);
+      break;
+    case 5: {  // PRT_PROBE_FRESNEL
+      const V3 F = fresnel_schlick(v3(a[0], a[1], a[2]), a[3], a[4]);
+      o[0] = F.x; o[1] = F.y; o[2] = F.z;
+      break;
+    }
+    case 6:  // PRT_PROBE_SHADOWED_F90
+      o[0] = shadowed_f90(v3(a[0], a[1], a[2]));
+      break;
+    case 7: {  // PRT_PROBE_VNDF
+      V2 u;
+      u.x = a[5]; u.y = a[6];
+      const V3 H = sample_ggx_vndf(v3(a[0], a[1], a[2]), a[3], a[4], u);
+      o[0] = H.x; o[1] = H.y; o[2] = H.z;
+      break;
+    }
+    default:
+      break;
+  }
+}
+hipError_t launch_brdf_probe(hipStream_t s, int32_t op, int32_t n, const float* in, float* out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_brdf_probe, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, op, n, in, out);
+  return hipGetLastError();
+}
+
 // ---- instance refit (BLASInstance::Update on the device): one thread per instance
 __global__ void k_refit(const InstSrc* __restrict__ src, int32_t n, InstDev* __restrict__ out) {
   const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);

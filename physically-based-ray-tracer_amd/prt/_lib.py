@@ -6,10 +6,11 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIBPATH = os.path.join(HERE, "libprt.so")
+# PRT_LIBPATH: another build of the library (A/B runs of two builds in one session; scripts/ab_bench.sh)
+LIBPATH = os.environ.get("PRT_LIBPATH") or os.path.join(HERE, "libprt.so")
 
 PRT_OK = 0
-ABI_VERSION = 9  # PRT_ABI_VERSION of the include/prt.h these structs mirror
+ABI_VERSION = 10  # PRT_ABI_VERSION of the include/prt.h these structs mirror
 FLAG_AA, FLAG_ACCUMULATE, FLAG_GAMMA, FLAG_NORMALMAP, FLAG_SKYBOX, FLAG_LIGHTED, FLAG_STOCHASTIC = (1 << i for i in range(7))
 FLAGS_DEFAULT = 0x7F
 OUT_DEVICE = 1
@@ -24,7 +25,7 @@ EXPORTS = [
     "prt_set_textures", "prt_set_meshes", "prt_set_instances", "prt_set_lights", "prt_set_sky", "prt_set_camera",
     "prt_camera_look_at", "prt_postfx_preset", "prt_set_postfx", "prt_render", "prt_reset_accumulation", "prt_tile_buffer_pixels", "prt_tile_pixel_map",
     "prt_render_tiles",
-    "prt_untile", "prt_trace_primary", "prt_intersect", "prt_occluded", "prt_get_scene_info", "prt_set_bvh_builder",
+    "prt_untile", "prt_trace_primary", "prt_intersect", "prt_occluded", "prt_brdf_probe", "prt_get_scene_info", "prt_set_bvh_builder",
     "prt_set_instance_materials", "prt_set_area_lights", "prt_shard_unique_id", "prt_shard_init_rccl",
     "prt_shard_attach_rccl", "prt_create_group", "prt_get_shard_info", "prt_accumulation_bytes",
     "prt_save_accumulation", "prt_load_accumulation", "prt_ray_totals", "prt_set_frames_in_flight", "prt_finish",
@@ -154,6 +155,7 @@ def load():
         "prt_trace_primary": ([vp, i32, i32, vp, u32, C.POINTER(Stats)], C.c_int),
         "prt_intersect": ([vp, i32, vp, vp, vp, vp], C.c_int),
         "prt_occluded": ([vp, i32, vp, vp, vp, vp], C.c_int),
+        "prt_brdf_probe": ([vp, i32, i32, vp, vp], C.c_int),
         "prt_get_scene_info": ([vp, C.POINTER(SceneInfo)], C.c_int),
         "prt_set_bvh_builder": ([vp, i32], C.c_int),
         "prt_set_instance_materials": ([vp, vp, i32], C.c_int),

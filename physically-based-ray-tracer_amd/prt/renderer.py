@@ -321,6 +321,13 @@ class Context:
         check(self.L.prt_occluded(self.h, O.shape[0], O.ctypes.data, D.ctypes.data, tm.ctypes.data, occ.ctypes.data))
         return occ
 
+    def brdf_probe(self, op, records):
+        """prt_brdf_probe: the device BRDF functions on n records (float32 [n, 24] in, [n, 8] out; include/prt.h)."""
+        rec = np.ascontiguousarray(records, np.float32).reshape(-1, 24)
+        out = np.zeros((rec.shape[0], 8), np.float32)
+        check(self.L.prt_brdf_probe(self.h, int(op), rec.shape[0], rec.ctypes.data, out.ctypes.data))
+        return out
+
     def tile_buffer_pixels(self, width, height, tile, world):
         n = C.c_int64(0)
         check(self.L.prt_tile_buffer_pixels(width, height, tile, world, C.byref(n)))

@@ -20,7 +20,7 @@ def test_header_symbols_exported():
     assert declared == set(_lib.EXPORTS)
     for name in declared:
         assert hasattr(L, name), name
-    assert L.prt_abi_version() == _lib.ABI_VERSION == 9
+    assert L.prt_abi_version() == _lib.ABI_VERSION == 10
 
 
 def test_ingest_header_symbols_exported():
