@@ -184,6 +184,12 @@ def cpu_baseline(sd, W, H, spp, bounces):
     return out
 
 
+def default_inflight(gpus):
+    """Frames in flight bench.py keeps by default (prt_set_frames_in_flight; profiles/r06_rank_shares.txt): 2 on one
+    GPU, 4 on several (each chain on half-size grids)."""
+    return 4 if gpus >= 2 else 2
+
+
 def spawn_ranks(n):
     """--gpus N without WORLD_SIZE: start N ranks of this script under torch.distributed.run (a child process;
     nothing here has touched a GPU) and return their exit status."""
@@ -208,7 +214,7 @@ def main():
                     help="c4 = the metric's workload (default); c5 = C4 + a quad area light with MIS at 4K, 16 spp, depth 8")
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=None, choices=[1, 2, 3, 4],
+    ap.add_argument("--inflight", type=int, default=None, choices=range(1, 9),
                     help="frames in flight (prt_set_frames_in_flight; default 2 on one GPU, 4 on several): "
                          "consecutive frames' wavefront chains overlap on internal streams; accumulation and "
                          "gathers stay in call order, the images are bit-identical to 1")
@@ -230,7 +236,7 @@ def main():
     # chains than free queues two chains share one and serialise behind each other's waits, so above 2 chains the
     # runtime is given 8 queues (set before anything initialises HIP)
     if args.inflight is None:
-        args.inflight = 4 if args.gpus >= 2 else 2
+        args.inflight = default_inflight(args.gpus)
     if args.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
 

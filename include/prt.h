@@ -169,7 +169,7 @@ int prt_destroy(prt_ctx* ctx);
 int prt_set_stream(prt_ctx* ctx, void* hip_stream);
 /* Frames in flight (ABI 9; the reference's Renderer::Tick renders one frame per call, Core/Renderer.cpp:43-141).
  * n = 1 (default): a prt_render call's work is complete in the context stream's order when the call returns.
- * n = 2..4: a prt_render with device outputs (or a prt_render_tiles) and no stats enqueues its frame on one of n
+ * n = 2..8 (ABI 10; 2..4 in ABI 9): a prt_render with device outputs (or a prt_render_tiles) and no stats enqueues its frame on one of n
  * internal streams, forked from the context stream, so its wavefront chain overlaps those of the previous n - 1
  * calls; the accumulation (and a sharded frame's gather and untile) still run in call order, so the results are
  * bit-identical to n = 1.  A call's outputs are complete in the context stream's order once n - 1 more render

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/prt.h"
@@ -92,7 +93,7 @@ struct ItemGroup {
 // a frame in flight (prt_set_frames_in_flight): the wavefront chain of one call on its own stream.  Slot 0 uses the
 // context's own wavefront state and frame buffer, the others their own; done = the call's last work (the
 // accumulation, and for a sharded frame its gather and untile), which the next call's accumulation waits for
-constexpr int kMaxFlights = 4;
+constexpr int kMaxFlights = 8;
 struct Flight {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
@@ -237,12 +238,63 @@ int join_flights(prt_ctx* c) {
   return PRT_OK;
 }
 
+// RCCL calls and waits that involve the peers are bounded (failure detection): a rank whose peers never
+// arrive -- at communicator set-up or in a frame's ncclGather -- fails after PRT_RCCL_TIMEOUT_S seconds (default
+// 120) with the communicator aborted, instead of hanging in the call or in a later stream wait
+double rccl_timeout_s() {
+  const char* e = std::getenv("PRT_RCCL_TIMEOUT_S");
+  const double v = e ? std::atof(e) : 120.0;
+  return v > 0.0 ? v : 120.0;
+}
+// a non-blocking communicator's call returned ncclInProgress: poll its async state until it settles (bounded)
+ncclResult_t rccl_settle(const Rccl* R, ncclComm_t comm, ncclResult_t r) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const double lim = rccl_timeout_s();
+  while (r == ncclInProgress) {
+    ncclResult_t st = ncclSuccess;
+    if (R->CommGetAsyncError(comm, &st) != ncclSuccess) return ncclSystemError;
+    r = st;
+    if (r != ncclInProgress) break;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > lim) return ncclInProgress;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  return r;
+}
+// wait for `s` on an RCCL-sharded context: stream completion, the communicator's async error, or the time limit
+// (then the communicator is aborted, which also ends its kernels, and the context cannot shard any more)
+int rccl_wait(prt_ctx* c, hipStream_t s, const char* what) {
+  const Rccl* R = rccl(nullptr);
+  const auto t0 = std::chrono::steady_clock::now();
+  const double lim = rccl_timeout_s();
+  while (true) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) break;
+    if (e != hipErrorNotReady) return fail(PRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    ncclResult_t ae = ncclSuccess;
+    const bool bad = R && c->comm && R->CommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess &&
+                     ae != ncclInProgress;
+    const bool late = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > lim;
+    if (bad || late) {
+      if (R && c->comm && R->CommAbort) (void)R->CommAbort(c->comm);
+      c->comm = nullptr;  // unusable from here on: later sharded frames fail up front
+      (void)hipStreamSynchronize(s);  // the aborted collective's kernels end
+      return fail(PRT_ERR_HIP, std::string(what) + (bad ? std::string(": RCCL communicator error: ") + R->GetErrorString(ae)
+                                                         : ": the RCCL collective did not complete within the time limit "
+                                                           "(PRT_RCCL_TIMEOUT_S); communicator aborted"));
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+  (void)hipGetLastError();  // hipStreamQuery's hipErrorNotReady
+  return PRT_OK;
+}
+
 // finish the frames queued on the context stream (and the frames in flight) before a setter overwrites (or frees)
 // resident buffers
 int drain(prt_ctx* c) {
   const int rc = join_flights(c);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(c->device));
+  if (c->sh_kind == 1 && c->comm) return rccl_wait(c, c->stream, "waiting for the context's frames");
   HIP_TRY(hipStreamSynchronize(c->stream));
   return PRT_OK;
 }
@@ -974,7 +1026,7 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
   if (fl) {
     const char* e = std::getenv("PRT_FLIGHT_GRID");
     const int v = e ? std::atoi(e) : (c->inflight >= 4 ? 2 : 1);
-    Gw = v >= 4 ? 4u : (v >= 2 ? 2u : 1u);
+    Gw = v >= 8 ? 8u : (v >= 4 ? 4u : (v >= 2 ? 2u : 1u));
   }
   // The single-workgroup instance-BVH build (tlas_small, one 1,024-thread workgroup with ~144 KB of LDS) can only
   // start on a CU the traversal waves have left; the traversal launches that follow must then not need that CU, or
@@ -1276,7 +1328,7 @@ void post_zero_gather(prt_ctx* c, size_t per) {
     recv = pick(c->gathered, rb, sendb);
   }
   if (send && (!root || recv) && hipMemsetAsync(send, 0, sb, c->stream) == hipSuccess) {
-    (void)R->Gather(send, recv, per * 4, ncclFloat32, 0, c->comm, c->stream);
+    (void)rccl_settle(R, c->comm, R->Gather(send, recv, per * 4, ncclFloat32, 0, c->comm, c->stream));
   } else if (R->CommAbort) {
     (void)R->CommAbort(c->comm);
     c->comm = nullptr;  // unusable from here on: later sharded frames fail up front
@@ -1369,7 +1421,7 @@ int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint
   }
   float4* g = root ? c->gathered.as<float4>() : nullptr;
   if (coll) {
-    const ncclResult_t r = R->Gather(c->shtiles.p, g, per * 4, ncclFloat32, 0, c->comm, st);
+    const ncclResult_t r = rccl_settle(R, c->comm, R->Gather(c->shtiles.p, g, per * 4, ncclFloat32, 0, c->comm, st));
     if (r != ncclSuccess) {
       if (f) (void)land_flight(c, *f);
       return fail(PRT_ERR_HIP, std::string("ncclGather: ") + R->GetErrorString(r));
@@ -1419,12 +1471,10 @@ int render_sharded(prt_ctx* c, const prt_render_params* p, float4* avg_dev, uint
     sum.ranks = (int32_t)all.size();
     HIP_TRY(hipSetDevice(c->device));
     if (c->sh_kind == 1) {
-      HIP_TRY(hipStreamSynchronize(c->stream));  // the gather is part of the frame
-      // a communicator that failed asynchronously (a peer's error, a lost link) is reported, not waited on
-      const Rccl* R = rccl(nullptr);
-      ncclResult_t ae = ncclSuccess;
-      if (R && R->CommGetAsyncError && R->CommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess)
-        return fail(PRT_ERR_HIP, std::string("RCCL communicator error: ") + R->GetErrorString(ae));
+      // the gather is part of the frame; a communicator that failed asynchronously (a peer's error, a lost link) or
+      // a gather whose peers never arrive is reported within the time limit, not waited on
+      const int wrc = rccl_wait(c, c->stream, "sharded frame");
+      if (wrc) return wrc;
     }
     *stats = sum;
   }
@@ -1523,6 +1573,7 @@ int prt_destroy(prt_ctx* c) {
   c->members.clear();
   (void)hipSetDevice(c->device);
   (void)join_flights(c);
+  if (c->sh_kind == 1 && c->comm) (void)rccl_wait(c, c->stream, "prt_destroy");  // (a stuck gather: aborted)
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (Flight& f : c->fl) {
     if (f.stream) (void)hipStreamSynchronize(f.stream);
@@ -1569,17 +1620,17 @@ int prt_set_stream(prt_ctx* c, void* s) {
 
 int prt_set_frames_in_flight(prt_ctx* c, int32_t n) {
   if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
-  if (n < 1 || n > kMaxFlights) return fail(PRT_ERR_INVALID_ARGUMENT, "frames in flight must be 1 to 4");
+  if (n < 1 || n > kMaxFlights) return fail(PRT_ERR_INVALID_ARGUMENT, "frames in flight must be 1 to 8");
   if (n > 1 && c->sh_kind == 2) return fail(PRT_ERR_UNSUPPORTED, "frames in flight on a local shard group");
   PRT_JOIN(c);
   HIP_TRY(hipSetDevice(c->device));
   if (n > 1) {
-    int lo = 0, hi = 0;
-    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    const char* ep = std::getenv("PRT_FLIGHT_PRIO");  // A/B (round 6): normal / high / low
-    const int prio = !ep ? 0 : (std::strcmp(ep, "high") == 0 ? hi : (std::strcmp(ep, "low") == 0 ? lo : 0));
-    for (Flight& f : c->fl) {
-      if (!f.stream) HIP_TRY(hipStreamCreateWithPriority(&f.stream, hipStreamNonBlocking, prio));
+    // only the slots used get a stream: HIP deals a process's streams over its hardware queues (GPU_MAX_HW_QUEUES,
+    // 4 by default) as they are created, so streams created and never used would still share queues with the
+    // chains that are
+    for (int32_t k = 0; k < n; k++) {
+      Flight& f = c->fl[k];
+      if (!f.stream) HIP_TRY(hipStreamCreateWithFlags(&f.stream, hipStreamNonBlocking));
       if (!f.done) HIP_TRY(hipEventCreateWithFlags(&f.done, hipEventDisableTiming));
     }
     if (!c->fl_fork) HIP_TRY(hipEventCreateWithFlags(&c->fl_fork, hipEventDisableTiming));
@@ -2250,7 +2301,20 @@ int prt_shard_init_rccl(prt_ctx* c, const uint8_t id[PRT_SHARD_ID_BYTES], int32_
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
   ncclComm_t comm = nullptr;
-  const ncclResult_t r = R->CommInitRank(&comm, world, u, rank);
+  ncclResult_t r;
+  if (R->CommInitRankConfig) {  // non-blocking set-up, polled: ranks that never join make it fail, not hang
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    r = R->CommInitRankConfig(&comm, world, u, rank, &cfg);
+    if (comm && (r == ncclSuccess || r == ncclInProgress)) r = rccl_settle(R, comm, r);
+    if (r == ncclInProgress) {
+      if (R->CommAbort) (void)R->CommAbort(comm);
+      return fail(PRT_ERR_HIP, "ncclCommInitRank: the other ranks did not join within the time limit (PRT_RCCL_TIMEOUT_S)");
+    }
+    if (r != ncclSuccess && comm && R->CommAbort) (void)R->CommAbort(comm);
+  } else {
+    r = R->CommInitRank(&comm, world, u, rank);
+  }
   if (r != ncclSuccess) return fail(PRT_ERR_HIP, std::string("ncclCommInitRank: ") + R->GetErrorString(r));
   c->comm = comm;
   c->own_comm = true;

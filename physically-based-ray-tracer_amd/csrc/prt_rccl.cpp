@@ -38,6 +38,8 @@ void load() {
     return;
   }
   r.CommAbort = reinterpret_cast<ncclResult_t (*)(ncclComm_t)>(dlsym(h, "ncclCommAbort"));
+  r.CommInitRankConfig = reinterpret_cast<ncclResult_t (*)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*)>(
+      dlsym(h, "ncclCommInitRankConfig"));
   g_ok = &g_rccl;
 }
 

@@ -19,6 +19,8 @@ struct Rccl {
   ncclResult_t (*Gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
   const char* (*GetErrorString)(ncclResult_t);
   ncclResult_t (*CommAbort)(ncclComm_t);  // optional (nullptr when the library lacks it)
+  // optional: a non-blocking communicator (config.blocking = 0), so a rank whose peers never arrive can give up
+  ncclResult_t (*CommInitRankConfig)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*);
 };
 
 // nullptr when RCCL cannot be loaded (the message is in *why)

@@ -1,8 +1,18 @@
 #!/usr/bin/env python3
-"""Per-rank frame time of the pixel-tile sharding on ONE GPU: rank 0's share of the C4 frame for
-world = 1, 2, 4, 8 (what each GPU of an N-GPU node renders), to estimate strong scaling without a node.
-`rank_time.py [c5] [worlds...]`: c5 = 3840x2160, 16 spp, depth 8 with the area light (bench.py --scene c5).
-The timed frames run without stats, as bench.py's do (no host wait per frame; rays from prt_ray_totals)."""
+"""Strong-scaling estimate of the pixel-tile sharding on ONE GPU: every rank's share of the
+C4 (or C5) frame for world = 2, 4, 8, each share warmed alone, plus the per-frame collective work rank 0 adds.
+
+For each world N and rank r = 0..N-1: PRT_RANK_WARM_S seconds of that rank's own share frames (the GPU's clock
+state follows the load), then n timed frames -> ms(r).  An N-GPU frame is gated by the slowest rank, so
+    frame(N) = max_r ms(r)                                  (collectives overlapped by the frames in flight)
+    frame(N, serial) = max_r ms(r) + gather + untile        (no overlap at all: an upper bound)
+gather = a world-1 RCCL ncclGather (torch.distributed "nccl" over this one GPU) of rank 0's tile buffer
+(W*H*16/N bytes), untile = prt_untile of the N gathered buffers into the W x H image; both timed with HIP
+events over 50 repetitions.  Efficiency = ms(world 1) / (N * frame(N)), against world 1 one frame at a time and
+with the same frames in flight.
+
+usage: rank_time.py [c5] [worlds...]   (env PRT_RANK_INFLIGHT: frames in flight of the shares, default 2)
+prints one line per (world, rank) and a summary line per world; the timed frames run without stats, as bench.py's."""
 import os
 import sys
 import time
@@ -11,45 +21,112 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "physically-based-ray-tracer_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 import prt  # noqa: E402
 from prt import scenes  # noqa: E402
 
 args = sys.argv[1:]
-INFLIGHT = int(os.environ.get("PRT_RANK_INFLIGHT", "1"))  # frames in flight (prt_set_frames_in_flight)
+INFLIGHT = int(os.environ.get("PRT_RANK_INFLIGHT", "2"))
+WARM_S = float(os.environ.get("PRT_RANK_WARM_S", "0.5"))
 C5 = bool(args) and args[0] == "c5"
 if C5:
     args = args[1:]
+WORLDS = [int(a) for a in args] or [2, 4, 8]
 sd = scenes.config_c5() if C5 else scenes.config_c4()
 W, H, SPP, BOUNCES = (3840, 2160, 16, 8) if C5 else (1920, 1080, 4, 4)
 FPC = SPP // 2
+TILE = 32
 ctx = prt.Context(0)
-ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+stream = torch.cuda.current_stream()
+ctx.set_stream(stream.cuda_stream)
 ctx.set_scene(prt.Scene.from_data(sd))
 ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
-ctx.set_frames_in_flight(INFLIGHT)
-base = None
-WORLDS = [int(a) for a in args] or [1, 2, 4, 8]
-WARM_S = float(os.environ.get("PRT_RANK_WARM_S", "0.5"))  # untimed frames first (clocks; bench.py --warmup-s)
-for world in WORLDS:
-    per = ctx.tile_buffer_pixels(W, H, 32, world)
+NT = 2 if C5 else 8  # timed frames per share
+
+
+def share_ms(world, rank, inflight):
+    """rank's share of the frame (world 1: the whole frame), warmed alone, n frames timed back to back."""
+    ctx.set_frames_in_flight(inflight)
+    per = ctx.tile_buffer_pixels(W, H, TILE, world)
     tiles = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
-    for i in range(1 if C5 else 2):
-        ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i)
+    avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+    rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+
+    def frame(i):
+        if world == 1:
+            ctx.render(W, H, SPP, BOUNCES, frame_index=FPC * i, avg=avg.data_ptr(), rgb8=rgb.data_ptr(),
+                       device_out=True, stats=False)
+        else:
+            ctx.render_tiles(W, H, SPP, BOUNCES, TILE, rank, world, tiles.data_ptr(), frame_index=FPC * i)
+    frame(0)
     torch.cuda.synchronize()
     tw = time.perf_counter()
-    while time.perf_counter() - tw < WARM_S:  # (a share of a few ms otherwise runs below the GPU's clocks)
-        for i in range(4):
-            ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i)
-        torch.cuda.synchronize()
+    k = 1
+    while time.perf_counter() - tw < WARM_S:
+        frame(k)
+        k += 1
+        if k % 4 == 0:
+            torch.cuda.synchronize()
+    ctx.finish()
     ctx.ray_totals(reset=True)
     torch.cuda.synchronize()
-    n = 2 if C5 else 8
     t0 = time.perf_counter()
-    for i in range(n):
-        ctx.render_tiles(W, H, SPP, BOUNCES, 32, 0, world, tiles.data_ptr(), frame_index=FPC * i)
+    for i in range(NT):
+        frame(i)
+    ctx.finish()
     torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) * 1e3 / n
+    ms = (time.perf_counter() - t0) * 1e3 / NT
     seg, sh = ctx.ray_totals(reset=True)
-    base = base or ms * world
-    print(f"world {world}: rank-0 frame {ms:.3f} ms  rays {(seg + sh) // n}  inflight {INFLIGHT}  "
-          f"ideal {base / world:.3f} ms  efficiency {base / world / ms:.2f}", flush=True)
+    return ms, (seg + sh) // NT
+
+
+def event_ms(fn, reps=50):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(reps):
+        fn()
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def collective_ms(world):
+    """world-1 RCCL gather of rank 0's tile buffer + prt_untile of world gathered buffers (rank 0's extra work)."""
+    per = ctx.tile_buffer_pixels(W, H, TILE, world)
+    part = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
+    bufs = [torch.zeros_like(part)]
+    g = event_ms(lambda: dist.gather(part, bufs, dst=0))
+    gathered = torch.zeros((world * per, 4), dtype=torch.float32, device="cuda")
+    avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+    rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    ctx.finish()
+    u = event_ms(lambda: ctx.untile(gathered.data_ptr(), W, H, TILE, world, avg.data_ptr(), rgb.data_ptr()))
+    return g, u, per * 16
+
+
+os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+os.environ.setdefault("MASTER_PORT", "29531")
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+scene = "c5" if C5 else "c4"
+w1_one, rays1 = share_ms(1, 0, 1)
+w1_fl, _ = share_ms(1, 0, INFLIGHT)
+print(f"{scene} world 1: frame {w1_one:.3f} ms one at a time, {w1_fl:.3f} ms with {INFLIGHT} in flight  rays {rays1}",
+      flush=True)
+for world in WORLDS:
+    ms = []
+    for r in range(world):
+        m, rays = share_ms(world, r, INFLIGHT)
+        ms.append(m)
+        print(f"  world {world} rank {r}: share {m:.3f} ms  rays {rays}", flush=True)
+    g, u, nbytes = collective_ms(world)
+    mx = max(ms)
+    ser = mx + g + u
+    print(f"{scene} world {world}: max share {mx:.3f} ms (rank {int(np.argmax(ms))}), mean {np.mean(ms):.3f}, "
+          f"min {min(ms):.3f}; gather {g:.3f} ms ({nbytes / 1e6:.2f} MB, world-1 RCCL) + untile {u:.3f} ms; "
+          f"efficiency vs {INFLIGHT}-in-flight world 1: {w1_fl / (world * mx):.3f} overlapped, "
+          f"{w1_fl / (world * ser):.3f} serial; vs one-at-a-time world 1: {w1_one / (world * mx):.3f} / "
+          f"{w1_one / (world * ser):.3f}", flush=True)
+ctx.close()
+dist.destroy_process_group()

@@ -117,33 +117,34 @@ def test_frames_in_flight_outputs_in_stream_order(flights):
         ref.close()
 
 
-def test_frames_in_flight_rccl_world1():
-    """An RCCL shard (world 1: the ncclGather path) with 2 frames in flight: each call's gather and untile run on
-    its slot's stream after the previous call's, and every frame equals the unsharded one."""
+@pytest.mark.parametrize("flights", [3, 4])
+def test_frames_in_flight_rccl_world1(flights):
+    """An RCCL shard (world 1: the ncclGather path) with 3 or 4 frames in flight (4: the setting bench.py uses on
+    several GPUs, with each chain on half-size grids): each call's gather and untile run on its slot's stream after
+    the previous call's; through an instance update, a camera change with an accumulation reset and a stats call,
+    every frame equals the unsharded one-at-a-time render bit for bit."""
     import torch
     import prt
-    sd = scenes.multi_instance(scenes.config_small(50, 40))
-    W, H = 90, 60
-    ref = prt.Context(0)
-    c = prt.Context(0)
-    try:
-        gpu_scene(ref, sd, W, H)
-        want = [ref.render(W, H, 4, 3, frame_index=2 * f)[:2] for f in range(4)]
-        c.shard_rccl(prt.Context.shard_unique_id(), 0, 1, 32)
-        gpu_scene(c, sd, W, H)
-        c.set_frames_in_flight(3)
-        outs = [(torch.zeros((W * H, 4), dtype=torch.float32, device="cuda"),
-                 torch.zeros(W * H, dtype=torch.int32, device="cuda")) for _ in range(4)]
-        for f, (o, g) in enumerate(outs):
-            c.render(W, H, 4, 3, frame_index=2 * f, avg=o.data_ptr(), rgb8=g.data_ptr(), device_out=True, stats=False)
-        c.finish()
-        torch.cuda.synchronize()
-        for f, ((o, g), (a, r)) in enumerate(zip(outs, want)):
-            assert np.array_equal(o.cpu().numpy(), a), f
-            assert np.array_equal(g.cpu().numpy().view(np.uint32), r), f
-    finally:
-        c.close()
-        ref.close()
+    sd = scenes.instance_field(120, seed=9)  # above 64 instances: the instance BVH is refitted between frames
+    W, H, n = 96, 64, 7
+    stream = torch.cuda.Stream()
+    res = []
+    for fl, shard in ((1, False), (flights, True)):
+        c = prt.Context(0)
+        try:
+            c.set_stream(stream.cuda_stream)
+            if shard:
+                c.shard_rccl(prt.Context.shard_unique_id(), 0, 1, 32)
+            gpu_scene(c, sd, W, H)
+            c.set_frames_in_flight(fl)
+            res.append(_frames(c, sd, W, H, n, 3, stream))
+        finally:
+            c.close()
+    (f1, last1, tot1), (f2, last2, tot2) = res
+    for k, ((a1, r1), (a2, r2)) in enumerate(zip(f1, f2)):
+        assert np.array_equal(a1, a2) and np.array_equal(r1, r2), k
+    assert np.array_equal(last1[0], last2[0]) and np.array_equal(last1[1], last2[1])
+    assert last1[2:] == last2[2:] and tot1 == tot2
 
 
 def test_frames_in_flight_sharded_frame_world1():
