@@ -349,7 +349,7 @@ def main():
         # launch of the last timed frame (stats.ms_closest sums them).  Counts per launch: rocprofv3 PMC passes of this same
         # command, committed under profiles/ (SQ_INSTS_VALU; FETCH_SIZE + WRITE_SIZE).
         launches = max(1, iters)
-        kern_ms = max(float(np.mean(ms_closest)) / launches, 1e-9)  # PRT_LAUNCH_TIMERS=0: no per-launch times
+        kern_ms = max(float(np.mean(ms_closest)) / launches, 1e-9)  # (the stats frame carries the per-launch events)
         seg_f, sh_f = seg_local / args.steps, shadow_local / args.steps  # rank 0's rays: its launches
         # the PMC passes are of each scene's default configuration at N = 1 (scripts/gpu_prof.sh)
         default_cfg = {"c3": (1920, 1080, 4, 4), "c4": (1920, 1080, 4, 4), "c5": (3840, 2160, 16, 8)}[args.scene]

@@ -183,9 +183,10 @@ int prt_finish(prt_ctx* ctx);
 int prt_set_textures(prt_ctx* ctx, const prt_texture* textures, int32_t count);
 int prt_set_meshes(prt_ctx* ctx, const prt_mesh* meshes, int32_t count);
 /* transforms: 16*count floats, row-major BLASInstance::transform; mesh_index: count.  Above 64 instances the rays
- * walk an instance BVH, rebuilt for every call up to 4,096 instances (a host SAH build, as the reference's per-frame
- * BVH::Build, uploaded in stream order: no wait on the GPU), refitted on the device and rebuilt on its node-area
- * trigger above that (PRT_TLAS_SMALL=1 selects the single-workgroup device build) */
+ * walk an instance BVH, rebuilt for every call as the reference's per-frame BVH::Build: a host SAH build uploaded in
+ * stream order (no wait on the GPU), on the calling thread up to 4,096 instances; above that on a worker thread,
+ * committed at the first call after it finished, with the device refitting the current tree to every call's boxes
+ * in between */
 int prt_set_instances(prt_ctx* ctx, const float* transforms, const uint32_t* mesh_index, int32_t count);
 int prt_set_lights(prt_ctx* ctx, const prt_lights* lights);
 /* kinds: one PRT_MAT_* per instance (count = the instance count), or count 0 = all textured.  Reset by
@@ -350,13 +351,12 @@ typedef struct {
     double  build_ms;       /* wall time of the last prt_set_meshes (BLAS builds + uploads) */
     int32_t builder;        /* PRT_BUILDER_* used by the last prt_set_meshes */
     int32_t tlas_depth;     /* levels of the instance BVH the rays walk (0: instances tested as a linear list) */
-    int32_t tlas_rebuilds;  /* (ABI 8) rebuilds of the instance BVH since the instance count last changed: host
-                               builds for an update (default, up to 4,096 instances) or device builds */
-    int32_t tlas_refits;    /* (ABI 8) updates since then that refitted the current tree instead (prt_set_instances
-                               with the same count) */
-    int32_t tlas_rejected;  /* (ABI 9) device rebuilds not committed since the context was created (deeper than
-                               the traversal stacks were sized for; the refitted tree stayed).  Reading it waits
-                               for the context's queued work. */
+    int32_t tlas_rebuilds;  /* (ABI 8) rebuilds of the instance BVH committed since the instance count last
+                               changed (every update up to 4,096 instances; above, each finished worker build) */
+    int32_t tlas_refits;    /* (ABI 8) updates since then that refitted the current tree instead (above 4,096
+                               instances, while the worker builds) */
+    int32_t tlas_rejected;  /* (ABI 9) always 0 from ABI 10: the instance BVH is built on the host only (kept for
+                               the struct layout) */
 } prt_scene_info;
 int prt_get_scene_info(prt_ctx* ctx, prt_scene_info* info);
 

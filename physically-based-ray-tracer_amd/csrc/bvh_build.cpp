@@ -46,6 +46,7 @@ struct Builder {
   std::vector<uint32_t> idx;
   std::vector<Node2> nodes;
   int max_leaf;
+  int nbins = kBins;  // SAH bins per axis (the instance BVH: 8, tinybvh's BVHBINS for its per-frame TLAS build)
 
   void build(int32_t T) {
     tb.resize(T);
@@ -79,38 +80,55 @@ struct Builder {
     }
     nodes[ni].box = b;
     if (count <= 1) return;
-    // binned SAH over centroid bins (C_trav = 1, C_int = 1 per triangle)
+    // binned SAH over centroid bins (C_trav = 1, C_int = 1 per triangle); a pair that must split (the instance BVH's
+    // one-instance leaves) has only the one split
     double best = 1e300;
+    if (count == 2 && count > max_leaf) {
+      emit_children(ni, first, count, first + 1, work);
+      return;
+    }
     int bax = -1, bsplit = -1;
+    // the three axes' bins filled in one pass over the primitives (each primitive's box and centroid read once)
+    const int nb = nbins;
+    Box bins[3][kBins];
+    int cnt[3][kBins] = {};
+    float blo[3], bsc[3];
+    bool live[3];
     for (int ax = 0; ax < 3; ax++) {
-      const float lo = cb.lo[ax], hi = cb.hi[ax];
-      if (!(hi > lo)) continue;
-      Box bins[kBins];
-      int cnt[kBins] = {0};
-      for (int k = 0; k < kBins; k++) bins[k].reset();
-      const float sc = kBins / (hi - lo);
-      for (int32_t i = first; i < first + count; i++) {
-        uint32_t p = idx[i];
-        int k = std::min(kBins - 1, std::max(0, (int)((cen[3 * (size_t)p + ax] - lo) * sc)));
-        cnt[k]++;
-        bins[k].grow(tb[p]);
+      blo[ax] = cb.lo[ax];
+      live[ax] = cb.hi[ax] > cb.lo[ax];
+      bsc[ax] = live[ax] ? nb / (cb.hi[ax] - cb.lo[ax]) : 0.0f;
+      for (int k = 0; k < nb; k++) bins[ax][k].reset();
+    }
+    for (int32_t i = first; i < first + count; i++) {
+      const uint32_t p = idx[i];
+      const Box& pb = tb[p];
+      const float* pc = &cen[3 * (size_t)p];
+      for (int ax = 0; ax < 3; ax++) {
+        if (!live[ax]) continue;
+        const int k = std::min(nb - 1, std::max(0, (int)((pc[ax] - blo[ax]) * bsc[ax])));
+        cnt[ax][k]++;
+        bins[ax][k].grow(pb);
       }
+    }
+    for (int ax = 0; ax < 3; ax++) {
+      if (!live[ax]) continue;
       double la[kBins - 1], ra[kBins - 1];
       int lc[kBins - 1], rc[kBins - 1];
       Box acc; acc.reset();
       int c = 0;
-      for (int k = 0; k < kBins - 1; k++) {
-        if (cnt[k]) acc.grow(bins[k]);
-        c += cnt[k];
+      for (int k = 0; k < nb - 1; k++) {
+        if (cnt[ax][k]) acc.grow(bins[ax][k]);
+        c += cnt[ax][k];
         la[k] = acc.area(); lc[k] = c;
       }
       acc.reset(); c = 0;
-      for (int k = kBins - 1; k > 0; k--) {
-        if (cnt[k]) acc.grow(bins[k]);
-        c += cnt[k];
+      for (int k = nb - 1; k > 0; k--) {
+        if (cnt[ax][k]) acc.grow(bins[ax][k]);
+        c += cnt[ax][k];
         ra[k - 1] = acc.area(); rc[k - 1] = c;
       }
-      for (int k = 0; k < kBins - 1; k++) {
+      for (int k = 0; k < nb - 1; k++) {
         if (!lc[k] || !rc[k]) continue;
         const double cost = la[k] * lc[k] + ra[k] * rc[k];
         if (cost < best) { best = cost; bax = ax; bsplit = k; }
@@ -124,14 +142,17 @@ struct Builder {
     if (bax < 0) {
       mid = first + count / 2;  // coincident centroids: split the range
     } else {
-      const float lo = cb.lo[bax], sc = kBins / (cb.hi[bax] - lo);
+      const float lo = cb.lo[bax], sc = nbins / (cb.hi[bax] - lo);
       auto it = std::partition(idx.begin() + first, idx.begin() + first + count, [&](uint32_t p) {
-        int k = std::min(kBins - 1, std::max(0, (int)((cen[3 * (size_t)p + bax] - lo) * sc)));
+        int k = std::min(nbins - 1, std::max(0, (int)((cen[3 * (size_t)p + bax] - lo) * sc)));
         return k <= bsplit;
       });
       mid = (int32_t)(it - idx.begin());
       if (mid == first || mid == first + count) mid = first + count / 2;
     }
+    emit_children(ni, first, count, mid, work);
+  }
+  void emit_children(int32_t ni, int32_t first, int32_t count, int32_t mid, std::vector<int32_t>& work) {
     int32_t l = (int32_t)nodes.size();
     nodes.push_back(Node2());
     nodes.push_back(Node2());
@@ -503,9 +524,10 @@ struct WideDp {
 constexpr float kWideNodeCost = 1.0f, kWideTriCost = 1.0f;  // tri cost swept 0.15-5 on C4: flat above 1
 
 template <class NodeT, class Fmt, class Out>
-void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out, bool spatial = false) {
+void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out, bool spatial = false, int bins = kBins) {
   Builder B;
   B.tri = triangles;
+  B.nbins = bins;
   B.max_leaf = std::max(1, std::min(4, max_leaf));
   if (spatial) {
     SpatialBuilder SB;
@@ -517,14 +539,9 @@ void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out, bool
   }
   for (int k = 0; k < 3; k++) { out.bmin[k] = B.nodes[0].box.lo[k]; out.bmax[k] = B.nodes[0].box.hi[k]; }
   out.tris.reserve(T);
-  const char* ce = std::getenv("PRT_COLLAPSE");
-  const bool greedy = ce && std::strcmp(ce, "greedy") == 0;
-  WideDp dp;
-  if (!greedy) {
-    const char* cr = std::getenv("PRT_COLLAPSE_TRI_COST");
-    dp.compute(B, kWideNodeCost, cr ? (float)std::atof(cr) : kWideTriCost);
-  }
-  auto is_leaf = [&](int32_t n) { return greedy ? B.nodes[n].leaf() : dp.leaf1[n] != 0; };
+  WideDp dp;  // the SAH-optimal collapse (round 1's greedy collapse: 2,636 against 3,529+ Mrays/s on C4, removed)
+  dp.compute(B, kWideNodeCost, kWideTriCost);
+  auto is_leaf = [&](int32_t n) { return dp.leaf1[n] != 0; };
   struct Item { int32_t n2; uint32_t n8; int depth; };
   std::vector<Item> work;
   out.nodes.push_back(NodeT());
@@ -535,27 +552,7 @@ void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out, bool
     out.depth = std::max(out.depth, it.depth);
     int32_t ch[8];
     int nc = 0;
-    const Node2& root = B.nodes[it.n2];
-    if (!greedy) {
-      nc = dp.expand(B, it.n2, ch);
-    } else if (root.leaf()) {  // greedy: open the largest-area interior child until 8 children
-      ch[nc++] = it.n2;
-    } else {
-      ch[nc++] = root.left;
-      ch[nc++] = root.right;
-      while (nc < 8) {
-        int bi = -1;
-        double ba = -1.0;
-        for (int i = 0; i < nc; i++) {
-          const Node2& c = B.nodes[ch[i]];
-          if (!c.leaf() && c.box.area() > ba) { ba = c.box.area(); bi = i; }
-        }
-        if (bi < 0) break;
-        const Node2& c = B.nodes[ch[bi]];
-        ch[bi] = c.left;
-        ch[nc++] = c.right;
-      }
-    }
+    nc = dp.expand(B, it.n2, ch);
     // inflated child boxes and the node grid
     float clo[8][3], chi[8][3];
     double nlo[3] = {1e300, 1e300, 1e300}, nhi[3] = {-1e300, -1e300, -1e300};
@@ -665,7 +662,7 @@ BuiltTlas8 build_tlas8(const float* boxes, int32_t n) {
     for (int k = 0; k < 3; k++) { t[k] = b[k]; t[4 + k] = b[3 + k]; t[8 + k] = b[k]; }
   }
   BuiltBlas8 w;
-  build_wide8<Node8, Fmt8>(fat.data(), n, 1, w);
+  build_wide8<Node8, Fmt8>(fat.data(), n, 1, w, false, 8);  // 8 bins: tinybvh's BVHBINS (Core/tiny_bvh.h:92-131)
   BuiltTlas8 out;
   out.depth = w.depth;
   out.nodes = std::move(w.nodes);

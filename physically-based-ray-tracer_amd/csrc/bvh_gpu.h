@@ -24,24 +24,6 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
                            TriMT* tris_out, GpuBlasInfo* info, bool ploc = false,
                            std::vector<uint32_t>* level_ends = nullptr, int trbvh = -1,  // trbvh < 0: PRT_TRBVH / default
                            int ploc_radius = 64);  // PLOC search radius: 64 (PRT_PLOC_R) or 512
-// single-workgroup PLOC (radius 64) + SAH-optimal collapse for n <= kGpuSmallBuild, in two launches on s with no host
-// synchronisation (the instance BVH's per-frame rebuild).  scratch: gpu_small_scratch_bytes(n) bytes of device memory.
-// out (device, 4 words): nodes written, TriMT written, wide-tree levels, error bits (nonzero: no usable tree, e.g.
-// deeper than max_levels); level_end (device, max_levels words): level d's nodes are [level_end[d-1], level_end[d]).
-// SmallTlasOut (optional, the instance BVH): the collapse launch also writes the leaf slots' instances (slot[8 j + s],
-// node j's tri_base = 8 j), the identity refit order and the tree's description (meta: TlasMeta's words, levels
-// deepest first, valid = 0 when the build failed or is deeper than depth_cap)
-constexpr int32_t kGpuSmallBuild = 4096;
-size_t gpu_small_scratch_bytes(int32_t n);
-// the build's counter words inside that scratch (diagnostics: phase clock at [8..19], PLOC iterations at [7])
-uint32_t* gpu_small_ctr(void* scratch, int32_t n);
-struct SmallTlasOut {
-  uint32_t *slot = nullptr, *order = nullptr, *meta = nullptr;
-  uint32_t depth_cap = 0;
-};
-hipError_t gpu_build_blas8_small(hipStream_t s, const float* tri_dev, int32_t n, int max_leaf, Node8* nodes_out,
-                                 TriMT* tris_out, void* scratch, uint32_t* out, uint32_t* level_end, int max_levels,
-                                 int radius = 0, SmallTlasOut tlas = SmallTlasOut{});
 // rebase a mesh's nodes into the concatenated arrays (in place) and record ShadeTri.pad[0] for its primitives
 hipError_t gpu_blas_finish(hipStream_t s, Node8* nodes, uint32_t n_nodes, uint32_t node_base, const TriMT* tris,
                            uint32_t n_tris, uint32_t tri_base, ShadeTri* stri, uint32_t prim_base);

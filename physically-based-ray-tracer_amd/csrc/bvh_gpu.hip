@@ -748,371 +748,6 @@ __global__ void __launch_bounds__(kB) k_collapse(const float4* __restrict__ tri,
   collapse_task(tasks[t], tri, keys, n, left, right, box, first, count, max_leaf, next, ctr, nodes, tris, dp);
 }
 
-// ---- single-workgroup build for small inputs (the instance BVH's per-frame rebuild): the same steps in one launch,
-// with no host round trip -- Morton keys bitonic-sorted in LDS, PLOC over the clusters' boxes in LDS (iterations
-// separated by barriers instead of launches), the SAH-optimal collapse level by level behind barriers.  The
-// scratch arrays are the multi-launch builder's (global, touched by this one workgroup only: plain loads see the
-// workgroup's own stores after a barrier).
-constexpr int kSmallThreads = 1024;
-// default PLOC search radius: 64 places (1,000 drifting instances: PLOC 0.57-0.60 against 1.13-1.21 ms at 512, frames
-// after the rebuild as fast, profiles/r05_tlas_rebuild.txt sessions q-t)
-constexpr int kSmallR = 64;
-struct SmallScratch {
-  unsigned long long* keys;  // n sorted keys
-  int *left, *right;         // 2n - 1
-  uint32_t* count;           // 2n - 1
-  float* box;                // 6 (2n - 1)
-  DpTab dp;                  // 8 (n - 1) doubles, n - 1 decisions
-  Task *ta, *tb;             // n each
-  uint32_t* ctr;             // 4
-};
-
-// exclusive prefix sum of one value per thread over the workgroup; *total = the sum
-__device__ __forceinline__ uint32_t small_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  uint32_t x = v;
-  for (uint32_t o = 1; o < 64; o <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[w] = x;
-  __syncthreads();
-  uint32_t before = 0, all = 0;
-  for (uint32_t k = 0; k < kSmallThreads / 64; k++) {
-    before += k < w ? wsum[k] : 0u;
-    all += wsum[k];
-  }
-  __syncthreads();
-  *total = all;
-  return before + x - v;
-}
-
-// diagnostic phase clock (s_memrealtime, 100 MHz) of the single-workgroup build: ctr[8 + 2k] (64-bit), read back by
-// the host with PRT_TLAS_SMALL_TIMES=1 (gpu_small_times)
-__device__ __forceinline__ void small_stamp(uint32_t* ctr, int k) {
-  if (threadIdx.x == 0) {
-    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-    ctr[8 + 2 * k] = (uint32_t)t;
-    ctr[9 + 2 * k] = (uint32_t)(t >> 32);
-  }
-}
-
-__global__ void __launch_bounds__(kSmallThreads) k_build_small(const float4* __restrict__ tri, int n, int max_leaf,
-                                                               SmallScratch sc, int radius) {
-  __shared__ union {
-    unsigned long long keys[kGpuSmallBuild];
-    float sbox[6 * kGpuSmallBuild];  // cluster boxes, component-major: sbox[k * kGpuSmallBuild + i] (conflict-free)
-  } U;
-  auto SB = [&](int i, int k) -> float& { return U.sbox[k * kGpuSmallBuild + i]; };
-  __shared__ int sclus[kGpuSmallBuild];
-  __shared__ int snn[kGpuSmallBuild];
-  __shared__ int snew[kGpuSmallBuild];  // cluster position after the compaction (PLOC incremental neighbours)
-  __shared__ uint32_t wsum[kSmallThreads / 64];
-  __shared__ uint32_t cb[6];
-  __shared__ int s_next;
-  __shared__ int s_ns;  // clusters searching in an incremental PLOC iteration
-  __shared__ uint32_t s_err;
-  const int tid = (int)threadIdx.x;
-  small_stamp(sc.ctr, 0);
-  if (tid < 3) { cb[tid] = 0xFFFFFFFFu; cb[3 + tid] = 0u; }
-  if (tid == 0) { s_err = 0u; s_next = n - 2; s_ns = 0; }
-  __syncthreads();
-  // 1. centroid bounds (k_centroid_bounds) and Morton keys (k_morton), padded to a power of two with ~0
-  for (int i = tid; i < n; i += kSmallThreads) {
-    const float4 a = tri[3 * i], b = tri[3 * i + 1], d = tri[3 * i + 2];
-    const float c[3] = {(a.x + b.x + d.x) * (1.0f / 3.0f), (a.y + b.y + d.y) * (1.0f / 3.0f),
-                        (a.z + b.z + d.z) * (1.0f / 3.0f)};
-    for (int k = 0; k < 3; k++) {
-      atomicMin(&cb[k], ord(c[k]));
-      atomicMax(&cb[3 + k], ord(c[k]));
-    }
-  }
-  __syncthreads();
-  int P = 2;
-  while (P < n) P <<= 1;
-  for (int i = tid; i < P; i += kSmallThreads) {
-    unsigned long long key = ~0ull;
-    if (i < n) {
-      const float4 a = tri[3 * i], b = tri[3 * i + 1], d = tri[3 * i + 2];
-      const float c[3] = {(a.x + b.x + d.x) * (1.0f / 3.0f), (a.y + b.y + d.y) * (1.0f / 3.0f),
-                          (a.z + b.z + d.z) * (1.0f / 3.0f)};
-      uint32_t q[3];
-      for (int k = 0; k < 3; k++) {
-        const float lo = unord(cb[k]), hi = unord(cb[3 + k]);
-        const float ext = hi - lo;
-        const float t = ext > 0.0f ? (c[k] - lo) / ext : 0.0f;
-        q[k] = (uint32_t)fminf(fmaxf(t * 1024.0f, 0.0f), 1023.0f);
-      }
-      const uint32_t code = (spread10(q[0]) << 2) | (spread10(q[1]) << 1) | spread10(q[2]);
-      key = ((unsigned long long)code << 32) | (uint32_t)i;
-    }
-    U.keys[i] = key;
-  }
-  __syncthreads();
-  small_stamp(sc.ctr, 1);
-  // 2. bitonic sort (ascending; keys are unique)
-  for (int k = 2; k <= P; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < P; i += kSmallThreads) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const unsigned long long a = U.keys[i], b = U.keys[ixj];
-          if ((a > b) == ((i & k) == 0)) { U.keys[i] = b; U.keys[ixj] = a; }
-        }
-      }
-      __syncthreads();
-    }
-  small_stamp(sc.ctr, 2);
-  // 3. leaves (k_ploc_leaves): binary leaf n - 1 + i = the i-th prim in key order
-  for (int i = tid; i < n; i += kSmallThreads) {
-    const unsigned long long key = U.keys[i];
-    sc.keys[i] = key;
-    const uint32_t prim = (uint32_t)key;
-    const float4 a = tri[3 * prim], b = tri[3 * prim + 1], c = tri[3 * prim + 2];
-    float* bx = sc.box + 6 * (size_t)(n - 1 + i);
-    bx[0] = fminf(fminf(a.x, b.x), c.x); bx[1] = fminf(fminf(a.y, b.y), c.y); bx[2] = fminf(fminf(a.z, b.z), c.z);
-    bx[3] = fmaxf(fmaxf(a.x, b.x), c.x); bx[4] = fmaxf(fmaxf(a.y, b.y), c.y); bx[5] = fmaxf(fmaxf(a.z, b.z), c.z);
-    sc.count[n - 1 + i] = 1u;
-    sclus[i] = n - 1 + i;
-  }
-  __syncthreads();  // the keys are read: U becomes the cluster boxes
-  for (int i = tid; i < n; i += kSmallThreads)
-    for (int k = 0; k < 6; k++) SB(i, k) = sc.box[6 * (size_t)(n - 1 + i) + k];
-  __syncthreads();
-  small_stamp(sc.ctr, 3);
-  // 4. PLOC iterations (k_ploc_nn / k_ploc_merge / compaction), the cluster list and boxes in LDS.
-  // Incremental neighbours: once a search window covers every cluster (m - 1 <= radius), a cluster whose nearest
-  // neighbour was not merged keeps it -- a merged cluster's box contains each of its parts, so no new cluster is
-  // nearer than the old neighbour -- and only new clusters and those whose neighbour was merged search again
-  // (snn = -1).  An iteration that merges nothing (possible only through exact area ties) searches everything
-  // again; a second one in a row is an error.
-  for (int i = tid; i < n; i += kSmallThreads) snn[i] = -1;
-  __syncthreads();
-  int m = n;
-  uint32_t ploc_iters = 0;
-  bool incr = false, stalled = false;  // (uniform across the workgroup)
-  unsigned long long tp_nn = 0, tp_merge = 0, tp_compact = 0, tp0 = 0;  // diagnostic phase clock (thread 0)
-  while (m > 1) {
-    if (tid == 0) tp0 = __builtin_amdgcn_s_memrealtime();
-    if (!incr) {
-      // every cluster searches its window, one cluster per lane (neighbouring lanes read neighbouring boxes)
-      for (int i = tid; i < m; i += kSmallThreads) {
-        const float b0 = SB(i, 0), b1 = SB(i, 1), b2 = SB(i, 2), b3 = SB(i, 3), b4 = SB(i, 4), b5 = SB(i, 5);
-        float best = 3.4e38f;
-        int bj = -1;
-        // The pair order of the multi-launch builder's tie rule -- equal areas go to the smaller (min, max) pair --
-        // is the order of j here (below i: min = j; above i: min = i, max = j), so the first minimum in j wins
-        auto cand = [&](int j) {
-          const float dx = fmaxf(b3, SB(j, 3)) - fminf(b0, SB(j, 0));
-          const float dy = fmaxf(b4, SB(j, 4)) - fminf(b1, SB(j, 1));
-          const float dz = fmaxf(b5, SB(j, 5)) - fminf(b2, SB(j, 2));
-          const float a = dx * dy + dy * dz + dz * dx;
-          if (bj < 0 || a < best) { best = a; bj = j; }
-        };
-        for (int j = max(0, i - radius); j < i; j++) cand(j);
-        for (int j = i + 1; j <= min(m - 1, i + radius); j++) cand(j);
-        snn[i] = bj;
-      }
-    } else {
-      // incremental: only the clusters listed here search, over every cluster (the last window covered them all),
-      // one wave per cluster -- a lane per candidate, then the wave's minimum of (area, j), the same first minimum in
-      // j as above.  One lane per searching cluster left most lanes idle while a few scanned m candidates in a row.
-      for (int i = tid; i < m; i += kSmallThreads)
-        if (snn[i] < 0) snew[atomicAdd(&s_ns, 1)] = i;  // (snew is free until the merge step)
-      __syncthreads();
-      const int ns = s_ns, lane = tid & 63;
-      for (int s = tid >> 6; s < ns; s += kSmallThreads / 64) {
-        const int i = snew[s];
-        const float b0 = SB(i, 0), b1 = SB(i, 1), b2 = SB(i, 2), b3 = SB(i, 3), b4 = SB(i, 4), b5 = SB(i, 5);
-        unsigned long long best = ~0ull;
-        for (int j = lane; j < m; j += 64) {
-          if (j == i) continue;
-          const float dx = fmaxf(b3, SB(j, 3)) - fminf(b0, SB(j, 0));
-          const float dy = fmaxf(b4, SB(j, 4)) - fminf(b1, SB(j, 1));
-          const float dz = fmaxf(b5, SB(j, 5)) - fminf(b2, SB(j, 2));
-          const float a = dx * dy + dy * dz + dz * dx;  // >= 0: its bits order as the value
-          const unsigned long long key = ((unsigned long long)__float_as_uint(a) << 32) | (uint32_t)j;
-          best = key < best ? key : best;
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-          const unsigned long long other = __shfl_xor(best, o);
-          best = other < best ? other : best;
-        }
-        if (lane == 0) snn[i] = (int)(uint32_t)best;
-      }
-    }
-    __syncthreads();
-    if (tid == 0) { const unsigned long long t = __builtin_amdgcn_s_memrealtime(); tp_nn += t - tp0; tp0 = t; }
-    // merge: thread t owns clusters 4t .. 4t + 3 (m <= 4 x 1024)
-    int nc[4], onn[4];  // onn: the kept neighbour's old position, or -1 (search again)
-    float nb[4][6];
-    uint32_t keep = 0;
-    for (int e = 0; e < 4; e++) {
-      const int i = 4 * tid + e;
-      if (i >= m) continue;
-      const int j = snn[i];
-      const bool mutual = j >= 0 && snn[j] == i;
-      if (mutual && i > j) continue;  // merged into the cluster at j
-      keep |= 1u << e;
-      onn[e] = -1;
-      if (!mutual) {
-        const int jj = j >= 0 ? snn[j] : -1;
-        if (j >= 0 && !(jj >= 0 && snn[jj] == j)) onn[e] = j;  // the neighbour survives this iteration
-        nc[e] = sclus[i];
-        for (int k = 0; k < 6; k++) nb[e][k] = SB(i, k);
-        continue;
-      }
-      const int lc = sclus[i], rc = sclus[j];
-      const int p = atomicSub(&s_next, 1);
-      if (p < 0) { atomicOr(&s_err, 1u); nc[e] = lc; for (int k = 0; k < 6; k++) nb[e][k] = SB(i, k); continue; }
-      float lb[6], rb[6];
-      for (int k = 0; k < 6; k++) { lb[k] = SB(i, k); rb[k] = SB(j, k); }
-      for (int k = 0; k < 3; k++) { nb[e][k] = fminf(lb[k], rb[k]); nb[e][3 + k] = fmaxf(lb[3 + k], rb[3 + k]); }
-      for (int k = 0; k < 6; k++) sc.box[6 * (size_t)p + k] = nb[e][k];
-      sc.left[p] = lc;
-      sc.right[p] = rc;
-      sc.count[p] = sc.count[lc] + sc.count[rc];
-      if (sc.dp.C) dp_node<true>(sc.dp, p, lc, rc, nb[e], lb, rb, (int)sc.count[p], n, max_leaf);
-      nc[e] = p;
-    }
-    uint32_t total = 0;
-    const uint32_t pos0 = small_scan((uint32_t)__popc(keep), wsum, &total);  // (its barriers order the reads above)
-    if (tid == 0) { const unsigned long long t = __builtin_amdgcn_s_memrealtime(); tp_merge += t - tp0; tp0 = t; }
-    uint32_t pos = pos0;
-    for (int e = 0; e < 4; e++)
-      if ((keep >> e) & 1u) snew[4 * tid + e] = (int)pos++;
-    __syncthreads();
-    pos = pos0;
-    const bool global = m - 1 <= radius;  // this iteration's search windows covered every cluster
-    for (int e = 0; e < 4; e++) {
-      if (!((keep >> e) & 1u)) continue;
-      sclus[pos] = nc[e];
-      for (int k = 0; k < 6; k++) SB(pos, k) = nb[e][k];
-      snn[pos] = onn[e] >= 0 ? snew[onn[e]] : -1;
-      pos++;
-    }
-    if (total >= (uint32_t)m) {  // no merge (exact ties under kept neighbours): search everything again
-      if (stalled || !incr) { if (tid == 0) s_err |= 2u; total = 1; }
-      stalled = true;
-      incr = false;
-    } else {
-      stalled = false;
-      incr = global;
-    }
-    m = (int)total;
-    if (tid == 0 && ploc_iters < 40) sc.ctr[20 + ploc_iters] = (uint32_t)m;  // diagnostic: clusters left
-    if (tid == 0) s_ns = 0;
-    ploc_iters++;
-    __syncthreads();
-    if (tid == 0) tp_compact += __builtin_amdgcn_s_memrealtime() - tp0;
-  }
-  if (tid == 0) {
-    sc.ctr[60] = (uint32_t)tp_nn;
-    sc.ctr[61] = (uint32_t)tp_merge;
-    sc.ctr[62] = (uint32_t)tp_compact;
-  }
-  small_stamp(sc.ctr, 4);
-  if (tid == 0) sc.ctr[7] = ploc_iters;
-  if (tid == 0 && s_next != -1 && n > 1) s_err |= 4u;  // not exactly n - 1 internal nodes
-  if (tid == 0) st_sc1_u(sc.ctr + 4, s_err);  // for k_collapse_small
-}
-
-// 5. the collapse of the single-workgroup build, one level per pass behind barriers (k_collapse), in a launch of its
-// own: a collapse task is one lane's long serial walk (the slot expansion, the octant assignment, the leaves), which
-// at the PLOC kernel's 128 VGPRs ran from scratch (~80 us a level); at 256 threads it has the registers it needs.
-// The binary tree it walks (children, counts, decisions, keys) is copied to LDS first: every walk is a chain of
-// dependent loads, ~100 cycles each from LDS instead of an L2 round trip.
-constexpr int kCollapseThreads = 256;
-__global__ void __launch_bounds__(kCollapseThreads) k_collapse_small(const float4* __restrict__ tri, int n,
-                                                                     int max_leaf, SmallScratch sc, Node8* nodes,
-                                                                     TriMT* tris, uint32_t* out, uint32_t* level_end,
-                                                                     int max_levels, SmallTlasOut tlas) {
-  __shared__ int lleft[kGpuSmallBuild], lright[kGpuSmallBuild];
-  __shared__ uint32_t ldec[kGpuSmallBuild];
-  __shared__ uint32_t lcount[2 * kGpuSmallBuild];
-  __shared__ unsigned long long lkeys[kGpuSmallBuild];
-  __shared__ uint32_t s_err;
-  const int tid = (int)threadIdx.x;
-  for (int i = tid; i < 2 * n - 1; i += kCollapseThreads) {
-    if (i < n - 1) {
-      lleft[i] = sc.left[i];
-      lright[i] = sc.right[i];
-      if (sc.dp.dec) ldec[i] = sc.dp.dec[i];
-    }
-    lcount[i] = sc.count[i];
-    if (i < n) lkeys[i] = sc.keys[i];
-  }
-  DpTab ldp = sc.dp;
-  if (ldp.dec) ldp.dec = ldec;
-  if (tid == 0) {
-    s_err = ld_sc1_u(sc.ctr + 4);
-    sc.ta[0] = Task{0, 0u};
-    st_sc1_u(sc.ctr + 0, 1u); st_sc1_u(sc.ctr + 1, 0u); st_sc1_u(sc.ctr + 2, 0u); st_sc1_u(sc.ctr + 3, 0u);
-    level_end[0] = 1u;
-  }
-  __syncthreads();
-  Task *ta = sc.ta, *tb = sc.tb;
-  uint32_t ntasks = s_err ? 0u : 1u;
-  int levels = 0;
-  while (ntasks) {
-    levels++;
-    for (uint32_t t = (uint32_t)tid; t < ntasks; t += kCollapseThreads)
-      collapse_task(ta[t], tri, lkeys, n, lleft, lright, sc.box, nullptr, lcount, max_leaf, tb, sc.ctr, nodes, tris,
-                    ldp);
-    __syncthreads();
-    ntasks = ld_sc1_u(sc.ctr + 2);
-    const uint32_t used = ld_sc1_u(sc.ctr + 0);
-    __syncthreads();
-    if (tid == 0) {
-      st_sc1_u(sc.ctr + 2, 0u);
-      if (ntasks && levels < max_levels) level_end[levels] = used;
-    }
-    if (levels >= max_levels && ntasks) {  // deeper than the caller's stacks hold
-      if (tid == 0) s_err |= 8u;
-      ntasks = 0;
-    }
-    __syncthreads();
-    Task* tt = ta; ta = tb; tb = tt;
-  }
-  __shared__ uint32_t s_out[4];
-  if (tid == 0) {
-    const uint32_t c0 = ld_sc1_u(sc.ctr + 0), c1 = ld_sc1_u(sc.ctr + 1), c3 = ld_sc1_u(sc.ctr + 3);
-    s_out[0] = c0;
-    s_out[1] = c1;
-    s_out[2] = (uint32_t)levels;
-    s_out[3] = s_err | ((c3 & 0x80000000u) ? 16u : 0u) | (c1 != (uint32_t)n ? 32u : 0u);
-    for (int k = 0; k < 4; k++) out[k] = s_out[k];
-  }
-  __syncthreads();
-  if (tlas.slot) {  // the instance BVH's epilogue (k_tlas_slots' conversion, its refit order and its TlasMeta)
-    const uint32_t nn = s_out[0], nl = s_out[2];
-    const bool valid = s_out[3] == 0u && nn > 0u && nl >= 1u && nl <= tlas.depth_cap;
-    if (valid)
-      for (uint32_t j = (uint32_t)tid; j < nn; j += kCollapseThreads) {
-        Node8& nd = nodes[j];
-        for (uint32_t q = 0; q < 8; q++)
-          tlas.slot[8 * (size_t)j + q] =
-              (!((nd.imask >> q) & 1u) && nd.meta[q]) ? tris[nd.tri_base + (nd.meta[q] >> 3)].prim : 0xFFFFFFFFu;
-        nd.tri_base = 8u * j;
-        tlas.order[j] = j;
-      }
-    if (tid == 0) {  // TlasMeta: n_nodes, nlevels, valid, depth, level_off[max_levels], level_cnt[max_levels]
-      uint32_t* m = tlas.meta;
-      m[0] = valid ? nn : 0u;
-      m[1] = valid ? nl : 0u;
-      m[2] = valid ? 1u : 0u;
-      m[3] = valid ? nl : 0u;
-      if (valid)
-        for (uint32_t l = nl, k = 0; l-- > 0; k++) {
-          const uint32_t b = l == 0 ? 0u : level_end[l - 1];
-          m[4 + k] = b;
-          m[4 + max_levels + k] = level_end[l] - b;
-        }
-    }
-  }
-  small_stamp(sc.ctr, 5);
-}
-
 // ShadeTri.pad[0] = the primitive's TriMT record (the cooperative traversal tail, prt_persist.h)
 __global__ void __launch_bounds__(kB) k_prim_records(const TriMT* __restrict__ tris, uint32_t n, uint32_t tri_base,
                                                      ShadeTri* stri, uint32_t prim_base) {
@@ -1300,46 +935,6 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
   if ((err = hipMemcpyAsync(rb, box, 24, hipMemcpyDeviceToHost, s)) || (err = hipStreamSynchronize(s))) return fail(err);
   for (int k = 0; k < 3; k++) { info->bmin[k] = rb[k]; info->bmax[k] = rb[3 + k]; }
   return fail(hipSuccess);
-}
-
-size_t gpu_small_scratch_bytes(int32_t n) {
-  const size_t nn = 2 * (size_t)std::max(n, 1) - 1, ni = (size_t)std::max(n - 1, 1);
-  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  return al(8 * (size_t)n) + 3 * al(4 * nn) + al(24 * nn) + al(64 * ni) + al(4 * ni) + 2 * al(sizeof(Task) * (size_t)n) +
-         al(16);
-}
-
-uint32_t* gpu_small_ctr(void* scratch, int32_t n) {
-  const size_t nn = 2 * (size_t)std::max(n, 1) - 1, ni = (size_t)std::max(n - 1, 1);
-  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  return reinterpret_cast<uint32_t*>(static_cast<char*>(scratch) + al(8 * (size_t)n) + 3 * al(4 * nn) + al(24 * nn) +
-                                     al(64 * ni) + al(4 * ni) + 2 * al(sizeof(Task) * (size_t)n));
-}
-
-hipError_t gpu_build_blas8_small(hipStream_t s, const float* tri_dev, int32_t n, int max_leaf, Node8* nodes_out,
-                                 TriMT* tris_out, void* scratch, uint32_t* out, uint32_t* level_end, int max_levels,
-                                 int radius, SmallTlasOut tlas) {
-  if (n <= 0 || n > kGpuSmallBuild) return hipErrorInvalidValue;
-  const size_t nn = 2 * (size_t)n - 1, ni = (size_t)std::max(n - 1, 1);
-  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  char* p = static_cast<char*>(scratch);
-  SmallScratch sc;
-  sc.keys = reinterpret_cast<unsigned long long*>(p); p += al(8 * (size_t)n);
-  sc.left = reinterpret_cast<int*>(p); p += al(4 * nn);
-  sc.right = reinterpret_cast<int*>(p); p += al(4 * nn);
-  sc.count = reinterpret_cast<uint32_t*>(p); p += al(4 * nn);
-  sc.box = reinterpret_cast<float*>(p); p += al(24 * nn);
-  sc.dp.C = reinterpret_cast<double*>(p); p += al(64 * ni);
-  sc.dp.dec = reinterpret_cast<uint32_t*>(p); p += al(4 * ni);
-  sc.ta = reinterpret_cast<Task*>(p); p += al(sizeof(Task) * (size_t)n);
-  sc.tb = reinterpret_cast<Task*>(p); p += al(sizeof(Task) * (size_t)n);
-  sc.ctr = reinterpret_cast<uint32_t*>(p);
-  if (n == 1) sc.dp = DpTab{nullptr, nullptr};  // the root is the single leaf
-  hipLaunchKernelGGL(k_build_small, dim3(1), dim3(kSmallThreads), 0, s, reinterpret_cast<const float4*>(tri_dev), n,
-                     max_leaf, sc, radius > 0 ? radius : kSmallR);
-  hipLaunchKernelGGL(k_collapse_small, dim3(1), dim3(kCollapseThreads), 0, s, reinterpret_cast<const float4*>(tri_dev),
-                     n, max_leaf, sc, nodes_out, tris_out, out, level_end, max_levels, tlas);
-  return hipGetLastError();
 }
 
 hipError_t gpu_blas_finish(hipStream_t s, Node8* nodes, uint32_t n_nodes, uint32_t node_base, const TriMT* tris,

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <string>
 #include <thread>
 #include <vector>
@@ -84,12 +85,6 @@ struct WaveState {
   uint32_t n = 0, levels = 0;
   bool ext = false, merge = false;
 };
-// a concurrent item group beyond the first: its own stream, wavefront state and join event
-struct ItemGroup {
-  hipStream_t stream = nullptr;
-  hipEvent_t done = nullptr;
-  WaveState ws;
-};
 // a frame in flight (prt_set_frames_in_flight): the wavefront chain of one call on its own stream.  Slot 0 uses the
 // context's own wavefront state and frame buffer, the others their own; done = the call's last work (the
 // accumulation, and for a sharded frame its gather and untile), which the next call's accumulation waits for
@@ -101,6 +96,19 @@ struct Flight {
   DevBuf frames;
   bool pending = false;  // done is not yet in the context stream's order
 };
+
+// one pinned staging buffer of ensure_instances' uploads (prt_ctx::stage): reused once its copies have run; the pool
+// grows to the updates the host is ahead of the GPU, up to kStageSlots (then the host waits for the oldest)
+constexpr size_t kStageSlots = 64;
+struct StageSlot {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipEvent_t ev = nullptr;
+  bool used = false;
+};
+// instance counts above which the per-update host build of the instance BVH runs on a worker thread
+// (ensure_instances; ~4 ms for 4,096 instances on the calling thread, 11-12 ms for 10,000)
+constexpr int32_t kHostSyncBuild = 4096;
 
 struct MeshHost {
   float bmin[3], bmax[3];
@@ -123,7 +131,7 @@ struct prt_ctx {
   std::vector<MeshHost> mesh_info;
   DevBuf nodes8, tris, stri, mesh;
   int max_depth = 0;
-  int builder = -1;  // BLAS builder: PRT_BUILDER_HOST_SAH / _GPU_LBVH / _HOST_SBVH (-1: PRT_BUILDER env, else host)
+  int builder = -1;  // BLAS builder (prt_set_bvh_builder): PRT_BUILDER_* (-1: PRT_BUILDER_HOST_SAH)
   double build_ms = 0;  // wall time of the last prt_set_meshes BLAS builds
   int built_with = PRT_BUILDER_HOST_SAH;
   // instances
@@ -132,38 +140,24 @@ struct prt_ctx {
   std::vector<uint32_t> inst_kind;  // prt_set_instance_materials (PRT_MAT_*), textured by default
   std::vector<InstSrc> inst_stage;  // host side of the refit input (prt_refit.h)
   DevBuf inst, inst_src;
-  // instance BVH (more than kLinearInstances instances, or PRT_TLAS=1): rebuilt on the host with the instances
+  // instance BVH (more than kLinearInstances instances, or PRT_TLAS=1), rebuilt for every prt_set_instances as the
+  // reference rebuilds its TLAS every frame (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770): the host SAH
+  // build + SAH-optimal collapse (bvh_build.h build_tlas8).  Up to kHostSyncBuild instances on the calling thread;
+  // above, on a worker thread (tlas_job) from the boxes of the update that started it, committed at the first
+  // update after it finished, and refitted on the device (prt_tlas.hip) to every update's boxes in between
   bool use_tlas = false;
   int tlas_depth = 0;
-  BuiltTlas8 tlas_host;  // the last host build (its topology is what the device refits)
-  TlasTopo tlas_topo;    // its nodes by depth, deepest first (prt_tlas.h)
-  int32_t tlas_n = -1;   // instance count of that build (-1: none)
+  TlasTopo tlas_topo;    // the current tree's nodes by depth, deepest first (prt_tlas.h): the device refit's order
+  int32_t tlas_n = -1;   // instance count of the current tree (-1: none)
   DevBuf tlas8, tlas_slot, tlas_order, tlas_aabb;
-  // device rebuild of the instance BVH when refitting has degraded it (ensure_instances): build scratch, the tree's
-  // SAH cost after every refit (device -> pinned host copy, read back without a host wait once its event is done)
-  DevBuf tlas_fat, tlas_tris, tlas_cost_dev, tlas_boxes;
-  // the rebuild runs on its own stream into back buffers while queued frames keep the current tree; the buffers
-  // swap behind an event (tlas_built) and the back buffers are written again only after the frames queued before
-  // the swap (tlas_back_free)
-  DevBuf tlas8_b, tlas_slot_b, tlas_order_b, tlas_aabb_b;
-  // up to kGpuSmallBuild instances (tlas_small): the tree is described on the device (TlasMeta: node count, refit
-  // levels), rebuilt by one workgroup from the side stream's own refit records (tlas_src -> tlas_inst) with no host
-  // round trip, and committed into the front buffers by a copy kernel on the render stream
-  bool tlas_small = false;
-  int tlas_depth_cap = 0;
-  TlasMeta tlas_meta_h{};  // host staging of the host build's meta (read by the async upload)
-  DevBuf tlas_meta, tlas_meta_b, tlas_small_scr, tlas_small_out, tlas_src, tlas_inst;
-  hipStream_t tlas_stream = nullptr;
-  hipEvent_t tlas_built = nullptr, tlas_back_free = nullptr;
-  bool tlas_back_busy = false;
-  double* tlas_cost_h = nullptr;  // pinned: [0] cost right after the last build, [1] after the latest refit
-  hipEvent_t tlas_cost_ev[2] = {nullptr, nullptr};
-  bool tlas_cost_pending[2] = {false, false};
-  double tlas_base_cost = 0.0;    // [0] once read
+  std::future<BuiltTlas8> tlas_job;  // the worker's build (large instance counts)
   uint32_t tlas_nodes = 0;
   int32_t tlas_rebuilds = 0, tlas_refits = 0;  // since the instance count last changed (diagnostics)
-  int32_t tlas_since_build = 0;                 // refits since the last build
-  bool tlas_build_pending = false;  // tlas_small: a build on the side stream awaits its commit at the next update
+  // pinned staging buffers of ensure_instances' uploads (instance sources, a new tree's nodes / slots / refit order;
+  // hipMemcpyAsync from pageable memory may block the host): a buffer is written again only after its copies have
+  // run, so the host never waits on queued frames unless it is kStageSlots updates ahead of the GPU
+  std::vector<StageSlot> stage;
+  size_t stage_next = 0;  // the oldest buffer in use (the one to wait for when the pool is full)
   DevBuf spill;  // traversal stack levels beyond the LDS ones (BVHs deeper than 17 levels)
   DevBuf diag;   // SceneDev::diag device counters ([0] traversal stack overflows, cumulative per context)
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
@@ -186,13 +180,9 @@ struct prt_ctx {
   int32_t accW = 0, accH = 0;
   DevBuf frames, avg, rgb8, counters, hits, tl;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  // wavefront state of the merged pipeline (the call's first item group)
+  // wavefront state of the merged pipeline (frame-in-flight slot 0 and calls in the context stream's order)
   WaveState ws;
   WaveTimers wt = {};
-  // concurrent item groups 1..G-1 of small calls (groups_for), created on first use
-  std::vector<ItemGroup> grp;
-  hipEvent_t fork = nullptr;
-  uint32_t last_groups = 1;
   // the last enqueued render, for its stats (read_stats)
   uint32_t last_iters = 0;
   bool last_timers = false;
@@ -299,33 +289,83 @@ int drain(prt_ctx* c) {
   return PRT_OK;
 }
 
-// triangles per leaf slot the builders may form (binary SAH leaves and the collapse's leaf slots); PRT_MAX_LEAF
-// overrides (A/B)
-int max_leaf_tris() {
-  const char* e = std::getenv("PRT_MAX_LEAF");
-  const int v = e ? std::atoi(e) : 3;
-  return v < 1 ? 1 : (v > 4 ? 4 : v);
-}
+// triangles per leaf slot the builders may form (binary SAH leaves and the collapse's leaf slots; 2 / 4 measured
+// no better on C4)
+int max_leaf_tris() { return 3; }
 
-// waves/SIMD of the persistent traversal kernels: the LDS stack (8 / 9 / 11 / 14 / 18 groups at 8 / 7 / 6 / 5 / 4
+// waves/SIMD of the persistent traversal kernels: the LDS stack (9 / 11 / 14 / 18 groups at 7 / 6 / 5 / 4
 // waves) must hold max_depth - 1 groups; deeper BVHs (depth_ok caps them at kMaxBvhDepth = 64 levels) run the
 // 4-wave form with HBM spill columns (ensure_spill)
-int occ_at(int d) {  // the occupancy a stack of d levels allows (PRT_OCC caps it; 8 only on request)
-  const char* e = std::getenv("PRT_OCC");
-  const int want = e ? std::atoi(e) : 7;
-  if (want >= 8 && d <= 9) return 8;
-  if (want >= 7 && d <= 10) return 7;
-  if (want >= 6 && d <= 12) return 6;
-  if (want >= 5 && d <= 15) return 5;
+int occ_at(int d) {  // the occupancy a stack of d levels allows (7 waves: re-measured best, profiles/r05_occupancy.txt)
+  if (d <= 10) return 7;
+  if (d <= 12) return 6;
+  if (d <= 15) return 5;
   return 4;
 }
 int occ_for(const prt_ctx* c) { return occ_at(stack_depth(c)); }
 
-// instance refit on the device (prt_refit.h): one async copy of the transforms + k_refit, both on the
-// render stream, so frames already queued keep reading the previous instances
+// a pinned staging buffer of at least `bytes` (prt_ctx::stage): a free one (its copies have run), a new one while
+// the pool holds fewer than kStageSlots, else the oldest once its copies have run (the only host wait)
+int stage_acquire(prt_ctx* c, size_t bytes, StageSlot*& out) {
+  StageSlot* pick = nullptr;
+  for (StageSlot& t : c->stage) {
+    if (t.used) {
+      const hipError_t q = hipEventQuery(t.ev);
+      if (q == hipErrorNotReady) {
+        (void)hipGetLastError();
+        continue;
+      }
+      HIP_TRY(q);
+      t.used = false;
+    }
+    if (!pick || (pick->bytes < bytes && t.bytes >= bytes)) pick = &t;
+  }
+  if (!pick && c->stage.size() < kStageSlots) {
+    c->stage.emplace_back();
+    pick = &c->stage.back();
+  }
+  if (!pick) {
+    pick = &c->stage[c->stage_next];
+    c->stage_next = (c->stage_next + 1) % c->stage.size();
+    HIP_TRY(hipEventSynchronize(pick->ev));
+    pick->used = false;
+  }
+  StageSlot& st = *pick;
+  if (st.bytes < bytes) {
+    if (st.p) HIP_TRY(hipHostFree(st.p));
+    st.p = nullptr;
+    st.bytes = 0;
+    HIP_TRY(hipHostMalloc(&st.p, bytes, hipHostMallocDefault));
+    st.bytes = bytes;
+  }
+  if (!st.ev) HIP_TRY(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
+  out = &st;
+  return PRT_OK;
+}
+// the copies out of the buffer are enqueued: it is free again once the stream has run them
+int stage_release(prt_ctx*, StageSlot& st, hipStream_t s) {
+  HIP_TRY(hipEventRecord(st.ev, s));
+  st.used = true;
+  return PRT_OK;
+}
+
+// Instance records on the device (prt_refit.h: MESA inverse, normal matrix, inflated world box): one async copy of
+// the transforms + k_refit on the render stream, so frames already queued keep reading the previous instances.
+// The instance BVH over those boxes (the same refit_instance on the host) is rebuilt for every update, as the
+// reference rebuilds its TLAS every frame (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770 BVH::Build over the
+// BLASInstances): up to kHostSyncBuild instances by the host SAH build + SAH-optimal collapse on the calling
+// thread, uploaded in stream order (~0.8 ms for 1,000 instances, no wait on the GPU; profiles/r05_tlas_rebuild.txt:
+// the drifting frames cost what a static frame costs); above kHostSyncBuild by the same build on a worker thread,
+// started from the boxes of one update and committed at the first update after it finished, the device refitting
+// the current tree to every update's boxes in between (the tree is at most one build old; no update waits for it)
 int ensure_instances(prt_ctx* c) {
   if (!c->inst_dirty) return PRT_OK;
   const int32_t n = (int32_t)c->inst_mesh.size();
+  const char* te = std::getenv("PRT_TLAS");  // 1: the instance BVH at any instance count (tests)
+  const bool use_tlas = n > kLinearInstances || (te && std::atoi(te) == 1);
+  // a materials-only update (prt_set_instance_materials) moves no box: the records' kinds are rewritten over
+  // unchanged inverses and boxes, and the instance BVH is left as it is
+  const bool tree_work = use_tlas && (c->tlas_dirty || !c->use_tlas || c->tlas_n != n);
   std::vector<InstSrc>& src = c->inst_stage;
   src.assign(n, InstSrc{});
   for (int32_t i = 0; i < n; i++) {
@@ -339,338 +379,92 @@ int ensure_instances(prt_ctx* c) {
     s.mesh = m;
     s.kind = i < (int32_t)c->inst_kind.size() ? c->inst_kind[i] : 0u;
   }
-  // buffers sized for n (at least the linear-list size); growing them frees what queued frames read: drain first
+  // the tree this update commits (sync build, or a finished worker build), and whether the device refits it
+  BuiltTlas8 tree;
+  bool have_tree = false, refit = false;
+  // the instances' world boxes (the same refit_instance as k_refit) and the host SAH build over them
+  auto build = [](const std::vector<InstSrc>& in) {
+    const int32_t m = (int32_t)in.size();
+    std::vector<float> boxes(6 * (size_t)m);
+    for (int32_t i = 0; i < m; i++) {
+      InstDev I;
+      refit_instance(in[i], I);
+      std::memcpy(&boxes[6 * (size_t)i], I.bmin, 12);
+      std::memcpy(&boxes[6 * (size_t)i + 3], I.bmax, 12);
+    }
+    return build_tlas8(boxes.data(), m);
+  };
+  if (tree_work) {
+    if (n <= kHostSyncBuild || c->tlas_n != n || !c->use_tlas) {
+      if (c->tlas_job.valid()) (void)c->tlas_job.get();  // a worker build for another instance set: dropped
+      tree = build(src);
+      have_tree = true;
+    } else {  // the worker computes the boxes too: the calling thread only copies the sources
+      if (c->tlas_job.valid() && c->tlas_job.wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
+        tree = c->tlas_job.get();
+        have_tree = true;
+      }
+      refit = true;  // the committed (or current) tree was built from earlier boxes
+      if (!c->tlas_job.valid()) c->tlas_job = std::async(std::launch::async, build, src);
+    }
+  }
+  // uploads through one pinned staging slot: the instance sources, then a new tree's nodes / slots / refit order
+  TlasTopo topo;
+  if (have_tree) topo = tlas_topology(tree.nodes);
+  const size_t sb_src = sizeof(InstSrc) * (size_t)n, sb_nodes = have_tree ? tree.nodes.size() * sizeof(Node8) : 0,
+               sb_slot = have_tree ? tree.slot.size() * 4 : 0, sb_order = have_tree ? topo.order.size() * 4 : 0;
+  // buffers sized for n (at least the linear-list size; a tree over n instances has at most n nodes), so later
+  // updates never reallocate (a reallocation frees what queued frames read: it drains first, a host wait)
   const size_t cap = (size_t)std::max(n, kLinearInstances);
-  if (c->inst.bytes < sizeof(InstDev) * cap || c->inst_src.bytes < sizeof(InstSrc) * cap) {
+  const size_t cap_nodes = have_tree ? std::max(tree.nodes.size(), (size_t)n) : 0;
+  if (c->inst.bytes < sizeof(InstDev) * cap || c->inst_src.bytes < sizeof(InstSrc) * cap ||
+      (have_tree && (c->tlas8.bytes < cap_nodes * sizeof(Node8) || c->tlas_slot.bytes < cap_nodes * 32 ||
+                     c->tlas_order.bytes < cap_nodes * 4 || c->tlas_aabb.bytes < cap_nodes * 24))) {
     const int rc = drain(c);
     if (rc) return rc;
     HIP_TRY(c->inst.ensure(sizeof(InstDev) * cap));
     HIP_TRY(c->inst_src.ensure(sizeof(InstSrc) * cap));
-  }
-  HIP_TRY(hipMemcpyAsync(c->inst_src.p, src.data(), sizeof(InstSrc) * n, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(launch_refit(c->stream, c->inst_src.as<InstSrc>(), n, c->inst.as<InstDev>()));
-  const char* te = std::getenv("PRT_TLAS");
-  const bool use_tlas = n > kLinearInstances || (te && std::atoi(te) == 1);
-  // a materials-only update (prt_set_instance_materials) moves no box: the refit above rewrote the records' kinds
-  // over unchanged inverses and boxes, and the instance BVH is neither refitted, measured nor rebuilt
-  if (!c->tlas_dirty && use_tlas == c->use_tlas && (!use_tlas || c->tlas_n == n)) {
-    c->inst_dirty = false;
-    return PRT_OK;
-  }
-  // instance BVH over the refit's world boxes (the same refit_instance on the host), BVH::Build over the
-  // BLASInstances every frame as the reference does (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770)
-  c->use_tlas = use_tlas;
-  // The instance BVH.  The reference rebuilds it every frame (Core/Renderer.cpp:33-41).  Here the host SAH builder
-  // builds it when the set of instances changes (its count), and by default for every update up to kGpuSmallBuild
-  // instances (below).  Otherwise:
-  //  - PRT_TLAS_SMALL=1 (up to kGpuSmallBuild instances): rebuilt on the device for every update by one workgroup on
-  //    a side stream from the side stream's own refit of the instance records (gpu_rebuild_tlas_small), committed
-  //    over the front tree by a copy kernel on the render stream -- no host BVH work and no host wait;
-  //  - above kGpuSmallBuild, or PRT_TLAS_SMALL=0: refitted on the device behind k_refit (prt_tlas.hip), and rebuilt
-  //    on the device by the multi-launch builder (PLOC + SAH-optimal collapse over host-computed boxes,
-  //    gpu_build_tlas8: one host round trip per PLOC iteration and collapse level) once refitting has raised the
-  //    tree's node-area cost above PRT_TLAS_REBUILD (default 1.05) times its cost right after the last build, or
-  //    after PRT_TLAS_MAX_REFITS refits (0: refit only).  The cost is measured on the device after every refit and
-  //    read back without a host wait (a pinned copy behind an event): a frame decides on the latest cost available.
-  // PRT_TLAS_REBUILD=always / <ratio> / 0 overrides the policy of either device builder.
-  // Up to kGpuSmallBuild instances the default is the host SAH build for every update (the reference's per-frame
-  // BVH::Build, on the calling thread, ~0.8 ms for 1,000 instances): measured on 1,000 drifting instances it costs
-  // the frames nothing (the host builds while the GPU renders the queued frames; no host wait), where every device
-  // build run beside the persistent traversal cost 5-7 % (profiles/r05_tlas_rebuild.txt session aa).
-  // PRT_TLAS_SMALL=1: the single-workgroup device build instead; PRT_TLAS_SMALL=0 or PRT_TLAS_REBUILD=<ratio> / 0:
-  // the device refit and the multi-launch builder's trigger; PRT_TLAS_HOST=1: the host build at any count.
-  const char* th = std::getenv("PRT_TLAS_HOST");
-  const char* tr = std::getenv("PRT_TLAS_REBUILD");
-  const char* ts = std::getenv("PRT_TLAS_SMALL");
-  const bool tr_always = tr && std::strcmp(tr, "always") == 0;
-  const bool host_tlas = (th && std::atoi(th) == 1) || (!ts && n <= kGpuSmallBuild && (!tr || tr_always));
-  const bool small_ok = ts && std::atoi(ts) == 1 && n <= kGpuSmallBuild && !host_tlas;
-  // the builder of the current tree decides the default policy (its instance count is unchanged on a refit)
-  const bool small_now = (use_tlas && c->tlas_n == n && !host_tlas) ? c->tlas_small : small_ok;
-  const bool rebuild_always = tr ? tr_always : small_now;
-  const double rebuild_ratio = rebuild_always ? 0.0 : (tr ? std::atof(tr) : 1.05);
-  // and at the latest after PRT_TLAS_MAX_REFITS refits (default 8): the node-area cost understates what a node
-  // stretched across the scene costs the rays that must now open it
-  const char* tm = std::getenv("PRT_TLAS_MAX_REFITS");
-  const int32_t max_refits = tm ? std::atoi(tm) : 8;
-  auto upload_order = [&]() -> int {
-    const size_t cap_nodes = std::max<size_t>(c->tlas_nodes, (c->tlas_small || host_tlas) ? (size_t)n : 1);
-    const size_t ob = 4 * std::max(c->tlas_topo.order.size(), cap_nodes), ab = 24 * cap_nodes;
-    if (c->tlas_order.bytes < ob || c->tlas_aabb.bytes < ab) {
-      const int rc = drain(c);
-      if (rc) return rc;
-      HIP_TRY(c->tlas_order.ensure(ob));
-      HIP_TRY(c->tlas_aabb.ensure(ab));
-    }
-    HIP_TRY(hipMemcpyAsync(c->tlas_order.p, c->tlas_topo.order.data(), 4 * c->tlas_topo.order.size(),
-                           hipMemcpyHostToDevice, c->stream));
-    return PRT_OK;
-  };
-  // the tree's cost over its current boxes into pinned slot k (0: right after a build, 1: after a refit)
-  auto measure_cost = [&](int k) -> int {
-    if (rebuild_ratio <= 0) return PRT_OK;
-    if (!c->tlas_cost_h) {
-      HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->tlas_cost_h), 2 * sizeof(double), hipHostMallocDefault));
-      for (auto& e : c->tlas_cost_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      HIP_TRY(c->tlas_cost_dev.ensure(2 * sizeof(double)));
-    }
-    HIP_TRY(launch_tlas_cost(c->stream, c->tlas8.as<Node8>(), c->tlas_nodes, c->tlas_aabb.as<float>(),
-                             c->inst.as<InstDev>(), c->tlas_slot.as<uint32_t>(), c->tlas_cost_dev.as<double>() + k,
-                             c->tlas_small ? c->tlas_meta.as<TlasMeta>() : nullptr));
-    HIP_TRY(hipMemcpyAsync(c->tlas_cost_h + k, c->tlas_cost_dev.as<double>() + k, sizeof(double),
-                           hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipEventRecord(c->tlas_cost_ev[k], c->stream));
-    c->tlas_cost_pending[k] = true;
-    return PRT_OK;
-  };
-  auto refit_tree = [&]() -> int {
-    if (c->tlas_small)
-      HIP_TRY(launch_tlas_refit_meta(c->stream, c->inst.as<InstDev>(), c->tlas_meta.as<TlasMeta>(),
-                                     c->tlas_order.as<uint32_t>(), c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(),
-                                     c->tlas_aabb.as<float>()));
-    else
-      HIP_TRY(launch_tlas_refit(c->stream, c->inst.as<InstDev>(), c->tlas_topo, c->tlas_order.as<uint32_t>(),
-                                c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(), c->tlas_aabb.as<float>()));
-    return PRT_OK;
-  };
-  if (c->use_tlas && c->tlas_n == n && !host_tlas) {
-    bool rebuild = rebuild_always ||
-                   (rebuild_ratio > 0 && max_refits > 0 && c->tlas_since_build >= max_refits);
-    if (rebuild_ratio > 0) {
-      for (int k = 0; k < 2; k++) {  // costs whose copies have landed (never waits)
-        if (!c->tlas_cost_pending[k]) continue;
-        const hipError_t q = hipEventQuery(c->tlas_cost_ev[k]);
-        if (q == hipErrorNotReady) {
-          (void)hipGetLastError();  // not an error here: the cost is read by a later update
-          continue;
-        }
-        HIP_TRY(q);
-        c->tlas_cost_pending[k] = false;
-        if (k == 0) c->tlas_base_cost = c->tlas_cost_h[0];
-        else if (c->tlas_base_cost > 0 && c->tlas_cost_h[1] > rebuild_ratio * c->tlas_base_cost) rebuild = true;
-      }
-    }
-    if (c->tlas_small) {
-      // Single-workgroup builder.  A build: the side stream refits its own copy of the instance records and one
-      // workgroup builds the tree into the back buffers (gpu_rebuild_tlas_small); a commit: a copy kernel on the
-      // render stream replaces the front tree with a finished build, unless it came out deeper than the stacks
-      // were sized for (k_tlas_commit); the back buffers are written again only after that copy (tlas_back_free).
-      // Then the front tree is refitted over this frame's boxes (k_refit above).  By default the build of this
-      // update's boxes is committed at once (the render stream waits for it, as the reference's BVH::Build
-      // precedes the frame); PRT_TLAS_PIPELINE=1 commits it at the next update instead (the build then runs
-      // beside this frame's rendering; measured slower, profiles/r05_tlas_rebuild.txt).  No host wait either way.
-      if (!c->tlas_stream) {
-        int lo = 0, hi = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIP_TRY(hipStreamCreateWithPriority(&c->tlas_stream, hipStreamNonBlocking, hi));
-        HIP_TRY(hipEventCreateWithFlags(&c->tlas_built, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&c->tlas_back_free, hipEventDisableTiming));
-      }
-      const char* tp = std::getenv("PRT_TLAS_PIPELINE");
-      const bool pipelined = tp && std::atoi(tp) == 1;
-      auto launch_build = [&]() -> int {
-        if (c->tlas_back_busy) HIP_TRY(hipStreamWaitEvent(c->tlas_stream, c->tlas_back_free, 0));
-        const size_t scr = gpu_small_scratch_bytes(n);
-        if (c->tlas_fat.bytes < 48ull * n || c->tlas_tris.bytes < sizeof(TriMT) * (size_t)n ||
-            c->tlas8_b.bytes < sizeof(Node8) * (size_t)n || c->tlas_slot_b.bytes < 32ull * n ||
-            c->tlas_order_b.bytes < 4ull * n || c->tlas_meta_b.bytes < sizeof(TlasMeta) ||
-            c->tlas_small_scr.bytes < scr || c->tlas_small_out.bytes < 4ull * (4 + kTlasMaxLevels) ||
-            c->tlas_src.bytes < sizeof(InstSrc) * (size_t)n || c->tlas_inst.bytes < sizeof(InstDev) * (size_t)n) {
-          const int drc = drain(c);  // the back buffers are free (commit read them) before they are reallocated
-          if (drc) return drc;
-          HIP_TRY(hipStreamSynchronize(c->tlas_stream));
-          HIP_TRY(c->tlas_fat.ensure(48ull * n));
-          HIP_TRY(c->tlas_tris.ensure(sizeof(TriMT) * (size_t)n));
-          HIP_TRY(c->tlas8_b.ensure(sizeof(Node8) * (size_t)n));
-          HIP_TRY(c->tlas_slot_b.ensure(32ull * n));
-          HIP_TRY(c->tlas_order_b.ensure(4ull * n));
-          HIP_TRY(c->tlas_meta_b.ensure(sizeof(TlasMeta)));
-          HIP_TRY(c->tlas_small_scr.ensure(scr));
-          HIP_TRY(c->tlas_small_out.ensure(4ull * (4 + kTlasMaxLevels)));
-          HIP_TRY(c->tlas_src.ensure(sizeof(InstSrc) * (size_t)n));
-          HIP_TRY(c->tlas_inst.ensure(sizeof(InstDev) * (size_t)n));
-        }
-        HIP_TRY(hipMemcpyAsync(c->tlas_src.p, src.data(), sizeof(InstSrc) * (size_t)n, hipMemcpyHostToDevice,
-                               c->tlas_stream));
-        HIP_TRY(launch_refit(c->tlas_stream, c->tlas_src.as<InstSrc>(), n, c->tlas_inst.as<InstDev>()));
-        HIP_TRY(gpu_rebuild_tlas_small(c->tlas_stream, c->tlas_inst.as<InstDev>(), n, c->tlas_fat.as<float>(),
-                                       c->tlas_tris.as<TriMT>(), c->tlas_small_scr.p, c->tlas_small_out.as<uint32_t>(),
-                                       c->tlas8_b.as<Node8>(), c->tlas_slot_b.as<uint32_t>(),
-                                       c->tlas_order_b.as<uint32_t>(), c->tlas_meta_b.as<TlasMeta>(),
-                                       c->tlas_depth_cap));
-        HIP_TRY(hipEventRecord(c->tlas_built, c->tlas_stream));
-        c->tlas_build_pending = true;
-        c->tlas_rebuilds++;
-        c->tlas_since_build = 0;
-        return PRT_OK;
-      };
-      int rc = PRT_OK;
-      if (rebuild && !pipelined) rc = launch_build();
-      if (rc) return rc;
-      const bool committed = c->tlas_build_pending;
-      if (committed) {
-        HIP_TRY(hipStreamWaitEvent(c->stream, c->tlas_built, 0));
-        HIP_TRY(launch_tlas_commit(c->stream, c->tlas_meta_b.as<TlasMeta>(), c->tlas8_b.as<Node8>(),
-                                   c->tlas_slot_b.as<uint32_t>(), c->tlas_order_b.as<uint32_t>(),
-                                   c->tlas_meta.as<TlasMeta>(), c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(),
-                                   c->tlas_order.as<uint32_t>(), c->diag.as<uint32_t>() + 2));
-        HIP_TRY(hipEventRecord(c->tlas_back_free, c->stream));
-        c->tlas_back_busy = true;
-        c->tlas_build_pending = false;
-      }
-      rc = refit_tree();
-      if (rc) return rc;
-      if (committed) {  // the trigger's reference cost: the committed tree over this frame's boxes
-        c->tlas_base_cost = 0;
-        c->tlas_cost_pending[1] = false;
-        rc = measure_cost(0);
-      } else if (!rebuild && !c->tlas_cost_pending[1]) {
-        rc = measure_cost(1);  // at most one refit cost in flight
-      }
-      if (rc) return rc;
-      if (!rebuild) {  // (an update that starts a build counts as a rebuild)
-        c->tlas_refits++;
-        c->tlas_since_build++;
-      }
-      if (rebuild && pipelined) rc = launch_build();
-      if (rc) return rc;
-    } else if (rebuild) {
-      // boxes of the instances' current transforms (the same refit_instance as k_refit), built on the side stream
-      // into the back buffers: the frames already queued keep walking the current tree, the host waits only for
-      // the build's own steps
-      if (!c->tlas_stream) {
-        // the highest stream priority: the build's short dependent launches are dispatched ahead of the render
-        // stream's queued work as CUs free up, so the host's waits on the build stay short
-        int lo = 0, hi = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIP_TRY(hipStreamCreateWithPriority(&c->tlas_stream, hipStreamNonBlocking, hi));
-        HIP_TRY(hipEventCreateWithFlags(&c->tlas_built, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&c->tlas_back_free, hipEventDisableTiming));
-      }
-      std::vector<float> boxes(6 * (size_t)n);
-      for (int32_t i = 0; i < n; i++) {
-        InstDev I;
-        refit_instance(src[i], I);
-        std::memcpy(&boxes[6 * (size_t)i], I.bmin, 12);
-        std::memcpy(&boxes[6 * (size_t)i + 3], I.bmax, 12);
-      }
-      if (c->tlas_back_busy) HIP_TRY(hipStreamWaitEvent(c->tlas_stream, c->tlas_back_free, 0));
-      if (c->tlas_fat.bytes < 48ull * n || c->tlas_tris.bytes < sizeof(TriMT) * (size_t)n ||
-          c->tlas8_b.bytes < sizeof(Node8) * (size_t)n || c->tlas_slot_b.bytes < 32ull * n ||
-          c->tlas_boxes.bytes < 24ull * n || c->tlas_order_b.bytes < 4ull * n || c->tlas_aabb_b.bytes < 24ull * n) {
-        HIP_TRY(hipStreamSynchronize(c->tlas_stream));  // the back buffers are free (tlas_back_free) before realloc
-        HIP_TRY(c->tlas_fat.ensure(48ull * n));
-        HIP_TRY(c->tlas_tris.ensure(sizeof(TriMT) * (size_t)n));
-        HIP_TRY(c->tlas8_b.ensure(sizeof(Node8) * (size_t)n));
-        HIP_TRY(c->tlas_slot_b.ensure(32ull * n));
-        HIP_TRY(c->tlas_boxes.ensure(24ull * n));
-        HIP_TRY(c->tlas_order_b.ensure(4ull * n));
-        HIP_TRY(c->tlas_aabb_b.ensure(24ull * n));
-      }
-      HIP_TRY(hipMemcpyAsync(c->tlas_boxes.p, boxes.data(), 24ull * n, hipMemcpyHostToDevice, c->tlas_stream));
-      TlasTopo topo;
-      int depth = 0;
-      uint32_t nn = 0;
-      HIP_TRY(gpu_build_tlas8(c->tlas_stream, c->tlas_boxes.as<float>(), n, c->tlas_fat.as<float>(),
-                              c->tlas_tris.as<TriMT>(), c->tlas8_b.as<Node8>(), c->tlas_slot_b.as<uint32_t>(), &topo,
-                              &depth, &nn));
-      HIP_TRY(hipMemcpyAsync(c->tlas_order_b.p, topo.order.data(), 4 * topo.order.size(), hipMemcpyHostToDevice,
-                             c->tlas_stream));
-      HIP_TRY(hipEventRecord(c->tlas_built, c->tlas_stream));
-      // swap: frames queued from here on walk the new tree (after the build, in stream order); the old one becomes
-      // the back buffer once the frames queued before this point are done
-      HIP_TRY(hipStreamWaitEvent(c->stream, c->tlas_built, 0));
-      HIP_TRY(hipEventRecord(c->tlas_back_free, c->stream));
-      c->tlas_back_busy = true;
-      std::swap(c->tlas8, c->tlas8_b);
-      std::swap(c->tlas_slot, c->tlas_slot_b);
-      std::swap(c->tlas_order, c->tlas_order_b);
-      std::swap(c->tlas_aabb, c->tlas_aabb_b);
-      c->tlas_topo = std::move(topo);
-      c->tlas_depth = depth;
-      c->tlas_nodes = nn;
-      int rc = refit_tree();  // the new tree re-quantised over this frame's boxes (k_refit above); its aabb for the cost
-      if (rc) return rc;
-      c->tlas_base_cost = 0;
-      c->tlas_cost_pending[1] = false;
-      rc = measure_cost(0);
-      if (rc) return rc;
-      c->tlas_rebuilds++;
-      c->tlas_since_build = 0;
-    } else {
-      int rc = refit_tree();
-      if (rc) return rc;
-      c->tlas_refits++;
-      c->tlas_since_build++;
-      if (!c->tlas_cost_pending[1]) {  // at most one refit cost in flight
-        rc = measure_cost(1);
-        if (rc) return rc;
-      }
-    }
-  } else if (c->use_tlas) {
-    std::vector<float> boxes(6 * (size_t)n);
-    for (int32_t i = 0; i < n; i++) {
-      InstDev I;
-      refit_instance(src[i], I);
-      std::memcpy(&boxes[6 * (size_t)i], I.bmin, 12);
-      std::memcpy(&boxes[6 * (size_t)i + 3], I.bmax, 12);
-    }
-    c->tlas_host = build_tlas8(boxes.data(), n);
-    c->tlas_depth = c->tlas_host.depth;
-    c->tlas_nodes = (uint32_t)c->tlas_host.nodes.size();
-    // the sync-free device rebuild (up to kGpuSmallBuild instances): the front buffers hold any tree of n instances,
-    // and the stacks are sized one level deeper than the host tree so a device tree of that depth is usable
-    c->tlas_small = small_ok && (rebuild_always || rebuild_ratio > 0);
-    c->tlas_build_pending = false;  // a build still on the side stream was for the previous instance set
-    if (c->tlas_small) {
-      // one level of slack for the device trees (a deeper build is not committed and the refitted tree stays:
-      // prt_scene_info.tlas_rejected counts them).  PRT_TLAS_SLACK=auto drops the slack where it costs the traversal
-      // kernels a wave per SIMD: on the 1,000-instance drift that rejected 20 % of the builds and was slower than
-      // running one wave fewer (profiles/r05_tlas_rebuild.txt)
-      const int d0 = c->max_depth + c->tlas_depth;
-      const char* sl = std::getenv("PRT_TLAS_SLACK");
-      const bool slack = !(sl && std::strcmp(sl, "auto") == 0) || occ_at(d0 + 1) == occ_at(d0);
-      c->tlas_depth_cap = c->tlas_depth + (slack ? 1 : 0);
-      c->tlas_depth = c->tlas_depth_cap;
-    }
-    // (a tree over n instances has at most n nodes: sized for that once, the builds for later updates, host or
-    // device, never reallocate -- a reallocation drains the queued frames, a host wait)
-    const size_t cap_nodes = (c->tlas_small || host_tlas) ? std::max<size_t>(c->tlas_host.nodes.size(), (size_t)n)
-                                                          : c->tlas_host.nodes.size();
-    const size_t nb = c->tlas_host.nodes.size() * sizeof(Node8), sb = c->tlas_host.slot.size() * 4;
-    if (c->tlas8.bytes < cap_nodes * sizeof(Node8) || c->tlas_slot.bytes < cap_nodes * 32 ||
-        (c->tlas_small && c->tlas_meta.bytes < sizeof(TlasMeta))) {
-      const int rc = drain(c);
-      if (rc) return rc;
+    if (have_tree) {
       HIP_TRY(c->tlas8.ensure(cap_nodes * sizeof(Node8)));
       HIP_TRY(c->tlas_slot.ensure(cap_nodes * 32));
-      if (c->tlas_small) HIP_TRY(c->tlas_meta.ensure(sizeof(TlasMeta)));
+      HIP_TRY(c->tlas_order.ensure(cap_nodes * 4));
+      HIP_TRY(c->tlas_aabb.ensure(cap_nodes * 24));
     }
-    c->tlas_topo = tlas_topology(c->tlas_host.nodes);
-    HIP_TRY(hipMemcpyAsync(c->tlas8.p, c->tlas_host.nodes.data(), nb, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->tlas_slot.p, c->tlas_host.slot.data(), sb, hipMemcpyHostToDevice, c->stream));
-    if (c->tlas_small) {
-      c->tlas_meta_h = tlas_meta(c->tlas_topo, c->tlas_nodes);
-      HIP_TRY(hipMemcpyAsync(c->tlas_meta.p, &c->tlas_meta_h, sizeof(TlasMeta), hipMemcpyHostToDevice, c->stream));
-    }
-    int rc = upload_order();
-    if (rc) return rc;
-    if (c->tlas_n != n) c->tlas_rebuilds = c->tlas_refits = 0;
-    else c->tlas_rebuilds++;  // a host build for an update of the same instance set
-    c->tlas_since_build = 0;
-    c->tlas_n = n;
-    if (rebuild_ratio > 0 && !host_tlas) {  // the cost right after the build (its refit's boxes)
-      rc = refit_tree();
-      if (rc) return rc;
-      c->tlas_base_cost = 0;
-      c->tlas_cost_pending[1] = false;
-      rc = measure_cost(0);
-      if (rc) return rc;
-    }
-  } else {
+  }
+  StageSlot* st = nullptr;
+  int rc = stage_acquire(c, sb_src + sb_nodes + sb_slot + sb_order, st);
+  if (rc) return rc;
+  char* hp = static_cast<char*>(st->p);
+  std::memcpy(hp, src.data(), sb_src);
+  HIP_TRY(hipMemcpyAsync(c->inst_src.p, hp, sb_src, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(launch_refit(c->stream, c->inst_src.as<InstSrc>(), n, c->inst.as<InstDev>()));
+  if (have_tree) {
+    char* q = hp + sb_src;
+    std::memcpy(q, tree.nodes.data(), sb_nodes);
+    std::memcpy(q + sb_nodes, tree.slot.data(), sb_slot);
+    std::memcpy(q + sb_nodes + sb_slot, topo.order.data(), sb_order);
+    HIP_TRY(hipMemcpyAsync(c->tlas8.p, q, sb_nodes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->tlas_slot.p, q + sb_nodes, sb_slot, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->tlas_order.p, q + sb_nodes + sb_slot, sb_order, hipMemcpyHostToDevice, c->stream));
+  }
+  rc = stage_release(c, *st, c->stream);
+  if (rc) return rc;
+  c->use_tlas = use_tlas;
+  if (!use_tlas) {
     c->tlas_depth = 0;
     c->tlas_n = -1;
-    c->tlas_small = false;
+  } else if (have_tree) {
+    c->tlas_topo = std::move(topo);
+    c->tlas_depth = tree.depth;
+    c->tlas_nodes = (uint32_t)tree.nodes.size();
+    if (c->tlas_n != n) c->tlas_rebuilds = c->tlas_refits = 0;
+    else c->tlas_rebuilds++;  // a rebuild for an update of the same instance set
+    c->tlas_n = n;
+  }
+  if (refit) {  // the tree's boxes re-quantised over this update's instance boxes, in stream order
+    HIP_TRY(launch_tlas_refit(c->stream, c->inst.as<InstDev>(), c->tlas_topo, c->tlas_order.as<uint32_t>(),
+                              c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(), c->tlas_aabb.as<float>()));
+    if (!have_tree) c->tlas_refits++;
   }
   c->inst_dirty = false;
   c->tlas_dirty = false;
@@ -905,35 +699,19 @@ struct RenderPlan {
   uint64_t per = 0;
   bool ext = false, merge = false;
   uint32_t iters = 0;
-  uint32_t groups = 1;
 };
 
 // The merged pipeline (prt_wave2.hip k_shade2m): AA frames of render mode 0 without extensions, in calls small
 // enough that their traversal launches are bound by their slowest rays (one launch fewer per frame: world-8 share
 // of C4 1.83-1.87 -> 1.74-1.77 ms), not by throughput (the path-2 first segments shaded in partly filled waves
-// cost a full C4 frame 1.5 %).  PRT_MERGE=0 / 1 forces it off / on; PRT_MERGE_MAX_ITEMS sets the size limit
-// (default 2^21 items per call).  Its shadow-queue entries index 4 x (slot x n + item) + k in 29 bits: at most 2^26
+// cost a full C4 frame 1.5 %), up to 2^21 items per call.  PRT_MERGE=0 / 1 forces it off / on (tests).  Its shadow-queue entries index 4 x (slot x n + item) + k in 29 bits: at most 2^26
 // items per pass.
 constexpr uint64_t kMaxMergedPassItems = 1ull << 26;
 bool merge_for(const prt_render_params* p, bool ext, uint64_t per) {
   const bool ok = !ext && p->render_mode == 0 && (p->flags & PRT_FLAG_AA) && p->bounces > 0 && per <= kMaxMergedPassItems;
   const char* e = std::getenv("PRT_MERGE");
   if (e) return ok && std::atoi(e) != 0;
-  const char* m = std::getenv("PRT_MERGE_MAX_ITEMS");
-  const uint64_t cap = m ? std::strtoull(m, nullptr, 10) : (1ull << 21);
-  return ok && per * (uint64_t)frames_of(p) <= cap;
-}
-
-// Concurrent item groups.  A call small enough that its traversal launches are bound by their
-// slowest rays (world-8 shares) can cut its items into G contiguous ranges, each with its own queues, stream and
-// launch chain, every grid 1/G of the resident blocks so the G chains co-reside and one chain's launch tail
-// overlaps another's busy phase.  PRT_GROUPS=1/2/4 (one-pass calls without HBM stack spill; default 1).
-uint32_t groups_for(const SceneDev& S, uint64_t items, int32_t npass) {
-  const char* e = std::getenv("PRT_GROUPS");
-  uint32_t g = e ? (uint32_t)std::max(1, std::atoi(e)) : 1u;
-  g = g >= 4 ? 4u : (g >= 2 ? 2u : 1u);
-  if (npass > 1 || S.spill || items < 256ull * g) g = 1;  // the spill columns are indexed by launch thread
-  return g;
+  return ok && per * (uint64_t)frames_of(p) <= (1ull << 21);
 }
 
 int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int32_t rank, RenderPlan& R,
@@ -978,25 +756,9 @@ int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int
     return fail(PRT_ERR_UNSUPPORTED, S.has_diel ? "dielectric path trees exceed the wavefront iteration limit (lower bounces)"
                                                 : "too many wavefront iterations");
   // sized for the first (largest) pass; later passes hold no more items
-  const uint64_t n0 = per * (uint64_t)F0;
-  const uint32_t G = fl ? 1u : groups_for(S, n0, npass);
-  for (uint32_t g = 0; g < G; g++) {
-    if (g > 0 && c->grp.size() < g) {  // a concurrent group's stream and join event (created once)
-      ItemGroup ig;
-      HIP_TRY(hipStreamCreateWithFlags(&ig.stream, hipStreamNonBlocking));
-      if (hipEventCreateWithFlags(&ig.done, hipEventDisableTiming) != hipSuccess) {
-        (void)hipStreamDestroy(ig.stream);
-        return fail(PRT_ERR_HIP, "hipEventCreate failed");
-      }
-      c->grp.push_back(std::move(ig));
-    }
-    if (g > 0 && !c->fork) HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
-    WaveState& w = g == 0 ? flight_ws(c, fl) : c->grp[g - 1].ws;
-    rc = ensure_wave(w, (uint32_t)(n0 * (g + 1) / G - n0 * g / G), p->bounces, ext, merge);
-    if (rc) return rc;
-  }
+  rc = ensure_wave(flight_ws(c, fl), (uint32_t)(per * (uint64_t)F0), p->bounces, ext, merge);
+  if (rc) return rc;
   R.F = F; R.fmax = fmax; R.npass = npass; R.F0 = F0; R.per = per; R.ext = ext; R.merge = merge; R.iters = iters;
-  R.groups = G;
   return PRT_OK;
 }
 
@@ -1014,36 +776,23 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
   const bool ext = R.ext;
   const uint32_t iters = R.iters;
   int rc = PRT_OK;
-  const uint32_t G = R.groups;
   const hipStream_t st = fl ? fl->stream : c->stream;
   WaveState& ws0 = flight_ws(c, fl);
   LaunchCfg L{st, occ_for(c), 1};
-  // frames in flight: PRT_FLIGHT_GRID = 2 / 4 runs each chain's wavefront grids at 1/2 / 1/4 of the resident blocks
-  // (A/B: the chains' persistent traversal launches co-reside instead of taking the whole GPU in turns)
-  // (default: half grids from 4 frames in flight on: world-8 share of C4 1.23-1.28 -> 1.15 ms, world 1 unchanged,
-  // profiles/r05_inflight.txt)
-  uint32_t Gw = G;
-  if (fl) {
-    const char* e = std::getenv("PRT_FLIGHT_GRID");
-    const int v = e ? std::atoi(e) : (c->inflight >= 4 ? 2 : 1);
-    Gw = v >= 8 ? 8u : (v >= 4 ? 4u : (v >= 2 ? 2u : 1u));
-  }
-  // The single-workgroup instance-BVH build (tlas_small, one 1,024-thread workgroup with ~144 KB of LDS) can only
-  // start on a CU the traversal waves have left; the traversal launches that follow must then not need that CU, or
-  // they end only after the build: their grid leaves one CU's worth of blocks out (PRT_SPARE_CU=0 / 1 forces it)
-  const char* esc = std::getenv("PRT_SPARE_CU");
-  const uint32_t spare = esc ? (std::atoi(esc) ? 1u : 0u) : ((c->use_tlas && c->tlas_small) ? 1u : 0u);
-  auto gws = [&](uint32_t g) -> WaveState& { return g == 0 ? ws0 : c->grp[g - 1].ws; };
-  auto gcfg = [&](uint32_t g) { return LaunchCfg{g == 0 ? st : c->grp[g - 1].stream, L.occ, Gw, spare}; };
+  // frames in flight: from 4 frames in flight on, each chain's wavefront grids are half the resident blocks, so the
+  // chains' persistent traversal launches co-reside instead of taking the whole GPU in turns (C4 world-8 share
+  // 1.32 ms with 2 in flight, 1.24 with 4 and half grids; quarter / eighth grids and 6 or 8 in flight 1.31-1.77 ms:
+  // profiles/r06_rank_shares.txt)
+  const uint32_t Gw = (fl && c->inflight >= 4) ? 2u : 1u;
+  const LaunchCfg Lw{st, L.occ, Gw};  // the wavefront chain's launches
   // the call's own events (prt_stats ms / ms_trace) only with stats: each record is a gap between kernels
   if (want_stats) HIP_TRY(hipEventRecord(c->ev[0], st));
   // PRT_TAIL=0 switches the cooperative traversal tail off (prt_persist.h; A/B runs only)
   const char* et = std::getenv("PRT_TAIL");
   const int32_t coop = (et && std::atoi(et) == 0) ? 0 : 1;
-  // per-launch traversal timers (HIP events around every k_trace launch) with stats, unless
-  // PRT_LAUNCH_TIMERS=0: each event record costs a few us between kernels (one-pass, one-group calls only)
-  const char* elt = std::getenv("PRT_LAUNCH_TIMERS");
-  const bool timers = want_stats && npass == 1 && G == 1 && !(elt && std::strcmp(elt, "0") == 0);
+  // per-launch traversal timers (HIP events around every k_trace launch) with stats (one-pass calls): each event
+  // record costs a few us between kernels, so only the stats calls carry them
+  const bool timers = want_stats && npass == 1;
   unsigned long long* tl = nullptr;
   if (want_stats && std::getenv("PRT_DEBUG_QUEUES")) {
     const size_t tlb = 32ull * kTlWaves * (kMaxIters + 2);
@@ -1058,37 +807,23 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
     const bool last = pass == npass - 1;
     A.frame_index = p->frame_index + f0;
     A.frames = Fb;
-    const uint64_t nb = per * (uint64_t)Fb;  // this pass's items, cut into G contiguous ranges
+    const uint64_t nb = per * (uint64_t)Fb;  // this pass's items
     float4* frames = flight_frames(c, fl).as<float4>();
-    if (G > 1) {  // the groups' streams start after everything already on the context stream
-      HIP_TRY(hipEventRecord(c->fork, st));
-      for (uint32_t g = 1; g < G; g++) HIP_TRY(hipStreamWaitEvent(gcfg(g).stream, c->fork, 0));
+    rc = ensure_wave(ws0, (uint32_t)nb, p->bounces, ext, R.merge);  // no allocation: prepare_render sized it for pass 0
+    if (rc) return rc;
+    ws0.wb.base = 0;
+    ws0.wb.coop_tail = coop;
+    ws0.wb.tl = tl;
+    {  // the queue counters and the fetch counters of the iterations this call uses (kMaxIters is the capacity)
+      const size_t qw = (size_t)(iters + 2) * 2 * kNSub * kCtrStride;
+      const size_t fbase = (size_t)(kMaxIters + 2) * 2 * kNSub * kCtrStride;
+      const size_t fw = (size_t)(iters + 2) * 2 * kParts * kCtrStride;
+      HIP_TRY(launch_clear2(Lw, ws0.wb.ctr, (uint32_t)qw, ws0.wb.ctr + fbase, (uint32_t)fw));
     }
-    for (uint32_t g = 0; g < G; g++) {
-      WaveState& w = gws(g);
-      const LaunchCfg Lg = gcfg(g);
-      const uint32_t b0 = (uint32_t)(nb * g / G), b1 = (uint32_t)(nb * (g + 1) / G);
-      rc = ensure_wave(w, b1 - b0, p->bounces, ext, R.merge);  // no allocation: prepare_render sized it for pass 0
-      if (rc) return rc;
-      w.wb.base = b0;
-      w.wb.coop_tail = coop;
-      w.wb.tl = g == 0 ? tl : nullptr;
-      {  // the queue counters and the fetch counters of the iterations this call uses (kMaxIters is the capacity)
-        const size_t qw = (size_t)(iters + 2) * 2 * kNSub * kCtrStride;
-        const size_t fbase = (size_t)(kMaxIters + 2) * 2 * kNSub * kCtrStride;
-        const size_t fw = (size_t)(iters + 2) * 2 * kParts * kCtrStride;
-        HIP_TRY(launch_clear2(Lg, w.wb.ctr, (uint32_t)qw, w.wb.ctr + fbase, (uint32_t)fw));
-      }
-      if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(w.wb.dst, 0, 4ull * w.wb.n, Lg.stream));
-      HIP_TRY(launch_wave_init(Lg, S, A, M, w.wb, frames + b0));
-    }
+    if (ext && S.has_diel) HIP_TRY(hipMemsetAsync(ws0.wb.dst, 0, 4ull * ws0.wb.n, st));
+    HIP_TRY(launch_wave_init(Lw, S, A, M, ws0.wb, frames));
     for (uint32_t it = 0; it <= iters; it++)
-      for (uint32_t g = 0; g < G; g++)
-        HIP_TRY(launch_wave2_iter(gcfg(g), S, A, M, gws(g).wb, frames + gws(g).wb.base, timers ? &c->wt : nullptr, it));
-    for (uint32_t g = 1; g < G; g++) {  // join: the accumulation reads every group's frame values
-      HIP_TRY(hipEventRecord(c->grp[g - 1].done, gcfg(g).stream));
-      HIP_TRY(hipStreamWaitEvent(st, c->grp[g - 1].done, 0));
-    }
+      HIP_TRY(launch_wave2_iter(Lw, S, A, M, ws0.wb, frames, timers ? &c->wt : nullptr, it));
     if (last && want_stats) HIP_TRY(hipEventRecord(c->ev[1], st));
     // post-processing (single-GPU image): the screen pass needs the average and, for the aberration, the
     // accumulator before the last frame
@@ -1103,14 +838,13 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
     HIP_TRY(launch_accumulate(L, M, Fb, p->flags, frames, c->acc.as<float4>(), c->nsamp.as<int32_t>(),
                               c->dist.as<float>(), avg_dev, post ? nullptr : rgb8_dev, tiles_dev, acc_prev,
                               ws0.wb.ctr, iters, ray_totals_dev(c)));
-    for (uint32_t g = 1; g < G; g++) HIP_TRY(launch_add_totals(L, gws(g).wb.ctr, iters, ray_totals_dev(c)));
     if (post && last) {
       // with !accumulates the accumulator held this frame's value until the end-of-frame memset
       const float4* acc_new = (p->flags & PRT_FLAG_ACCUMULATE) ? c->acc.as<float4>() : avg_dev;
       HIP_TRY(launch_postfx(L, post_params(c, p->width, p->height), acc_new, acc_prev, c->nsamp.as<int32_t>(),
                             avg_dev, rgb8_dev));
     }
-    if (want_stats && !last) {  // this pass's ray counts, before the next pass clears the counters (G == 1)
+    if (want_stats && !last) {  // this pass's ray counts, before the next pass clears the counters
       std::vector<uint32_t> ctr((size_t)(iters + 2) * 2 * kNSub * kCtrStride);
       HIP_TRY(hipMemcpyAsync(ctr.data(), ws0.wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
@@ -1124,7 +858,6 @@ int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, Ren
   if (want_stats) HIP_TRY(hipEventRecord(c->ev[2], st));
   c->last_iters = iters;
   c->last_timers = timers;
-  c->last_groups = G;
   c->last_paths = tile_image_pixels(M) * (uint64_t)F * ((p->flags & PRT_FLAG_AA) ? 2u : 1u);
   return check_layout_once(c, st);
 }
@@ -1205,13 +938,6 @@ int read_stats(prt_ctx* c, prt_stats* stats) {
     // the queue counters of the iterations this render used (the whole array with the queue dump)
     std::vector<uint32_t> ctr(dump ? kCtrWords : (size_t)(iters + 2) * 2 * kNSub * kCtrStride);
     HIP_TRY(hipMemcpyAsync(ctr.data(), c->ws.wb.ctr, 4 * ctr.size(), hipMemcpyDeviceToHost, c->stream));
-    // concurrent item groups: their queue counters add up (the render joined them into the context stream)
-    std::vector<uint32_t> gctr(ctr.size());
-    for (uint32_t g = 1; g < c->last_groups && g <= c->grp.size(); g++) {
-      HIP_TRY(hipMemcpyAsync(gctr.data(), c->grp[g - 1].ws.wb.ctr, 4 * gctr.size(), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      for (size_t i = 0; i < ctr.size(); i++) ctr[i] += gctr[i];
-    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     const WaveTimers& wt = c->wt;
     for (uint32_t k = 0; k <= iters + 1; k++) {  // iteration iters + 1: the merged path-2 primaries (Q2)
@@ -1587,20 +1313,11 @@ int prt_destroy(prt_ctx* c) {
   }
   c->comm = nullptr;
   if (c->sh_ev) (void)hipEventDestroy(c->sh_ev);
-  for (ItemGroup& g : c->grp) {
-    if (g.stream) (void)hipStreamSynchronize(g.stream);
-    if (g.done) (void)hipEventDestroy(g.done);
-    if (g.stream) (void)hipStreamDestroy(g.stream);
+  if (c->tlas_job.valid()) (void)c->tlas_job.get();  // the worker's build (host memory only)
+  for (StageSlot& st : c->stage) {  // the pinned upload ring (its copies ran: the streams are synchronised)
+    if (st.ev) (void)hipEventDestroy(st.ev);
+    if (st.p) (void)hipHostFree(st.p);
   }
-  c->grp.clear();
-  if (c->fork) (void)hipEventDestroy(c->fork);
-  for (auto e : c->tlas_cost_ev)
-    if (e) (void)hipEventDestroy(e);
-  if (c->tlas_stream) (void)hipStreamSynchronize(c->tlas_stream);
-  if (c->tlas_built) (void)hipEventDestroy(c->tlas_built);
-  if (c->tlas_back_free) (void)hipEventDestroy(c->tlas_back_free);
-  if (c->tlas_stream) (void)hipStreamDestroy(c->tlas_stream);
-  if (c->tlas_cost_h) (void)hipHostFree(c->tlas_cost_h);
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto e : c->wt.ev)
@@ -1672,14 +1389,7 @@ int prt_set_meshes(prt_ctx* c, const prt_mesh* m_in, int32_t n) {
   const prt_mesh* m = m_in;
   if (!c || !m || n <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad meshes");
   PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
-  int builder = c->builder;
-  if (builder < 0) {
-    const char* e = std::getenv("PRT_BUILDER");
-    builder = (e && std::strcmp(e, "gpu") == 0)    ? PRT_BUILDER_GPU_LBVH
-              : (e && std::strcmp(e, "ploc") == 0) ? PRT_BUILDER_GPU_PLOC
-              : (e && std::strcmp(e, "sbvh") == 0) ? PRT_BUILDER_HOST_SBVH
-                                                   : PRT_BUILDER_HOST_SAH;
-  }
+  const int builder = c->builder < 0 ? PRT_BUILDER_HOST_SAH : c->builder;
   const bool gpu = builder == PRT_BUILDER_GPU_LBVH || builder == PRT_BUILDER_GPU_PLOC;
   int rc = drain(c);
   if (rc) return rc;
@@ -2403,14 +2113,7 @@ int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
   info->tlas_depth = c->use_tlas ? c->tlas_depth : 0;
   info->tlas_rebuilds = c->tlas_rebuilds;
   info->tlas_refits = c->tlas_refits;
-  if (c->diag.p) {  // the commit kernel's count (diag word 2), after the queued work
-    PRT_JOIN(c);
-    uint32_t rej = 0;
-    HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemcpyAsync(&rej, c->diag.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    info->tlas_rejected = (int32_t)rej;
-  }
+  info->tlas_rejected = 0;  // (ABI 10: instance BVHs are built on the host only, none is ever rejected)
   info->build_ms = c->build_ms;
   info->builder = c->built_with;
   info->device_bytes = (int64_t)(c->nodes8.bytes + c->tris.bytes + c->stri.bytes + c->texels.bytes + c->sky.bytes +

@@ -17,11 +17,9 @@ struct HitOut {
 };
 struct LaunchCfg {
   hipStream_t stream;
-  int occ;     // persistent traversal waves/SIMD: 8 / 7 / 6 / 5 / 4 (8 / 9 / 11 / 14 / 18 LDS stack groups)
-  uint32_t groups = 1;  // concurrent item groups of the call: every wavefront grid is 1/groups of the resident
-                        // blocks, so the groups' launch chains co-reside on the SIMDs (prt_api.cpp)
-  uint32_t spare_cus = 0;  // CUs' worth of persistent traversal blocks left out of the grid (prt_api.cpp: room for
-                           // the instance-BVH build beside the traversal)
+  int occ;     // persistent traversal waves/SIMD: 7 / 6 / 5 / 4 (9 / 11 / 14 / 18 LDS stack groups)
+  uint32_t groups = 1;  // grid divisor: every wavefront grid is 1/groups of the resident blocks (frames in flight:
+                        // the chains' persistent launches co-reside on the SIMDs, prt_api.cpp enqueue_render)
 };
 
 // wavefront pipeline buffers (SoA over n work items; R/T hold (bounces-1) x n entries)
@@ -96,8 +94,6 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
                              const WaveBufs& B, float4* out, WaveTimers* tm, uint32_t it);
 // zero na words at a and nb words at b (one dispatch)
 hipError_t launch_clear2(const LaunchCfg& c, uint32_t* a, uint32_t na, uint32_t* b, uint32_t nb);
-// one concurrent item group's ray counts (queue counters ctr of `iters` iterations) added to totals
-hipError_t launch_add_totals(const LaunchCfg& c, const uint32_t* ctr, uint32_t iters, Counters* totals);
 // acc_prev (nullable): the accumulator state before the last frame of the call (screen-pass input);
 // totals (nullable): running ray totals, incremented by the queue counters ctr of the pass's `iters` iterations
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,

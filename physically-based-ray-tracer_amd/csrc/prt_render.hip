@@ -20,26 +20,6 @@ __device__ __forceinline__ void wave_count(Counters* c, uint32_t seg, uint32_t s
   }
 }
 
-// the ray counts of one concurrent item group's queue counters added to the running totals (one wave; the
-// call's first group is counted by k_accumulate)
-__global__ void __launch_bounds__(64) k_add_totals(const uint32_t* __restrict__ ctr, uint32_t iters,
-                                                   Counters* __restrict__ totals) {
-  unsigned long long seg = 0, sh = 0;
-  for (uint32_t j = threadIdx.x; j < (iters + 2u) * kNSub; j += 64) {  // (+2: P(iters + 1) holds the merged path-2 primaries)
-    const uint32_t k = j / kNSub, s = j % kNSub;
-    seg += ctr[((k * 2u + 0u) * kNSub + s) * kCtrStride];
-    sh += ctr[((k * 2u + 1u) * kNSub + s) * kCtrStride];
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    seg += __shfl_xor(seg, off, 64);
-    sh += __shfl_xor(sh, off, 64);
-  }
-  if (threadIdx.x == 0) {
-    atomicAdd(&totals->segments, seg);
-    atomicAdd(&totals->shadow, sh);
-  }
-}
-
 // Core/Renderer.cpp:81-104,137.  tiles_out != null: write the average in item (tile-compact) order.
 // totals != null: the first wave also adds this pass's ray counts (the closest / shadow queue counters of its
 // `iters` wavefront iterations) to the context's running totals (prt_ray_totals), so a caller can count rays
@@ -228,10 +208,6 @@ hipError_t launch_clear2(const LaunchCfg& c, uint32_t* a, uint32_t na, uint32_t*
   return hipGetLastError();
 }
 
-hipError_t launch_add_totals(const LaunchCfg& c, const uint32_t* ctr, uint32_t iters, Counters* totals) {
-  hipLaunchKernelGGL(k_add_totals, dim3(1), dim3(64), 0, c.stream, ctr, iters, totals);
-  return hipGetLastError();
-}
 
 hipError_t launch_accumulate(const LaunchCfg& c, const TileMap& M, int32_t frames, uint32_t flags, const float4* fr,
                              float4* acc, int32_t* nsamp, float* dist, float4* avg, uint32_t* rgb8, float4* tiles,

@@ -820,10 +820,10 @@ template <int STACK, int WAVES, int TAILN>
 void launch_t2(const LaunchCfg& c, const SceneDev& S, const WaveBufs& B, uint32_t it, uint32_t iters) {
   static_assert(2 * STACK * 256 + 264 + 4 * 3 * TAILN <= 163840 / (4 * WAVES), "LDS over the occupancy budget");
   if (S.tlas)
-    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, true>), dim3((256u - c.spare_cus) * 4u * WAVES / c.groups), dim3(64), 0,
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, true>), dim3(256u * 4u * WAVES / c.groups), dim3(64), 0,
                        c.stream, S, B, it, iters);
   else
-    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, false>), dim3((256u - c.spare_cus) * 4u * WAVES / c.groups), dim3(64), 0,
+    hipLaunchKernelGGL((k_trace2<PRT_REFILL, STACK, WAVES, TAILN, false>), dim3(256u * 4u * WAVES / c.groups), dim3(64), 0,
                        c.stream, S, B, it, iters);
 }
 // persistent traversal occupancy (waves/SIMD) -> LDS stack groups per lane; a BVH deeper than the 18 LDS
@@ -836,8 +836,7 @@ static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs&
     else
       hipLaunchKernelGGL((k_trace2<32, 18, 4, 32, false, true>), dim3(kSpillTraceBlocks / c.groups), dim3(64), 0,
                          c.stream, S, B, it, iters);
-  } else if (c.occ == 8) launch_t2<8, 8, 32>(c, S, B, it, iters);
-  else if (c.occ == 7) launch_t2<9, 7, 64>(c, S, B, it, iters);
+  } else if (c.occ == 7) launch_t2<9, 7, 64>(c, S, B, it, iters);
   else if (c.occ == 6) launch_t2<11, 6, 64>(c, S, B, it, iters);
   else if (c.occ == 5) launch_t2<14, 5, 32>(c, S, B, it, iters);
   else launch_t2<18, 4, 32>(c, S, B, it, iters);

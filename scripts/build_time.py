@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """BLAS build time and traversal rate per builder: the host SAH + SAH-optimal collapse
-against the device LBVH + SAH-optimal collapse (and its greedy collapse, PRT_COLLAPSE=greedy), on the bench scene (C4, 1M triangles) at the bench workload."""
+against the host SBVH and the device LBVH / PLOC builders (each + SAH-optimal collapse), on the bench scene (C4, 1M
+triangles) at the bench workload."""
 import os
 import sys
 import time
@@ -26,18 +27,13 @@ scene = prt.Scene.from_data(sd)
 avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
 rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
 print(f"BLAS builders ({sd.name}):", flush=True)
-for name, b, col in (("host SAH", _lib.BUILDER_HOST_SAH, None), ("host SBVH", _lib.BUILDER_HOST_SBVH, None),
-                     ("GPU LBVH + optimal collapse", _lib.BUILDER_GPU_LBVH, None),
-                     ("GPU PLOC + optimal collapse", _lib.BUILDER_GPU_PLOC, None),
-                     ("GPU LBVH + greedy collapse", _lib.BUILDER_GPU_LBVH, "greedy")):
+for name, b in (("host SAH", _lib.BUILDER_HOST_SAH), ("host SBVH", _lib.BUILDER_HOST_SBVH),
+                ("GPU LBVH + optimal collapse", _lib.BUILDER_GPU_LBVH),
+                ("GPU PLOC + optimal collapse", _lib.BUILDER_GPU_PLOC)):
     if "only-ploc" in sys.argv and "PLOC" not in name:  # A/B of PLOC variants (library builds)
         continue
-    if "only-gpu" in sys.argv and ("GPU" not in name or "greedy" in name):  # the device builders (PRT_TRBVH A/B)
+    if "only-gpu" in sys.argv and "GPU" not in name:  # the device builders (PRT_TRBVH A/B)
         continue
-    if col:
-        os.environ["PRT_COLLAPSE"] = col
-    else:
-        os.environ.pop("PRT_COLLAPSE", None)
     ctx.set_bvh_builder(b)
     ctx.set_scene(scene)
     ctx.set_scene(scene)  # second upload: warm caches / kernels

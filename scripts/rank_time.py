@@ -11,7 +11,7 @@ gather = a world-1 RCCL ncclGather (torch.distributed "nccl" over this one GPU) 
 events over 50 repetitions.  Efficiency = ms(world 1) / (N * frame(N)), against world 1 one frame at a time and
 with the same frames in flight.
 
-usage: rank_time.py [c5] [worlds...]   (env PRT_RANK_INFLIGHT: frames in flight of the shares, default 2)
+usage: rank_time.py [c5] [worlds...]   (env PRT_RANK_INFLIGHT: frames in flight of the shares; default bench.py's)
 prints one line per (world, rank) and a summary line per world; the timed frames run without stats, as bench.py's."""
 import os
 import sys
@@ -26,7 +26,11 @@ import prt  # noqa: E402
 from prt import scenes  # noqa: E402
 
 args = sys.argv[1:]
-INFLIGHT = int(os.environ.get("PRT_RANK_INFLIGHT", "2"))
+sys.path.insert(0, ROOT)
+from bench import default_inflight  # noqa: E402
+# frames in flight of the shares (default: bench.py's on several GPUs) and of the world-1 frame (bench.py's on one)
+INFLIGHT = int(os.environ.get("PRT_RANK_INFLIGHT", str(default_inflight(8))))
+INFLIGHT1 = default_inflight(1)
 WARM_S = float(os.environ.get("PRT_RANK_WARM_S", "0.5"))
 C5 = bool(args) and args[0] == "c5"
 if C5:
@@ -111,9 +115,9 @@ os.environ.setdefault("MASTER_PORT", "29531")
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
 scene = "c5" if C5 else "c4"
 w1_one, rays1 = share_ms(1, 0, 1)
-w1_fl, _ = share_ms(1, 0, INFLIGHT)
-print(f"{scene} world 1: frame {w1_one:.3f} ms one at a time, {w1_fl:.3f} ms with {INFLIGHT} in flight  rays {rays1}",
-      flush=True)
+w1_fl, _ = share_ms(1, 0, INFLIGHT1)
+print(f"{scene} world 1: frame {w1_one:.3f} ms one at a time, {w1_fl:.3f} ms with {INFLIGHT1} in flight  rays {rays1}; "
+      f"shares below with {INFLIGHT} in flight", flush=True)
 for world in WORLDS:
     ms = []
     for r in range(world):
@@ -125,7 +129,7 @@ for world in WORLDS:
     ser = mx + g + u
     print(f"{scene} world {world}: max share {mx:.3f} ms (rank {int(np.argmax(ms))}), mean {np.mean(ms):.3f}, "
           f"min {min(ms):.3f}; gather {g:.3f} ms ({nbytes / 1e6:.2f} MB, world-1 RCCL) + untile {u:.3f} ms; "
-          f"efficiency vs {INFLIGHT}-in-flight world 1: {w1_fl / (world * mx):.3f} overlapped, "
+          f"efficiency vs {INFLIGHT1}-in-flight world 1: {w1_fl / (world * mx):.3f} overlapped, "
           f"{w1_fl / (world * ser):.3f} serial; vs one-at-a-time world 1: {w1_one / (world * mx):.3f} / "
           f"{w1_one / (world * ser):.3f}", flush=True)
 ctx.close()

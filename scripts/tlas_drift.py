@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
-"""Instance-BVH drift: N tori drift across the field for F frames (every instance moved before
-every frame, wrapping at the field's edge; frames queued back to back, 1280x720, 2 spp, depth 3).  Per rebuild
-policy: ms per frame over the drift, the host time spent inside set_instances per frame, then ms per frame of
-static frames at the final positions against a fresh host SAH tree over the same positions (PRT_TLAS_HOST=1).
-Modes (TLAS_MODES): unset = refit only / the default (up to 4,096 instances: the host SAH build for every update) /
-the single-workgroup device build for every update / the multi-launch builder on the node-area trigger and every
-frame; default / device / host = one of them once (host: a synchronous host SAH build per update)."""
+"""Instance-BVH drift: N tori drift across the field for F frames (every instance moved
+before every frame, wrapping at the field's edge; frames queued back to back, 1280x720, 2 spp, depth 3), under the
+library's one policy (prt_api.cpp ensure_instances: a host SAH build for every update, on the calling thread up to
+4,096 instances, on a worker thread above with device refits until each build is committed).
+
+Reports: ms per frame over the drift; the host time spent inside prt_set_instances per frame (mean, max); the
+rebuilds / refits the context counted; ms per frame of static frames at the final positions on the drifted tree,
+against a fresh context's tree built over those same positions (the static reference frame).
+usage: tlas_drift.py [N] [F]"""
+import dataclasses
 import os
 import sys
 import time
@@ -23,13 +26,11 @@ sd = scenes.instance_field(N, seed=17)
 W, H = 1280, 720
 rng = np.random.default_rng(3)
 vel = rng.uniform(-0.08, 0.08, (len(sd.instances), 2)).astype(np.float32)
-vel *= np.float32(os.environ.get("DRIFT_VEL", "1"))  # DRIFT_VEL=0: every instance re-set in place (the update machinery alone)
 
 
 def drift(inst):
-    """Every torus moves by its velocity in x and z, wrapping at the field's edge.  inst = (mesh ids uint32,
-    transforms float32 [N,4,4]), updated in numpy (a per-instance Python loop took 3-4 ms a frame, close to the
-    frame itself: the drift numbers would measure Python)."""
+    """Every torus moves by its velocity in x and z, wrapping at the field's edge (numpy: a per-instance Python loop
+    would take as long as the frame)."""
     mi, T = inst
     T = T.copy()
     mv = mi == 1
@@ -45,10 +46,17 @@ def set_instances(ctx, inst):  # the ABI call itself (prt_set_instances), withou
     _lib.check(ctx.L.prt_set_instances(ctx.h, T.ctypes.data, mi.ctypes.data, len(mi)))
 
 
-HOST_MS = []  # host time inside set_instances, per call
+def context(inst):
+    """a fresh context whose first instance BVH is built over `inst` (the scene's own instances)"""
+    ctx = prt.Context(0)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    mi, T = inst
+    ctx.set_scene(prt.Scene.from_data(dataclasses.replace(sd, instances=[(int(m), T[k]) for k, m in enumerate(mi)])))
+    ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
+    return ctx
 
 
-def timed(ctx, avg, rgb, n, inst=None):
+def frames(ctx, avg, rgb, n, inst=None, host_ms=None):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(n):
@@ -56,82 +64,29 @@ def timed(ctx, avg, rgb, n, inst=None):
             inst = drift(inst)
             h0 = time.perf_counter()
             set_instances(ctx, inst)
-            HOST_MS.append((time.perf_counter() - h0) * 1e3)
+            host_ms.append((time.perf_counter() - h0) * 1e3)
         ctx.render(W, H, 2, 3, frame_index=i, avg=avg.data_ptr(), rgb8=rgb.data_ptr(), device_out=True, stats=False)
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) * 1e3 / n, inst
 
 
-MODES = [("refit only", "0", None), ("default (host SAH build, every update)", None, None),
-         ("single-workgroup device build, every frame", None, "S"),
-         ("multi-launch builder, trigger", "1.05", "M"), ("multi-launch builder, every frame", "always", "M")]
-if os.environ.get("TLAS_MODES") == "trbvh":  # A/B of the device tree's treelet-restructuring passes
-    MODES = [(f"device rebuild every frame, {k} TRBVH passes", "always", k) for k in ("0", "1", "2", "3")]
-if os.environ.get("TLAS_MODES") == "radius":  # A/B of the device tree's PLOC radius (0 / 1 TRBVH passes)
-    MODES = [(f"device rebuild every frame, PLOC radius {r}, {k} TRBVH passes", "always", k + ":" + r)
-             for r, k in (("64", "0"), ("512", "0"), ("512", "1"))]
-if os.environ.get("TLAS_MODES") == "small":  # the single-workgroup builder's policies
-    MODES = [("small builder, trigger", "1.05", None), ("small builder, every frame", "always", None)]
-if os.environ.get("TLAS_MODES") == "default":  # the default policy only, once (timeline sessions)
-    MODES = MODES[1:2]
-if os.environ.get("TLAS_MODES") == "device":  # the single-workgroup device build only, once
-    MODES = MODES[2:3]
-if os.environ.get("TLAS_MODES") == "host":  # a host SAH build for every update (the host waits; timeline sessions)
-    MODES = [("host SAH build, every frame", None, "H")]
-for mode, env, trbvh in MODES + (MODES if os.environ.get("TLAS_MODES") not in ("default", "host", "device") else []):
-    os.environ.pop("PRT_TLAS_SMALL", None)
-    host_every = trbvh == "H"
-    if host_every:
-        trbvh = None
-    if trbvh == "S":  # the single-workgroup device build
-        os.environ["PRT_TLAS_SMALL"] = "1"
-        trbvh = "keep"
-    if trbvh == "M":  # the multi-launch builder
-        os.environ["PRT_TLAS_SMALL"] = "0"
-        trbvh = None
-    if trbvh in (None, "keep"):
-        os.environ.pop("PRT_TLAS_TRBVH", None)
-        os.environ.pop("PRT_TLAS_PLOC_R", None)
-    else:  # (the treelet / radius knobs are the multi-launch builder's)
-        os.environ["PRT_TLAS_SMALL"] = "0"
-        os.environ["PRT_TLAS_TRBVH"] = trbvh.split(":")[0]
-        if ":" in trbvh:
-            os.environ["PRT_TLAS_PLOC_R"] = trbvh.split(":")[1]
-    os.environ.pop("PRT_TLAS_HOST", None)
-    if host_every:
-        os.environ["PRT_TLAS_HOST"] = "1"
-    if env is None:
-        os.environ.pop("PRT_TLAS_REBUILD", None)
-    else:
-        os.environ["PRT_TLAS_REBUILD"] = env
-    ctx = prt.Context(0)
-    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
-    ctx.set_scene(prt.Scene.from_data(sd))
-    ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
-    avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
-    rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
-    inst = (np.ascontiguousarray([m for m, _ in sd.instances], np.uint32),
-            np.ascontiguousarray(np.stack([np.asarray(T, np.float32) for _, T in sd.instances])))
-    timed(ctx, avg, rgb, 2)
-    t_first, _ = timed(ctx, avg, rgb, 10)
-    blocks = []
-    HOST_MS.clear()
-    for b in range(F // 20):
-        ms, inst = timed(ctx, avg, rgb, 20, inst)
-        blocks.append(round(ms, 3))
-    si = ctx.scene_info()
-    t_end, _ = timed(ctx, avg, rgb, 20)
-    os.environ["PRT_TLAS_HOST"] = "1"
-    set_instances(ctx, inst)  # a fresh host SAH tree over the final positions
-    os.environ.pop("PRT_TLAS_HOST")
-    os.environ["PRT_TLAS_REBUILD"] = "0"
-    os.environ.pop("PRT_TLAS_SMALL", None)
-    t_fresh, _ = timed(ctx, avg, rgb, 20)
-    hd = ctx.scene_info().tlas_depth
-    hms = np.array(HOST_MS)
-    print(f"{N} instances, {F} frames, {mode}: static frame at start {t_first:.3f} ms; drift ms/frame per 20 frames "
-          f"{blocks}; set_instances host time median {np.median(hms):.3f} / max {hms.max():.3f} ms; "
-          f"{si.tlas_rebuilds} rebuilds ({si.tlas_rejected} device builds not committed) / {si.tlas_refits} refits; static frame at the end "
-          f"{t_end:.3f} ms vs fresh host SAH tree {t_fresh:.3f} ms (depth {hd}) ({100 * (t_end / t_fresh - 1):+.1f} %)",
-          flush=True)
-    ctx.close()
+avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+inst0 = (np.array([m for m, _ in sd.instances], np.uint32), np.stack([np.array(T, np.float32) for _, T in sd.instances]))
+ctx = context(inst0)
+frames(ctx, avg, rgb, 10)  # warm
+host = []
+ms_drift, inst = frames(ctx, avg, rgb, F, inst0, host)
+si = ctx.scene_info()
+time.sleep(0.3)  # (above 4,096 instances: the worker's last build finishes; the next update commits it)
+set_instances(ctx, inst)
+ms_end, _ = frames(ctx, avg, rgb, 20)
+ctx.close()
+ref = context(inst)
+frames(ref, avg, rgb, 5)
+ms_ref, _ = frames(ref, avg, rgb, 20)
+ref.close()
+print(f"{N} instances, {F} frames of drift: {ms_drift:.3f} ms/frame; set_instances host {np.mean(host):.3f} ms mean, "
+      f"{np.max(host):.3f} ms max; {si.tlas_rebuilds} rebuilds / {si.tlas_refits} refits; static at the end "
+      f"{ms_end:.3f} ms/frame vs {ms_ref:.3f} on a fresh tree ({(ms_end / ms_ref - 1) * 100:+.1f} %); drift vs "
+      f"fresh static {ms_drift / ms_ref:.3f}x", flush=True)
