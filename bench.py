@@ -98,6 +98,18 @@ def profile_record(scene, kernel):
     return _pmc_kernel(os.path.join(ROOT, "profiles", f"current_{scene}.json"), kernel)
 
 
+def memory_record(scene, kernel):
+    """Derived vector-memory figures of `kernel` in profiles/current_<scene>_mem.json (scripts/gpu_mem.sh +
+    summarize_mem.py: TA / TD / TCP / TCC / SQ passes of `bench.py --scene <scene>`), with its code hash."""
+    path = os.path.join(ROOT, "profiles", f"current_{scene}_mem.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as fh:
+        t = json.load(fh)
+    d = t.get("kernels", {}).get(kernel)
+    return d, t.get("name")
+
+
 def host_cpu():
     """CPU model, logical CPUs of the host, and the CPUs this process may use (affinity / cgroup quota)."""
     model = "unknown"
@@ -166,21 +178,8 @@ def cpu_baseline(sd, W, H, spp, bounces):
            "sample": f"{sd.name}: {what}, {spp} spp, depth {bounces}, {threads} threads "
                      f"(this GPU's CPU share of a {nproc}-CPU host)",
            "legs": legs}
-    if len(points) >= 2:
-        # whole host: not measured (the pool gives one GPU's job its share of the CPUs).  The reference leg's
-        # measured thread points are fitted with Amdahl's t(p) = a + b / p (least squares in 1/p) and the fit
-        # is evaluated at every logical CPU of the host -- an estimate, derived from the points listed
-        x = np.array([1.0 / p["threads"] for p in points])
-        y = np.array([p["seconds"] for p in points])
-        b, a = np.polyfit(x, y, 1)
-        a = max(a, 0.0)
-        rays = points[-1]["rays"]
-        t_host = a + b / nproc
+    if len(points) >= 2:  # measured only: the reference leg at 1, 4 and all usable threads of this GPU's CPU share
         out["thread_points"] = [{"threads": p["threads"], "value": p["value"], "seconds": p["seconds"]} for p in points]
-        out["amdahl_fit"] = {"serial_s": round(a, 4), "parallel_s": round(b, 4),
-                             "serial_fraction": round(a / (a + b), 4) if a + b > 0 else None}
-        out["whole_host_estimate"] = {"value": round(rays / t_host / 1e6, 1), "threads": nproc,
-                                      "how": "Amdahl fit of thread_points evaluated at host_logical_cpus (not measured)"}
     return out
 
 
@@ -363,6 +362,8 @@ def main():
         valu = rec if ok and "SQ_INSTS_VALU" in rec else None
         traffic = int(rec["hbm_bytes_per_launch"]) if ok and "hbm_bytes_per_launch" in rec else None
         stall = rec.get("stall") if ok else None
+        mrec, mrec_src = memory_record(args.scene, TRACE_KERNEL) if priced else (None, None)
+        mem = mrec.get("derived") if mrec and fresh(mrec, live_hash) else None
         valu_rate = valu["SQ_INSTS_VALU"] / (kern_ms / 1e3) / 1e9 if valu else None
         hbm_rate = traffic / (kern_ms / 1e3) / 1e9 if traffic else None
         bpr = algorithmic_bytes_per_ray()
@@ -377,7 +378,9 @@ def main():
         if not stall:
             bound = None
         elif stall["wait"] > stall["issuing"] + stall["issue_stall"]:
-            bound = "latency"
+            # parked on s_waitcnt most of the time: with the memory pipeline's counters, the vector-memory path
+            # (the L1's misses in flight: TD busy / TCP pending stalls) when its data unit is near saturation
+            bound = "vector-memory" if mem and mem.get("td_busy", 0) >= 0.8 else "latency"
         else:
             bound = "valu"
         if valu_rate is not None:
@@ -396,11 +399,16 @@ def main():
         else:  # no fresh VALU pass for this config: price the measured HBM bytes (or nothing)
             roof = {"bound": bound, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": hbm["frac"], "traffic": traffic}
+        if mem:
+            roof["memory"] = {k: mem[k] for k in ("ta_busy", "td_busy", "td_tc_stall", "tcp_pending_stall", "l1_hit_rate",
+                                                 "l2_hit_rate", "l2_read_latency_cycles") if k in mem}
+            roof["memory"]["source"] = mrec_src
         if stall:
             roof["stall"] = {k: round(v, 4) for k, v in stall.items()}
             roof["bound_basis"] = ("stall = fractions of SQ_WAVE_CYCLES: wait = parked on s_waitcnt (SQ_WAIT_ANY), "
                                    "issue_stall = SQ_WAIT_INST_ANY, issuing = SQ_ACTIVE_INST_ANY; bound = latency "
-                                   "when wait > issuing + issue_stall")
+                                   "when wait > issuing + issue_stall, vector-memory when moreover the texture data "
+                                   "unit is busy >= 0.8 of the kernel's cycles (memory.td_busy)")
         roof["stale_profile"] = stale
         roof["code_hash"] = live_hash[:16] if live_hash else None
         roof.update({
@@ -408,12 +416,16 @@ def main():
             "launch_ms": round(kern_ms, 4), "launch_timing": "HIP events around each launch of the last timed frame",
             "hbm": hbm,
             "algorithmic_bytes_per_launch": round(ref_bytes),
-            "reference_layout_equiv_GBps": round(ref_bytes / (kern_ms / 1e3) / 1e9, 1),
-            "own_layout_GBps": round(own_bytes / (kern_ms / 1e3) / 1e9, 1) if own_bytes else None,
+            # SURVEY 8d's per-ray bytes priced in the reference's BVH8_CPU layout (256-B nodes, 192-B leaves), as if
+            # every visit came from HBM: above the HBM peak, so not an HBM figure (the tree sits in L2 / MALL)
+            "reference_layout_equiv": {"GBps": round(ref_bytes / (kern_ms / 1e3) / 1e9, 1),
+                                       "note": "not an HBM figure (SURVEY 8d reference-layout bytes / launch time; "
+                                               "exceeds the 8 TB/s peak)"},
+            "own_layout_equiv_GBps": round(own_bytes / (kern_ms / 1e3) / 1e9, 1) if own_bytes else None,
             "basis": "frac = PMC-measured VALU wave-instructions (SQ_INSTS_VALU) per second over the issue peak "
                      "(1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction, MI355X_MICROARCH.md); "
-                     "hbm = PMC-measured HBM bytes over the HBM peak; reference_layout_equiv_GBps = SURVEY 8d "
-                     "bytes in the reference's BVH8_CPU layout over the launch time (not HBM traffic)",
+                     "hbm = PMC-measured HBM bytes over the HBM peak; memory = the vector-memory path's busy / stall "
+                     "fractions (scripts/gpu_mem.sh TA / TD / TCP / TCC passes)",
             "bytes_per_ray": {k: round(v, 1) for k, v in bpr.items()},
         })
         out = {

@@ -183,10 +183,9 @@ int prt_finish(prt_ctx* ctx);
 int prt_set_textures(prt_ctx* ctx, const prt_texture* textures, int32_t count);
 int prt_set_meshes(prt_ctx* ctx, const prt_mesh* meshes, int32_t count);
 /* transforms: 16*count floats, row-major BLASInstance::transform; mesh_index: count.  Above 64 instances the rays
- * walk an instance BVH, rebuilt for every call as the reference's per-frame BVH::Build: a host SAH build uploaded in
- * stream order (no wait on the GPU), on the calling thread up to 4,096 instances; above that on a worker thread,
- * committed at the first call after it finished, with the device refitting the current tree to every call's boxes
- * in between */
+ * walk an instance BVH, rebuilt for every call as the reference's per-frame BVH::Build (a host SAH build): on the
+ * calling thread when the instance count changes, otherwise on the context's worker thread, the context stream
+ * waiting for that build before its upload (the caller neither builds nor waits) */
 int prt_set_instances(prt_ctx* ctx, const float* transforms, const uint32_t* mesh_index, int32_t count);
 int prt_set_lights(prt_ctx* ctx, const prt_lights* lights);
 /* kinds: one PRT_MAT_* per instance (count = the instance count), or count 0 = all textured.  Reset by
@@ -332,8 +331,8 @@ int prt_brdf_probe(prt_ctx* ctx, int32_t op, int32_t n, const float* in, float* 
 
 /* ---- BLAS builder (the reference builds on the CPU, Core/tiny_bvh.h:1968-2284,3706-3781)
  * HOST_SAH (default): binned SAH binary tree + SAH-optimal 8-wide collapse on the host.
- * GPU_LBVH: Morton-code LBVH (Karras 2012) + SAH-optimal 8-wide collapse on the device (PRT_COLLAPSE=greedy:
- * the greedy collapse), Node8 layout only.
+ * GPU_LBVH: Morton-code LBVH (Karras 2012) + treelet restructuring + SAH-optimal 8-wide collapse on the device,
+ * Node8 layout only.
  * Applies to the next prt_set_meshes.  Hits do not depend on the builder (order-independent hit rule). */
 #define PRT_BUILDER_HOST_SAH 0
 #define PRT_BUILDER_GPU_LBVH 1
@@ -351,12 +350,14 @@ typedef struct {
     double  build_ms;       /* wall time of the last prt_set_meshes (BLAS builds + uploads) */
     int32_t builder;        /* PRT_BUILDER_* used by the last prt_set_meshes */
     int32_t tlas_depth;     /* levels of the instance BVH the rays walk (0: instances tested as a linear list) */
-    int32_t tlas_rebuilds;  /* (ABI 8) rebuilds of the instance BVH committed since the instance count last
-                               changed (every update up to 4,096 instances; above, each finished worker build) */
-    int32_t tlas_refits;    /* (ABI 8) updates since then that refitted the current tree instead (above 4,096
-                               instances, while the worker builds) */
-    int32_t tlas_rejected;  /* (ABI 9) always 0 from ABI 10: the instance BVH is built on the host only (kept for
-                               the struct layout) */
+    int32_t tlas_rebuilds;  /* rebuilds of the instance BVH since the instance count last changed: one per
+                               prt_set_instances */
+    int32_t tlas_async;     /* (ABI 10) of those, built on the context's worker thread in stream order (every update
+                               after the one that set the instance count) */
+    int32_t tlas_median;    /* (ABI 10) of the worker's builds, balanced median-split trees: the SAH tree was deeper
+                               than the traversal stacks were sized for at the instance count's first build */
+    float   tlas_build_ms;     /* (ABI 10) wall time of the worker's last build (instance boxes + build + collapse) */
+    float   tlas_build_cpu_ms; /* (ABI 10) its thread CPU time */
 } prt_scene_info;
 int prt_get_scene_info(prt_ctx* ctx, prt_scene_info* info);
 

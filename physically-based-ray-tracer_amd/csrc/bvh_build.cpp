@@ -47,6 +47,7 @@ struct Builder {
   std::vector<Node2> nodes;
   int max_leaf;
   int nbins = kBins;  // SAH bins per axis (the instance BVH: 8, tinybvh's BVHBINS for its per-frame TLAS build)
+  bool median = false;  // median splits on the widest centroid axis: a balanced tree of height ceil(log2 n)
 
   void build(int32_t T) {
     tb.resize(T);
@@ -80,6 +81,19 @@ struct Builder {
     }
     nodes[ni].box = b;
     if (count <= 1) return;
+    if (median) {
+      if (count <= max_leaf) return;
+      int ax = 0;
+      for (int k = 1; k < 3; k++)
+        if (cb.hi[k] - cb.lo[k] > cb.hi[ax] - cb.lo[ax]) ax = k;
+      const int32_t mid = first + count / 2;
+      std::nth_element(idx.begin() + first, idx.begin() + mid, idx.begin() + first + count, [&](uint32_t a, uint32_t c) {
+        const float ca = cen[3 * (size_t)a + ax], cc = cen[3 * (size_t)c + ax];
+        return ca < cc || (ca == cc && a < c);
+      });
+      emit_children(ni, first, count, mid, work);
+      return;
+    }
     // binned SAH over centroid bins (C_trav = 1, C_int = 1 per triangle); a pair that must split (the instance BVH's
     // one-instance leaves) has only the one split
     double best = 1e300;
@@ -518,16 +532,35 @@ struct WideDp {
   }
 };
 
+// the fixed collapse of a median-split tree: every wide node takes the binary nodes three levels below it (or the
+// leaves above that), so the wide tree has ceil(height / 3) levels (tlas8_median_depth)
+struct LevelCollapse {
+  const Builder* B;
+  void collect(int32_t n, int lvl, int32_t* out, int& nc) const {
+    if (lvl == 0 || B->nodes[n].leaf()) { out[nc++] = n; return; }
+    collect(B->nodes[n].left, lvl - 1, out, nc);
+    collect(B->nodes[n].right, lvl - 1, out, nc);
+  }
+  int expand(int32_t n, int32_t* out) const {
+    int nc = 0;
+    if (B->nodes[n].leaf()) { out[nc++] = n; return nc; }
+    collect(B->nodes[n].left, 2, out, nc);
+    collect(B->nodes[n].right, 2, out, nc);
+    return nc;
+  }
+};
+
 // relative SAH costs of an 8-wide node visit and of one triangle test in the traversal kernels
-// (measured optimum on C4 at 1 : 1 with the persistent kernels; PRT_COLLAPSE_TRI_COST overrides, and
-// PRT_COLLAPSE=greedy restores the area-greedy collapse)
+// (measured optimum on C4 at 1 : 1 with the persistent kernels)
 constexpr float kWideNodeCost = 1.0f, kWideTriCost = 1.0f;  // tri cost swept 0.15-5 on C4: flat above 1
 
 template <class NodeT, class Fmt, class Out>
-void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out, bool spatial = false, int bins = kBins) {
+void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out, bool spatial = false, int bins = kBins,
+                 bool median = false) {
   Builder B;
   B.tri = triangles;
   B.nbins = bins;
+  B.median = median;
   B.max_leaf = std::max(1, std::min(4, max_leaf));
   if (spatial) {
     SpatialBuilder SB;
@@ -540,8 +573,9 @@ void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out, bool
   for (int k = 0; k < 3; k++) { out.bmin[k] = B.nodes[0].box.lo[k]; out.bmax[k] = B.nodes[0].box.hi[k]; }
   out.tris.reserve(T);
   WideDp dp;  // the SAH-optimal collapse (round 1's greedy collapse: 2,636 against 3,529+ Mrays/s on C4, removed)
-  dp.compute(B, kWideNodeCost, kWideTriCost);
-  auto is_leaf = [&](int32_t n) { return dp.leaf1[n] != 0; };
+  const LevelCollapse lv{&B};  // (median trees)
+  if (!median) dp.compute(B, kWideNodeCost, kWideTriCost);
+  auto is_leaf = [&](int32_t n) { return median ? B.nodes[n].leaf() : dp.leaf1[n] != 0; };
   struct Item { int32_t n2; uint32_t n8; int depth; };
   std::vector<Item> work;
   out.nodes.push_back(NodeT());
@@ -552,7 +586,7 @@ void build_wide8(const float* triangles, int32_t T, int max_leaf, Out& out, bool
     out.depth = std::max(out.depth, it.depth);
     int32_t ch[8];
     int nc = 0;
-    nc = dp.expand(B, it.n2, ch);
+    nc = median ? lv.expand(it.n2, ch) : dp.expand(B, it.n2, ch);
     // inflated child boxes and the node grid
     float clo[8][3], chi[8][3];
     double nlo[3] = {1e300, 1e300, 1e300}, nhi[3] = {-1e300, -1e300, -1e300};
@@ -653,7 +687,13 @@ BuiltBlas8 build_blas8(const float* triangles, int32_t T, int max_leaf, bool spa
   return out;
 }
 
-BuiltTlas8 build_tlas8(const float* boxes, int32_t n) {
+int tlas8_median_depth(int32_t n) {
+  int h = 0;  // height of the median-split binary tree: ceil(log2 n)
+  while (h < 31 && (int64_t(1) << h) < n) h++;
+  return std::max(1, (h + 2) / 3);
+}
+
+BuiltTlas8 build_tlas8(const float* boxes, int32_t n, int max_depth) {
   // each instance box as a degenerate "triangle" {lo, hi, lo}: its bounds are the box, its centroid the box centre
   std::vector<float> fat(12 * (size_t)n, 0.0f);
   for (int32_t i = 0; i < n; i++) {
@@ -664,6 +704,11 @@ BuiltTlas8 build_tlas8(const float* boxes, int32_t n) {
   BuiltBlas8 w;
   build_wide8<Node8, Fmt8>(fat.data(), n, 1, w, false, 8);  // 8 bins: tinybvh's BVHBINS (Core/tiny_bvh.h:92-131)
   BuiltTlas8 out;
+  if (max_depth > 0 && w.depth > max_depth) {  // deeper than the caller's stacks: the balanced tree instead
+    w = BuiltBlas8();
+    build_wide8<Node8, Fmt8>(fat.data(), n, 1, w, false, 8, true);
+    out.median = true;
+  }
   out.depth = w.depth;
   out.nodes = std::move(w.nodes);
   out.slot.assign(8 * out.nodes.size(), 0xFFFFFFFFu);

@@ -57,8 +57,12 @@ struct BuiltTlas8 {
   std::vector<Node8> nodes;     // node 0 = root
   std::vector<uint32_t> slot;   // 8 per node: instance id of each leaf slot (0xFFFFFFFF elsewhere)
   int depth = 0;
+  bool median = false;          // the SAH tree exceeded max_depth: the balanced median-split tree was built instead
 };
-BuiltTlas8 build_tlas8(const float* boxes, int32_t n);  // boxes: n x {lo[3], hi[3]} world AABBs (inflated)
+// boxes: n x {lo[3], hi[3]} world AABBs (inflated).  max_depth > 0 (>= tlas8_median_depth(n)): a tree of at most
+// that many levels (the SAH tree, or the median-split one when the SAH tree is deeper); at most max(n, 1) nodes
+BuiltTlas8 build_tlas8(const float* boxes, int32_t n, int max_depth = 0);
+int tlas8_median_depth(int32_t n);  // levels of the median-split instance BVH over n instances: ceil(ceil(log2 n) / 3)
 
 // Same inflation rule the traversal relies on (see bvh_build.cpp).
 void inflate_box(float* lo, float* hi);

@@ -13,7 +13,6 @@
 //      from its children's tables, in double, with the chosen split of the slots (Dk) and the leaf decision
 //   5. 8-wide collapse, one launch per level: a wide node takes the <= 8 slots the table chose for it (a slot
 //      whose single-slot form is a leaf becomes a leaf child with all its triangles, contiguous in key order).
-//      PRT_COLLAPSE=greedy instead opens the largest-area child with more than max_leaf triangles until 8.
 //      Nodes are quantised and laid out exactly as the host builder's Node8 (bvh_build.h): interior
 //      children contiguous (one atomic per node), leaf triangles contiguous (one atomic per node)
 //   (LBVH and PLOC trees can be refined by treelet restructuring before step 5, PRT_TRBVH: see k_trbvh)
@@ -161,16 +160,13 @@ __global__ void __launch_bounds__(kB) k_radix_tree(const unsigned long long* __r
 // collapse table of internal node p from its children's (a binary leaf, id >= n - 1: one triangle, every C its
 // leaf cost); children's tables were written earlier in this launch (sc1, after the arrival atomic) or by an
 // earlier launch
-// WG: the children's tables were written by this workgroup (the single-workgroup build): plain loads after its
-// barriers, served by the L2 instead of the agent-coherent path
-template <bool WG = false>
 __device__ __forceinline__ void dp_node(const DpTab& dp, int p, int lc, int rc, const float* pb, const float* lb,
                                         const float* rb, int cnt, int n, int max_leaf) {
   double cl[9], cr[9];
   const double al = area6d(lb) * kDpTri, ar = area6d(rb) * kDpTri;
   for (int i = 1; i <= 8; i++) {
-    cl[i] = lc >= n - 1 ? al : (WG ? dp.C[8 * (size_t)lc + i - 1] : ld_sc1_d(dp.C + 8 * (size_t)lc + i - 1));
-    cr[i] = rc >= n - 1 ? ar : (WG ? dp.C[8 * (size_t)rc + i - 1] : ld_sc1_d(dp.C + 8 * (size_t)rc + i - 1));
+    cl[i] = lc >= n - 1 ? al : ld_sc1_d(dp.C + 8 * (size_t)lc + i - 1);
+    cr[i] = rc >= n - 1 ? ar : ld_sc1_d(dp.C + 8 * (size_t)rc + i - 1);
   }
   const double A = fmax(area6d(pb), 1e-30);
   const double leafc = cnt <= max_leaf ? A * kDpTri * (double)cnt : 1e300;
@@ -188,10 +184,7 @@ __device__ __forceinline__ void dp_node(const DpTab& dp, int p, int lc, int rc, 
   const double intc = A * kDpNode + D[8];
   if (cnt <= max_leaf && leafc <= intc) dec |= 1u << 31;
   double C = fmin(leafc, intc);
-  auto put = [&](size_t at, double v) {
-    if (WG) dp.C[at] = v;
-    else st_sc1_d(dp.C + at, v);
-  };
+  auto put = [&](size_t at, double v) { st_sc1_d(dp.C + at, v); };
   put(8 * (size_t)p, C);
   for (int i = 2; i <= 8; i++) {
     if (C <= D[i]) dec |= 1u << (24 + i - 2);
@@ -335,11 +328,7 @@ __global__ void __launch_bounds__(kB) k_ploc_merge(const int* __restrict__ clus,
   out[i] = p;
 }
 
-// ---- 5. greedy 8-wide collapse, one level per launch
-__device__ __forceinline__ float area6(const float* b) {
-  const float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
-  return dx * dy + dy * dz + dz * dx;
-}
+// ---- 5. box helpers of the collapse (bvh_build.cpp's inflation and grid exponent)
 __device__ __forceinline__ void inflate(float* lo, float* hi) {  // inflate_box (bvh_build.cpp)
   for (int k = 0; k < 3; k++) {
     const float ext = fmaxf(fabsf(lo[k]), fabsf(hi[k]));
@@ -566,10 +555,10 @@ __device__ __forceinline__ void collapse_task(const Task tk, const float4* __res
   const int nn = 2 * n - 1;
   if (tk.n2 < 0 || tk.n2 >= nn || tk.n8 >= (uint32_t)n) { atomicOr(ctr + 3, 0x80000000u); return; }
   // a child slot's form: leaf (all its triangles) or a wide node of its own
-  auto is_leaf = [&](int v) { return v >= n - 1 || (dp.dec ? (dp.dec[v] >> 31) != 0 : (int)count[v] <= max_leaf); };
+  auto is_leaf = [&](int v) { return v >= n - 1 || (dp.dec[v] >> 31) != 0; };  // (n == 1: no table, one leaf)
   int ch[8];
   int nc = 0;
-  if (dp.dec && !is_leaf(tk.n2)) {
+  if (!is_leaf(tk.n2)) {
     // the slots the table chose: expand(n) = collect(left, Dk[n][8]) + collect(right, 8 - Dk[n][8]), where
     // collect(v, i) = v if i == 1 or v is a leaf / its own form; collect(v, i - 1) if prev; else split again
     int st_n[16], st_i[16], sp = 0;
@@ -589,24 +578,8 @@ __device__ __forceinline__ void collapse_task(const Task tk, const float4* __res
       st_n[sp] = right[v]; st_i[sp++] = i - k;
       st_n[sp] = left[v]; st_i[sp++] = k;
     }
-  } else if (is_leaf(tk.n2)) {
-    ch[nc++] = tk.n2;
   } else {
-    ch[nc++] = left[tk.n2];
-    ch[nc++] = right[tk.n2];
-    while (nc < 8) {
-      int bi = -1;
-      float ba = -1.0f;
-      for (int i = 0; i < nc; i++)
-        if (!is_leaf(ch[i])) {
-          const float a = area6(box + 6 * (size_t)ch[i]);
-          if (a > ba) { ba = a; bi = i; }
-        }
-      if (bi < 0) break;
-      const int c = ch[bi];
-      ch[bi] = left[c];
-      ch[nc++] = right[c];
-    }
+    ch[nc++] = tk.n2;
   }
   for (int i = 0; i < nc; i++)
     if (ch[i] < 0 || ch[i] >= nn) { atomicOr(ctr + 3, 0x80000000u); return; }
@@ -808,8 +781,7 @@ hipError_t gpu_build_blas8(hipStream_t s, const float* tri_dev, int32_t n_tris, 
       (err = hipMallocAsync(reinterpret_cast<void**>(&box), 24 * nn, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&ta), sizeof(Task) * (size_t)n, s)) ||
       (err = hipMallocAsync(reinterpret_cast<void**>(&tb), sizeof(Task) * (size_t)n, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&ctr), 16, s)) || (err = hipMallocAsync(reinterpret_cast<void**>(&cb), 24, s)))
     return fail(err);
-  const char* ce = std::getenv("PRT_COLLAPSE");
-  if (!(ce && std::strcmp(ce, "greedy") == 0) && n > 1) {
+  if (n > 1) {
     if ((err = hipMallocAsync(reinterpret_cast<void**>(&dp.C), 8 * sizeof(double) * (size_t)(n - 1), s)) ||
         (err = hipMallocAsync(reinterpret_cast<void**>(&dp.dec), sizeof(uint32_t) * (size_t)(n - 1), s)))
       return fail(err);

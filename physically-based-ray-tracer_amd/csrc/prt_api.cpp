@@ -5,10 +5,14 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <future>
+#include <ctime>
+#include <deque>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -17,7 +21,6 @@
 #include "bvh_build.h"
 #include "bvh_gpu.h"
 #include "prt_launch.h"
-#include "prt_tlas.h"
 #include "prt_rccl.h"
 #include "prt_refit.h"
 
@@ -97,18 +100,136 @@ struct Flight {
   bool pending = false;  // done is not yet in the context stream's order
 };
 
-// one pinned staging buffer of ensure_instances' uploads (prt_ctx::stage): reused once its copies have run; the pool
-// grows to the updates the host is ahead of the GPU, up to kStageSlots (then the host waits for the oldest)
-constexpr size_t kStageSlots = 64;
+// one pinned staging buffer of ensure_instances' uploads (prt_ctx::stage): reused once its copies have run.  The
+// kStageSlots buffers are allocated when an instance set is first built (pinned allocation in the update path cost
+// 20-190 ms per buffer on the GPU box, profiles/r06_tlas_drift.txt); an update that finds all of them in use waits
+// for the oldest one's copies (the host at most kStageSlots updates ahead of the GPU)
+constexpr size_t kStageSlots = 8;
 struct StageSlot {
   void* p = nullptr;
   size_t bytes = 0;
   hipEvent_t ev = nullptr;
   bool used = false;
 };
-// instance counts above which the per-update host build of the instance BVH runs on a worker thread
-// (ensure_instances; ~4 ms for 4,096 instances on the calling thread, 11-12 ms for 10,000)
-constexpr int32_t kHostSyncBuild = 4096;
+// The instance BVH's per-update build (ensure_instances) on the context's worker thread: each update's job builds
+// the tree over that update's instance boxes into the update's pinned staging buffer; the render stream waits for
+// the job at a host function (hipLaunchHostFunc) placed before the tree's upload, so the calling thread never
+// builds nor waits, and the frames already queued run while the worker builds.  Jobs run in submission order; the
+// worker never calls HIP, so every stream wait it is behind ends.
+struct TlasJob {
+  const InstSrc* src = nullptr;  // the update's instances (in its pinned staging buffer, uploaded before the tree)
+  int32_t n = 0;
+  char* dst = nullptr;           // pinned: cap Node8 records, then 8 * cap slot words
+  size_t cap = 0;            // nodes the upload moves (a tree over n instances has at most max(n, 1) nodes)
+  int max_depth = 0;         // levels the traversal stacks were sized for (build_tlas8's cap)
+  bool done = false;
+};
+class TlasWorker {
+ public:
+  TlasWorker() : th_([this] { run(); }) {}
+  ~TlasWorker() {  // after the streams are synchronised: the queue is empty (every job's stream wait has ended)
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void seed(const BuiltTlas8& t) {  // the tree a failed build falls back to (its instance set's first tree)
+    std::lock_guard<std::mutex> g(m_);
+    good_nodes_ = t.nodes;
+    good_slot_ = t.slot;
+  }
+  void submit(const std::shared_ptr<TlasJob>& j) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(j);
+    }
+    cv_.notify_all();
+  }
+  void wait(const std::shared_ptr<TlasJob>& j) {
+    std::unique_lock<std::mutex> g(m_);
+    done_cv_.wait(g, [&] { return j->done; });
+  }
+  // diagnostics of the finished jobs
+  struct Stats { double ms = 0, cpu_ms = 0; int32_t median = 0, failed = 0; std::string err; };
+  Stats stats() {
+    std::lock_guard<std::mutex> g(m_);
+    return st_;
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      std::shared_ptr<TlasJob> j;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;  // stop_ with nothing queued
+        j = q_.front();
+        q_.pop_front();
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      timespec c0{}, c1{};
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c0);
+      bool median = false, ok = false;
+      std::string err;
+      BuiltTlas8 t;
+      try {  // the instances' world boxes (the same refit_instance as k_refit), the SAH build over them
+        const int32_t m = j->n;
+        std::vector<float> boxes(6 * (size_t)m);
+        for (int32_t i = 0; i < m; i++) {
+          InstDev I;
+          refit_instance(j->src[i], I);
+          std::memcpy(&boxes[6 * (size_t)i], I.bmin, 12);
+          std::memcpy(&boxes[6 * (size_t)i + 3], I.bmax, 12);
+        }
+        t = build_tlas8(boxes.data(), m, j->max_depth);
+        median = t.median;
+        ok = t.nodes.size() <= j->cap && t.depth <= j->max_depth;
+        if (!ok) err = "instance BVH larger than planned";
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      std::lock_guard<std::mutex> g(m_);
+      const std::vector<Node8>& nodes = ok ? t.nodes : good_nodes_;  // failed: the last good tree (valid links)
+      const std::vector<uint32_t>& slot = ok ? t.slot : good_slot_;
+      std::memcpy(j->dst, nodes.data(), std::min(nodes.size(), j->cap) * sizeof(Node8));
+      std::memcpy(j->dst + j->cap * sizeof(Node8), slot.data(), std::min(slot.size(), 8 * j->cap) * 4);
+      if (ok) {
+        good_nodes_ = std::move(t.nodes);
+        good_slot_ = std::move(t.slot);
+      } else {
+        st_.failed++;
+        st_.err = err;
+      }
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c1);
+      st_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      st_.cpu_ms = (c1.tv_sec - c0.tv_sec) * 1e3 + (c1.tv_nsec - c0.tv_nsec) * 1e-6;
+      st_.median += median ? 1 : 0;
+      j->done = true;
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  std::deque<std::shared_ptr<TlasJob>> q_;
+  bool stop_ = false;
+  std::vector<Node8> good_nodes_;
+  std::vector<uint32_t> good_slot_;
+  Stats st_;
+  std::thread th_;  // last: started once the members above exist
+};
+// the render stream's wait for one job (hipLaunchHostFunc; runs on the runtime's callback thread)
+struct TlasWait {
+  TlasWorker* w;
+  std::shared_ptr<TlasJob> j;
+};
+void tlas_wait_cb(void* p) {
+  TlasWait* tw = static_cast<TlasWait*>(p);
+  tw->w->wait(tw->j);
+  delete tw;
+}
 
 struct MeshHost {
   float bmin[3], bmax[3];
@@ -142,22 +263,20 @@ struct prt_ctx {
   DevBuf inst, inst_src;
   // instance BVH (more than kLinearInstances instances, or PRT_TLAS=1), rebuilt for every prt_set_instances as the
   // reference rebuilds its TLAS every frame (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770): the host SAH
-  // build + SAH-optimal collapse (bvh_build.h build_tlas8).  Up to kHostSyncBuild instances on the calling thread;
-  // above, on a worker thread (tlas_job) from the boxes of the update that started it, committed at the first
-  // update after it finished, and refitted on the device (prt_tlas.hip) to every update's boxes in between
+  // build + SAH-optimal collapse (bvh_build.h build_tlas8), on the calling thread when the instance set changes,
+  // on the worker thread (tlas_worker) in stream order for every later update (ensure_instances)
   bool use_tlas = false;
-  int tlas_depth = 0;
-  TlasTopo tlas_topo;    // the current tree's nodes by depth, deepest first (prt_tlas.h): the device refit's order
+  int tlas_depth = 0;    // levels the traversal stacks are sized for (>= the current tree's depth)
   int32_t tlas_n = -1;   // instance count of the current tree (-1: none)
-  DevBuf tlas8, tlas_slot, tlas_order, tlas_aabb;
-  std::future<BuiltTlas8> tlas_job;  // the worker's build (large instance counts)
-  uint32_t tlas_nodes = 0;
-  int32_t tlas_rebuilds = 0, tlas_refits = 0;  // since the instance count last changed (diagnostics)
+  DevBuf tlas8, tlas_slot;
+  std::unique_ptr<TlasWorker> tlas_worker;
+  int32_t tlas_rebuilds = 0, tlas_async = 0;  // since the instance count last changed (diagnostics)
   // pinned staging buffers of ensure_instances' uploads (instance sources, a new tree's nodes / slots / refit order;
   // hipMemcpyAsync from pageable memory may block the host): a buffer is written again only after its copies have
   // run, so the host never waits on queued frames unless it is kStageSlots updates ahead of the GPU
   std::vector<StageSlot> stage;
   size_t stage_next = 0;  // the oldest buffer in use (the one to wait for when the pool is full)
+  size_t stage_bytes = 0;  // the size the pool was last allocated for
   DevBuf spill;  // traversal stack levels beyond the LDS ones (BVHs deeper than 17 levels)
   DevBuf diag;   // SceneDev::diag device counters ([0] traversal stack overflows, cumulative per context)
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
@@ -353,11 +472,10 @@ int stage_release(prt_ctx*, StageSlot& st, hipStream_t s) {
 // the transforms + k_refit on the render stream, so frames already queued keep reading the previous instances.
 // The instance BVH over those boxes (the same refit_instance on the host) is rebuilt for every update, as the
 // reference rebuilds its TLAS every frame (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770 BVH::Build over the
-// BLASInstances): up to kHostSyncBuild instances by the host SAH build + SAH-optimal collapse on the calling
-// thread, uploaded in stream order (~0.8 ms for 1,000 instances, no wait on the GPU; profiles/r05_tlas_rebuild.txt:
-// the drifting frames cost what a static frame costs); above kHostSyncBuild by the same build on a worker thread,
-// started from the boxes of one update and committed at the first update after it finished, the device refitting
-// the current tree to every update's boxes in between (the tree is at most one build old; no update waits for it)
+// BLASInstances), by the host SAH build + SAH-optimal collapse: on the calling thread when the instance set changes
+// (its depth sizes the traversal stacks), and for every later update on the context's worker thread, the render
+// stream waiting for that update's build at a host function before its upload (TlasWorker).  The caller only
+// copies the update's transforms; every frame walks the tree built over its own instances.
 int ensure_instances(prt_ctx* c) {
   if (!c->inst_dirty) return PRT_OK;
   const int32_t n = (int32_t)c->inst_mesh.size();
@@ -366,86 +484,109 @@ int ensure_instances(prt_ctx* c) {
   // a materials-only update (prt_set_instance_materials) moves no box: the records' kinds are rewritten over
   // unchanged inverses and boxes, and the instance BVH is left as it is
   const bool tree_work = use_tlas && (c->tlas_dirty || !c->use_tlas || c->tlas_n != n);
-  std::vector<InstSrc>& src = c->inst_stage;
-  src.assign(n, InstSrc{});
-  for (int32_t i = 0; i < n; i++) {
-    InstSrc& s = src[i];
-    const uint32_t m = c->inst_mesh[i];
-    if (m >= c->mesh_host.size()) return fail(PRT_ERR_INVALID_ARGUMENT, "instance references a missing mesh");
-    std::memcpy(s.T, &c->inst_xf[16 * (size_t)i], sizeof(s.T));
-    const MeshHost& mh = c->mesh_info[m];
-    std::memcpy(s.bmin, mh.bmin, sizeof(s.bmin));
-    std::memcpy(s.bmax, mh.bmax, sizeof(s.bmax));
-    s.mesh = m;
-    s.kind = i < (int32_t)c->inst_kind.size() ? c->inst_kind[i] : 0u;
+  const bool async = tree_work && c->use_tlas && c->tlas_n == n && c->tlas_worker;
+  if (c->tlas_worker) {
+    const TlasWorker::Stats ws = c->tlas_worker->stats();
+    if (ws.failed) return fail(PRT_ERR_HIP, "instance BVH build failed on the worker thread: " + ws.err);
   }
-  // the tree this update commits (sync build, or a finished worker build), and whether the device refits it
+  for (int32_t i = 0; i < n; i++)
+    if (c->inst_mesh[i] >= c->mesh_host.size()) return fail(PRT_ERR_INVALID_ARGUMENT, "instance references a missing mesh");
+  auto fill = [&](InstSrc* src) {  // the refit input of every instance (prt_refit.h)
+    for (int32_t i = 0; i < n; i++) {
+      InstSrc& s = src[i];
+      const uint32_t m = c->inst_mesh[i];
+      std::memcpy(s.T, &c->inst_xf[16 * (size_t)i], sizeof(s.T));
+      const MeshHost& mh = c->mesh_info[m];
+      std::memcpy(s.bmin, mh.bmin, sizeof(s.bmin));
+      std::memcpy(s.bmax, mh.bmax, sizeof(s.bmax));
+      s.mesh = m;
+      s.kind = i < (int32_t)c->inst_kind.size() ? c->inst_kind[i] : 0u;
+    }
+  };
+  std::vector<InstSrc>& src = c->inst_stage;  // (the calling thread's builds; the worker reads the staging buffer)
+  if (!async) {
+    src.resize(n);
+    fill(src.data());
+  }
+  // a new instance set: its first tree on the calling thread; the stacks are sized for the largest depth that keeps
+  // the traversal's occupancy (and at least the median-split tree's), the cap of the worker's builds
   BuiltTlas8 tree;
-  bool have_tree = false, refit = false;
-  // the instances' world boxes (the same refit_instance as k_refit) and the host SAH build over them
-  auto build = [](const std::vector<InstSrc>& in) {
-    const int32_t m = (int32_t)in.size();
-    std::vector<float> boxes(6 * (size_t)m);
-    for (int32_t i = 0; i < m; i++) {
+  int depth_cap = c->tlas_depth;
+  if (tree_work && !async) {
+    std::vector<float> boxes(6 * (size_t)n);
+    for (int32_t i = 0; i < n; i++) {
       InstDev I;
-      refit_instance(in[i], I);
+      refit_instance(src[i], I);
       std::memcpy(&boxes[6 * (size_t)i], I.bmin, 12);
       std::memcpy(&boxes[6 * (size_t)i + 3], I.bmax, 12);
     }
-    return build_tlas8(boxes.data(), m);
-  };
-  if (tree_work) {
-    if (n <= kHostSyncBuild || c->tlas_n != n || !c->use_tlas) {
-      if (c->tlas_job.valid()) (void)c->tlas_job.get();  // a worker build for another instance set: dropped
-      tree = build(src);
-      have_tree = true;
-    } else {  // the worker computes the boxes too: the calling thread only copies the sources
-      if (c->tlas_job.valid() && c->tlas_job.wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
-        tree = c->tlas_job.get();
-        have_tree = true;
-      }
-      refit = true;  // the committed (or current) tree was built from earlier boxes
-      if (!c->tlas_job.valid()) c->tlas_job = std::async(std::launch::async, build, src);
-    }
+    tree = build_tlas8(boxes.data(), n);
+    const int occ = occ_at(c->max_depth + tree.depth);
+    depth_cap = std::max(tree.depth, tlas8_median_depth(n));
+    while (depth_cap < tree.depth + 4 && occ_at(c->max_depth + depth_cap + 1) == occ &&
+           c->max_depth + depth_cap + 1 <= kMaxBvhDepth)
+      depth_cap++;
   }
-  // uploads through one pinned staging slot: the instance sources, then a new tree's nodes / slots / refit order
-  TlasTopo topo;
-  if (have_tree) topo = tlas_topology(tree.nodes);
-  const size_t sb_src = sizeof(InstSrc) * (size_t)n, sb_nodes = have_tree ? tree.nodes.size() * sizeof(Node8) : 0,
-               sb_slot = have_tree ? tree.slot.size() * 4 : 0, sb_order = have_tree ? topo.order.size() * 4 : 0;
-  // buffers sized for n (at least the linear-list size; a tree over n instances has at most n nodes), so later
-  // updates never reallocate (a reallocation frees what queued frames read: it drains first, a host wait)
+  // buffers sized for n (at least the linear-list size; a tree over n instances has at most max(n, 1) nodes), so
+  // later updates never reallocate (a reallocation frees what queued frames read: it drains first, a host wait)
   const size_t cap = (size_t)std::max(n, kLinearInstances);
-  const size_t cap_nodes = have_tree ? std::max(tree.nodes.size(), (size_t)n) : 0;
+  const size_t cap_nodes = (size_t)std::max(n, 1);
   if (c->inst.bytes < sizeof(InstDev) * cap || c->inst_src.bytes < sizeof(InstSrc) * cap ||
-      (have_tree && (c->tlas8.bytes < cap_nodes * sizeof(Node8) || c->tlas_slot.bytes < cap_nodes * 32 ||
-                     c->tlas_order.bytes < cap_nodes * 4 || c->tlas_aabb.bytes < cap_nodes * 24))) {
+      (tree_work && (c->tlas8.bytes < cap_nodes * sizeof(Node8) || c->tlas_slot.bytes < cap_nodes * 32))) {
     const int rc = drain(c);
     if (rc) return rc;
     HIP_TRY(c->inst.ensure(sizeof(InstDev) * cap));
     HIP_TRY(c->inst_src.ensure(sizeof(InstSrc) * cap));
-    if (have_tree) {
+    if (tree_work) {
       HIP_TRY(c->tlas8.ensure(cap_nodes * sizeof(Node8)));
       HIP_TRY(c->tlas_slot.ensure(cap_nodes * 32));
-      HIP_TRY(c->tlas_order.ensure(cap_nodes * 4));
-      HIP_TRY(c->tlas_aabb.ensure(cap_nodes * 24));
+    }
+  }
+  // uploads through one pinned staging slot: the instance sources, then the tree's nodes and slots
+  const size_t sb_src = sizeof(InstSrc) * (size_t)n;
+  const size_t sb_nodes = !tree_work ? 0 : async ? cap_nodes * sizeof(Node8) : tree.nodes.size() * sizeof(Node8);
+  const size_t sb_slot = !tree_work ? 0 : async ? cap_nodes * 32 : tree.slot.size() * 4;
+  const size_t per = sb_src + (use_tlas ? cap_nodes * (sizeof(Node8) + 32) : 0);
+  if (c->stage.size() < kStageSlots || c->stage_bytes < per) {  // the staging buffers this instance set's updates use
+    c->stage_bytes = per;
+    for (size_t k = c->stage.size(); k < kStageSlots; k++) c->stage.emplace_back();
+    for (StageSlot& t : c->stage) {
+      if (t.used && hipEventQuery(t.ev) == hipSuccess) t.used = false;
+      (void)hipGetLastError();  // (hipErrorNotReady of a buffer still in use)
+      if (!t.used && t.bytes < per) {
+        if (t.p) HIP_TRY(hipHostFree(t.p));
+        t.p = nullptr;
+        t.bytes = 0;
+        HIP_TRY(hipHostMalloc(&t.p, per, hipHostMallocDefault));
+        t.bytes = per;
+      }
     }
   }
   StageSlot* st = nullptr;
-  int rc = stage_acquire(c, sb_src + sb_nodes + sb_slot + sb_order, st);
+  int rc = stage_acquire(c, sb_src + sb_nodes + sb_slot, st);
   if (rc) return rc;
   char* hp = static_cast<char*>(st->p);
-  std::memcpy(hp, src.data(), sb_src);
+  if (async) fill(reinterpret_cast<InstSrc*>(hp));
+  else std::memcpy(hp, src.data(), sb_src);
   HIP_TRY(hipMemcpyAsync(c->inst_src.p, hp, sb_src, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(launch_refit(c->stream, c->inst_src.as<InstSrc>(), n, c->inst.as<InstDev>()));
-  if (have_tree) {
+  if (tree_work) {
     char* q = hp + sb_src;
-    std::memcpy(q, tree.nodes.data(), sb_nodes);
-    std::memcpy(q + sb_nodes, tree.slot.data(), sb_slot);
-    std::memcpy(q + sb_nodes + sb_slot, topo.order.data(), sb_order);
+    if (async) {  // the worker writes the tree into q; the stream's upload waits for it
+      auto job = std::make_shared<TlasJob>();
+      job->src = reinterpret_cast<const InstSrc*>(hp);
+      job->n = n;
+      job->dst = q;
+      job->cap = cap_nodes;
+      job->max_depth = c->tlas_depth;
+      c->tlas_worker->submit(job);
+      HIP_TRY(hipLaunchHostFunc(c->stream, tlas_wait_cb, new TlasWait{c->tlas_worker.get(), job}));
+    } else {
+      std::memcpy(q, tree.nodes.data(), sb_nodes);
+      std::memcpy(q + sb_nodes, tree.slot.data(), sb_slot);
+    }
     HIP_TRY(hipMemcpyAsync(c->tlas8.p, q, sb_nodes, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->tlas_slot.p, q + sb_nodes, sb_slot, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->tlas_order.p, q + sb_nodes + sb_slot, sb_order, hipMemcpyHostToDevice, c->stream));
   }
   rc = stage_release(c, *st, c->stream);
   if (rc) return rc;
@@ -453,18 +594,15 @@ int ensure_instances(prt_ctx* c) {
   if (!use_tlas) {
     c->tlas_depth = 0;
     c->tlas_n = -1;
-  } else if (have_tree) {
-    c->tlas_topo = std::move(topo);
-    c->tlas_depth = tree.depth;
-    c->tlas_nodes = (uint32_t)tree.nodes.size();
-    if (c->tlas_n != n) c->tlas_rebuilds = c->tlas_refits = 0;
-    else c->tlas_rebuilds++;  // a rebuild for an update of the same instance set
+  } else if (tree_work && !async) {  // a new instance set
+    if (!c->tlas_worker) c->tlas_worker.reset(new TlasWorker());
+    c->tlas_worker->seed(tree);
+    c->tlas_depth = depth_cap;
+    c->tlas_rebuilds = c->tlas_async = 0;
     c->tlas_n = n;
-  }
-  if (refit) {  // the tree's boxes re-quantised over this update's instance boxes, in stream order
-    HIP_TRY(launch_tlas_refit(c->stream, c->inst.as<InstDev>(), c->tlas_topo, c->tlas_order.as<uint32_t>(),
-                              c->tlas8.as<Node8>(), c->tlas_slot.as<uint32_t>(), c->tlas_aabb.as<float>()));
-    if (!have_tree) c->tlas_refits++;
+  } else if (async) {
+    c->tlas_rebuilds++;
+    c->tlas_async++;
   }
   c->inst_dirty = false;
   c->tlas_dirty = false;
@@ -1313,7 +1451,7 @@ int prt_destroy(prt_ctx* c) {
   }
   c->comm = nullptr;
   if (c->sh_ev) (void)hipEventDestroy(c->sh_ev);
-  if (c->tlas_job.valid()) (void)c->tlas_job.get();  // the worker's build (host memory only)
+  c->tlas_worker.reset();  // every job is done: each one's stream wait ran before the synchronisations above
   for (StageSlot& st : c->stage) {  // the pinned upload ring (its copies ran: the streams are synchronised)
     if (st.ev) (void)hipEventDestroy(st.ev);
     if (st.p) (void)hipHostFree(st.p);
@@ -2112,8 +2250,15 @@ int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
   info->max_depth = c->max_depth;
   info->tlas_depth = c->use_tlas ? c->tlas_depth : 0;
   info->tlas_rebuilds = c->tlas_rebuilds;
-  info->tlas_refits = c->tlas_refits;
-  info->tlas_rejected = 0;  // (ABI 10: instance BVHs are built on the host only, none is ever rejected)
+  info->tlas_async = c->tlas_async;
+  info->tlas_median = 0;
+  info->tlas_build_ms = info->tlas_build_cpu_ms = 0.0f;
+  if (c->tlas_worker) {
+    const TlasWorker::Stats ws = c->tlas_worker->stats();
+    info->tlas_median = ws.median;
+    info->tlas_build_ms = (float)ws.ms;
+    info->tlas_build_cpu_ms = (float)ws.cpu_ms;
+  }
   info->build_ms = c->build_ms;
   info->builder = c->built_with;
   info->device_bytes = (int64_t)(c->nodes8.bytes + c->tris.bytes + c->stri.bytes + c->texels.bytes + c->sky.bytes +

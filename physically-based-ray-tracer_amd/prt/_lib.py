@@ -102,8 +102,8 @@ class ShardInfo(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("blas_nodes", C.c_int64), ("blas_leaves", C.c_int64), ("device_bytes", C.c_int64),
                 ("max_depth", C.c_int32), ("triangles", C.c_int32), ("build_ms", C.c_double), ("builder", C.c_int32),
-                ("tlas_depth", C.c_int32), ("tlas_rebuilds", C.c_int32), ("tlas_refits", C.c_int32),
-                ("tlas_rejected", C.c_int32)]
+                ("tlas_depth", C.c_int32), ("tlas_rebuilds", C.c_int32), ("tlas_async", C.c_int32),
+                ("tlas_median", C.c_int32), ("tlas_build_ms", C.c_float), ("tlas_build_cpu_ms", C.c_float)]
 
 
 _lib = None

@@ -99,6 +99,8 @@ def main():
     path = os.path.join(ROOT, "profiles", f"{tag}_{scene}_mem.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
+    with open(os.path.join(ROOT, "profiles", f"current_{scene}_mem.json"), "w") as f:  # what bench.py reads
+        json.dump(out, f, indent=1)
     for k in ("k_trace2", "k_shade2", "k_res2d"):
         if k in K:
             print(k, json.dumps(K[k]["derived"]))

@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
 """Instance-BVH drift: N tori drift across the field for F frames (every instance moved
-before every frame, wrapping at the field's edge; frames queued back to back, 1280x720, 2 spp, depth 3), under the
-library's one policy (prt_api.cpp ensure_instances: a host SAH build for every update, on the calling thread up to
-4,096 instances, on a worker thread above with device refits until each build is committed).
+before every frame, wrapping at the field's edge; 1280x720, 2 spp, depth 3), under the library's policy
+(prt_api.cpp ensure_instances: a host SAH build for every update, on the context's worker thread, the stream waiting
+for each update's build before its upload).
 
-Reports: ms per frame over the drift; the host time spent inside prt_set_instances per frame (mean, max); the
-rebuilds / refits the context counted; ms per frame of static frames at the final positions on the drifted tree,
-against a fresh context's tree built over those same positions (the static reference frame).
+The frames are paced as a render loop presenting them would: at most PACE (env PRT_DRIFT_PACE, default 3; 0: no
+pacing, frames queued back to back) frames are queued when an update is made, the wait for the oldest outside the
+timed call.  Reports: ms per frame over the drift; the host time inside prt_set_instances per update (mean, p99,
+max); the rebuilds the context counted, the worker's last build (wall and CPU ms) and its median-split fallbacks;
+ms per frame of static frames at the final positions, against a fresh context's tree built over those positions.
 usage: tlas_drift.py [N] [F]"""
+import collections
 import dataclasses
 import os
 import sys
@@ -24,6 +27,8 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
 F = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 sd = scenes.instance_field(N, seed=17)
 W, H = 1280, 720
+PACE = int(os.environ.get("PRT_DRIFT_PACE", "3"))
+INFLIGHT = int(os.environ.get("PRT_DRIFT_INFLIGHT", "1"))  # frames in flight of both contexts
 rng = np.random.default_rng(3)
 vel = rng.uniform(-0.08, 0.08, (len(sd.instances), 2)).astype(np.float32)
 
@@ -53,19 +58,28 @@ def context(inst):
     mi, T = inst
     ctx.set_scene(prt.Scene.from_data(dataclasses.replace(sd, instances=[(int(m), T[k]) for k, m in enumerate(mi)])))
     ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
+    ctx.set_frames_in_flight(INFLIGHT)
     return ctx
 
 
 def frames(ctx, avg, rgb, n, inst=None, host_ms=None):
     torch.cuda.synchronize()
+    queued = collections.deque()
     t0 = time.perf_counter()
     for i in range(n):
         if inst is not None:
             inst = drift(inst)
+            while PACE and len(queued) >= PACE:  # the render loop's present of the oldest queued frame
+                queued.popleft().synchronize()
             h0 = time.perf_counter()
             set_instances(ctx, inst)
             host_ms.append((time.perf_counter() - h0) * 1e3)
         ctx.render(W, H, 2, 3, frame_index=i, avg=avg.data_ptr(), rgb8=rgb.data_ptr(), device_out=True, stats=False)
+        if PACE:
+            ev = torch.cuda.Event()
+            ev.record()
+            queued.append(ev)
+    ctx.finish()
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) * 1e3 / n, inst
 
@@ -78,15 +92,16 @@ frames(ctx, avg, rgb, 10)  # warm
 host = []
 ms_drift, inst = frames(ctx, avg, rgb, F, inst0, host)
 si = ctx.scene_info()
-time.sleep(0.3)  # (above 4,096 instances: the worker's last build finishes; the next update commits it)
-set_instances(ctx, inst)
 ms_end, _ = frames(ctx, avg, rgb, 20)
 ctx.close()
 ref = context(inst)
 frames(ref, avg, rgb, 5)
 ms_ref, _ = frames(ref, avg, rgb, 20)
 ref.close()
-print(f"{N} instances, {F} frames of drift: {ms_drift:.3f} ms/frame; set_instances host {np.mean(host):.3f} ms mean, "
-      f"{np.max(host):.3f} ms max; {si.tlas_rebuilds} rebuilds / {si.tlas_refits} refits; static at the end "
-      f"{ms_end:.3f} ms/frame vs {ms_ref:.3f} on a fresh tree ({(ms_end / ms_ref - 1) * 100:+.1f} %); drift vs "
-      f"fresh static {ms_drift / ms_ref:.3f}x", flush=True)
+print(f"{N} instances, {F} frames of drift (pace {PACE}, {INFLIGHT} in flight; stacks for {si.max_depth} + "
+      f"{si.tlas_depth} levels): {ms_drift:.3f} ms/frame; set_instances host "
+      f"{np.mean(host):.3f} ms mean, {np.percentile(host, 99):.3f} p99, {np.max(host):.3f} max; {si.tlas_rebuilds} "
+      f"rebuilds ({si.tlas_async} on the worker, {si.tlas_median} median-split), last worker build "
+      f"{si.tlas_build_ms:.2f} ms ({si.tlas_build_cpu_ms:.2f} ms CPU); static at the end {ms_end:.3f} ms/frame vs "
+      f"{ms_ref:.3f} on a fresh tree ({(ms_end / ms_ref - 1) * 100:+.1f} %); drift vs fresh static "
+      f"{ms_drift / ms_ref:.3f}x", flush=True)

@@ -122,8 +122,8 @@ def test_extensions_match_oracle(gpu_ctx, case, flags):
     a_g, r_g, s_g = gpu_ctx.render(W, H, spp, 4, flags)
     err = rmse(a_o, a_g)
     exact = float(np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)))
-    assert err <= RMSE_TOL, (case, err, exact)
-    assert exact >= 0.999, (case, exact)
+    assert err <= RMSE_TOL, (case, err, exact)  # BASELINE.json's bar; achieved and asserted: bit-identical
+    assert err == 0.0 and exact == 1.0 and np.array_equal(r_o, r_g), (case, err, exact)
     assert (s_o.segments, s_o.shadow_rays) == (s_g.segments, s_g.shadow_rays)
 
 

@@ -49,7 +49,9 @@ def test_random_rays_closest_and_anyhit(gpu_ctx):
     assert np.array_equal(osc.occluded(O, D, tmax), gpu_ctx.occluded(O, D, tmax))
 
 
-def _compare_render(gpu_ctx, sd, W, H, spp, bounces, flags=oracle.DEFAULT_FLAGS, mode=0, exact_frac=0.999):
+def _compare_render(gpu_ctx, sd, W, H, spp, bounces, flags=oracle.DEFAULT_FLAGS, mode=0, exact_frac=1.0):
+    """GPU frame against the oracle's: the bar is BASELINE.json's per-channel RMSE <= 1e-4 (RMSE_TOL); what the
+    kernels achieve, and what is asserted, is every pixel and every RGB8 value identical (exact_frac 1.0)."""
     gpu_scene(gpu_ctx, sd, W, H)
     osc = oracle.OracleScene(sd, W, H)
     a_o, r_o, _, s_o = osc.render(W, H, spp=spp, bounces=bounces, flags=flags, mode=mode)
@@ -59,6 +61,8 @@ def _compare_render(gpu_ctx, sd, W, H, spp, bounces, flags=oracle.DEFAULT_FLAGS,
     assert err <= RMSE_TOL, (err, exact)
     assert exact >= exact_frac, (err, exact)
     assert np.mean(r_o == r_g) >= exact_frac
+    if exact_frac == 1.0:
+        assert err == 0.0
     assert s_g.segments == s_o.segments or abs(int(s_g.segments) - int(s_o.segments)) <= 0.001 * s_o.segments
     return err, exact, s_g
 
@@ -127,7 +131,7 @@ def test_progressive_accumulation(gpu_ctx):
         a_o, r_o, st, _ = osc.render(W, H, spp=2, bounces=3, frame_index=f, state=st)
         a_g, r_g, _ = gpu_ctx.render(W, H, 2, 3, frame_index=f)
         assert rmse(a_o, a_g) <= RMSE_TOL
-    assert np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)) > 0.999
+        assert np.array_equal(a_o[:, :3], a_g[:, :3]) and np.array_equal(r_o, r_g), f  # every frame exact
 
 
 def test_ray_totals_match_stats(gpu_ctx, monkeypatch):
@@ -247,7 +251,7 @@ def test_c4_full_size_matches_oracle(gpu_ctx):
     """BASELINE's headline workload itself against the oracle: C4 (1M triangles), 1920x1080, 4 spp, depth 4, all
     reference features on.  The oracle renders the full frame on the host cores (OpenMP, ~1-2 s at 16 threads), so
     the bench frame is compared directly, not only through size-independent properties: per-channel RMSE
-    <= 1e-4 (BASELINE.json), >= 99.9 % bit-identical pixels, identical ray counts."""
+    <= 1e-4 is BASELINE.json's bar; asserted is RMSE 0, every pixel and RGB8 value identical, identical ray counts."""
     import os
     sd = scenes.config_c4()
     W, H = 1920, 1080
@@ -258,15 +262,15 @@ def test_c4_full_size_matches_oracle(gpu_ctx):
     err = rmse(a_o, a_g)
     exact = float(np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)))
     assert err <= RMSE_TOL, (err, exact)
-    assert exact >= 0.999, (err, exact)
-    assert np.mean(r_o == r_g) >= 0.999
+    assert err == 0.0 and exact == 1.0, (err, exact)
+    assert np.array_equal(r_o, r_g)
     assert (s_g.segments, s_g.shadow_rays) == (s_o.segments, s_o.shadow_rays)
 
 
 def test_c3_full_size_matches_oracle(gpu_ctx):
     """Config C3 (the 100k-triangle scene) at its own size, 1920x1080, 4 spp, depth 4, full BRDF + shadow rays,
-    against the oracle: per-channel RMSE <= 1e-4 (BASELINE.json), >= 99.9 % bit-identical pixels, identical ray
-    counts (the reduced-size fixtures cover it against the reference traversal, tests/test_golden_ref.py)."""
+    against the oracle: RMSE 0 (BASELINE.json's bar is <= 1e-4), every pixel and RGB8 value identical, identical
+    ray counts (the reduced-size fixtures cover it against the reference traversal, tests/test_golden_ref.py)."""
     import os
     sd = scenes.config_c3()
     W, H = 1920, 1080
@@ -277,15 +281,15 @@ def test_c3_full_size_matches_oracle(gpu_ctx):
     err = rmse(a_o, a_g)
     exact = float(np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)))
     assert err <= RMSE_TOL, (err, exact)
-    assert exact >= 0.999, (err, exact)
-    assert np.mean(r_o == r_g) >= 0.999
+    assert err == 0.0 and exact == 1.0, (err, exact)
+    assert np.array_equal(r_o, r_g)
     assert (s_g.segments, s_g.shadow_rays) == (s_o.segments, s_o.shadow_rays)
 
 
 def test_c5_full_size_matches_oracle(gpu_ctx):
     """Config C5 (C4 + the quad area light with MIS, 16 spp, depth 8) at its own 3840x2160 (592M rays; the
-    bench's --scene c5 frame) against the oracle's extension restatement: RMSE <= 1e-4, >= 99.9 % identical
-    pixels, identical ray counts."""
+    bench's --scene c5 frame) against the oracle's extension restatement: RMSE 0 (the bar is <= 1e-4), every
+    pixel identical, identical ray counts."""
     import os
     sd = scenes.config_c5()
     W, H = 3840, 2160
@@ -296,7 +300,7 @@ def test_c5_full_size_matches_oracle(gpu_ctx):
     err = rmse(a_o, a_g)
     exact = float(np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)))
     assert err <= RMSE_TOL, (err, exact)
-    assert exact >= 0.999, (err, exact)
+    assert err == 0.0 and exact == 1.0, (err, exact)
     assert (s_g.segments, s_g.shadow_rays) == (s_o.segments, s_o.shadow_rays)
 
 
@@ -324,8 +328,7 @@ def test_postfx_matches_oracle(gpu_ctx, preset, over, flags):
             a_o, r_o, state, _ = osc.render(W, H, spp=4, bounces=3, flags=flags, frame_index=2 * call, state=state)
             a_g, r_g, _ = gpu_ctx.render(W, H, 4, 3, flags, frame_index=2 * call)
             assert rmse(a_o, a_g) <= RMSE_TOL
-            assert np.mean(np.all(a_o[:, :3] == a_g[:, :3], axis=1)) >= 0.999
-            assert np.mean(r_o == r_g) >= 0.999
+            assert np.array_equal(a_o[:, :3], a_g[:, :3]) and np.array_equal(r_o, r_g)
     finally:
         gpu_ctx.set_postfx(None)
 
@@ -477,11 +480,10 @@ def test_frame_passes_match_one_pass(gpu_ctx, monkeypatch):
 
 @pytest.mark.parametrize("n", [65, 1000, 5000])
 def test_device_tlas_moving_instances(gpu_ctx, n):
-    """Above 64 instances the rays walk an instance BVH rebuilt for every prt_set_instances: up to 4,096 instances by
-    the host SAH build on the calling thread, above that by the same build on a worker thread with the device
-    refitting the current tree (prt_tlas.hip) to every update's boxes until a build is committed.  Every instance moves
-    before every frame, frames are queued back to back with no host synchronisation, and each equals the oracle's
-    render of its transforms."""
+    """Above 64 instances the rays walk an instance BVH rebuilt for every prt_set_instances: by the host SAH build on
+    the calling thread when the instance count changes, then on the context's worker thread, the stream waiting for
+    each update's build before its upload.  Every instance moves before every frame, frames are queued back to back
+    with no host synchronisation, and each equals the oracle's render of its transforms."""
     import dataclasses
     import torch
     sd0 = scenes.instance_field(n, seed=11)
@@ -512,26 +514,20 @@ def test_device_tlas_moving_instances(gpu_ctx, n):
         a_o, _, _, _ = oracle.OracleScene(sd, W, H).render(W, H, spp=2, bounces=3, flags=flags)
         assert np.array_equal(o.cpu().numpy(), a_o)
     si = gpu_ctx.scene_info()
-    if n <= 4096:  # a host build for every update
-        assert si.tlas_rebuilds == len(frames) and si.tlas_refits == 0, (si.tlas_rebuilds, si.tlas_refits)
-    else:  # worker builds committed when done, refits in between
-        assert si.tlas_rebuilds + si.tlas_refits == len(frames), (si.tlas_rebuilds, si.tlas_refits)
+    assert si.tlas_rebuilds == si.tlas_async == len(frames), (si.tlas_rebuilds, si.tlas_async)
 
 
 @pytest.mark.parametrize("mode", ["default", "large"])
 def test_device_tlas_rebuild_long_motion(gpu_ctx, mode):
     """instances drift across the field (every instance moves before every frame, the frames
     queued back to back with device outputs and no host wait).  The instance BVH is rebuilt for every update, the
-    reference's per-frame BVH::Build.  "default": 1,000 tori, 120 frames, a host SAH build on the calling thread for
-    every update (one rebuild per set_instances); "large": 10,000 tori, 40 frames, above the calling thread's
-    4,096: the worker thread's builds committed as they finish, device refits in between (and, after a pause, the
-    next update commits a build).  Every 10th frame equals the oracle's render of that frame's transforms."""
+    reference's per-frame BVH::Build, on the context's worker thread in stream order: "default" 1,000 tori, 120
+    frames; "large" 10,000 tori, 40 frames.  One worker build per set_instances; every 10th frame equals the oracle's
+    render of that frame's transforms."""
     import dataclasses
-    import time
     import torch
     import prt
     n, nframes = (10000, 40) if mode == "large" else (1000, 120)
-    every_frame = mode == "default"
     sd0 = scenes.instance_field(n, seed=17)
     W, H = 64, 48
     flags = oracle.DEFAULT_FLAGS & ~oracle.ACCUMULATE
@@ -565,13 +561,8 @@ def test_device_tlas_rebuild_long_motion(gpu_ctx, mode):
         torch.cuda.synchronize()
         si = c.scene_info()
         assert si.tlas_depth > 0
-        if every_frame:  # one host rebuild per set_instances
-            assert si.tlas_rebuilds == nframes and si.tlas_refits == 0, (si.tlas_rebuilds, si.tlas_refits)
-        else:  # worker builds and refits, one per update
-            assert si.tlas_rebuilds + si.tlas_refits == nframes and si.tlas_refits > 0, (si.tlas_rebuilds, si.tlas_refits)
-            time.sleep(0.5)  # the worker's build of the last boxes is done: the next update commits it
-            c.set_instances(frames[-1].instances)
-            assert c.scene_info().tlas_rebuilds > si.tlas_rebuilds
+        assert si.tlas_rebuilds == si.tlas_async == nframes, (si.tlas_rebuilds, si.tlas_async)
+        assert si.tlas_build_ms > 0.0
         for f, o in out.items():
             a_o, _, _, _ = oracle.OracleScene(frames[f], W, H).render(W, H, spp=2, bounces=3, flags=flags)
             assert np.array_equal(o.cpu().numpy(), a_o), f
@@ -598,16 +589,16 @@ def test_materials_only_update_leaves_instance_bvh(gpu_ctx):
         c.set_materials(None)
         c.set_materials(kinds)
         si1 = c.scene_info()
-        assert (si1.tlas_rebuilds, si1.tlas_refits) == (si0.tlas_rebuilds, si0.tlas_refits)
+        assert si1.tlas_rebuilds == si0.tlas_rebuilds
         a_g, _, _ = c.render(W, H, 2, 2, flags)
         si2 = c.scene_info()
-        assert (si2.tlas_rebuilds, si2.tlas_refits) == (si0.tlas_rebuilds, si0.tlas_refits)
+        assert si2.tlas_rebuilds == si0.tlas_rebuilds
         sdm = scenes.with_extensions(sd, materials=kinds)
         a_o, _, _, _ = oracle.OracleScene(sdm, W, H).render(W, H, spp=2, bounces=2, flags=flags)
         assert np.array_equal(a_g, a_o)
         c.set_instances(sd.instances)  # a transform update still rebuilds
         si3 = c.scene_info()
-        assert si3.tlas_rebuilds + si3.tlas_refits == si0.tlas_rebuilds + si0.tlas_refits + 1
+        assert si3.tlas_rebuilds == si0.tlas_rebuilds + 1
     finally:
         c.close()
 
