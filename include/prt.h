@@ -173,8 +173,10 @@ int prt_set_stream(prt_ctx* ctx, void* hip_stream);
  * internal streams, forked from the context stream, so its wavefront chain overlaps those of the previous n - 1
  * calls; the accumulation (and a sharded frame's gather and untile) still run in call order, so the results are
  * bit-identical to n = 1.  A call's outputs are complete in the context stream's order once n - 1 more render
- * calls have been enqueued, or after prt_finish.  Every other entry point (and a render with host outputs or
- * stats) joins the frames in flight first.  Local shard groups: n = 1 only (PRT_ERR_UNSUPPORTED). */
+ * calls have been enqueued, or after prt_finish.  prt_set_instances / prt_set_instance_materials (ABI 10) do not
+ * join them: the instance state has n + 1 device copies and an update writes the next one once the frames that
+ * read it are done (a stream wait).  Every other entry point (and a render with host outputs or stats) joins the
+ * frames in flight first.  Local shard groups: n = 1 only (PRT_ERR_UNSUPPORTED). */
 int prt_set_frames_in_flight(prt_ctx* ctx, int32_t n);
 /* the context stream waits for every frame in flight (no host wait) */
 int prt_finish(prt_ctx* ctx);

@@ -111,6 +111,14 @@ struct StageSlot {
   hipEvent_t ev = nullptr;
   bool used = false;
 };
+// One copy of the instance state the frames read (prt_ctx::isets): instance records, their refit input, the instance
+// BVH.  An update writes the next copy in the ring while the frames in flight still read theirs; a copy is
+// rewritten only after the context stream has waited for the frames that read it (one event per stream they ran on)
+struct InstSet {
+  DevBuf inst, inst_src, tlas8, tlas_slot;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;  // the last frame that read this copy, per stream
+  size_t nuse = 0;
+};
 // The instance BVH's per-update build (ensure_instances) on the context's worker thread: each update's job builds
 // the tree over that update's instance boxes into the update's pinned staging buffer; the render stream waits for
 // the job at a host function (hipLaunchHostFunc) placed before the tree's upload, so the calling thread never
@@ -260,7 +268,9 @@ struct prt_ctx {
   std::vector<uint32_t> inst_mesh;
   std::vector<uint32_t> inst_kind;  // prt_set_instance_materials (PRT_MAT_*), textured by default
   std::vector<InstSrc> inst_stage;  // host side of the refit input (prt_refit.h)
-  DevBuf inst, inst_src;
+  // the device instance state, one copy per frame in flight + 1 (InstSet); isets[icur] is what the next frame reads
+  std::vector<InstSet> isets = std::vector<InstSet>(1);
+  size_t icur = 0;
   // instance BVH (more than kLinearInstances instances, or PRT_TLAS=1), rebuilt for every prt_set_instances as the
   // reference rebuilds its TLAS every frame (Core/Renderer.cpp:33-41, Core/tiny_bvh.h:1732-1770): the host SAH
   // build + SAH-optimal collapse (bvh_build.h build_tlas8), on the calling thread when the instance set changes,
@@ -268,7 +278,6 @@ struct prt_ctx {
   bool use_tlas = false;
   int tlas_depth = 0;    // levels the traversal stacks are sized for (>= the current tree's depth)
   int32_t tlas_n = -1;   // instance count of the current tree (-1: none)
-  DevBuf tlas8, tlas_slot;
   std::unique_ptr<TlasWorker> tlas_worker;
   int32_t tlas_rebuilds = 0, tlas_async = 0;  // since the instance count last changed (diagnostics)
   // pinned staging buffers of ensure_instances' uploads (instance sources, a new tree's nodes / slots / refit order;
@@ -508,6 +517,14 @@ int ensure_instances(prt_ctx* c) {
     src.resize(n);
     fill(src.data());
   }
+  // the copy of the instance state this update writes: the next one in the ring (frames in flight + 1 copies), once
+  // the context stream has waited for the frames that read it
+  if (c->isets.size() < (size_t)c->inflight + 1) c->isets.resize((size_t)c->inflight + 1);
+  const size_t nx = (c->icur + 1) % c->isets.size();
+  InstSet& cur = c->isets[c->icur];
+  InstSet& X = c->isets[nx];
+  for (size_t k = 0; k < X.nuse; k++) HIP_TRY(hipStreamWaitEvent(c->stream, X.uses[k].second, 0));
+  X.nuse = 0;
   // a new instance set: its first tree on the calling thread; the stacks are sized for the largest depth that keeps
   // the traversal's occupancy (and at least the median-split tree's), the cap of the worker's builds
   BuiltTlas8 tree;
@@ -531,15 +548,15 @@ int ensure_instances(prt_ctx* c) {
   // later updates never reallocate (a reallocation frees what queued frames read: it drains first, a host wait)
   const size_t cap = (size_t)std::max(n, kLinearInstances);
   const size_t cap_nodes = (size_t)std::max(n, 1);
-  if (c->inst.bytes < sizeof(InstDev) * cap || c->inst_src.bytes < sizeof(InstSrc) * cap ||
-      (tree_work && (c->tlas8.bytes < cap_nodes * sizeof(Node8) || c->tlas_slot.bytes < cap_nodes * 32))) {
+  if (X.inst.bytes < sizeof(InstDev) * cap || X.inst_src.bytes < sizeof(InstSrc) * cap ||
+      (use_tlas && (X.tlas8.bytes < cap_nodes * sizeof(Node8) || X.tlas_slot.bytes < cap_nodes * 32))) {
     const int rc = drain(c);
     if (rc) return rc;
-    HIP_TRY(c->inst.ensure(sizeof(InstDev) * cap));
-    HIP_TRY(c->inst_src.ensure(sizeof(InstSrc) * cap));
-    if (tree_work) {
-      HIP_TRY(c->tlas8.ensure(cap_nodes * sizeof(Node8)));
-      HIP_TRY(c->tlas_slot.ensure(cap_nodes * 32));
+    HIP_TRY(X.inst.ensure(sizeof(InstDev) * cap));
+    HIP_TRY(X.inst_src.ensure(sizeof(InstSrc) * cap));
+    if (use_tlas) {
+      HIP_TRY(X.tlas8.ensure(cap_nodes * sizeof(Node8)));
+      HIP_TRY(X.tlas_slot.ensure(cap_nodes * 32));
     }
   }
   // uploads through one pinned staging slot: the instance sources, then the tree's nodes and slots
@@ -568,8 +585,8 @@ int ensure_instances(prt_ctx* c) {
   char* hp = static_cast<char*>(st->p);
   if (async) fill(reinterpret_cast<InstSrc*>(hp));
   else std::memcpy(hp, src.data(), sb_src);
-  HIP_TRY(hipMemcpyAsync(c->inst_src.p, hp, sb_src, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(launch_refit(c->stream, c->inst_src.as<InstSrc>(), n, c->inst.as<InstDev>()));
+  HIP_TRY(hipMemcpyAsync(X.inst_src.p, hp, sb_src, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(launch_refit(c->stream, X.inst_src.as<InstSrc>(), n, X.inst.as<InstDev>()));
   if (tree_work) {
     char* q = hp + sb_src;
     if (async) {  // the worker writes the tree into q; the stream's upload waits for it
@@ -585,8 +602,11 @@ int ensure_instances(prt_ctx* c) {
       std::memcpy(q, tree.nodes.data(), sb_nodes);
       std::memcpy(q + sb_nodes, tree.slot.data(), sb_slot);
     }
-    HIP_TRY(hipMemcpyAsync(c->tlas8.p, q, sb_nodes, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->tlas_slot.p, q + sb_nodes, sb_slot, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(X.tlas8.p, q, sb_nodes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(X.tlas_slot.p, q + sb_nodes, sb_slot, hipMemcpyHostToDevice, c->stream));
+  } else if (use_tlas && &X != &cur) {  // a materials-only update: the current tree, into this copy
+    HIP_TRY(hipMemcpyAsync(X.tlas8.p, cur.tlas8.p, cap_nodes * sizeof(Node8), hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(X.tlas_slot.p, cur.tlas_slot.p, cap_nodes * 32, hipMemcpyDeviceToDevice, c->stream));
   }
   rc = stage_release(c, *st, c->stream);
   if (rc) return rc;
@@ -604,8 +624,29 @@ int ensure_instances(prt_ctx* c) {
     c->tlas_rebuilds++;
     c->tlas_async++;
   }
+  c->icur = nx;
   c->inst_dirty = false;
   c->tlas_dirty = false;
+  return PRT_OK;
+}
+
+// a frame enqueued on stream st reads the current copy of the instance state: the next update that rewrites it
+// waits for this point of st (InstSet)
+int record_inst_use(prt_ctx* c, hipStream_t st) {
+  InstSet& I = c->isets[c->icur];
+  for (size_t k = 0; k < I.nuse; k++)
+    if (I.uses[k].first == st) {
+      HIP_TRY(hipEventRecord(I.uses[k].second, st));
+      return PRT_OK;
+    }
+  if (I.nuse == I.uses.size()) {
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    I.uses.push_back({st, e});
+  }
+  I.uses[I.nuse].first = st;
+  HIP_TRY(hipEventRecord(I.uses[I.nuse].second, st));
+  I.nuse++;
   return PRT_OK;
 }
 
@@ -641,13 +682,13 @@ int scene_ready(prt_ctx* c, SceneDev& S) {
   S.srgb = c->srgb.as<float>();
   S.texels = c->texels.as<uint32_t>();
   S.tex = c->tex.as<TexDev>();
-  S.inst = c->inst.as<InstDev>();
+  S.inst = c->isets[c->icur].inst.as<InstDev>();
   S.mesh = c->mesh.as<MeshDev>();
   S.sky = (c->skyw > 0) ? c->sky.as<float>() : nullptr;
   S.ninst = (int32_t)c->inst_mesh.size();
   S.tlas = c->use_tlas ? 1 : 0;
-  S.tlas8 = c->use_tlas ? c->tlas8.as<Node8>() : nullptr;
-  S.tlas_slot = c->use_tlas ? c->tlas_slot.as<uint32_t>() : nullptr;
+  S.tlas8 = c->use_tlas ? c->isets[c->icur].tlas8.as<Node8>() : nullptr;
+  S.tlas_slot = c->use_tlas ? c->isets[c->icur].tlas_slot.as<uint32_t>() : nullptr;
   {  // packed hit word: prim bits for the largest mesh, instance bits above
     uint32_t maxt = 1;
     for (const MeshDev& m : c->mesh_host) maxt = std::max(maxt, m.tri_count);
@@ -904,9 +945,18 @@ int prepare_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, int
 // render on the context stream; want_stats: per-launch timers + read_stats() afterwards
 // fl: a frame in flight (its stream, wavefront state and frame buffer; the accumulation first waits for acc_after,
 // the previous call's last work), else the context stream and state
+int enqueue_render_body(prt_ctx* c, const prt_render_params* p, const TileMap& M, RenderPlan& R, float4* avg_dev,
+                        uint32_t* rgb8_dev, float4* tiles_dev, bool want_stats, Flight* fl, hipEvent_t acc_after);
+// one call's frames on the flight's stream (or the context stream), then the mark of its read of the instance state
 int enqueue_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, RenderPlan& R, float4* avg_dev,
                    uint32_t* rgb8_dev, float4* tiles_dev, bool want_stats, Flight* fl = nullptr,
                    hipEvent_t acc_after = nullptr) {
+  const int rc = enqueue_render_body(c, p, M, R, avg_dev, rgb8_dev, tiles_dev, want_stats, fl, acc_after);
+  const int urc = record_inst_use(c, fl ? fl->stream : c->stream);
+  return rc ? rc : urc;
+}
+int enqueue_render_body(prt_ctx* c, const prt_render_params* p, const TileMap& M, RenderPlan& R, float4* avg_dev,
+                        uint32_t* rgb8_dev, float4* tiles_dev, bool want_stats, Flight* fl, hipEvent_t acc_after) {
   SceneDev& S = R.S;
   TraceArgs& A = R.A;
   const int32_t F = R.F, fmax = R.fmax, npass = R.npass;
@@ -1452,6 +1502,8 @@ int prt_destroy(prt_ctx* c) {
   c->comm = nullptr;
   if (c->sh_ev) (void)hipEventDestroy(c->sh_ev);
   c->tlas_worker.reset();  // every job is done: each one's stream wait ran before the synchronisations above
+  for (InstSet& I : c->isets)
+    for (auto& u : I.uses) (void)hipEventDestroy(u.second);
   for (StageSlot& st : c->stage) {  // the pinned upload ring (its copies ran: the streams are synchronised)
     if (st.ev) (void)hipEventDestroy(st.ev);
     if (st.p) (void)hipHostFree(st.p);
@@ -1683,7 +1735,7 @@ int prt_set_bvh_builder(prt_ctx* c, int32_t builder) {
 
 int prt_set_instances(prt_ctx* c, const float* xf, const uint32_t* mi, int32_t n) {
   if (!c || !xf || !mi || n <= 0) return fail(PRT_ERR_INVALID_ARGUMENT, "bad instances");
-  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
+  // (no join of the frames in flight: the update writes the next copy of the instance state, InstSet)
   if (n > kMaxInstances) return fail(PRT_ERR_UNSUPPORTED, "more than 2^24 instances");
   c->inst_xf.assign(xf, xf + 16 * (size_t)n);
   if ((size_t)n != c->inst_mesh.size()) c->inst_kind.clear();  // materials survive transform updates only
@@ -1701,7 +1753,7 @@ int prt_set_instances(prt_ctx* c, const float* xf, const uint32_t* mi, int32_t n
 
 int prt_set_instance_materials(prt_ctx* c, const int32_t* kinds, int32_t n) {
   if (!c) return fail(PRT_ERR_INVALID_ARGUMENT, "ctx is NULL");
-  PRT_JOIN(c);  // frames in flight complete first (prt_set_frames_in_flight)
+  // (no join of the frames in flight: the update writes the next copy of the instance state, InstSet)
   if (n == 0 || !kinds) {
     c->inst_kind.clear();
   } else {
@@ -2261,8 +2313,9 @@ int prt_get_scene_info(prt_ctx* c, prt_scene_info* info) {
   }
   info->build_ms = c->build_ms;
   info->builder = c->built_with;
-  info->device_bytes = (int64_t)(c->nodes8.bytes + c->tris.bytes + c->stri.bytes + c->texels.bytes + c->sky.bytes +
-                                 c->inst.bytes);
+  size_t ib = 0;
+  for (const InstSet& I : c->isets) ib += I.inst.bytes + I.inst_src.bytes + I.tlas8.bytes + I.tlas_slot.bytes;
+  info->device_bytes = (int64_t)(c->nodes8.bytes + c->tris.bytes + c->stri.bytes + c->texels.bytes + c->sky.bytes + ib);
   return PRT_OK;
 }
 

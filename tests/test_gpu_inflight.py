@@ -2,8 +2,9 @@
 device outputs enqueues its wavefront chain on one of two internal streams, so consecutive calls overlap, while the
 accumulation (the reference's progressive mean, Core/Renderer.cpp:81-104) and a sharded frame's gather stay in call
 order.  Every frame must equal the one-at-a-time render bit for bit: outputs, ray totals, through instance updates
-(the instance BVH refitted between frames), a camera change with an accumulation reset, a stats call in between,
-the merged and unmerged pipelines and the RCCL gather."""
+(the instance BVH rebuilt between frames; an update writes the next copy of the instance state while the frames in
+flight read theirs), a camera change with an accumulation reset, a stats call in between, the merged and unmerged
+pipelines and the RCCL gather."""
 import numpy as np
 import pytest
 
@@ -13,17 +14,20 @@ from prt import scenes
 pytestmark = pytest.mark.gpu
 
 
-def _frames(c, sd, W, H, n, moves, stream):
-    """n accumulating frames with device outputs (one output pair per frame), instance moves before frame
-    `moves`, a camera change + accumulation reset before frame n - 2 and a stats render at the end."""
+def _frames(c, sd, W, H, n, moves, stream, materials_at=-1):
+    """n accumulating frames with device outputs (one output pair per frame), instance moves before the frames in
+    `moves`, mirror materials on every 5th instance before frame `materials_at`, a camera change + accumulation
+    reset before frame n - 2 and a stats render at the end."""
     import torch
     import prt
     outs = []
     inst = [(m, np.array(T, np.float32)) for m, T in sd.instances]
     for f in range(n):
-        if f == moves:
+        if f in moves:
             inst = [(m, _shift(T, m)) for m, T in inst]
             c.set_instances(inst)
+        if f == materials_at:
+            c.set_materials([2 if i % 5 == 1 else 0 for i in range(len(inst))])
         if f == n - 2:
             cam = prt.Camera(np.asarray(sd.cam_pos, np.float32) + np.float32(0.25), sd.cam_target,
                              np.float32(W) / np.float32(H))
@@ -67,7 +71,35 @@ def test_frames_in_flight_match_one_at_a_time(monkeypatch, merge, flights):
             c.set_stream(stream.cuda_stream)
             gpu_scene(c, sd, W, H)
             c.set_frames_in_flight(fl)
-            res.append(_frames(c, sd, W, H, n, 3, stream))
+            res.append(_frames(c, sd, W, H, n, {3}, stream))
+        finally:
+            c.close()
+    (f1, last1, tot1), (f2, last2, tot2) = res
+    for k, ((a1, r1), (a2, r2)) in enumerate(zip(f1, f2)):
+        assert np.array_equal(a1, a2) and np.array_equal(r1, r2), k
+    assert np.array_equal(last1[0], last2[0]) and np.array_equal(last1[1], last2[1])
+    assert last1[2:] == last2[2:] and tot1 == tot2
+
+
+@pytest.mark.parametrize("flights,n_inst", [(2, 120), (4, 120), (3, 40)])
+def test_frames_in_flight_instance_updates_every_frame(flights, n_inst):
+    """Instances moved before every frame and a materials update, with frames in flight: prt_set_instances does not
+    join the frames in flight, each update writing the next of flights + 1 copies of the instance state (records,
+    refit input, instance BVH) once the frames that read it are done; every frame equals the one-at-a-time render
+    (120 instances: the instance BVH, built on the worker thread in stream order; 40: the linear list)."""
+    import torch
+    import prt
+    sd = scenes.instance_field(n_inst, seed=9)
+    W, H, n = 96, 64, 9
+    stream = torch.cuda.Stream()
+    res = []
+    for fl in (1, flights):
+        c = prt.Context(0)
+        try:
+            c.set_stream(stream.cuda_stream)
+            gpu_scene(c, sd, W, H)
+            c.set_frames_in_flight(fl)
+            res.append(_frames(c, sd, W, H, n, set(range(1, n)), stream, materials_at=4))
         finally:
             c.close()
     (f1, last1, tot1), (f2, last2, tot2) = res
@@ -137,7 +169,7 @@ def test_frames_in_flight_rccl_world1(flights):
                 c.shard_rccl(prt.Context.shard_unique_id(), 0, 1, 32)
             gpu_scene(c, sd, W, H)
             c.set_frames_in_flight(fl)
-            res.append(_frames(c, sd, W, H, n, 3, stream))
+            res.append(_frames(c, sd, W, H, n, set(range(1, n)), stream))
         finally:
             c.close()
     (f1, last1, tot1), (f2, last2, tot2) = res
