@@ -105,11 +105,13 @@ struct Flight {
 // 20-190 ms per buffer on the GPU box, profiles/r06_tlas_drift.txt); an update that finds all of them in use waits
 // for the oldest one's copies (the host at most kStageSlots updates ahead of the GPU)
 constexpr size_t kStageSlots = 8;
+constexpr double kHostWaitLimitS = 30.0;  // the stream's wait for a worker build (a build takes ~6 ms at 10,000)
 struct StageSlot {
   void* p = nullptr;
   size_t bytes = 0;
   hipEvent_t ev = nullptr;
   bool used = false;
+  uint64_t seq = 0;  // when it was last acquired
 };
 // One copy of the instance state the frames read (prt_ctx::isets): instance records, their refit input, the instance
 // BVH.  An update writes the next copy in the ring while the frames in flight still read theirs; a copy is
@@ -120,17 +122,19 @@ struct InstSet {
   size_t nuse = 0;
 };
 // The instance BVH's per-update build (ensure_instances) on the context's worker thread: each update's job builds
-// the tree over that update's instance boxes into the update's pinned staging buffer; the render stream waits for
-// the job at a host function (hipLaunchHostFunc) placed before the tree's upload, so the calling thread never
-// builds nor waits, and the frames already queued run while the worker builds.  Jobs run in submission order; the
-// worker never calls HIP, so every stream wait it is behind ends.
+// the tree over that update's instance boxes into the update's pinned staging buffer, then sets the update's flag
+// word; the render stream waits for the flag in a one-lane kernel (launch_wait_host) placed before the tree's
+// upload, so the calling thread never builds nor waits, and the frames already queued run while the worker builds.
+// (A host function, hipLaunchHostFunc, made the next enqueue on the stream block the calling thread until it had
+// run: 5-11 ms per update with frames queued, scripts/inst_update_probe.py.)  Jobs run in submission order and every
+// job sets its flag, also when its build fails; the worker never calls HIP.
 struct TlasJob {
   const InstSrc* src = nullptr;  // the update's instances (in its pinned staging buffer, uploaded before the tree)
   int32_t n = 0;
   char* dst = nullptr;           // pinned: cap Node8 records, then 8 * cap slot words
-  size_t cap = 0;            // nodes the upload moves (a tree over n instances has at most max(n, 1) nodes)
-  int max_depth = 0;         // levels the traversal stacks were sized for (build_tlas8's cap)
-  bool done = false;
+  size_t cap = 0;                // nodes the upload moves (a tree over n instances has at most max(n, 1) nodes)
+  int max_depth = 0;             // levels the traversal stacks were sized for (build_tlas8's cap)
+  uint32_t* flag = nullptr;      // coherent pinned word: set to 1 once dst holds the tree
 };
 class TlasWorker {
  public:
@@ -154,10 +158,6 @@ class TlasWorker {
       q_.push_back(j);
     }
     cv_.notify_all();
-  }
-  void wait(const std::shared_ptr<TlasJob>& j) {
-    std::unique_lock<std::mutex> g(m_);
-    done_cv_.wait(g, [&] { return j->done; });
   }
   // diagnostics of the finished jobs
   struct Stats { double ms = 0, cpu_ms = 0; int32_t median = 0, failed = 0; std::string err; };
@@ -215,12 +215,11 @@ class TlasWorker {
       st_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       st_.cpu_ms = (c1.tv_sec - c0.tv_sec) * 1e3 + (c1.tv_nsec - c0.tv_nsec) * 1e-6;
       st_.median += median ? 1 : 0;
-      j->done = true;
-      done_cv_.notify_all();
+      __atomic_store_n(j->flag, 1u, __ATOMIC_RELEASE);  // the tree is in dst: the stream's wait ends
     }
   }
   std::mutex m_;
-  std::condition_variable cv_, done_cv_;
+  std::condition_variable cv_;
   std::deque<std::shared_ptr<TlasJob>> q_;
   bool stop_ = false;
   std::vector<Node8> good_nodes_;
@@ -228,16 +227,6 @@ class TlasWorker {
   Stats st_;
   std::thread th_;  // last: started once the members above exist
 };
-// the render stream's wait for one job (hipLaunchHostFunc; runs on the runtime's callback thread)
-struct TlasWait {
-  TlasWorker* w;
-  std::shared_ptr<TlasJob> j;
-};
-void tlas_wait_cb(void* p) {
-  TlasWait* tw = static_cast<TlasWait*>(p);
-  tw->w->wait(tw->j);
-  delete tw;
-}
 
 struct MeshHost {
   float bmin[3], bmax[3];
@@ -284,8 +273,10 @@ struct prt_ctx {
   // hipMemcpyAsync from pageable memory may block the host): a buffer is written again only after its copies have
   // run, so the host never waits on queued frames unless it is kStageSlots updates ahead of the GPU
   std::vector<StageSlot> stage;
-  size_t stage_next = 0;  // the oldest buffer in use (the one to wait for when the pool is full)
+  uint64_t stage_seq = 0;  // acquisitions so far (StageSlot::seq: the oldest buffer is waited for when all are in use)
   size_t stage_bytes = 0;  // the size the pool was last allocated for
+  uint32_t* stage_flag = nullptr;      // one coherent pinned word per staging buffer (64-B stride): TlasJob::flag
+  uint32_t* stage_flag_dev = nullptr;  // its device address
   DevBuf spill;  // traversal stack levels beyond the LDS ones (BVHs deeper than 17 levels)
   DevBuf diag;   // SceneDev::diag device counters ([0] traversal stack overflows, cumulative per context)
   // area light (prt_set_area_lights): p0, eu, ev, n, Le, area
@@ -452,12 +443,13 @@ int stage_acquire(prt_ctx* c, size_t bytes, StageSlot*& out) {
     c->stage.emplace_back();
     pick = &c->stage.back();
   }
-  if (!pick) {
-    pick = &c->stage[c->stage_next];
-    c->stage_next = (c->stage_next + 1) % c->stage.size();
+  if (!pick) {  // every buffer in use: wait for the one acquired first
+    for (StageSlot& t : c->stage)
+      if (!pick || t.seq < pick->seq) pick = &t;
     HIP_TRY(hipEventSynchronize(pick->ev));
     pick->used = false;
   }
+  pick->seq = ++c->stage_seq;
   StageSlot& st = *pick;
   if (st.bytes < bytes) {
     if (st.p) HIP_TRY(hipHostFree(st.p));
@@ -512,11 +504,11 @@ int ensure_instances(prt_ctx* c) {
       s.kind = i < (int32_t)c->inst_kind.size() ? c->inst_kind[i] : 0u;
     }
   };
-  std::vector<InstSrc>& src = c->inst_stage;  // (the calling thread's builds; the worker reads the staging buffer)
-  if (!async) {
-    src.resize(n);
-    fill(src.data());
-  }
+  // (filled in ordinary memory and copied into the pinned staging buffer in one memcpy: field-by-field stores into
+  // pinned memory cost ~10 ms per 10,000 instances on the GPU box, profiles/r06_tlas_drift.txt)
+  std::vector<InstSrc>& src = c->inst_stage;
+  src.resize(n);
+  fill(src.data());
   // the copy of the instance state this update writes: the next one in the ring (frames in flight + 1 copies), once
   // the context stream has waited for the frames that read it
   if (c->isets.size() < (size_t)c->inflight + 1) c->isets.resize((size_t)c->inflight + 1);
@@ -567,6 +559,11 @@ int ensure_instances(prt_ctx* c) {
   if (c->stage.size() < kStageSlots || c->stage_bytes < per) {  // the staging buffers this instance set's updates use
     c->stage_bytes = per;
     for (size_t k = c->stage.size(); k < kStageSlots; k++) c->stage.emplace_back();
+    if (!c->stage_flag) {
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->stage_flag), kStageSlots * 64, hipHostMallocCoherent));
+      std::memset(c->stage_flag, 0, kStageSlots * 64);
+      HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->stage_flag_dev), c->stage_flag, 0));
+    }
     for (StageSlot& t : c->stage) {
       if (t.used && hipEventQuery(t.ev) == hipSuccess) t.used = false;
       (void)hipGetLastError();  // (hipErrorNotReady of a buffer still in use)
@@ -583,21 +580,23 @@ int ensure_instances(prt_ctx* c) {
   int rc = stage_acquire(c, sb_src + sb_nodes + sb_slot, st);
   if (rc) return rc;
   char* hp = static_cast<char*>(st->p);
-  if (async) fill(reinterpret_cast<InstSrc*>(hp));
-  else std::memcpy(hp, src.data(), sb_src);
+  std::memcpy(hp, src.data(), sb_src);  // (the worker reads the sources from here)
   HIP_TRY(hipMemcpyAsync(X.inst_src.p, hp, sb_src, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(launch_refit(c->stream, X.inst_src.as<InstSrc>(), n, X.inst.as<InstDev>()));
   if (tree_work) {
     char* q = hp + sb_src;
     if (async) {  // the worker writes the tree into q; the stream's upload waits for it
+      const size_t k = (size_t)(st - c->stage.data());  // this buffer's flag word (free with the buffer)
       auto job = std::make_shared<TlasJob>();
       job->src = reinterpret_cast<const InstSrc*>(hp);
       job->n = n;
       job->dst = q;
       job->cap = cap_nodes;
       job->max_depth = c->tlas_depth;
+      job->flag = c->stage_flag + 16 * k;
+      __atomic_store_n(job->flag, 0u, __ATOMIC_RELAXED);
+      HIP_TRY(launch_wait_host(c->stream, c->stage_flag_dev + 16 * k, c->diag.as<uint32_t>() + 2, kHostWaitLimitS));
       c->tlas_worker->submit(job);
-      HIP_TRY(hipLaunchHostFunc(c->stream, tlas_wait_cb, new TlasWait{c->tlas_worker.get(), job}));
     } else {
       std::memcpy(q, tree.nodes.data(), sb_nodes);
       std::memcpy(q + sb_nodes, tree.slot.data(), sb_slot);
@@ -1101,13 +1100,15 @@ int run_render(prt_ctx* c, const prt_render_params* p, const TileMap& M, float4*
 }
 
 // the context's traversal stack overflow count (SceneDev::diag[0]); waits for the context stream.  diag[1] != 0:
-// a kernel found its kernarg layout assumption broken (prt_wave2.hip Shade2Args) and did no work
-uint64_t diag_overflows(prt_ctx* c, bool* layout_ok = nullptr) {
-  uint32_t v[2] = {0, 0};
-  if (hipMemcpyAsync(v, c->diag.p, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+// a kernel found its kernarg layout assumption broken (prt_wave2.hip Shade2Args) and did no work; diag[2] != 0: the
+// stream's wait for a worker build of the instance BVH timed out (k_wait_host)
+uint64_t diag_overflows(prt_ctx* c, bool* layout_ok = nullptr, bool* wait_ok = nullptr) {
+  uint32_t v[3] = {0, 0, 0};
+  if (hipMemcpyAsync(v, c->diag.p, 12, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return ~0ull;  // unreadable counts as overflowed: never report a clean run that was not checked
   if (layout_ok) *layout_ok = v[1] == 0;
+  if (wait_ok) *wait_ok = v[2] == 0;
   return v[0];
 }
 
@@ -1196,9 +1197,10 @@ int read_stats(prt_ctx* c, prt_stats* stats) {
         }
       }
     }
-    bool layout_ok = true;
-    stats->stack_overflows = diag_overflows(c, &layout_ok);
+    bool layout_ok = true, wait_ok = true;
+    stats->stack_overflows = diag_overflows(c, &layout_ok, &wait_ok);
     if (!layout_ok) return fail(PRT_ERR_HIP, "k_shade2: kernel-argument layout check failed (Shade2Args)");
+    if (!wait_ok) return fail(PRT_ERR_HIP, "the stream's wait for an instance-BVH build timed out");
     stats->segments += c->carry_segments;  // earlier passes of a call above 2^30 work items
     stats->shadow_rays += c->carry_shadow;
     stats->pipeline = 2;
@@ -1504,6 +1506,7 @@ int prt_destroy(prt_ctx* c) {
   c->tlas_worker.reset();  // every job is done: each one's stream wait ran before the synchronisations above
   for (InstSet& I : c->isets)
     for (auto& u : I.uses) (void)hipEventDestroy(u.second);
+  if (c->stage_flag) (void)hipHostFree(c->stage_flag);
   for (StageSlot& st : c->stage) {  // the pinned upload ring (its copies ran: the streams are synchronised)
     if (st.ev) (void)hipEventDestroy(st.ev);
     if (st.p) (void)hipHostFree(st.p);
@@ -1910,12 +1913,13 @@ int prt_ray_totals(prt_ctx* c, uint64_t* segments, uint64_t* shadow_rays, int32_
   for (prt_ctx* m : all) {
     HIP_TRY(hipSetDevice(m->device));
     Counters h{};
-    uint32_t dg[2] = {0, 0};
+    uint32_t dg[3] = {0, 0, 0};
     HIP_TRY(hipMemcpyAsync(&h, ray_totals_dev(m), sizeof(h), hipMemcpyDeviceToHost, m->stream));
-    HIP_TRY(hipMemcpyAsync(dg, m->diag.p, 8, hipMemcpyDeviceToHost, m->stream));
+    HIP_TRY(hipMemcpyAsync(dg, m->diag.p, 12, hipMemcpyDeviceToHost, m->stream));
     if (reset) HIP_TRY(hipMemsetAsync(ray_totals_dev(m), 0, sizeof(Counters), m->stream));
     HIP_TRY(hipStreamSynchronize(m->stream));
     if (dg[1] != 0) return fail(PRT_ERR_HIP, "k_shade2: kernel-argument layout check failed (Shade2Args)");
+    if (dg[2] != 0) return fail(PRT_ERR_HIP, "the stream's wait for an instance-BVH build timed out");
     seg += h.segments;
     sh += h.shadow;
   }

@@ -111,6 +111,9 @@ constexpr uint32_t kSpillTraceBlocks = 256u * 4u * 4u;
 constexpr int kSpillTraceStack = 18;
 // device refit of the instances (prt_refit.h)
 hipError_t launch_refit(hipStream_t s, const InstSrc* src, int32_t n, InstDev* out);
+// the stream waits until *flag (coherent pinned host memory, device address) is nonzero; after `seconds` it stops
+// waiting and sets *err (prt_render.hip k_wait_host)
+hipError_t launch_wait_host(hipStream_t s, uint32_t* flag, uint32_t* err, double seconds);
 hipError_t launch_primary_hits(const LaunchCfg& c, const SceneDev& S, const TileMap& M, HitOut* out, Counters* cnt);
 hipError_t launch_intersect(const LaunchCfg& c, const SceneDev& S, int32_t n, const float* O, const float* D,
                             const float* tmax, HitOut* out);

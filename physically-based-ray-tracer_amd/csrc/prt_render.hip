@@ -320,6 +320,32 @@ hipError_t launch_brdf_probe(hipStream_t s, int32_t op, int32_t n, const float* 
   return hipGetLastError();
 }
 
+// ---- the stream's wait for a host producer (prt_api.cpp ensure_instances: the worker thread's build of the instance
+// BVH, written into pinned memory before its upload): one lane polls a word of coherent pinned host memory until the
+// producer sets it, sleeping between polls.  A kernel, not a host function: work enqueued behind a pending host
+// function blocks the enqueuing thread on this runtime, a kernel does not.  After `limit` wall-clock ticks it gives
+// up and flags err (device memory), so a producer that never comes cannot hold the GPU.
+__global__ void k_wait_host(uint32_t* flag, uint32_t* err, uint64_t limit) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+    if (wall_clock64() - t0 > limit) {
+      *err = 1u;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(32);
+  }
+}
+hipError_t launch_wait_host(hipStream_t s, uint32_t* flag, uint32_t* err, double seconds) {
+  int dev = 0, khz = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  if (e != hipSuccess) return e;
+  const uint64_t limit = (uint64_t)(seconds * 1e3 * (double)(khz > 0 ? khz : 100000));
+  hipLaunchKernelGGL(k_wait_host, dim3(1), dim3(64), 0, s, flag, err, limit);
+  return hipGetLastError();
+}
+
 // ---- instance refit (BLASInstance::Update on the device): one thread per instance
 __global__ void k_refit(const InstSrc* __restrict__ src, int32_t n, InstDev* __restrict__ out) {
   const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);

@@ -41,8 +41,14 @@ W, H, SPP, BOUNCES = (3840, 2160, 16, 8) if C5 else (1920, 1080, 4, 4)
 FPC = SPP // 2
 TILE = 32
 ctx = prt.Context(0)
-stream = torch.cuda.current_stream()
-ctx.set_stream(stream.cuda_stream)
+# the context on a torch side stream: the untile's events below are recorded in its order (torch's current stream is
+# the null stream, and prt_set_stream(NULL) would mean the context's own stream, which torch's events do not see)
+stream = torch.cuda.Stream()
+if os.environ.get("PRT_RANK_STREAM", "side") == "own":  # A/B: the context's own stream (what NULL selects)
+    ctx.set_stream(None)
+    stream = None
+else:
+    ctx.set_stream(stream.cuda_stream)
 ctx.set_scene(prt.Scene.from_data(sd))
 ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
 NT = 2 if C5 else 8  # timed frames per share
@@ -55,6 +61,7 @@ def share_ms(world, rank, inflight):
     tiles = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
     avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
     rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # (the buffers are filled on the null stream, the frames run on the side stream)
 
     def frame(i):
         if world == 1:
@@ -84,14 +91,15 @@ def share_ms(world, rank, inflight):
     return ms, (seg + sh) // NT
 
 
-def event_ms(fn, reps=50):
+def event_ms(fn, on, reps=50):
+    """mean ms of fn over reps, HIP events on stream `on` (the stream fn's work runs on)"""
     fn()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(stream)
+    a.record(on)
     for _ in range(reps):
         fn()
-    b.record(stream)
+    b.record(on)
     torch.cuda.synchronize()
     return a.elapsed_time(b) / reps
 
@@ -101,12 +109,14 @@ def collective_ms(world):
     per = ctx.tile_buffer_pixels(W, H, TILE, world)
     part = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
     bufs = [torch.zeros_like(part)]
-    g = event_ms(lambda: dist.gather(part, bufs, dst=0))
+    g = event_ms(lambda: dist.gather(part, bufs, dst=0), torch.cuda.current_stream())  # (torch's RCCL ordering)
     gathered = torch.zeros((world * per, 4), dtype=torch.float32, device="cuda")
     avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
     rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     ctx.finish()
-    u = event_ms(lambda: ctx.untile(gathered.data_ptr(), W, H, TILE, world, avg.data_ptr(), rgb.data_ptr()))
+    torch.cuda.synchronize()
+    u = event_ms(lambda: ctx.untile(gathered.data_ptr(), W, H, TILE, world, avg.data_ptr(), rgb.data_ptr()),
+                 stream or torch.cuda.current_stream())  # (own stream: the untile is not on the events' stream)
     return g, u, per * 16
 
 

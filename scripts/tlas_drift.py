@@ -29,6 +29,9 @@ sd = scenes.instance_field(N, seed=17)
 W, H = 1280, 720
 PACE = int(os.environ.get("PRT_DRIFT_PACE", "3"))
 INFLIGHT = int(os.environ.get("PRT_DRIFT_INFLIGHT", "1"))  # frames in flight of both contexts
+# the contexts' stream: a torch side stream, so the pacing events below are recorded in the frames' order (torch's
+# current stream is the null stream here, and prt_set_stream(NULL) means the context's own stream)
+STREAM = torch.cuda.Stream()
 rng = np.random.default_rng(3)
 vel = rng.uniform(-0.08, 0.08, (len(sd.instances), 2)).astype(np.float32)
 
@@ -54,7 +57,7 @@ def set_instances(ctx, inst):  # the ABI call itself (prt_set_instances), withou
 def context(inst):
     """a fresh context whose first instance BVH is built over `inst` (the scene's own instances)"""
     ctx = prt.Context(0)
-    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.set_stream(STREAM.cuda_stream)
     mi, T = inst
     ctx.set_scene(prt.Scene.from_data(dataclasses.replace(sd, instances=[(int(m), T[k]) for k, m in enumerate(mi)])))
     ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
@@ -77,7 +80,7 @@ def frames(ctx, avg, rgb, n, inst=None, host_ms=None):
         ctx.render(W, H, 2, 3, frame_index=i, avg=avg.data_ptr(), rgb8=rgb.data_ptr(), device_out=True, stats=False)
         if PACE:
             ev = torch.cuda.Event()
-            ev.record()
+            ev.record(STREAM)
             queued.append(ev)
     ctx.finish()
     torch.cuda.synchronize()
