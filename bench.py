@@ -212,6 +212,9 @@ def main():
     ap.add_argument("--scene", default="c4", choices=["c3", "c4", "c5"],
                     help="c4 = the metric's workload (default); c5 = C4 + a quad area light with MIS at 4K, 16 spp, depth 8")
     ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--context-stream", default="own", choices=["own", "side"],
+                    help="the context's HIP stream: its own (default; torch's null stream maps to it) or a torch side "
+                         "stream (A/B, profiles/r06_stream_ab.txt)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=None, choices=range(1, 9),
                     help="frames in flight (prt_set_frames_in_flight; default 2 on one GPU, 4 on several): "
@@ -264,7 +267,11 @@ def main():
     args.bounces = args.bounces if args.bounces is not None else (8 if big else 4)
     W, H = args.width, args.height
     ctx = prt.Context(local)
-    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    # torch's current stream is the null stream here, so the context runs on its own (non-blocking) stream; a torch
+    # side stream measured 3,880-3,887 Mrays/s at N = 1 against 4,040 (the two frames in flight did not overlap;
+    # profiles/r06_stream_ab.txt)
+    cstream = torch.cuda.Stream(device=dev) if args.context_stream == "side" else None
+    ctx.set_stream(cstream.cuda_stream if cstream is not None else torch.cuda.current_stream().cuda_stream)
     scene = prt.Scene.from_data(sd)
     ctx.set_scene(scene)
     ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))

@@ -40,17 +40,21 @@ sd = scenes.config_c5() if C5 else scenes.config_c4()
 W, H, SPP, BOUNCES = (3840, 2160, 16, 8) if C5 else (1920, 1080, 4, 4)
 FPC = SPP // 2
 TILE = 32
+# bench.py's order on several GPUs: RCCL first (torch.distributed; here world 1, for the gather timing), then the
+# context on its own stream (torch's null stream maps to it) with its frames-in-flight streams created at once --
+# HIP deals a process's streams over its hardware queues as they are created (profiles/r06_stream_ab.txt).
+# PRT_RANK_STREAM=side puts the context on a torch side stream instead (A/B).  The untile is timed on a side stream
+# either way, so that torch's events see it.
+os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+os.environ.setdefault("MASTER_PORT", "29531")
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
 ctx = prt.Context(0)
-# the context on a torch side stream: the untile's events below are recorded in its order (torch's current stream is
-# the null stream, and prt_set_stream(NULL) would mean the context's own stream, which torch's events do not see)
-stream = torch.cuda.Stream()
-if os.environ.get("PRT_RANK_STREAM", "side") == "own":  # A/B: the context's own stream (what NULL selects)
-    ctx.set_stream(None)
-    stream = None
-else:
-    ctx.set_stream(stream.cuda_stream)
+SIDE = os.environ.get("PRT_RANK_STREAM", "own") == "side"
+side = torch.cuda.Stream() if SIDE else None
+ctx.set_stream(side.cuda_stream if SIDE else None)
 ctx.set_scene(prt.Scene.from_data(sd))
 ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
+ctx.set_frames_in_flight(max(INFLIGHT, INFLIGHT1))
 NT = 2 if C5 else 8  # timed frames per share
 
 
@@ -61,7 +65,7 @@ def share_ms(world, rank, inflight):
     tiles = torch.zeros((per, 4), dtype=torch.float32, device="cuda")
     avg = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
     rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
-    torch.cuda.synchronize()  # (the buffers are filled on the null stream, the frames run on the side stream)
+    torch.cuda.synchronize()  # (the buffers are filled on the null stream, the frames run on the context's stream)
 
     def frame(i):
         if world == 1:
@@ -115,14 +119,13 @@ def collective_ms(world):
     rgb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
     ctx.finish()
     torch.cuda.synchronize()
-    u = event_ms(lambda: ctx.untile(gathered.data_ptr(), W, H, TILE, world, avg.data_ptr(), rgb.data_ptr()),
-                 stream or torch.cuda.current_stream())  # (own stream: the untile is not on the events' stream)
+    us = side or torch.cuda.Stream()
+    ctx.set_stream(us.cuda_stream)
+    u = event_ms(lambda: ctx.untile(gathered.data_ptr(), W, H, TILE, world, avg.data_ptr(), rgb.data_ptr()), us)
+    ctx.set_stream(side.cuda_stream if SIDE else None)
     return g, u, per * 16
 
 
-os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-os.environ.setdefault("MASTER_PORT", "29531")
-dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
 scene = "c5" if C5 else "c4"
 w1_one, rays1 = share_ms(1, 0, 1)
 w1_fl, _ = share_ms(1, 0, INFLIGHT1)

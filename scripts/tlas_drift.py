@@ -32,6 +32,9 @@ INFLIGHT = int(os.environ.get("PRT_DRIFT_INFLIGHT", "1"))  # frames in flight of
 # the contexts' stream: a torch side stream, so the pacing events below are recorded in the frames' order (torch's
 # current stream is the null stream here, and prt_set_stream(NULL) means the context's own stream)
 STREAM = torch.cuda.Stream()
+OWN = os.environ.get("PRT_DRIFT_STREAM", "side") == "own"  # A/B: the context's own stream (pacing then off)
+if OWN:
+    PACE = 0
 rng = np.random.default_rng(3)
 vel = rng.uniform(-0.08, 0.08, (len(sd.instances), 2)).astype(np.float32)
 
@@ -57,7 +60,7 @@ def set_instances(ctx, inst):  # the ABI call itself (prt_set_instances), withou
 def context(inst):
     """a fresh context whose first instance BVH is built over `inst` (the scene's own instances)"""
     ctx = prt.Context(0)
-    ctx.set_stream(STREAM.cuda_stream)
+    ctx.set_stream(None if OWN else STREAM.cuda_stream)
     mi, T = inst
     ctx.set_scene(prt.Scene.from_data(dataclasses.replace(sd, instances=[(int(m), T[k]) for k, m in enumerate(mi)])))
     ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
@@ -101,7 +104,7 @@ ref = context(inst)
 frames(ref, avg, rgb, 5)
 ms_ref, _ = frames(ref, avg, rgb, 20)
 ref.close()
-print(f"{N} instances, {F} frames of drift (pace {PACE}, {INFLIGHT} in flight; stacks for {si.max_depth} + "
+print(f"{N} instances, {F} frames of drift ({'own' if OWN else 'side'} stream, pace {PACE}, {INFLIGHT} in flight; stacks for {si.max_depth} + "
       f"{si.tlas_depth} levels): {ms_drift:.3f} ms/frame; set_instances host "
       f"{np.mean(host):.3f} ms mean, {np.percentile(host, 99):.3f} p99, {np.max(host):.3f} max; {si.tlas_rebuilds} "
       f"rebuilds ({si.tlas_async} on the worker, {si.tlas_median} median-split), last worker build "

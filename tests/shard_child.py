@@ -47,8 +47,9 @@ def bench(flights, W, H):
 
     def run(shard):
         c = prt.Context(0)
+        side = torch.cuda.Stream()  # the context's stream, as bench.py sets it (outputs allocated in its order)
         try:
-            c.set_stream(torch.cuda.current_stream().cuda_stream)
+            c.set_stream(side.cuda_stream)
             c.set_scene(scene)
             c.set_camera(cam)
             world = 1
@@ -59,8 +60,9 @@ def bench(flights, W, H):
             for f in range(6):
                 if f == 3:
                     c.set_instances(moved)
-                avg = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
-                rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+                with torch.cuda.stream(side):
+                    avg = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+                    rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
                 c.render(W, H, 4, 4, frame_index=2 * f, avg=avg.data_ptr(), rgb8=rgb.data_ptr(), device_out=True,
                          stats=False)
                 outs.append((avg, rgb))
