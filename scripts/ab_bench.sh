@@ -14,9 +14,10 @@ for r in $(seq 1 "$R"); do
   i=0
   for v in "$@"; do
     i=$((i + 1))
-    envs=${v%%::*}; args=""
+    envs=$(echo ${v%%::*}); args=""  # (echo trims the blanks around the assignments)
     [[ "$v" == *"::"* ]] && args=${v#*::}
     [ "$envs" = "-" ] && envs=""
+    case "$envs" in -*) echo "bad variant '$v': assignments only (VAR=value ...), or '-'"; exit 2 ;; esac
     log=gpurun_out/ab_${T}_${r}_${i}.log
     env $envs timeout -k 10 300 python3 bench.py --no-cpu-baseline $args > "$log" 2>&1
     rc=$?

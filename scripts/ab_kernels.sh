@@ -16,6 +16,7 @@ for r in $(seq 1 "$R"); do
     i=$((i + 1))
     envs=$v
     [ "$envs" = "-" ] && envs=""
+    case "$envs" in -*) echo "bad variant '$v': assignments only (VAR=value ...), or '-'"; exit 2 ;; esac
     D=gpurun_out/abk_${T}_${r}_${i}
     rm -rf "$D"
     env $envs timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$D" -o run -- \
