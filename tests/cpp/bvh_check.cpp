@@ -5,9 +5,12 @@
 //                                   (the conservative-box contract the traversal's hit rule relies on), interior
 //                                   children and triangle ranges are in bounds, the depth the builder reports is the
 //                                   tree's depth
-//   tlas <boxes.bin>                every instance sits in exactly one leaf slot of the instance BVH, inside the box
+//   tlas <boxes.bin> [max_depth]    every instance sits in exactly one leaf slot of the instance BVH, inside the box;
+//                                   with a depth cap (build_tlas8's max_depth), the tree has at most that many levels
+//                                   (the median-split tree when the SAH tree is deeper) and at most max(n, 1) nodes
 // tris.bin: float32 fat triangles (Model::triangles, 3 x float4 per triangle); boxes.bin: float32 {lo[3], hi[3]}.
 // Prints one JSON line; exit status 0 = all invariants hold.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -99,9 +102,24 @@ static int check_blas(const std::vector<float>& t, bool spatial) {
   return 0;
 }
 
-static int check_tlas(const std::vector<float>& bx) {
+static int tree_depth(const std::vector<Node8>& nodes, uint32_t j) {  // levels below and including node j
+  int d = 0;
+  for (int s = 0; s < 8; s++)
+    if ((nodes[j].imask >> s) & 1u) {
+      const uint32_t c = nodes[j].child_base + __builtin_popcount(nodes[j].imask & ((1u << s) - 1u));
+      if (c >= nodes.size() || c <= j) return 1000;  // out of range or not below its parent
+      d = std::max(d, tree_depth(nodes, c));
+    }
+  return d + 1;
+}
+
+static int check_tlas(const std::vector<float>& bx, int max_depth) {
   const int32_t n = (int32_t)(bx.size() / 6);
-  const BuiltTlas8 t = build_tlas8(bx.data(), n);
+  const BuiltTlas8 t = build_tlas8(bx.data(), n, max_depth);
+  const int d = tree_depth(t.nodes, 0);
+  if (d != t.depth) return fail("reported depth differs", d, t.depth);
+  if (max_depth > 0 && t.depth > max_depth) return fail("deeper than the cap", t.depth, max_depth);
+  if ((int64_t)t.nodes.size() > std::max(n, 1)) return fail("more nodes than instances", (long)t.nodes.size(), n);
   std::vector<int> seen(n, 0);
   for (size_t j = 0; j < t.nodes.size(); j++) {
     const Node8& nd = t.nodes[j];
@@ -119,7 +137,8 @@ static int check_tlas(const std::vector<float>& bx) {
   }
   for (int32_t i = 0; i < n; i++)
     if (seen[i] != 1) return fail("instance not in exactly one slot", i, seen[i]);
-  std::printf("{\"ok\": true, \"instances\": %d, \"nodes\": %zu, \"depth\": %d}\n", n, t.nodes.size(), t.depth);
+  std::printf("{\"ok\": true, \"instances\": %d, \"nodes\": %zu, \"depth\": %d, \"median\": %d, \"median_depth\": %d}\n", n,
+              t.nodes.size(), t.depth, (int)t.median, tlas8_median_depth(n));
   return 0;
 }
 
@@ -128,6 +147,6 @@ int main(int argc, char** argv) {
   const std::vector<float> v = read_f32(argv[2]);
   if (v.empty()) return 2;
   if (!std::strcmp(argv[1], "blas")) return check_blas(v, argc > 3 && std::atoi(argv[3]) != 0);
-  if (!std::strcmp(argv[1], "tlas")) return check_tlas(v);
+  if (!std::strcmp(argv[1], "tlas")) return check_tlas(v, argc > 3 ? std::atoi(argv[3]) : 0);
   return 2;
 }

@@ -84,4 +84,24 @@ def test_tlas_invariants(checker, tmp_path):
     path = str(tmp_path / "boxes.bin")
     np.asarray(boxes, np.float32).tofile(path)
     out = _run(checker, "tlas", path)
-    assert out["instances"] == len(sd.instances) and out["depth"] >= 3
+    assert out["instances"] == len(sd.instances) and out["depth"] >= 3 and not out["median"]
+
+
+@pytest.mark.parametrize("n", [1, 2, 9, 65, 1000, 5000])
+def test_tlas_depth_cap_and_median_fallback(checker, tmp_path, n):
+    """build_tlas8's depth cap (prt_api.cpp ensure_instances sizes the traversal stacks at an instance count's first
+    build and caps the worker's later builds there): a cap at the SAH tree's own depth keeps the SAH tree; a cap
+    below it yields the balanced median-split tree, within tlas8_median_depth(n) levels; both keep every instance in
+    exactly one slot, inside its slot's box, and at most max(n, 1) nodes."""
+    rng = np.random.default_rng(n)
+    c = rng.uniform(-4.5, 4.5, (n, 3)).astype(np.float32)
+    c[:, 1] *= np.float32(0.1)
+    h = np.array([0.4, 0.15, 0.4], np.float32)
+    path = str(tmp_path / "boxes.bin")
+    np.concatenate([c - h, c + h], axis=1).astype(np.float32).tofile(path)
+    free = _run(checker, "tlas", path)
+    same = _run(checker, "tlas", path, str(free["depth"]))
+    assert not same["median"] and same["depth"] == free["depth"] and same["nodes"] == free["nodes"]
+    capped = _run(checker, "tlas", path, str(free["median_depth"]))
+    assert capped["depth"] <= free["median_depth"]
+    assert capped["median"] == (free["depth"] > free["median_depth"])
