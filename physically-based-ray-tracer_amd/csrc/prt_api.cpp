@@ -111,7 +111,8 @@ struct StageSlot {
   size_t bytes = 0;
   hipEvent_t ev = nullptr;
   bool used = false;
-  uint64_t seq = 0;  // when it was last acquired
+  bool lost = false;  // an update failed while enqueuing from it: never handed out again (its copies may be pending)
+  uint64_t seq = 0;   // when it was last acquired
 };
 // One copy of the instance state the frames read (prt_ctx::isets): instance records, their refit input, the instance
 // BVH.  An update writes the next copy in the ring while the frames in flight still read theirs; a copy is
@@ -428,6 +429,7 @@ int occ_for(const prt_ctx* c) { return occ_at(stack_depth(c)); }
 int stage_acquire(prt_ctx* c, size_t bytes, StageSlot*& out) {
   StageSlot* pick = nullptr;
   for (StageSlot& t : c->stage) {
+    if (t.lost) continue;
     if (t.used) {
       const hipError_t q = hipEventQuery(t.ev);
       if (q == hipErrorNotReady) {
@@ -445,7 +447,8 @@ int stage_acquire(prt_ctx* c, size_t bytes, StageSlot*& out) {
   }
   if (!pick) {  // every buffer in use: wait for the one acquired first
     for (StageSlot& t : c->stage)
-      if (!pick || t.seq < pick->seq) pick = &t;
+      if (!t.lost && (!pick || t.seq < pick->seq)) pick = &t;
+    if (!pick) return fail(PRT_ERR_HIP, "no usable staging buffer (earlier updates failed)");
     HIP_TRY(hipEventSynchronize(pick->ev));
     pick->used = false;
   }
@@ -567,7 +570,7 @@ int ensure_instances(prt_ctx* c) {
     for (StageSlot& t : c->stage) {
       if (t.used && hipEventQuery(t.ev) == hipSuccess) t.used = false;
       (void)hipGetLastError();  // (hipErrorNotReady of a buffer still in use)
-      if (!t.used && t.bytes < per) {
+      if (!t.used && !t.lost && t.bytes < per) {
         if (t.p) HIP_TRY(hipHostFree(t.p));
         t.p = nullptr;
         t.bytes = 0;
@@ -580,6 +583,7 @@ int ensure_instances(prt_ctx* c) {
   int rc = stage_acquire(c, sb_src + sb_nodes + sb_slot, st);
   if (rc) return rc;
   char* hp = static_cast<char*>(st->p);
+  st->lost = true;  // until the copies out of it are enqueued (a failure below leaves it out of the pool)
   std::memcpy(hp, src.data(), sb_src);  // (the worker reads the sources from here)
   HIP_TRY(hipMemcpyAsync(X.inst_src.p, hp, sb_src, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(launch_refit(c->stream, X.inst_src.as<InstSrc>(), n, X.inst.as<InstDev>()));
@@ -609,6 +613,7 @@ int ensure_instances(prt_ctx* c) {
   }
   rc = stage_release(c, *st, c->stream);
   if (rc) return rc;
+  st->lost = false;
   c->use_tlas = use_tlas;
   if (!use_tlas) {
     c->tlas_depth = 0;
