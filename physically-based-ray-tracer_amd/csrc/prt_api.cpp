@@ -105,7 +105,9 @@ struct Flight {
 // 20-190 ms per buffer on the GPU box, profiles/r06_tlas_drift.txt); an update that finds all of them in use waits
 // for the oldest one's copies (the host at most kStageSlots updates ahead of the GPU)
 constexpr size_t kStageSlots = 8;
-constexpr double kHostWaitLimitS = 30.0;  // the stream's wait for a worker build (a build takes ~6 ms at 10,000)
+// the stream's wait for a worker build: a build takes ~6 ms at 10,000 instances and the jobs of up to kStageSlots
+// queued updates run one after another, so the limit only catches a producer that never comes
+constexpr double kHostWaitLimitS = 120.0;
 struct StageSlot {
   void* p = nullptr;
   size_t bytes = 0;
