@@ -234,9 +234,9 @@ def main():
         sys.exit(spawn_ranks(args.gpus))
     # Frames in flight: the best measured setting per share size (profiles/r05_inflight.txt): 2 for the whole
     # frame, 4 (with half grids per chain) for the shares of 2-8 GPUs.  Each chain runs on its own HIP stream, and
-    # HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default) round-robin: with more
-    # chains than free queues two chains share one and serialise behind each other's waits, so above 2 chains the
-    # runtime is given 8 queues (set before anything initialises HIP)
+    # HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default) round-robin.  The headline
+    # runs on the runtime's own queue count; --hw-queues is an explicit opt-in (set before anything initialises
+    # HIP), and at world 8 the 4-queue share measured the faster one (profiles/r06_rank_shares_inflight_queues.txt)
     if args.inflight is None:
         args.inflight = default_inflight(args.gpus)
     if args.hw_queues:
