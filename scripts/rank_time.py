@@ -55,7 +55,9 @@ ctx.set_stream(side.cuda_stream if SIDE else None)
 ctx.set_scene(prt.Scene.from_data(sd))
 ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
 ctx.set_frames_in_flight(max(INFLIGHT, INFLIGHT1))
-NT = 2 if C5 else 8  # timed frames per share
+# timed frames per share (env PRT_RANK_FRAMES): 40 C4 frames (≈ 45 ms at world 8) -- with 8, one slow frame
+# moved a rank's share by up to 10 % and the max over ranks with it
+NT = int(os.environ.get("PRT_RANK_FRAMES", "4" if C5 else "40"))
 
 
 def share_ms(world, rank, inflight):
