@@ -185,7 +185,7 @@ def cpu_baseline(sd, W, H, spp, bounces):
 
 def default_inflight(gpus):
     """Frames in flight bench.py keeps by default (prt_set_frames_in_flight; profiles/r06_rank_shares.txt): 2 on one
-    GPU, 4 on several (each chain on half-size grids)."""
+    GPU, 4 on several (each chain on a third or half of the resident blocks)."""
     return 4 if gpus >= 2 else 2
 
 
@@ -233,7 +233,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
     # Frames in flight: the best measured setting per share size (profiles/r05_inflight.txt): 2 for the whole
-    # frame, 4 (with half grids per chain) for the shares of 2-8 GPUs.  Each chain runs on its own HIP stream, and
+    # frame, 4 (with cut grids per chain) for the shares of 2-8 GPUs.  Each chain runs on its own HIP stream, and
     # HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default) round-robin.  The headline
     # runs on the runtime's own queue count; --hw-queues is an explicit opt-in (set before anything initialises
     # HIP), and at world 8 the 4-queue share measured the faster one (profiles/r06_rank_shares_inflight_queues.txt)

@@ -973,11 +973,16 @@ int enqueue_render_body(prt_ctx* c, const prt_render_params* p, const TileMap& M
   const hipStream_t st = fl ? fl->stream : c->stream;
   WaveState& ws0 = flight_ws(c, fl);
   LaunchCfg L{st, occ_for(c), 1};
-  // frames in flight: from 4 frames in flight on, each chain's wavefront grids are half the resident blocks, so the
-  // chains' persistent traversal launches co-reside instead of taking the whole GPU in turns (C4 world-8 share
-  // 1.32 ms with 2 in flight, 1.24 with 4 and half grids; quarter / eighth grids and 6 or 8 in flight 1.31-1.77 ms:
-  // profiles/r06_rank_shares.txt)
-  const uint32_t Gw = (fl && c->inflight >= 4) ? 2u : 1u;
+  // frames in flight: from 4 frames in flight on, each chain's wavefront grids are a fraction of the resident blocks,
+  // so the chains' persistent traversal launches co-reside instead of taking the whole GPU in turns: a third for
+  // calls of up to 2^20 items (C4 world-8 share 1.101-1.109 ms with half grids, 1.055-1.062 with a third, 1.079-1.085
+  // with a quarter, 1.32 with an eighth; world 4: 1.940-1.949 / 1.878-1.907 / 1.945-1.953 ms), half above (world 2:
+  // 3.56-3.57 ms with half grids, 3.72-3.74 with a quarter) -- profiles/r06_ab_flight_grids.txt
+#ifdef PRT_FLIGHT_GW  // (A/B builds only)
+  const uint32_t Gw = (fl && c->inflight >= 4) ? (uint32_t)PRT_FLIGHT_GW : 1u;
+#else
+  const uint32_t Gw = (fl && c->inflight >= 4) ? (per * (uint64_t)R.F0 <= (1ull << 20) ? 3u : 2u) : 1u;
+#endif
   const LaunchCfg Lw{st, L.occ, Gw};  // the wavefront chain's launches
   // the call's own events (prt_stats ms / ms_trace) only with stats: each record is a gap between kernels
   if (want_stats) HIP_TRY(hipEventRecord(c->ev[0], st));

@@ -842,11 +842,19 @@ static void launch_trace2(const LaunchCfg& c, const SceneDev& S, const WaveBufs&
   else launch_t2<18, 4, 32>(c, S, B, it, iters);
 }
 
+// producer grids (the kernels that append to the sub-queues: k_wave_init, the shading kernels): a multiple of kNSub,
+// so that block b appends to sub-queue b % kNSub exactly the chunks c == b (mod kNSub) it consumes -- the bound
+// ensure_wave sizes each sub-queue by (qcap).  1/groups of the resident blocks, rounded down to that multiple
+__host__ inline unsigned producer_blocks(const LaunchCfg& c) {
+  const unsigned g = 256u * 4u / c.groups;
+  return g < kNSub ? kNSub : g - g % kNSub;
+}
+
 // one iteration of the merged pipeline: trace P(it) + S(it - 1), resolve P(it - 1), miss + shade P(it)
 hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                              const WaveBufs& B, float4* out, WaveTimers* tm, uint32_t it) {
   if (B.n == 0) return hipSuccess;
-  const unsigned gprod = 256u * 4u / c.groups;  // producer blocks (multiple of kNSub for groups <= 32)
+  const unsigned gprod = producer_blocks(c);
   // k_shade2 over 4x the resident blocks when a call holds >= 2^21 items: the extra blocks queue behind the
   // resident ones and even out the kernel's end (C4 frame -1 to -2 %); below that the extra launch width costs
   // more than it evens out (world-8 shares). PRT_SHADE_GRID overrides (A/B runs).
@@ -898,7 +906,7 @@ hipError_t launch_wave2_iter(const LaunchCfg& c, const SceneDev& S, const TraceA
 
 hipError_t launch_wave_init(const LaunchCfg& c, const SceneDev& S, const TraceArgs& A, const TileMap& M,
                             const WaveBufs& B, float4* out) {
-  hipLaunchKernelGGL(k_wave_init, dim3(256u * 4u / c.groups), dim3(kBlock), 0, c.stream, S, A, M, B, out);
+  hipLaunchKernelGGL(k_wave_init, dim3(producer_blocks(c)), dim3(kBlock), 0, c.stream, S, A, M, B, out);
   return hipGetLastError();
 }
 

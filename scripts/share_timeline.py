@@ -101,6 +101,7 @@ while time.perf_counter() - tw < 0.5:
     if k % 4 == 0:
         torch.cuda.synchronize()
 ctx.finish()
+ctx.ray_totals(reset=True)
 torch.cuda.synchronize()
 NT = int(os.environ.get("PRT_TL_FRAMES", "20"))
 t0 = time.perf_counter()
@@ -108,7 +109,9 @@ for i in range(NT):
     frame(k + i)
 ctx.finish()
 torch.cuda.synchronize()
-print(f"world {WORLD} rank {RANK}: {INFLIGHT} in flight, {(time.perf_counter() - t0) * 1e3 / NT:.3f} ms per frame "
-      f"over the last {NT} frames", flush=True)
+ms = (time.perf_counter() - t0) * 1e3 / NT
+seg, sh = ctx.ray_totals(reset=True)
+print(f"world {WORLD} rank {RANK}: {INFLIGHT} in flight, {ms:.3f} ms per frame over the last {NT} frames, "
+      f"{(seg + sh) // NT} rays per frame", flush=True)
 ctx.close()
 dist.destroy_process_group()

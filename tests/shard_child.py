@@ -6,7 +6,7 @@ Prints one JSON line.
   shard_child.py bench <frames_in_flight> <W> <H>
       bench.py's configuration on several GPUs, on this one: a torch.distributed "nccl" group (world 1 here), the
       context sharded inside the boundary (prt.tiles.join_rccl -> prt_shard_init_rccl, one ncclGather per frame),
-      the given frames in flight (4 = bench.py's default from 2 GPUs, whose chains run on half-size grids), C4's
+      the given frames in flight (4 = bench.py's default from 2 GPUs, whose chains run on cut grids), C4's
       1M-triangle scene at W x H, 4 spp, depth 4; 6 accumulating frames with device outputs and an instance update
       before frame 3.  Every frame is compared with an unsharded context rendering the same sequence one frame at
       a time: {"frames": 6, "mismatch": [...], "world": 1, "queues": ...}

@@ -1,6 +1,6 @@
 """bench.py's multi-GPU configuration exercised on one GPU: the first 8-GPU run
 executes exactly this -- an RCCL-sharded context (prt_shard_init_rccl inside the boundary, one ncclGather per
-frame), bench.py's frames in flight on several GPUs with half-size chain grids, the process's hardware-queue
+frame), bench.py's frames in flight on several GPUs with cut chain grids, the process's hardware-queue
 setting read before any HIP call -- so it runs here in a child process with those settings, and every frame must
 equal the unsharded one bit for bit.  A communicator whose peers never arrive must fail within the time limit
 (prt_shard_init_rccl with a non-blocking, polled RCCL set-up) instead of hanging."""

@@ -152,7 +152,7 @@ def test_frames_in_flight_outputs_in_stream_order(flights):
 @pytest.mark.parametrize("flights", [3, 4])
 def test_frames_in_flight_rccl_world1(flights):
     """An RCCL shard (world 1: the ncclGather path) with 3 or 4 frames in flight (4: the setting bench.py uses on
-    several GPUs, with each chain on half-size grids): each call's gather and untile run on its slot's stream after
+    several GPUs, with each chain on cut grids): each call's gather and untile run on its slot's stream after
     the previous call's; through an instance update, a camera change with an accumulation reset and a stats call,
     every frame equals the unsharded one-at-a-time render bit for bit."""
     import torch
