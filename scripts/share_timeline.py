@@ -72,7 +72,8 @@ from bench import default_inflight  # noqa: E402
 WORLD = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 RANK = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 INFLIGHT = int(os.environ.get("PRT_RANK_INFLIGHT", str(default_inflight(WORLD))))
-W, H, SPP, BOUNCES, TILE = 1920, 1080, 4, 4, 32
+C5 = os.environ.get("PRT_TL_SCENE", "c4") == "c5"  # PRT_TL_SCENE=c5: the C5 frame (3840x2160, 16 spp, depth 8)
+W, H, SPP, BOUNCES, TILE = (3840, 2160, 16, 8, 32) if C5 else (1920, 1080, 4, 4, 32)
 FPC = SPP // 2
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29533")
@@ -80,7 +81,7 @@ os.environ.setdefault("MASTER_PORT", "29533")
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
 ctx = prt.Context(0)
 ctx.set_stream(None)
-sd = scenes.config_c4()
+sd = scenes.config_c5() if C5 else scenes.config_c4()
 ctx.set_scene(prt.Scene.from_data(sd))
 ctx.set_camera(prt.Camera(sd.cam_pos, sd.cam_target, np.float32(W) / np.float32(H)))
 ctx.set_frames_in_flight(INFLIGHT)
